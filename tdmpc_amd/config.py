@@ -1,0 +1,114 @@
+"""Planner configuration: the subset of the reference cfg that `TDMPC.plan` reads.
+
+The reference builds its cfg with OmegaConf (`src/cfg.py:6-48`): `cfgs/default.yaml` <- CLI <-
+`cfgs/{modality}.yaml` <- `cfgs/tasks/{domain}.yaml`. OmegaConf is not a dependency here, and only
+attribute access is needed on the hot path, so the cfg is a plain namespace. `make_cfg(task)` resolves
+the same precedence for the keys `plan()` touches; the values are cited below so they can be checked.
+
+`obs_shape` / `action_dim` are injected at runtime by the reference's `make_env` (`envs/env.py:284-286`);
+dm_control is not installed here, so the DMControl task dims are listed in `TASK_DIMS`.
+"""
+from __future__ import annotations
+
+import re
+from types import SimpleNamespace
+
+# cfgs/default.yaml values used by TDMPC / TOLD (line numbers in that file).
+DEFAULTS = dict(
+    modality="state",            # :3
+    discount=0.99,               # :4
+    iterations=6,                # :10
+    num_samples=512,             # :11 says 256 ("256 for icem, 512 default"); 512 is the TD-MPC default the
+                                 #     north-star metric is quoted on (BASELINE.json metric: N=512)
+    num_elites=64,               # :12 says 32 ("32 for icem, 64 default"); 64 at N=512
+    mixture_coef=0.5,            # :13
+    min_std=0.05,                # :14
+    temperature=0.5,             # :15
+    momentum=0.1,                # :16
+    horizon=5,                   # :29 is 6; BASELINE.json pins H=5 for every config
+    std_schedule="linear(0.5, 0.05, 25000, 0)",      # :45 (min_std substituted)
+    horizon_schedule="linear(2, 5, 25000, 0)",       # :46 (horizon substituted)
+    seed_steps=5000,             # :48
+    enc_dim=256,                 # :72
+    mlp_dim=512,                 # :73
+    latent_dim=50,               # :74
+    lr=1e-3,                     # :60 (unused by plan, kept for TDMPC.__init__ parity)
+    # pixels.yaml
+    frame_stack=3,               # cfgs/pixels.yaml:2
+    num_channels=32,             # cfgs/pixels.yaml:3
+    img_size=84,                 # cfgs/pixels.yaml:4
+)
+
+# obs_dim / action_dim of the DMControl tasks the configs name (dm_control task specs).
+TASK_DIMS = {
+    "cartpole": (5, 1),
+    "cheetah": (17, 6),
+    "humanoid": (67, 21),
+    "dog": (223, 38),
+    "quadruped": (78, 12),
+}
+
+# cfgs/tasks/{domain}.yaml overrides of keys the planner reads.
+TASK_OVERRIDES = {
+    "humanoid": dict(latent_dim=100),   # cfgs/tasks/humanoid.yaml:6 (iterations:3 / num_samples:4 are
+                                        # overridden by BASELINE.json's N=512, iters=6)
+    "dog": dict(latent_dim=100),        # cfgs/tasks/dog.yaml:4
+    "cartpole": dict(),                 # cfgs/tasks/cartpole.yaml: action_repeat only
+}
+
+# The BASELINE.json configs (name -> overrides). N/H/I come from BASELINE.json itself.
+BENCH_CONFIGS = {
+    "cartpole-swingup": dict(task="cartpole", num_samples=64, num_elites=32, iterations=3, horizon=5),
+    "cheetah-run": dict(task="cheetah", num_samples=512, num_elites=64, iterations=6, horizon=5),
+    "humanoid-run": dict(task="humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5),
+    "humanoid-run-l512": dict(task="humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5,
+                              latent_dim=512),
+    "dog-run": dict(task="dog", num_samples=512, num_elites=64, iterations=6, horizon=5),
+    "quadruped-run-pixels": dict(task="quadruped", modality="pixels", num_samples=512, num_elites=64,
+                                 iterations=6, horizon=5),
+}
+
+
+def make_cfg(task: str = "humanoid", **overrides) -> SimpleNamespace:
+    """Resolve a planner cfg: defaults <- task yaml <- overrides (mirrors `src/cfg.py:8-32` precedence)."""
+    d = dict(DEFAULTS)
+    d.update(TASK_OVERRIDES.get(task, {}))
+    d.update(overrides)
+    obs_dim, act_dim = TASK_DIMS[task]
+    if d["modality"] == "pixels":
+        d["obs_shape"] = (3 * d["frame_stack"], d["img_size"], d["img_size"])
+    else:
+        d["obs_shape"] = (obs_dim,)
+    d["action_dim"] = act_dim
+    d["task"] = task
+    d["device"] = "cuda"
+    # schedules are written with the resolved min_std / horizon, as OmegaConf interpolation would.
+    if "std_schedule" not in overrides:
+        d["std_schedule"] = f"linear(0.5, {d['min_std']}, 25000, 0)"
+    if "horizon_schedule" not in overrides:
+        d["horizon_schedule"] = f"linear(2, {d['horizon']}, 25000, 0)"
+    return SimpleNamespace(**d)
+
+
+def bench_cfg(name: str, **overrides) -> SimpleNamespace:
+    spec = dict(BENCH_CONFIGS[name])
+    spec.update(overrides)
+    task = spec.pop("task")
+    return make_cfg(task, **spec)
+
+
+def linear_schedule(schdl, step) -> float:
+    """Reference `helper.linear_schedule` (`src/algorithm/helper.py:639-652`).
+
+    A float (or float string) is returned as is; `linear(init,final,duration,start)` mixes linearly
+    with mix = clip((step-start)/duration, 0, 1), computed in float64 like numpy does there.
+    """
+    try:
+        return float(schdl)
+    except (TypeError, ValueError):
+        m = re.match(r"linear\((.+),(.+),(.+),(.+)\)", schdl)
+        if m:
+            init, final, duration, start = [float(g) for g in m.groups()]
+            mix = min(max((step - start) / duration, 0.0), 1.0)
+            return (1.0 - mix) * init + mix * final
+    raise NotImplementedError(schdl)

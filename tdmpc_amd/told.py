@@ -1,0 +1,123 @@
+"""TOLD parameter container with the reference's module tree and state_dict key names.
+
+Reference: `TOLD` in `src/algorithm/tdmpc.py:9-50`, built from `helper.enc` (`helper.py:119-133`),
+`helper.mlp` (`helper.py:169-176`) and `helper.q` (`helper.py:197-201`).
+
+The module exists so that a reference checkpoint (`{'model': sd, 'model_target': sd}`, `tdmpc.py:68-81`)
+loads with `load_state_dict` unchanged and so that `TDMPC.model` exposes the same attributes. Planning does
+NOT run these modules: `TDMPC.plan` packs the parameters into one device buffer and runs the HIP kernels.
+The eager `forward`-style helpers (`h`, `next`, `pi`, `Q`) are kept for inspection and for the learner,
+which is outside this round's scope.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+
+def _enc(cfg) -> nn.Sequential:
+    if cfg.modality == "pixels":
+        c = int(3 * cfg.frame_stack)
+        nc = cfg.num_channels
+        layers = [nn.Identity(),  # NormalizeImg (x/255) is parameter-free; index 0 like the reference
+                  nn.Conv2d(c, nc, 7, stride=2), nn.ReLU(),
+                  nn.Conv2d(nc, nc, 5, stride=2), nn.ReLU(),
+                  nn.Conv2d(nc, nc, 3, stride=2), nn.ReLU(),
+                  nn.Conv2d(nc, nc, 3, stride=2), nn.ReLU()]
+        s = cfg.img_size
+        for k in (7, 5, 3, 3):
+            s = (s - k) // 2 + 1
+        layers += [nn.Flatten(), nn.Linear(nc * s * s, cfg.latent_dim)]
+        return nn.Sequential(*layers)
+    return nn.Sequential(nn.Linear(cfg.obs_shape[0], cfg.enc_dim), nn.ELU(),
+                         nn.Linear(cfg.enc_dim, cfg.latent_dim))
+
+
+def _mlp(in_dim, mlp_dim, out_dim) -> nn.Sequential:
+    return nn.Sequential(nn.Linear(in_dim, mlp_dim), nn.ELU(),
+                         nn.Linear(mlp_dim, mlp_dim), nn.ELU(),
+                         nn.Linear(mlp_dim, out_dim))
+
+
+def _q(cfg) -> nn.Sequential:
+    m = cfg.mlp_dim
+    return nn.Sequential(nn.Linear(cfg.latent_dim + cfg.action_dim, m), nn.LayerNorm(m), nn.Tanh(),
+                         nn.Linear(m, m), nn.LayerNorm(m), nn.ELU(),
+                         nn.Linear(m, 1))
+
+
+def pixel_enc_out_hw(cfg) -> int:
+    s = cfg.img_size
+    for k in (7, 5, 3, 3):
+        s = (s - k) // 2 + 1
+    return s
+
+
+class TOLD(nn.Module):
+    """Task-Oriented Latent Dynamics: encoder h, dynamics d, reward R, policy pi, twin Q."""
+
+    def __init__(self, cfg, init: str = "reference"):
+        super().__init__()
+        self.cfg = cfg
+        self._encoder = _enc(cfg)
+        self._dynamics = _mlp(cfg.latent_dim + cfg.action_dim, cfg.mlp_dim, cfg.latent_dim)
+        self._reward = _mlp(cfg.latent_dim + cfg.action_dim, cfg.mlp_dim, 1)
+        self._pi = _mlp(cfg.latent_dim, cfg.mlp_dim, cfg.action_dim)
+        self._Q1, self._Q2 = _q(cfg), _q(cfg)
+        if init == "reference":
+            # tdmpc.py:20-23: orthogonal init (helper.py:35-45), then zero the last layer of R, Q1, Q2.
+            self.apply(_orthogonal_init)
+            for m in (self._reward, self._Q1, self._Q2):
+                m[-1].weight.data.fill_(0)
+                m[-1].bias.data.fill_(0)
+
+    # Eager forms of the four heads (tdmpc.py:30-50); not used by the HIP planner.
+    def h(self, obs):
+        if self.cfg.modality == "pixels":
+            obs = obs / 255.0
+        return self._encoder(obs)
+
+    def next(self, z, a):
+        x = torch.cat([z, a], dim=-1)
+        return self._dynamics(x), self._reward(x)
+
+    def Q(self, z, a):
+        x = torch.cat([z, a], dim=-1)
+        return self._Q1(x), self._Q2(x)
+
+
+def _orthogonal_init(m):
+    if isinstance(m, nn.Linear):
+        nn.init.orthogonal_(m.weight.data)
+        if m.bias is not None:
+            nn.init.zeros_(m.bias)
+    elif isinstance(m, nn.Conv2d):
+        nn.init.orthogonal_(m.weight.data, nn.init.calculate_gain("relu"))
+        if m.bias is not None:
+            nn.init.zeros_(m.bias)
+
+
+def synthetic_state_dict(cfg, seed: int = 0) -> dict:
+    """Deterministic non-degenerate TOLD weights (BASELINE.md "Inputs"): every tensor of the reference
+    state_dict drawn from `np.random.RandomState(seed + i)` in key order. Linear/conv weights are
+    N(0, 1/fan_in) -- including the last layers of R/Q1/Q2, which the reference zero-inits and which would
+    make every candidate's value identical (SURVEY.md §5 "Zero-init makes values degenerate"). Biases are
+    N(0, 0.05^2); LayerNorm gains 1 + N(0, 0.1^2), shifts N(0, 0.1^2)."""
+    model = TOLD(cfg, init="none")
+    sd = {}
+    for i, (k, v) in enumerate(model.state_dict().items()):
+        rs = np.random.RandomState(seed * 1000 + i)
+        shape = tuple(v.shape)
+        is_ln = any(k.startswith(f"_Q{j}.{li}.") for j in (1, 2) for li in (1, 4))
+        if is_ln and k.endswith("weight"):
+            arr = 1.0 + 0.1 * rs.standard_normal(shape)
+        elif is_ln:
+            arr = 0.1 * rs.standard_normal(shape)
+        elif k.endswith("weight"):
+            fan_in = int(np.prod(shape[1:]))
+            arr = rs.standard_normal(shape) / np.sqrt(fan_in)
+        else:
+            arr = 0.05 * rs.standard_normal(shape)
+        sd[k] = torch.from_numpy(arr.astype(np.float32))
+    return sd
