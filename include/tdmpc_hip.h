@@ -1,0 +1,146 @@
+/*
+ * tdmpc_hip.h -- C ABI of libtdmpc_hip.so, the MI355X (gfx950) TD-MPC planner.
+ *
+ * This is the drop-in boundary of the planning hot path. The reference has no FFI: its
+ * boundary is the Python method `TDMPC.plan(obs, eval_mode=False, step=None, t0=True)`
+ * (/root/reference/src/algorithm/tdmpc.py:94-163). `tdmpc_amd.TDMPC.plan` keeps that signature and calls
+ * the entry points below through ctypes; any other host (C, C++, a cgo/JNI stub) can call them directly.
+ *
+ * Conventions
+ *   - Every pointer argument except `dims`, `params`, `layout` and the host-side arrays documented as such
+ *     is a DEVICE pointer owned by the caller. No entry point allocates device memory or synchronises.
+ *   - `stream` is a hipStream_t (NULL = default stream). Work is enqueued in stream order, so a call can be
+ *     captured into a hipGraph.
+ *   - Return 0 on success, a negative TDMPC_E* code otherwise. No exceptions cross the ABI.
+ *   - fp32 everywhere except the elite-choice uniform `u` (float64, like numpy's random_sample).
+ *   - Thread safety: no global mutable state; calls on distinct streams with distinct workspaces are safe.
+ */
+#ifndef TDMPC_HIP_H
+#define TDMPC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TDMPC_ABI_VERSION 1
+
+#define TDMPC_OK 0
+#define TDMPC_E_DIMS (-1)     /* unsupported or inconsistent dims / params */
+#define TDMPC_E_HIP (-2)      /* a HIP runtime call failed (hipGetLastError after a launch) */
+#define TDMPC_E_NULL (-3)     /* a required pointer is NULL */
+#define TDMPC_E_SIZE (-4)     /* a caller buffer is smaller than tdmpc_sizes() says */
+
+/* Static shape of one planner instance. Mirrors the cfg keys the reference reads
+ * (cfgs/default.yaml:10-16,29,72-74; obs_shape/action_dim from envs/env.py:284-286). */
+typedef struct tdmpc_dims {
+    int32_t modality;      /* 0 = state, 1 = pixels (helper.enc, helper.py:119-133) */
+    int32_t obs_dim;       /* state: obs_shape[0]; pixels: unused */
+    int32_t img_c;         /* pixels: 3*frame_stack */
+    int32_t img_hw;        /* pixels: img_size */
+    int32_t num_channels;  /* pixels: conv channels */
+    int32_t action_dim;    /* A */
+    int32_t latent_dim;    /* L */
+    int32_t mlp_dim;       /* M (hidden width of d, R, pi, Q); must be 512 or a multiple of 64 */
+    int32_t enc_dim;       /* E (state encoder hidden width) */
+    int32_t num_samples;   /* N  (cfg.num_samples) */
+    int32_t num_pi;        /* P = int(mixture_coef * N) */
+    int32_t num_elites;    /* K */
+    int32_t max_horizon;   /* largest H any call will use (workspace is sized for it) */
+    int32_t max_iterations;/* largest cfg.iterations any call will use */
+    int32_t max_batch;     /* largest number of environments planned per call */
+} tdmpc_dims;
+
+/* Per-call scalars (tdmpc.py:106-149). */
+typedef struct tdmpc_plan_params {
+    int32_t horizon;       /* H = int(min(cfg.horizon, linear_schedule(horizon_schedule, step))) */
+    int32_t iterations;    /* cfg.iterations */
+    int32_t batch;         /* number of environments in this call (<= max_batch) */
+    int32_t warm_start;    /* 1: mean[:-1] = prev_mean[1:] (not t0 and prev_mean exists) */
+    int32_t eval_mode;     /* 1: no final action noise (tdmpc.py:157) */
+    float min_std;         /* cfg.min_std (TruncatedNormal scale for pi) */
+    float temperature;     /* cfg.temperature */
+    float momentum;        /* cfg.momentum, as float32 */
+    float one_minus_momentum; /* float32(1 - momentum) computed in float64 like Python does */
+    float std_floor;       /* self.std: lower clamp of the CEM std (tdmpc.py:148) */
+    float discount_pow[17];/* float32(discount**t) for t = 0..H, the running Python-float product */
+} tdmpc_plan_params;
+
+/* Byte sizes the caller must allocate (all 256-byte aligned). */
+typedef struct tdmpc_sizes {
+    size_t packed_weight_bytes;  /* packed TOLD parameter buffer (tdmpc_pack_weights) */
+    size_t workspace_bytes;      /* scratch for one tdmpc_plan call at max dims */
+    size_t noise_floats_per_env; /* floats of the per-env noise stream at max horizon / iterations */
+} tdmpc_sizes;
+
+/* Returns TDMPC_ABI_VERSION. */
+int tdmpc_abi_version(void);
+
+/* Fill `out` for `dims`. */
+int tdmpc_sizes_for(const tdmpc_dims* dims, tdmpc_sizes* out);
+
+/* Number of floats of the per-env noise stream for a call with horizon H and I iterations:
+ *   H*P*A  (pre-rollout TruncatedNormal eps, tdmpc.py:117 / helper.py:88)
+ * + I*(H*N*A + T*A)  (per CEM iteration: torch.randn(H,N,A) tdmpc.py:131, then pi eps at the horizon
+ *                     tdmpc.py:91), T = N+P
+ * + A  (final action noise, tdmpc.py:158)
+ * laid out in exactly that (reference draw) order. */
+size_t tdmpc_noise_floats(const tdmpc_dims* dims, int32_t horizon, int32_t iterations);
+
+/* Number of parameter tensors tdmpc_pack_weights expects: the reference state_dict order
+ * (TOLD, tdmpc.py:9-23): _encoder.*, _dynamics.{0,2,4}.{weight,bias}, _reward.{0,2,4}.*, _pi.{0,2,4}.*,
+ * _Q1.{0,1,3,4,6}.*, _Q2.{0,1,3,4,6}.*  (state encoder: 4 tensors; pixel encoder: 10). */
+int tdmpc_num_param_tensors(const tdmpc_dims* dims);
+
+/* Pack the TOLD parameters (device pointers, reference state_dict order, fp32, contiguous nn.Linear
+ * [out,in] / Conv2d [out,in,kh,kw] layout) into `packed` (replaces TDMPC.model for planning). Enqueued on
+ * `stream`; re-run whenever the parameters change (after TDMPC.update). */
+int tdmpc_pack_weights(const tdmpc_dims* dims, const float* const* tensors, int32_t n_tensors,
+                       void* packed, size_t packed_bytes, void* stream);
+
+/* TOLD.h for `batch` observations (tdmpc.py:115,121 / helper.enc). obs: state fp32 [batch, obs_dim]; pixels
+ * uint8 [batch, C, S, S] if obs_is_u8 else fp32 of the same shape (raw 0..255 values, /255 inside).
+ * z0: fp32 [batch, L]. */
+int tdmpc_encode(const tdmpc_dims* dims, const void* packed, const void* obs, int32_t obs_is_u8,
+                 int32_t batch, void* workspace, float* z0, void* stream);
+
+/* One full TDMPC.plan for `params->batch` independent environments (tdmpc.py:94-163 minus the seed-step
+ * branch, which needs no model):
+ *   obs        [batch, obs...]        observation (fp32, or uint8 pixels when obs_is_u8)
+ *   noise      [batch, tdmpc_noise_floats(H, I)]  per-env noise streams in reference draw order
+ *   u          [batch] float64        the uniform numpy draws inside np.random.choice (tdmpc.py:153)
+ *   prev_mean  [batch, H, A] in/out   self._prev_mean (read when warm_start, always written)
+ *   action     [batch, A]      out    the planned action a (tdmpc.py:155-158)
+ *   metrics    [batch, 2]      out    {external_reward_mean, current_std} (tdmpc.py:160)
+ *   elite_out  [batch, H, K, A] out   optional (NULL ok): last iteration's elite actions
+ *   score_out  [batch, K]      out    optional: last iteration's softmax scores
+ *   value_out  [batch, I, T]   out    optional: every iteration's estimate_value output (tdmpc.py:137)
+ *   mean_out / std_out [batch, I, H, A] out optional: CEM mean/std after each iteration (tdmpc.py:149) */
+int tdmpc_plan(const tdmpc_dims* dims, const tdmpc_plan_params* params, const void* packed,
+               const void* obs, int32_t obs_is_u8, const float* noise, const double* u,
+               float* prev_mean, float* action, float* metrics,
+               float* elite_out, float* score_out, float* value_out, float* mean_out, float* std_out,
+               void* workspace, size_t workspace_bytes, void* stream);
+
+/* Building blocks of tdmpc_plan, exposed for unit parity tests (each is one part of the reference):
+ * rollout values for explicit candidate action sequences -- TDMPC.estimate_value (tdmpc.py:83-92) for
+ * `batch` envs with T rows each starting from z0[env]:
+ *   actions   [batch, H, T, A]   candidate actions (rows 0..T-1)
+ *   eps_term  [batch, T, A]      TruncatedNormal eps of the pi call at the horizon
+ *   value     [batch, T] out     G after nan_to_num
+ *   reward_last [batch, T] out   reward at t = H-1 (its mean is estimate_value's second output)
+ *   z_last    [batch, T, L] out  optional: latent after H steps */
+int tdmpc_estimate_value(const tdmpc_dims* dims, const tdmpc_plan_params* params, const void* packed,
+                         const float* z0, const float* actions, const float* eps_term, int32_t rows,
+                         float* value, float* reward_last, float* z_last,
+                         void* workspace, size_t workspace_bytes, void* stream);
+
+/* Last HIP error string seen by this thread (for diagnostics). */
+const char* tdmpc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TDMPC_HIP_H */

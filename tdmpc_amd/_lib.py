@@ -1,0 +1,100 @@
+"""ctypes binding of libtdmpc_hip.so (the C ABI declared in include/tdmpc_hip.h).
+
+The library is built in-tree (`python -m tdmpc_amd.build` or `__graft_entry__.build()`). There is no CPU
+fallback: if the shared object is missing or fails to load, `lib()` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libtdmpc_hip.so")
+
+EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc_num_param_tensors",
+            "tdmpc_pack_weights", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_last_error")
+
+
+class Dims(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "modality", "obs_dim", "img_c", "img_hw", "num_channels", "action_dim", "latent_dim", "mlp_dim",
+        "enc_dim", "num_samples", "num_pi", "num_elites", "max_horizon", "max_iterations", "max_batch")]
+
+
+class PlanParams(C.Structure):
+    _fields_ = [("horizon", C.c_int32), ("iterations", C.c_int32), ("batch", C.c_int32),
+                ("warm_start", C.c_int32), ("eval_mode", C.c_int32),
+                ("min_std", C.c_float), ("temperature", C.c_float), ("momentum", C.c_float),
+                ("one_minus_momentum", C.c_float), ("std_floor", C.c_float),
+                ("discount_pow", C.c_float * 17)]
+
+
+class Sizes(C.Structure):
+    _fields_ = [("packed_weight_bytes", C.c_size_t), ("workspace_bytes", C.c_size_t),
+                ("noise_floats_per_env", C.c_size_t)]
+
+
+_LIB = None
+
+
+def lib():
+    """Load (once) and return the library. Raises if it is not built: no silent fallback."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m tdmpc_amd.build` "
+                           "(hipcc --offload-arch=gfx950). The planner has no CPU fallback.")
+    import torch  # noqa: F401  -- load torch's libamdhip64 first so both share one HIP runtime
+    L = C.CDLL(LIB_PATH)
+    vp, i32, sz = C.c_void_p, C.c_int32, C.c_size_t
+    L.tdmpc_abi_version.restype = C.c_int
+    L.tdmpc_sizes_for.argtypes = [C.POINTER(Dims), C.POINTER(Sizes)]
+    L.tdmpc_noise_floats.argtypes = [C.POINTER(Dims), i32, i32]
+    L.tdmpc_noise_floats.restype = sz
+    L.tdmpc_num_param_tensors.argtypes = [C.POINTER(Dims)]
+    L.tdmpc_pack_weights.argtypes = [C.POINTER(Dims), C.POINTER(vp), i32, vp, sz, vp]
+    L.tdmpc_encode.argtypes = [C.POINTER(Dims), vp, vp, i32, i32, vp, vp, vp]
+    L.tdmpc_plan.argtypes = [C.POINTER(Dims), C.POINTER(PlanParams), vp, vp, i32, vp, vp, vp, vp, vp,
+                             vp, vp, vp, vp, vp, vp, sz, vp]
+    L.tdmpc_estimate_value.argtypes = [C.POINTER(Dims), C.POINTER(PlanParams), vp, vp, vp, vp, i32, vp, vp,
+                                       vp, vp, sz, vp]
+    L.tdmpc_last_error.restype = C.c_char_p
+    for name in EXPORTED:
+        if not hasattr(L, name):
+            raise RuntimeError(f"{LIB_PATH} does not export {name}")
+    if L.tdmpc_abi_version() != 1:
+        raise RuntimeError("libtdmpc_hip ABI version mismatch")
+    _LIB = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().tdmpc_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed with code {rc}: {msg}")
+
+
+def dims_from_cfg(cfg, max_batch: int = 1, max_horizon=None, max_iterations=None) -> Dims:
+    d = Dims()
+    pixels = cfg.modality == "pixels"
+    d.modality = 1 if pixels else 0
+    d.obs_dim = 0 if pixels else int(cfg.obs_shape[0])
+    d.img_c = int(3 * cfg.frame_stack) if pixels else 0
+    d.img_hw = int(cfg.img_size) if pixels else 0
+    d.num_channels = int(cfg.num_channels) if pixels else 0
+    d.action_dim = int(cfg.action_dim)
+    d.latent_dim = int(cfg.latent_dim)
+    d.mlp_dim = int(cfg.mlp_dim)
+    d.enc_dim = int(cfg.enc_dim)
+    d.num_samples = int(cfg.num_samples)
+    d.num_pi = int(cfg.mixture_coef * cfg.num_samples)
+    d.num_elites = int(cfg.num_elites)
+    d.max_horizon = int(max_horizon or cfg.horizon)
+    d.max_iterations = int(max_iterations or cfg.iterations)
+    d.max_batch = int(max_batch)
+    return d
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()

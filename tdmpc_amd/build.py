@@ -1,0 +1,41 @@
+"""Build libtdmpc_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
+
+    python -m tdmpc_amd.build           # -> tdmpc_amd/libtdmpc_hip.so
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "tdmpc_kernels.hip")
+OUT = os.path.join(HERE, "libtdmpc_hip.so")
+ARCH = os.environ.get("TDMPC_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    deps = [SRC, os.path.join(REPO, "include", "tdmpc_hip.h")]
+    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
+        return OUT
+    tmp = OUT + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-I", os.path.join(REPO, "include"), "-o", tmp, SRC]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

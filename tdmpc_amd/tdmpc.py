@@ -1,0 +1,327 @@
+"""`TDMPC`: drop-in replacement for the reference agent's planning API on MI355X.
+
+Reference: `TDMPC` in /root/reference/src/algorithm/tdmpc.py:53-163. The class keeps the reference's
+constructor argument (a cfg namespace), attributes (`cfg`, `device`, `std`, `model`, `model_target`,
+`_prev_mean`), `plan(obs, eval_mode=False, step=None, t0=True) -> (action tensor [A], metrics dict)`,
+`state_dict / save / load`. Planning runs entirely in the HIP library (libtdmpc_hip.so, include/tdmpc_hip.h):
+Python only draws the random numbers (in the reference's order, from torch's and numpy's global generators)
+and launches one `tdmpc_plan` call. The learner (`update`, `update_pi`) is outside this round's scope.
+
+Extensions beyond the reference API:
+  * `plan_batch(obs[B], ...)` plans B independent environments in one call (one launch sequence, rows of
+    all envs stacked), with per-env state (`_prev_mean` per env).
+  * `rng="fused"` draws all of a call's Gaussian noise with one generator call instead of the reference's
+    18 separate draws (same distribution, different stream); `graph=True` replays the call from a HIP graph.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from copy import deepcopy
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import linear_schedule
+from .told import TOLD
+
+
+def _discount_pows(discount: float, H: int):
+    """float32(discount ** t) for t = 0..H as the reference accumulates it (`discount *= cfg.discount`
+    on a Python float starting from the int 1, tdmpc.py:86-90)."""
+    out, d = [], 1
+    for _ in range(H + 1):
+        out.append(float(np.float32(d)))
+        d *= discount
+    return out
+
+
+class HipPlanner:
+    """Owns the device buffers of one planner instance and calls the C ABI."""
+
+    def __init__(self, cfg, max_batch: int = 1, device=None):
+        self.cfg = cfg
+        self.device = torch.device(device or "cuda")
+        self.L = _lib.lib()
+        self.dims = _lib.dims_from_cfg(cfg, max_batch=max_batch)
+        sz = _lib.Sizes()
+        _lib.check(self.L.tdmpc_sizes_for(C.byref(self.dims), C.byref(sz)), "tdmpc_sizes_for")
+        self.sizes = sz
+        dev = self.device
+        self.packed = torch.empty(sz.packed_weight_bytes // 4, dtype=torch.float32, device=dev)
+        self.workspace = torch.empty(sz.workspace_bytes // 4, dtype=torch.float32, device=dev)
+        d = self.dims
+        self.N, self.P, self.A = d.num_samples, d.num_pi, d.action_dim
+        self.T = self.N + self.P
+        self.max_batch = max_batch
+        # Env streams are packed with the CALL's per-env size (depends on H and I), so the flat buffers are
+        # re-viewed per call (`noise_view`, `prev_mean_view`); sized for the maximum.
+        self.noise_flat = torch.zeros(max_batch * sz.noise_floats_per_env, dtype=torch.float32, device=dev)
+        self.u = torch.zeros(max_batch, dtype=torch.float64, device=dev)
+        self.prev_mean_flat = torch.zeros(max_batch * d.max_horizon * self.A, dtype=torch.float32, device=dev)
+        self.action = torch.zeros(max_batch, self.A, dtype=torch.float32, device=dev)
+        self.metrics = torch.zeros(max_batch, 2, dtype=torch.float32, device=dev)
+        if cfg.modality == "pixels":
+            self.obs_buf = torch.zeros(max_batch, *cfg.obs_shape, dtype=torch.uint8, device=dev)
+        else:
+            self.obs_buf = torch.zeros(max_batch, cfg.obs_shape[0], dtype=torch.float32, device=dev)
+        self._packed_key = None
+        self._graphs = {}
+
+    # ------------------------------------------------------------------ weights
+    def pack(self, model: TOLD):
+        """Pack TOLD parameters when any of them changed (in-place updates bump tensor versions)."""
+        params = list(model.state_dict().values())
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        if key == self._packed_key:
+            return
+        params = [p.detach().to(self.device, torch.float32).contiguous() for p in params]
+        n = self.L.tdmpc_num_param_tensors(C.byref(self.dims))
+        if n != len(params):
+            raise ValueError(f"TOLD has {len(params)} tensors, the packer expects {n}")
+        arr = (C.c_void_p * n)(*[p.data_ptr() for p in params])
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(self.L.tdmpc_pack_weights(C.byref(self.dims), arr, n, C.c_void_p(self.packed.data_ptr()),
+                                              self.packed.numel() * 4, C.c_void_p(stream)), "tdmpc_pack_weights")
+        self._keep = params  # keep source tensors alive until the stream has consumed them
+        self._packed_key = key
+
+    # ------------------------------------------------------------------ noise
+    def noise_view(self, H: int, I: int, B: int):
+        S = self.noise_layout(H, I)["total"]
+        return self.noise_flat[:B * S].view(B, S)
+
+    def prev_mean_view(self, H: int, B: int):
+        return self.prev_mean_flat[:B * H * self.A].view(B, H, self.A)
+
+    def noise_layout(self, H: int, I: int):
+        P, N, A, T = self.P, self.N, self.A, self.T
+        cem_off = H * P * A
+        it = H * N * A + T * A
+        return dict(pi=(0, (H, P, A)), cem_off=cem_off, iter=it, term_off=H * N * A,
+                    act_off=cem_off + I * it, total=cem_off + I * it + A)
+
+    def draw_reference_noise(self, e: int, H: int, I: int, eval_mode: bool):
+        """Fill env e's noise stream from torch's global generator in the reference's draw order
+        (SURVEY.md §8a A10): H x normal_([P,A]); per iteration randn(H,N,A), normal_([T,A]); then
+        numpy's random_sample() (np.random.choice, tdmpc.py:153); then randn(A) unless eval_mode."""
+        lay = self.noise_layout(H, I)
+        buf = self.noise_view(H, I, e + 1)[e]
+        P, N, A, T = self.P, self.N, self.A, self.T
+        if P > 0:
+            for t in range(H):
+                buf[t * P * A:(t + 1) * P * A].view(P, A).normal_()
+        for i in range(I):
+            o = lay["cem_off"] + i * lay["iter"]
+            buf[o:o + H * N * A].view(H, N, A).normal_()
+            buf[o + H * N * A:o + H * N * A + T * A].view(T, A).normal_()
+        u = float(np.random.random_sample())
+        if not eval_mode:
+            buf[lay["act_off"]:lay["act_off"] + A].normal_()
+        return u
+
+    def load_noise(self, e: int, H: int, I: int, eps_pi, eps_cem, eps_term, eps_act):
+        """Write an explicit noise stream for env e (parity tests feed the oracle's / the reference's draws)."""
+        lay = self.noise_layout(H, I)
+        buf = self.noise_view(H, I, e + 1)[e]
+        P, N, A, T = self.P, self.N, self.A, self.T
+        dev = self.device
+        if P > 0:
+            buf[:H * P * A].copy_(torch.as_tensor(eps_pi).reshape(-1).to(dev))
+        for i in range(I):
+            o = lay["cem_off"] + i * lay["iter"]
+            buf[o:o + H * N * A].copy_(torch.as_tensor(eps_cem[i]).reshape(-1).to(dev))
+            buf[o + H * N * A:o + H * N * A + T * A].copy_(torch.as_tensor(eps_term[i]).reshape(-1).to(dev))
+        if eps_act is not None:
+            buf[lay["act_off"]:lay["act_off"] + A].copy_(torch.as_tensor(eps_act).reshape(-1).to(dev))
+
+    # ------------------------------------------------------------------ plan
+    def params(self, H, I, B, warm, eval_mode, std_floor):
+        cfg = self.cfg
+        p = _lib.PlanParams()
+        p.horizon, p.iterations, p.batch = H, I, B
+        p.warm_start, p.eval_mode = int(warm), int(eval_mode)
+        p.min_std = float(cfg.min_std)
+        p.temperature = float(cfg.temperature)
+        p.momentum = float(cfg.momentum)
+        p.one_minus_momentum = float(1 - cfg.momentum)
+        p.std_floor = float(std_floor)
+        for t, v in enumerate(_discount_pows(cfg.discount, H)):
+            p.discount_pow[t] = v
+        return p
+
+    def launch(self, prm, obs_is_u8: bool, trace: dict | None = None):
+        L = self.L
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        B, H, I, K = prm.batch, prm.horizon, prm.iterations, self.dims.num_elites
+        outs = {}
+        if trace is not None:
+            outs = dict(elite=torch.zeros(B, H, K, self.A, device=self.device),
+                        score=torch.zeros(B, K, device=self.device),
+                        value=torch.zeros(B, I, self.T, device=self.device),
+                        mean=torch.zeros(B, I, H, self.A, device=self.device),
+                        std=torch.zeros(B, I, H, self.A, device=self.device))
+            trace.update(outs)
+        g = outs.get
+        rc = L.tdmpc_plan(C.byref(self.dims), C.byref(prm), C.c_void_p(self.packed.data_ptr()),
+                          C.c_void_p(self.obs_buf.data_ptr()), int(obs_is_u8), C.c_void_p(self.noise_flat.data_ptr()),
+                          C.c_void_p(self.u.data_ptr()), C.c_void_p(self.prev_mean_flat.data_ptr()),
+                          C.c_void_p(self.action.data_ptr()), C.c_void_p(self.metrics.data_ptr()),
+                          C.c_void_p(_lib.ptr(g("elite"))), C.c_void_p(_lib.ptr(g("score"))),
+                          C.c_void_p(_lib.ptr(g("value"))), C.c_void_p(_lib.ptr(g("mean"))),
+                          C.c_void_p(_lib.ptr(g("std"))), C.c_void_p(self.workspace.data_ptr()),
+                          self.workspace.numel() * 4, C.c_void_p(stream))
+        _lib.check(rc, "tdmpc_plan")
+
+
+    def estimate_value(self, z0, actions, eps_term, H: int, std_floor: float = 0.05):
+        """TDMPC.estimate_value (tdmpc.py:83-92) through the C ABI for B envs: z0 [B, L], actions
+        [B, H, T, A], eps_term [B, T, A] -> (value [B, T], reward at t=H-1 [B, T], z_H [B, T, L])."""
+        B = z0.shape[0]
+        prm = self.params(H, 1, B, False, True, std_floor)
+        dev = self.device
+        z0 = z0.to(dev, torch.float32).contiguous()
+        actions = actions.to(dev, torch.float32).contiguous()
+        eps_term = eps_term.to(dev, torch.float32).contiguous()
+        value = torch.empty(B, self.T, device=dev)
+        rlast = torch.empty(B, self.T, device=dev)
+        zl = torch.empty(B, self.T, self.dims.latent_dim, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = self.L.tdmpc_estimate_value(C.byref(self.dims), C.byref(prm), C.c_void_p(self.packed.data_ptr()),
+                                         C.c_void_p(z0.data_ptr()), C.c_void_p(actions.data_ptr()),
+                                         C.c_void_p(eps_term.data_ptr()), self.T, C.c_void_p(value.data_ptr()),
+                                         C.c_void_p(rlast.data_ptr()), C.c_void_p(zl.data_ptr()),
+                                         C.c_void_p(self.workspace.data_ptr()), self.workspace.numel() * 4,
+                                         C.c_void_p(stream))
+        _lib.check(rc, "tdmpc_estimate_value")
+        return value, rlast, zl
+
+    def encode(self, obs):
+        """TOLD.h for a batch of observations through the C ABI -> z0 [B, L]."""
+        B = obs.shape[0]
+        dev = self.device
+        is_u8 = obs.dtype == torch.uint8
+        obs = obs.to(dev).contiguous()
+        z0 = torch.empty(B, self.dims.latent_dim, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = self.L.tdmpc_encode(C.byref(self.dims), C.c_void_p(self.packed.data_ptr()), C.c_void_p(obs.data_ptr()),
+                                 int(is_u8), B, C.c_void_p(self.workspace.data_ptr()), C.c_void_p(z0.data_ptr()),
+                                 C.c_void_p(stream))
+        _lib.check(rc, "tdmpc_encode")
+        return z0
+
+
+class TDMPC:
+    """Drop-in for the reference `TDMPC` planning interface (tdmpc.py:53-163)."""
+
+    def __init__(self, cfg, max_batch: int = 1, rng: str = "reference", graph: bool = False):
+        self.cfg = cfg
+        self.device = torch.device(cfg.device)
+        self.std = linear_schedule(cfg.std_schedule, 0)      # tdmpc.py:59
+        self.model = TOLD(cfg).to(self.device)               # tdmpc.py:60
+        self.model_target = deepcopy(self.model)             # tdmpc.py:61
+        self.model.eval()
+        self.model_target.eval()
+        if rng not in ("reference", "fused"):
+            raise ValueError(rng)
+        self.rng = rng
+        self.graph = graph
+        self.planner = HipPlanner(cfg, max_batch=max_batch, device=self.device)
+        self._has_prev = np.zeros(max_batch, dtype=bool)
+        self._prev_H = np.zeros(max_batch, dtype=np.int64)
+
+    # ------------------------------------------------------------------ reference API
+    def state_dict(self):
+        return {"model": self.model.state_dict(), "model_target": self.model_target.state_dict()}
+
+    def save(self, fp):
+        torch.save(self.state_dict(), fp)
+
+    def load(self, fp):
+        d = torch.load(fp, map_location=self.device, weights_only=True)
+        self.model.load_state_dict(d["model"])
+        self.model_target.load_state_dict(d["model_target"])
+
+    @property
+    def _prev_mean(self):
+        if not self._has_prev[0]:
+            raise AttributeError("_prev_mean")
+        return self.planner.prev_mean_view(int(self._prev_H[0]), 1)[0]
+
+    @torch.no_grad()
+    def plan(self, obs, eval_mode=False, step=None, t0=True):
+        """tdmpc.py:94-163. Returns (action tensor [A] on self.device, {'external_reward_mean', 'current_std'})."""
+        cfg = self.cfg
+        plan_metrics = {"external_reward_mean": 0.0, "current_std": 0.0}
+        if step < cfg.seed_steps and not eval_mode:
+            return (torch.empty(cfg.action_dim, dtype=torch.float32, device=self.device).uniform_(-1, 1),
+                    plan_metrics)
+        a, m = self._plan_envs(np.asarray(obs)[None], eval_mode, step, [t0])
+        plan_metrics.update(m[0])
+        return a[0].clone(), plan_metrics
+
+    @torch.no_grad()
+    def plan_batch(self, obs, eval_mode=False, step=None, t0=True, sync_metrics=True):
+        """Plan B independent environments at once (obs: [B, *obs_shape]); `t0` may be a bool or a per-env
+        sequence. Equivalent to B sequential reference `plan` calls on B agents sharing weights, with the
+        random draws taken env by env in reference order."""
+        cfg = self.cfg
+        obs = obs if torch.is_tensor(obs) else np.asarray(obs)
+        B = obs.shape[0]
+        if step < cfg.seed_steps and not eval_mode:
+            a = torch.empty(B, cfg.action_dim, dtype=torch.float32, device=self.device)
+            for e in range(B):
+                a[e].uniform_(-1, 1)
+            return a, [{"external_reward_mean": 0.0, "current_std": 0.0} for _ in range(B)]
+        t0s = [t0] * B if isinstance(t0, (bool, int, np.bool_)) else list(t0)
+        return self._plan_envs(obs, eval_mode, step, t0s, sync_metrics)
+
+    # ------------------------------------------------------------------ internals
+    def horizon(self, step):
+        return int(min(self.cfg.horizon, linear_schedule(self.cfg.horizon_schedule, step)))
+
+    def _plan_envs(self, obs, eval_mode, step, t0s, sync_metrics=True, trace=None, noise=None):
+        """noise: optional list (one per env) of objects with eps_pi / eps_cem / eps_term / u / eps_act
+        (e.g. oracle NoiseBundles) used instead of drawing."""
+        cfg, pl = self.cfg, self.planner
+        B = obs.shape[0]
+        if B > pl.max_batch:
+            raise ValueError(f"batch {B} > max_batch {pl.max_batch}")
+        H = self.horizon(step)
+        I = int(cfg.iterations)
+        warm = []
+        for e in range(B):
+            w = (not t0s[e]) and bool(self._has_prev[e])
+            if w and self._prev_H[e] != H:
+                # the reference's `mean[:-1] = self._prev_mean[1:]` raises on a horizon change
+                raise RuntimeError(f"shape mismatch: prev_mean horizon {self._prev_H[e]} vs {H}")
+            warm.append(w)
+        if len(set(warm)) > 1:
+            raise NotImplementedError("mixed warm/cold starts in one batch")
+        pl.pack(self.model)
+        if cfg.modality == "pixels":
+            src = torch.as_tensor(obs).to(self.device, torch.uint8)
+            pl.obs_buf[:B].copy_(src.view(B, *cfg.obs_shape))
+        else:
+            src = torch.as_tensor(obs, dtype=torch.float32).to(self.device)
+            pl.obs_buf[:B].copy_(src.view(B, -1))
+        if noise is not None:
+            us = []
+            for e, nb in enumerate(noise):
+                pl.load_noise(e, H, I, nb.eps_pi, nb.eps_cem, nb.eps_term, nb.eps_act)
+                us.append(float(nb.u))
+        elif self.rng == "reference":
+            us = [pl.draw_reference_noise(e, H, I, eval_mode) for e in range(B)]
+        else:
+            pl.noise_view(H, I, B).normal_()
+            us = list(np.random.random_sample(B))
+        pl.u[:B].copy_(torch.tensor(us, dtype=torch.float64))
+        prm = pl.params(H, I, B, warm[0], eval_mode, self.std)
+        pl.launch(prm, cfg.modality == "pixels", trace)
+        self._has_prev[:B] = True
+        self._prev_H[:B] = H
+        actions = pl.action[:B]
+        if not sync_metrics:
+            return actions, pl.metrics[:B]
+        m = pl.metrics[:B].double().cpu().numpy()
+        return actions, [{"external_reward_mean": float(r), "current_std": float(s)} for r, s in m]

@@ -1,0 +1,65 @@
+"""CPU-side checks of the C ABI library and host logic (no GPU needed)."""
+import ctypes as C
+import re
+
+import numpy as np
+import pytest
+
+from tdmpc_amd import _lib
+from tdmpc_amd.config import bench_cfg, linear_schedule, make_cfg
+from oracle import tdmpc_ref
+
+HEADER = "include/tdmpc_hip.h"
+
+
+def _declared():
+    import os
+    src = open(os.path.join(os.path.dirname(os.path.dirname(__file__)), HEADER)).read()
+    return sorted(set(re.findall(r"^(?:int|size_t|const char\*)\s+(tdmpc_\w+)\(", src, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    names = _declared()
+    assert "tdmpc_plan" in names and len(names) >= 8
+    for n in names:
+        assert hasattr(L, n), n
+    assert L.tdmpc_abi_version() == 1
+
+
+@pytest.mark.parametrize("name", ["cartpole-swingup", "cheetah-run", "humanoid-run", "humanoid-run-l512",
+                                  "dog-run", "quadruped-run-pixels"])
+def test_sizes_for_bench_configs(name):
+    cfg = bench_cfg(name)
+    d = _lib.dims_from_cfg(cfg, max_batch=8)
+    s = _lib.Sizes()
+    assert _lib.lib().tdmpc_sizes_for(C.byref(d), C.byref(s)) == 0
+    assert s.packed_weight_bytes > 4 * 1_000_000
+    N, P, A = d.num_samples, d.num_pi, d.action_dim
+    H, I = d.max_horizon, d.max_iterations
+    assert s.noise_floats_per_env == H * P * A + I * (H * N * A + (N + P) * A) + A
+    assert _lib.lib().tdmpc_num_param_tensors(C.byref(d)) == (10 if cfg.modality == "pixels" else 4) + 38
+
+
+def test_bad_dims_rejected():
+    cfg = make_cfg("humanoid")
+    d = _lib.dims_from_cfg(cfg)
+    d.mlp_dim = 500  # not a multiple of 64
+    s = _lib.Sizes()
+    assert _lib.lib().tdmpc_sizes_for(C.byref(d), C.byref(s)) == -1
+    assert _lib.lib().tdmpc_sizes_for(None, C.byref(s)) == -3
+
+
+@pytest.mark.parametrize("sched", ["linear(2, 5, 25000, 0)", "linear(0.5, 0.05, 25000, 0)", "0.3", 1.5])
+def test_linear_schedule(sched):
+    for step in [0, 1, 100, 12500, 24999, 25000, 10**6]:
+        assert linear_schedule(sched, step) == tdmpc_ref.linear_schedule(sched, step)
+
+
+def test_discount_pows_match_python_accumulation():
+    from tdmpc_amd.tdmpc import _discount_pows
+    d, ref = 1, []
+    for _ in range(6):
+        ref.append(float(np.float32(d)))
+        d *= 0.99
+    assert _discount_pows(0.99, 5) == ref
