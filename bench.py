@@ -1,0 +1,248 @@
+"""bench.py -- plan-steps/sec of TDMPC.plan on MI355X (BASELINE.json metric), one process per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config humanoid-run] [--envs-per-gpu B]
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+A "step" is one planning call: one full TDMPC.plan (N=512 candidates, H=5, 6 CEM iterations, the
+pi pre-rollout, final elite choice) for each of the B environments a GPU owns. Inputs (observations, weights)
+are synthetic and resident on the device; noise is drawn on the device inside the timed region.
+
+Multi-GPU: environments are independent units; each rank plans its own B envs with its own
+weight replica. With --envs-per-gpu > 1 (the vectorised-env config) every step ends with one RCCL
+all-gather of the per-env results ([B, A+2]: action + reward-mean + std) so every rank holds the whole
+vectorised env batch; with one env per GPU the ranks are independent replicas (no collective).
+
+Rank 0 prints ONE JSON line (the driver's contract), including
+  roofline     : the dominant kernel (linear_kernel<1,0,64>: every hidden 512x512 Linear) -- algorithmic
+                 FLOPs per launch / its average launch time, HIP events on its stream over the timed region;
+  cpu_baseline : the oracle's CPU restatement of the reference plan() (bit-exact to the reference, see
+                 tests/test_oracle.py) timed on this host's cores over a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from tdmpc_amd import _lib  # noqa: E402
+from tdmpc_amd.config import bench_cfg  # noqa: E402
+from tdmpc_amd.tdmpc import TDMPC  # noqa: E402
+from tdmpc_amd.told import synthetic_state_dict  # noqa: E402
+
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector peak (spec)
+DOMINANT = (1, 0, 64)      # linear_kernel<WN=1, PRO_PLAIN, KCH=64>: the M x M hidden layers
+
+
+def plan_flops(cfg, executed: bool) -> float:
+    """Algorithmic FLOPs of one plan-step: 2*[P*H*(pi+d+R) + I*T*(H*(d+R) + pi + 2Q) + enc].
+    executed=True counts what this build runs: the pi rows' H-step rollout is computed once per plan
+    (identical in every CEM iteration) so per iteration only N rows are rolled out."""
+    L, A, M, E = cfg.latent_dim, cfg.action_dim, cfg.mlp_dim, cfg.enc_dim
+    N = cfg.num_samples
+    P = int(cfg.mixture_coef * N)
+    T, H, I = N + P, cfg.horizon, cfg.iterations
+    d = (L + A) * M + M * M + M * L
+    R = (L + A) * M + M * M + M
+    pi = L * M + M * M + M * A
+    Q = (L + A) * M + M * M + M
+    if cfg.modality == "pixels":
+        enc = 0  # conv encoder counted separately below
+        s, c, ch = cfg.img_size, 3 * cfg.frame_stack, cfg.num_channels
+        for k in (7, 5, 3, 3):
+            so = (s - k) // 2 + 1
+            enc += ch * so * so * c * k * k
+            s, c = so, ch
+        enc += ch * s * s * L
+    else:
+        enc = cfg.obs_shape[0] * E + E * L
+    if executed:
+        macs = P * H * (pi + d + R) + I * (N * H * (d + R) + T * (pi + 2 * Q)) + enc
+    else:
+        macs = P * H * (pi + d + R) + I * T * (H * (d + R) + pi + 2 * Q) + enc
+    return 2.0 * macs
+
+
+def synthetic_obs(cfg, B, seed=0):
+    rs = np.random.RandomState(seed)
+    if cfg.modality == "pixels":
+        return rs.randint(0, 256, size=(B,) + tuple(cfg.obs_shape)).astype(np.uint8)
+    return rs.standard_normal((B,) + tuple(cfg.obs_shape)).astype(np.float32)
+
+
+def cpu_baseline(cfg, budget_s: float):
+    """Time the oracle (CPU restatement of the reference plan(), pinned bit-exact to the reference's golden
+    vectors) on this host: 2 warm-up calls, then calls until `budget_s` of CPU work (>= 5 calls)."""
+    from oracle import tdmpc_ref
+    threads = int(os.environ.get("TDMPC_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    torch.set_num_threads(threads)
+    told = tdmpc_ref.RefTOLD(synthetic_state_dict(cfg, 0), cfg)
+    st = tdmpc_ref.PlanState(0.05)
+    obs = synthetic_obs(cfg, 1)[0]
+    step = 10**6
+    times = []
+    for i in range(2 + 200):
+        nb = tdmpc_ref.draw_noise(cfg, step, False)
+        t = time.perf_counter()
+        tdmpc_ref.plan(told, cfg, st, obs, nb, eval_mode=False, step=step, t0=(i == 0))
+        dt = time.perf_counter() - t
+        if i >= 2:
+            times.append(dt)
+        if i >= 6 and sum(times) > budget_s:
+            break
+    med = float(np.median(times))
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(1.0 / med, 3), "unit": "plan-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{len(times)} plan() calls of {cfg.task} N={cfg.num_samples} H={cfg.horizon} "
+                      f"I={cfg.iterations} after 2 warm-up (median), torch CPU fp32, {cpu_model}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="humanoid-run")
+    ap.add_argument("--envs-per-gpu", type=int, default=1)
+    ap.add_argument("--rng", default="fused", choices=["fused", "reference"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = bench_cfg(args.config)
+    cfg.device = f"cuda:{local}"
+    B = args.envs_per_gpu
+    torch.manual_seed(1 + rank)
+    np.random.seed(2 + rank)
+    agent = TDMPC(cfg, max_batch=B, rng=args.rng, graph=not args.no_graph)
+    agent.model.load_state_dict(synthetic_state_dict(cfg, 0))
+    agent.std = 0.05
+    obs_np = synthetic_obs(cfg, B, seed=rank)
+    obs = torch.from_numpy(obs_np).to(dev)
+    step = 10**6
+    gather_buf = None
+    if dist is not None and B > 1:
+        gather_buf = torch.empty(world, B, cfg.action_dim + 2, device=dev)
+
+    def one_step(i):
+        a, m = agent.plan_batch(obs, step=step, t0=(i % 100 == 0), sync_metrics=False)
+        if gather_buf is not None:
+            local_res = torch.cat([a, m], dim=1)
+            dist.all_gather_into_tensor(gather_buf, local_res)
+        return a
+
+    for i in range(args.warmup):
+        one_step(i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one_step(args.warmup + i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * B * args.steps / elapsed
+
+    # ---- roofline of the dominant kernel: HIP events around every launch of it, eager replay of the same
+    # steps (graph replay cannot carry events), same stream the kernel runs on.
+    roof = None
+    if not args.no_roofline:
+        L = _lib.lib()
+        steps_r = max(3, min(args.steps, 10))
+        graph_state = agent.graph
+        agent.graph = False
+        one_step(0)
+        torch.cuda.synchronize()
+        _lib.check(L.tdmpc_profile_begin(*DOMINANT, cfg.mlp_dim, 4096), "profile_begin")
+        for i in range(steps_r):
+            one_step(1 + i)
+        n, ms, fl = C.c_int32(), C.c_double(), C.c_double()
+        _lib.check(L.tdmpc_profile_end(C.byref(n), C.byref(ms), C.byref(fl)), "profile_end")
+        agent.graph = graph_state
+        avg_s = ms.value / max(n.value, 1) * 1e-3
+        per_launch = fl.value / max(n.value, 1)
+        achieved = per_launch / avg_s / 1e12
+        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                "kernel": "linear_kernel<1,0,64> (hidden MxM Linear, fp32 MFMA 32x32x2)",
+                "launches": n.value, "avg_launch_us": round(avg_s * 1e6, 3),
+                "flops_per_launch": per_launch}
+        pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                roof["traffic"] = json.load(open(pmc)).get(args.config)
+            except (OSError, ValueError):
+                pass
+
+    fl_alg = plan_flops(cfg, executed=False)
+    fl_exec = plan_flops(cfg, executed=True)
+    plan_roof = {"flop_per_plan_step_algorithmic": fl_alg, "flop_per_plan_step_executed": fl_exec,
+                 "tflops_per_gpu_algorithmic": round(value / world * fl_alg / 1e12, 3),
+                 "frac_of_fp32_peak": round(value / world * min(fl_alg, fl_exec) / 1e12 / FP32_PEAK_TFLOPS, 4)}
+
+    cpu = None
+    if rank == 0 and not args.no_cpu and world == 1:
+        cpu = cpu_baseline(cfg, args.cpu_budget)
+
+    if rank == 0:
+        out = {
+            "metric": "plan-steps/sec (N=512, H=5, iters=6) at 1/2/4/8 MI355X vs CPU ref",
+            "value": round(value, 3), "unit": "plan-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (seeded N(0,1/fan_in) TOLD weights, N(0,1) obs; noise drawn on device)",
+            "config": {"workload": f"{args.config}: TDMPC.plan N={cfg.num_samples} H={cfg.horizon} "
+                                   f"iters={cfg.iterations} L={cfg.latent_dim} A={cfg.action_dim}",
+                       "envs_per_gpu": B, "global_envs": B * world,
+                       "parallelism": f"env-shard x{world}" + (" + rccl all-gather" if gather_buf is not None
+                                                               else " (independent replicas)"),
+                       "rng": args.rng, "hip_graph": not args.no_graph},
+            "roofline": roof,
+            "plan_roofline": plan_roof,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            out["speedup_vs_cpu"] = round(value / world / cpu["value"], 2)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

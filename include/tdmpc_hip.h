@@ -137,6 +137,15 @@ int tdmpc_estimate_value(const tdmpc_dims* dims, const tdmpc_plan_params* params
                          float* value, float* reward_last, float* z_last,
                          void* workspace, size_t workspace_bytes, void* stream);
 
+/* Diagnostic kernel timer for the roofline report (bench.py). Arms a per-thread recorder: every later
+ * linear_kernel launch of instance (wn, pro, kch) issued from this thread -- restricted to K == N == kdim
+ * when kdim > 0 (the hidden kdim x kdim layers) -- is bracketed by HIP events on its stream (at most
+ * max_launches). tdmpc_profile_end waits for the events and returns the launch count,
+ * the summed kernel time in ms and the summed algorithmic FLOPs (2*M*N*K per GEMM problem). Eager use
+ * only (the events are not graph-capturable). */
+int tdmpc_profile_begin(int32_t wn, int32_t pro, int32_t kch, int32_t kdim, int32_t max_launches);
+int tdmpc_profile_end(int32_t* launches, double* total_ms, double* flops);
+
 /* Last HIP error string seen by this thread (for diagnostics). */
 const char* tdmpc_last_error(void);
 

@@ -12,7 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libtdmpc_hip.so")
 
 EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc_num_param_tensors",
-            "tdmpc_pack_weights", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_last_error")
+            "tdmpc_pack_weights", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_last_error",
+            "tdmpc_profile_begin", "tdmpc_profile_end")
 
 
 class Dims(C.Structure):
@@ -60,6 +61,8 @@ def lib():
     L.tdmpc_estimate_value.argtypes = [C.POINTER(Dims), C.POINTER(PlanParams), vp, vp, vp, vp, i32, vp, vp,
                                        vp, vp, sz, vp]
     L.tdmpc_last_error.restype = C.c_char_p
+    L.tdmpc_profile_begin.argtypes = [i32, i32, i32, i32, i32]
+    L.tdmpc_profile_end.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_double), C.POINTER(C.c_double)]
     for name in EXPORTED:
         if not hasattr(L, name):
             raise RuntimeError(f"{LIB_PATH} does not export {name}")

@@ -19,6 +19,8 @@
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <vector>
@@ -299,7 +301,10 @@ __global__ void __launch_bounds__(512) linear_kernel(const LinArgs args) {
 
     // ---- epilogue: TPR threads per row, each owns 4-column chunks
     const int nw = nthr >> 6;
-    const int tpr = nthr / 32;
+    // threads per row: a power of two (<= 16) so a row's threads are consecutive lanes of one wave and
+    // the xor-shuffle row reductions are exact; surplus threads sit out the epilogue.
+    const int tpr = nthr >= 512 ? 16 : nthr >= 256 ? 8 : nthr >= 128 ? 4 : 2;
+    if (threadIdx.x >= 32 * tpr) return;
     const int row = threadIdx.x / tpr, q = threadIdx.x % tpr;
     const int lm = m0 + row;
     const bool rval = lm < args.M;
@@ -726,6 +731,16 @@ int init_attrs() {
     return 0;
 }
 
+// Diagnostic kernel timer (tdmpc_profile_*): when armed on this thread, every linear_kernel launch whose
+// (WN, PRO, KCH) instance matches is bracketed by HIP events on its stream, and its algorithmic FLOPs
+// (2*M*N*K per problem) are recorded. Used by bench.py for the live roofline of the dominant kernel.
+struct Profiler {
+    int armed = 0, wn = 0, pro = 0, kch = 0, n = 0, cap = 0, kdim = 0;
+    hipEvent_t* ev = nullptr;
+    double flops = 0.0;
+};
+thread_local Profiler g_prof;
+
 template <int WN, int PRO, int KCH>
 int launch_lin_t(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
     const int nw = (a.K + KCH - 1) / KCH;
@@ -734,8 +749,17 @@ int launch_lin_t(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
     dim3 grid((a.M + 31) / 32, (nmax + 32 * WN - 1) / (32 * WN), nprob);
     dim3 block(64 * nw);
     const size_t lds = (size_t)nw * 32 * (32 * WN + 4) * 4;
+    Profiler& pf = g_prof;
+    const bool prof = pf.armed && pf.wn == WN && pf.pro == PRO && pf.kch == KCH && pf.n + 2 <= pf.cap &&
+                      (pf.kdim == 0 || (a.K == pf.kdim && nmax == pf.kdim));
+    if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], s));
     hipLaunchKernelGGL((linear_kernel<WN, PRO, KCH>), grid, block, lds, s, b);
     HIPCHK(hipGetLastError());
+    if (prof) {
+        HIPCHK(hipEventRecord(pf.ev[pf.n + 1], s));
+        pf.n += 2;
+        for (int q = 0; q < nprob; ++q) pf.flops += 2.0 * a.M * std::min(a.p[q].N, nmax) * a.K;
+    }
     return 0;
 }
 
@@ -1145,6 +1169,36 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     if ((rc = terminal_q(c, prm->discount_pow[H], nullptr, 1, 0))) return rc;
     HIPCHK(hipMemcpyAsync(value, c.k.value, (size_t)B * T * 4, hipMemcpyDeviceToDevice, c.s));
     HIPCHK(hipMemcpyAsync(reward_last, c.k.rlast, (size_t)B * T * 4, hipMemcpyDeviceToDevice, c.s));
+    return 0;
+}
+
+int tdmpc_profile_begin(int32_t wn, int32_t pro, int32_t kch, int32_t kdim, int32_t max_launches) {
+    Profiler& pf = g_prof;
+    if (pf.ev) {
+        for (int i = 0; i < pf.cap; ++i) (void)hipEventDestroy(pf.ev[i]);
+        free(pf.ev);
+    }
+    pf = Profiler();
+    pf.cap = 2 * std::max(1, (int)max_launches);
+    pf.ev = (hipEvent_t*)calloc(pf.cap, sizeof(hipEvent_t));
+    for (int i = 0; i < pf.cap; ++i) HIPCHK(hipEventCreate(&pf.ev[i]));
+    pf.wn = wn; pf.pro = pro; pf.kch = kch; pf.kdim = kdim; pf.armed = 1;
+    return 0;
+}
+
+int tdmpc_profile_end(int32_t* launches, double* total_ms, double* flops) {
+    Profiler& pf = g_prof;
+    pf.armed = 0;
+    double tot = 0.0;
+    for (int i = 0; i + 1 < pf.n; i += 2) {
+        HIPCHK(hipEventSynchronize(pf.ev[i + 1]));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, pf.ev[i], pf.ev[i + 1]));
+        tot += ms;
+    }
+    if (launches) *launches = pf.n / 2;
+    if (total_ms) *total_ms = tot;
+    if (flops) *flops = pf.flops;
     return 0;
 }
 

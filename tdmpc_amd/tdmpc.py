@@ -104,7 +104,12 @@ class HipPlanner:
     def draw_reference_noise(self, e: int, H: int, I: int, eval_mode: bool):
         """Fill env e's noise stream from torch's global generator in the reference's draw order
         (SURVEY.md §8a A10): H x normal_([P,A]); per iteration randn(H,N,A), normal_([T,A]); then
-        numpy's random_sample() (np.random.choice, tdmpc.py:153); then randn(A) unless eval_mode."""
+        numpy's random_sample() (np.random.choice, tdmpc.py:153); then randn(A) unless eval_mode.
+        torch and numpy generators are independent, so the numpy draw is returned separately."""
+        self.draw_reference_torch(e, H, I, eval_mode)
+        return float(np.random.random_sample())
+
+    def draw_reference_torch(self, e: int, H: int, I: int, eval_mode: bool):
         lay = self.noise_layout(H, I)
         buf = self.noise_view(H, I, e + 1)[e]
         P, N, A, T = self.P, self.N, self.A, self.T
@@ -115,10 +120,8 @@ class HipPlanner:
             o = lay["cem_off"] + i * lay["iter"]
             buf[o:o + H * N * A].view(H, N, A).normal_()
             buf[o + H * N * A:o + H * N * A + T * A].view(T, A).normal_()
-        u = float(np.random.random_sample())
         if not eval_mode:
             buf[lay["act_off"]:lay["act_off"] + A].normal_()
-        return u
 
     def load_noise(self, e: int, H: int, I: int, eps_pi, eps_cem, eps_term, eps_act):
         """Write an explicit noise stream for env e (parity tests feed the oracle's / the reference's draws)."""
@@ -305,19 +308,40 @@ class TDMPC:
         else:
             src = torch.as_tensor(obs, dtype=torch.float32).to(self.device)
             pl.obs_buf[:B].copy_(src.view(B, -1))
+        obs_u8 = cfg.modality == "pixels"
+        prm = pl.params(H, I, B, warm[0], eval_mode, self.std)
         if noise is not None:
             us = []
             for e, nb in enumerate(noise):
                 pl.load_noise(e, H, I, nb.eps_pi, nb.eps_cem, nb.eps_term, nb.eps_act)
                 us.append(float(nb.u))
-        elif self.rng == "reference":
-            us = [pl.draw_reference_noise(e, H, I, eval_mode) for e in range(B)]
         else:
-            pl.noise_view(H, I, B).normal_()
-            us = list(np.random.random_sample(B))
+            us = list(np.random.random_sample(B)) if self.rng == "fused" else \
+                [float(np.random.random_sample()) for _ in range(B)]
         pl.u[:B].copy_(torch.tensor(us, dtype=torch.float64))
-        prm = pl.params(H, I, B, warm[0], eval_mode, self.std)
-        pl.launch(prm, cfg.modality == "pixels", trace)
+
+        def device_work():
+            if noise is None:
+                if self.rng == "reference":
+                    for e in range(B):
+                        pl.draw_reference_torch(e, H, I, eval_mode)
+                else:
+                    pl.noise_view(H, I, B).normal_()
+            pl.launch(prm, obs_u8, trace)
+
+        if self.graph and noise is None and trace is None:
+            key = (H, I, B, bool(warm[0]), bool(eval_mode), float(self.std), self.rng)
+            g = pl._graphs.get(key)
+            if g is None:
+                # No eager warm-up: the library has no lazy initialisation left after pack(), and an eager
+                # run would advance the planner state (prev_mean) before the captured replay.
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    device_work()
+                pl._graphs[key] = g
+            g.replay()
+        else:
+            device_work()
         self._has_prev[:B] = True
         self._prev_H[:B] = H
         actions = pl.action[:B]
