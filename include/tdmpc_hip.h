@@ -138,12 +138,13 @@ int tdmpc_estimate_value(const tdmpc_dims* dims, const tdmpc_plan_params* params
                          void* workspace, size_t workspace_bytes, void* stream);
 
 /* Diagnostic kernel timer for the roofline report (bench.py). Arms a per-thread recorder: every later
- * linear_kernel launch of instance (wn, pro, kch) issued from this thread -- restricted to K == N == kdim
- * when kdim > 0 (the hidden kdim x kdim layers) -- is bracketed by HIP events on its stream (at most
- * max_launches). tdmpc_profile_end waits for the events and returns the launch count,
+ * linear_kernel launch issued from this thread with launch configuration `cfg` (1 = latency 32x32 tile,
+ * 2 = latency 32x64 tile, 3 = throughput 128x128 tile, 0 = any) and prologue `pro` (0 plain, 1 LayerNorm,
+ * -1 any) -- restricted to K == N == kdim when kdim > 0 (the hidden kdim x kdim layers) -- is bracketed by
+ * HIP events on its stream (at most max_launches). tdmpc_profile_end waits for the events and returns the launch count,
  * the summed kernel time in ms and the summed algorithmic FLOPs (2*M*N*K per GEMM problem). Eager use
  * only (the events are not graph-capturable). */
-int tdmpc_profile_begin(int32_t wn, int32_t pro, int32_t kch, int32_t kdim, int32_t max_launches);
+int tdmpc_profile_begin(int32_t cfg, int32_t pro, int32_t kdim, int32_t max_launches);
 int tdmpc_profile_end(int32_t* launches, double* total_ms, double* flops);
 
 /* Last HIP error string seen by this thread (for diagnostics). */

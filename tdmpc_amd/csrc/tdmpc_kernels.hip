@@ -4,32 +4,54 @@
 // heads tdmpc.py:30-50 built from helper.py:119-133 (enc), 169-176 (mlp), 197-201 (q), 71-96
 // (TruncatedNormal). See DESIGN.md for the decomposition, data layout and rooflines.
 //
+// Data layout. Every matrix an MFMA reads (weights and activations) is stored in the "panel" layout
+//   [rows/32][cols/4][32][4]   element (r, c) at (r>>5)*(cols*32) + (c>>2)*128 + (r&31)*4 + (c&3)
+// so that the A or B operand of v_mfma_f32_32x32x2_f32 for one 8-deep k group is ONE contiguous 1 KiB
+// wave load (lanes 0-31 read k-quad q of 32 rows, lanes 32-63 quad q+1). The k order inside an 8-group is
+// permuted identically for A and B, which leaves the dot product unchanged.
+//
 // Kernel families
-//   linear_kernel<WN,PRO,KCH>  fused Linear layer on f32 MFMA (v_mfma_f32_32x32x2_f32): one workgroup owns
-//                              a 32-row x (32*WN)-column output tile, its waves split K, the partial tiles
-//                              are reduced through LDS and a fused epilogue applies bias + ELU / tanh +
-//                              TruncatedNormal sampling / LayerNorm partial moments / reward-head dot /
-//                              discounted-return accumulation. Prologue may apply LayerNorm + act to A.
-//   value_kernel               Q heads' LayerNorm+ELU+Linear(512->1), min(Q1,Q2), G + gamma^H Q, nan_to_num.
-//   cem_kernel                 one workgroup per env: top-k, softmax, weighted mean/std refit, momentum,
-//                              next-iteration sampling, final elite choice (np.random.choice cdf).
-//   encode_state_kernel / conv kernels   TOLD.h for state / pixel observations, z0 broadcast.
+//   linear_kernel<WN,PRO,KCH>  one fused nn.Linear on f32 MFMA: a workgroup owns a 32-row x (32*WN)-col
+//       output tile, its waves split K (KCH each) and reduce through LDS; fused epilogues: bias + ELU /
+//       TruncatedNormal policy sample / LayerNorm partial moments / reward-head dot / discounted return.
+//       Fused prologues: LayerNorm+tanh of A; CEM action sampling clamp(mean+std*eps) for the action
+//       columns; broadcast of the encoder output z0 for the latent columns at t = 0.
+//   value_kernel   Q heads' LayerNorm+ELU+Linear(M->1), min(Q1,Q2), G + gamma^H Q, nan_to_num.
+//   cem_kernel     one workgroup per env: bitonic top-k, softmax, weighted mean/std refit, momentum, and
+//                  on the last iteration the elite choice (np.random.choice cdf) and the output action.
+//   encode_kernel / conv_relu_kernel   TOLD.h (state MLP or pixel conv stack) + CEM mean/std init.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
 #include <stdint.h>
-#include <string.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
-#include <vector>
 
 #include "../../include/tdmpc_hip.h"
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 #define DEVI __device__ __forceinline__
+
+// Diagnostic build only (tools/mb, -DTDMPC_STAMPS): per-workgroup phase timestamps of linear_kernel.
+#ifdef TDMPC_STAMPS
+__device__ unsigned long long* g_stamps;   // null unless the diagnostic host sets it
+__device__ unsigned int g_stamp_n;
+__device__ unsigned int g_stamp_cap;
+#define STAMP(slot)                                                                                   \
+    do {                                                                                              \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        unsigned long long t_;                                                                        \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                     \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        st_[slot] = t_;                                                                               \
+    } while (0)
+#else
+#define STAMP(slot) do {} while (0)
+#endif
 
 namespace {
 
@@ -38,19 +60,20 @@ thread_local char g_err[512] = "";
 __host__ __device__ inline size_t rup(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // ------------------------------------------------------------------------------------------------ layout
-// Packed parameter buffer (float offsets, each tensor 64-float aligned). X rows are [a | 0 | z | 0]:
-// action columns first so that every 8-wide K group of the MFMA loop is all-action or all-latent.
+// Packed parameter buffer (float offsets, each tensor 64-float aligned). First-layer inputs are
+// x = [a | 0 | z | 0] (action columns first, each part padded to a multiple of 8) so that every 8-deep
+// k group is all-action or all-latent.
 struct Layout {
     int A, L, M, E, Ap, Lp, Kx, Ar, Lr;
     int modality, obs_dim, img_c, img_hw, nch, conv_hw[5], flat;
-    size_t enc_w1, enc_b1, enc_w2, enc_b2;           // state encoder (raw nn.Linear layouts)
-    size_t cw[4], cb[4], pl_w, pl_b;                 // pixel encoder
-    size_t w1x, b1x;                                 // [2M][Kx]: dynamics.0 rows then reward.0 rows
-    size_t w2d, b2d, w2r, b2r;                       // [M][M]
-    size_t w3d, b3d, w3r, b3r;                       // [Lr][M], [M]
-    size_t wp1, bp1, wp2, bp2, wp3, bp3;             // pi: [M][Lp], [M][M], [Ar][M]
-    size_t wq1x, bq1x, g1, be1;                      // [2M][Kx], LN1 gamma/beta [2M]
-    size_t wq2, bq2, g2, be2;                        // [2][M][M], LN2 [2M]
+    size_t enc_w1t, enc_b1, enc_w2t, enc_b2;         // state encoder, weights transposed [in][out]
+    size_t cw[4], cb[4], pl_wt, pl_b;                // pixel encoder (conv dense, linear transposed)
+    size_t w1x, b1x;                                 // panel [2M][Kx]: dynamics.0 rows then reward.0 rows
+    size_t w2d, b2d, w2r, b2r;                       // panel [M][M]
+    size_t w3d, b3d, w3r, b3r;                       // panel [Lr][M]; reward.4 dense [M]
+    size_t wp1, bp1, wp2, bp2, wp3, bp3;             // pi: panel [M][Lp], [M][M], [Ar][M]
+    size_t wq1x, bq1x, g1, be1;                      // panel [2M][Kx]; LN1 gamma/beta [2M]
+    size_t wq2, bq2, g2, be2;                        // 2 panels [M][M]; LN2 [2M]
     size_t wq3, bq3;                                 // [2][M], [2]
     size_t total;
 };
@@ -59,15 +82,15 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
     if (!d || d->action_dim <= 0 || d->latent_dim <= 0 || d->mlp_dim <= 0 || d->mlp_dim % 64) return false;
     w->A = d->action_dim; w->L = d->latent_dim; w->M = d->mlp_dim; w->E = d->enc_dim;
     w->Ap = (int)rup(w->A, 8); w->Lp = (int)rup(w->L, 8); w->Kx = w->Ap + w->Lp;
-    w->Ar = (int)rup(w->A, 64); w->Lr = (int)rup(w->L, 64);
+    w->Ar = (int)rup(w->A, 32); w->Lr = (int)rup(w->L, 32);
     w->modality = d->modality; w->obs_dim = d->obs_dim;
     w->img_c = d->img_c; w->img_hw = d->img_hw; w->nch = d->num_channels;
     size_t o = 0;
     auto take = [&](size_t n) { size_t r = o; o += rup(n, 64); return r; };
     if (d->modality == 0) {
         if (d->obs_dim <= 0 || d->enc_dim <= 0) return false;
-        w->enc_w1 = take((size_t)w->E * d->obs_dim); w->enc_b1 = take(w->E);
-        w->enc_w2 = take((size_t)w->L * w->E); w->enc_b2 = take(w->L);
+        w->enc_w1t = take((size_t)w->E * d->obs_dim); w->enc_b1 = take(w->E);
+        w->enc_w2t = take((size_t)w->L * w->E); w->enc_b2 = take(w->L);
         w->flat = 0;
     } else {
         if (d->img_c <= 0 || d->img_hw <= 0 || d->num_channels <= 0) return false;
@@ -82,7 +105,7 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
             if (s <= 0) return false;
         }
         w->flat = w->nch * s * s;
-        w->pl_w = take((size_t)w->L * w->flat); w->pl_b = take(w->L);
+        w->pl_wt = take((size_t)w->L * w->flat); w->pl_b = take(w->L);
     }
     const size_t M = w->M;
     w->w1x = take(2 * M * w->Kx); w->b1x = take(2 * M);
@@ -99,40 +122,40 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
 
 // ------------------------------------------------------------------------------------------------ workspace
 struct Work {
-    float* X;        // [(Hmax+1)][B*T][Kx] step inputs [a|z]; X_H is the terminal input
-    float* H1;       // [B*T][2M]
-    float* H2;       // [B*T][2M]
+    float* X;        // (Hmax+1) panels [Xrows][Kx]: step inputs [a|z]; X_H is the terminal input
+    float* H1;       // panel [Xrows][2M]
+    float* H2;       // panel [Xrows][2M]
     float2* st1;     // [B*T][2M/64] LayerNorm partial moments of Q layer 0
     float2* st2;     // [B*T][2M/64] of Q layer 1
     float* rpart;    // [B*T][M/32] reward-head partial dots
-    float* G;        // [B*T] discounted return so far (physical rows)
+    float* G;        // [B*T] discounted return so far
     float* rlast;    // [B*T] reward at t = H-1
     float* value;    // [B*T]
-    float* z0;       // [B][Lp]
+    float* z0;       // [B][Lp] dense
     float* mean;     // [B][Hmax][A]
     float* stdv;     // [B][Hmax][A]
-    float* elite;    // [B][Hmax][K][A]
-    float* score;    // [B][K]
-    float* enc_tmp;  // pixel conv activations [B][max conv act]
+    float* enc_tmp;  // pixel conv activations
     size_t x_stride; // floats per X_t
+    int xrows;       // rup(B*T, 32)
     size_t total;
 };
 
 size_t pixel_act_floats(const Layout& w) {
     size_t m = 0;
     for (int i = 1; i <= 4; ++i) m = std::max(m, (size_t)w.nch * w.conv_hw[i] * w.conv_hw[i]);
-    return 2 * m;
+    return m;
 }
 
-bool make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k) {
+void make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k) {
     const size_t B = d->max_batch, N = d->num_samples, P = d->num_pi, T = N + P, H = d->max_horizon;
     const size_t M = w.M;
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += rup(bytes, 256); return base ? base + r : nullptr; };
-    k->x_stride = B * T * w.Kx;
+    k->xrows = (int)rup(B * T, 32);
+    k->x_stride = (size_t)k->xrows * w.Kx;
     k->X = (float*)take((H + 1) * k->x_stride * 4);
-    k->H1 = (float*)take(B * T * 2 * M * 4);
-    k->H2 = (float*)take(B * T * 2 * M * 4);
+    k->H1 = (float*)take((size_t)k->xrows * 2 * M * 4);
+    k->H2 = (float*)take((size_t)k->xrows * 2 * M * 4);
     k->st1 = (float2*)take(B * T * (2 * M / 64) * 8);
     k->st2 = (float2*)take(B * T * (2 * M / 64) * 8);
     k->rpart = (float*)take(B * T * (M / 32) * 4);
@@ -142,26 +165,25 @@ bool make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k) {
     k->z0 = (float*)take(B * w.Lp * 4);
     k->mean = (float*)take(B * H * w.A * 4);
     k->stdv = (float*)take(B * H * w.A * 4);
-    k->elite = (float*)take(B * H * d->num_elites * w.A * 4);
-    k->score = (float*)take(B * d->num_elites * 4);
-    k->enc_tmp = (float*)take(d->modality ? B * pixel_act_floats(w) * 4 : 256);
+    k->enc_tmp = (float*)take(d->modality ? 2 * B * pixel_act_floats(w) * 4 : 256);
     k->total = o;
-    return true;
+}
+
+size_t cem_lds_bytes(int T, int H, int K, int A) {
+    const size_t nl = (T + 63) / 64;
+    return nl * 64 * 8 + ((size_t)H * K * A + 64 + 4 * rup((size_t)H * A, 4) + 64 + 32) * 4;
 }
 
 bool check_dims(const tdmpc_dims* d) {
     if (!d) return false;
     if (d->num_samples <= 0 || d->num_pi < 0 || d->num_elites <= 0 || d->max_horizon <= 0 ||
         d->max_horizon > 16 || d->max_iterations <= 0 || d->max_batch <= 0) return false;
-    if (d->num_elites > d->num_samples + d->num_pi || d->num_elites > 1024) return false;
-    if (d->num_samples + d->num_pi > 8192) return false;
+    const int T = d->num_samples + d->num_pi;
+    if (d->num_elites > T || d->num_elites > 64 || T > 4096) return false;
     Layout w;
     if (!make_layout(d, &w)) return false;
-    if (w.Kx > 1024 || w.M > 1024 || w.L > 1024) return false;
-    // cem_kernel LDS: values[T] + elite actions [H][K][A] + misc
-    size_t lds = (size_t)(d->num_samples + d->num_pi) * 4 + (size_t)d->max_horizon * d->num_elites * w.A * 4 +
-                 (size_t)d->num_elites * 12 + (size_t)2 * d->max_horizon * w.A * 4 + 256;
-    if (lds > 160 * 1024) return false;
+    if (w.Kx > 1024 || w.M > 1024 || w.L > 1024 || w.A > 256 || w.E > 1024) return false;
+    if (cem_lds_bytes(T, d->max_horizon, d->num_elites, w.A) > 160 * 1024) return false;
     return true;
 }
 
@@ -169,13 +191,15 @@ bool check_dims(const tdmpc_dims* d) {
 DEVI float elu1(float x) { return x > 0.f ? x : expm1f(x); }
 DEVI float fmul(float a, float b) { return __fmul_rn(a, b); }
 DEVI float fadd(float a, float b) { return __fadd_rn(a, b); }
-DEVI float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
-// torch.clamp propagates NaN; fminf/fmaxf would drop it.
-DEVI float tclamp(float x, float lo, float hi) { return x != x ? x : clampf(x, lo, hi); }
+// torch.clamp propagates NaN; plain fminf/fmaxf would drop it.
+DEVI float tclamp(float x, float lo, float hi) { return x != x ? x : fminf(fmaxf(x, lo), hi); }
 DEVI float nan_to_num(float x) {
     if (x != x) return 0.f;
     if (isinf(x)) return x > 0 ? 3.402823466e38f : -3.402823466e38f;
     return x;
+}
+__host__ __device__ inline size_t pidx(size_t r, size_t c, size_t cols) {
+    return (r >> 5) * (cols * 32) + (c >> 2) * 128 + (r & 31) * 4 + (c & 3);
 }
 
 struct RowMap {  // logical row m -> physical row (m / G) * S + O + m % G
@@ -183,21 +207,38 @@ struct RowMap {  // logical row m -> physical row (m / G) * S + O + m % G
 };
 DEVI int map_row(const RowMap& r, int m) { return (m / r.G) * r.S + r.O + (m % r.G); }
 
+// Panel operand: element (r, k) at p + (r>>5)*ts + (q0 + (k>>2))*128 + (r&31)*4 + (k&3)
+struct Opnd {
+    const float* p; long ts; int q0;
+};
+struct Outp {
+    float* p; long ts; int q0;
+};
+
 // ------------------------------------------------------------------------------------------------ linear
 enum { PRO_PLAIN = 0, PRO_LN_TANH = 1 };
-enum { EPI_ELU = 0, EPI_LIN_Z = 1, EPI_PI = 2, EPI_LNSTATS = 3, EPI_ELU_DOT = 4, EPI_LIN = 5 };
+enum { EPI_ELU = 0, EPI_LIN_Z = 1, EPI_PI = 2, EPI_LNSTATS = 3, EPI_ELU_DOT = 4 };
+
+// Cheap activations for the hot loops: |error| < 2e-7 against libm over the value range here, well inside
+// the parity tolerance (tests/test_gpu_plan.py). ELU uses exp(x) - 1 like ATen's scalar path.
+DEVI float elu_f(float x) { return x > 0.f ? x : __expf(x) - 1.f; }
+DEVI float tanh_f(float x) {
+    const float e = __expf(-2.f * fabsf(x));
+    return copysignf(__fdividef(1.f - e, 1.f + e), x);
+}
 
 struct LinProb {
-    const float* A; int lda;      // activations (A + col offset), row stride in floats
-    const float* W; int ldw;      // weights [Npad][K] row-major (nn.Linear layout)
-    const float* bias;            // [Npad]
-    float* C; int ldc;            // output (EPI-dependent)
-    int N;                        // valid output columns
+    Opnd A; Opnd W;
+    const float* bias;            // [>= grid columns]
+    Outp C;
+    int N;                        // output columns covered by the grid (tiles beyond return early)
+    int nvalid;                   // real output columns; columns >= nvalid are written as 0
+    int nstore;                   // stored columns (multiple of 4)
     int epi;
-    const float2* ln_stats; int ln_ld; int ln_t0; int ln_nt;   // PRO_LN_*: moments [row][ln_ld] tiles
+    const float2* ln_stats; int ln_ld; int ln_t0; int ln_nt;   // PRO_LN_TANH: per-64-col (mean, M2)
     const float* ln_g; const float* ln_b;                      // LN affine for this problem's K columns
-    float2* st_out; int st_ld;                                 // EPI_LNSTATS
-    const float* dotw; float* dot_out; int dot_ld;             // EPI_ELU_DOT
+    float2* st_out; int st_ld;                                 // EPI_LNSTATS: per-64-col moments out
+    const float* dotw; float* dot_out; int dot_ld;             // EPI_ELU_DOT: per-block partial dots
 };
 
 struct LinArgs {
@@ -205,372 +246,556 @@ struct LinArgs {
     int M, K, kch;
     int a_mapped, c_mapped;
     RowMap amap, cmap;
-    // EPI_LIN_Z (dynamics head of step t): reward bookkeeping
+    // A-operand sources for first-layer inputs x = [a|z] (column quads < apq are the action part)
+    int apq, rows_per_env;
+    int zmode;                    // z part from z0[env][Lp] (t = 0: every row starts at h(obs))
+    const float* z0; int Lp;
+    int smode;                    // action part of rows with (row % rows_per_env) < s_rows sampled:
+    int s_rows;                   //   clamp(mean_t + std_t * eps, -1, 1)
+    const float* mean_t; const float* std_t; int mstride;
+    const float* seps; long seps_env; long seps_off; int A;
+    // EPI_LIN_Z: reward head + return
     const float* rpart; int rpart_nt; const float* b3r;
     float* G; float* rlast; float disc; int first, last;
     // EPI_PI
-    const float* eps; int eps_G; long eps_env; long eps_off; int A; float min_std; float lo, hi;
+    const float* eps; int eps_G; long eps_env; long eps_off; float min_std, lo, hi;
 };
 
-template <int WN, int PRO, int KCH>
+// A operand quad (4 consecutive k of one row) for first-layer / plain inputs.
+DEVI float4 load_a(const LinArgs& args, const float* Abase, int colq, int arow, int env) {
+    if (args.smode && colq < args.apq) {
+        const int n = arow % args.rows_per_env;
+        if (n < args.s_rows) {
+            // CEM candidates (tdmpc.py:130-132): clamp(mean + std * randn, -1, 1), mul then add
+            const float* ep = args.seps + (size_t)env * args.seps_env + args.seps_off + (size_t)n * args.A;
+            const float* mt = args.mean_t + (size_t)env * args.mstride;
+            const float* sd = args.std_t + (size_t)env * args.mstride;
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c = colq * 4 + i;
+                v[i] = c < args.A ? tclamp(fadd(mt[c], fmul(sd[c], ep[c])), -1.f, 1.f) : 0.f;
+            }
+            return make_float4(v[0], v[1], v[2], v[3]);
+        }
+    }
+    if (args.zmode && colq >= args.apq)
+        return *(const float4*)(args.z0 + (size_t)env * args.Lp + (colq - args.apq) * 4);
+    return *(const float4*)(Abase + (size_t)colq * 128);
+}
+
+// Fused nn.Linear on v_mfma_f32_32x32x2_f32.
+//   Workgroup tile: R = 32*TM*WGM rows x C = 32*TN*WGN columns; waves = WGM*WGN*KS where KS (runtime,
+//   blockDim / (64*WGM*WGN)) splits K into chunks of KCH. Each wave owns a (32*TM) x (32*TN) register tile.
+//   ROLL = false: a wave preloads its whole K chunk (<= KCH/8 groups) -- the latency configuration for
+//   small row counts. ROLL = true: KS = 1 and a 4-deep prefetch ring walks the full K -- the throughput
+//   configuration for large row counts.
+template <int TM, int TN, int WGM, int WGN, int PRO, int KCH, bool ROLL>
 __global__ void __launch_bounds__(512) linear_kernel(const LinArgs args) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int BN = 32 * WN;
-    constexpr int LDW = BN + 4;
+    constexpr int R = 32 * TM * WGM, C = 32 * TN * WGN, LDC = C + 4;
+    constexpr int BW = C >= 64 ? 64 : C;     // row-reduction block width
+    constexpr int NB = C / BW;
     const LinProb& P = args.p[blockIdx.z];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nthr = blockDim.x;
     const int r = lane & 31, h = lane >> 5;
-    const int m0 = blockIdx.x * 32, n0 = blockIdx.y * BN;
-    if (n0 >= P.N) return;  // whole workgroup uniform
-    const int m = m0 + r;
-    const bool mval = m < args.M;
-    const int mm = mval ? m : 0;
-    const int arow = args.a_mapped ? map_row(args.amap, mm) : mm;
-    const float* Arow = P.A + (size_t)arow * P.lda;
-
-    float mu = 0.f, rs = 1.f;
-    if (PRO == PRO_LN_TANH) {
-        // Chan-combine the producer's per-64-column (mean, M2) into this row's mean / 1/sqrt(var+eps).
-        const float2* st = P.ln_stats + (size_t)mm * P.ln_ld + P.ln_t0;
-        float n = 0.f, mean = 0.f, m2 = 0.f;
-        for (int i = 0; i < P.ln_nt; ++i) {
-            float2 s = st[i];
-            float nb = 64.f, nn = n + nb, delta = s.x - mean;
-            mean += delta * nb / nn;
-            m2 += s.y + delta * delta * n * nb / nn;
-            n = nn;
-        }
-        mu = mean;
-        rs = 1.0f / sqrtf(fmaxf(m2 / n, 0.f) + 1e-5f);
-    }
-
-    floatx16 acc[WN];
-#pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
-
-    const int kbeg = wave * args.kch;
-    const int kend = min(kbeg + args.kch, args.K);
-    const float* Wrow[WN];
-#pragma unroll
-    for (int j = 0; j < WN; ++j) Wrow[j] = P.W + (size_t)(n0 + 32 * j + r) * P.ldw;
-
-    constexpr int NG = KCH / 8;
-    float4 av[NG], bv[NG][WN];
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-        const int k = kbeg + 8 * g + 4 * h;
-        if (kbeg + 8 * g < kend) {
-            av[g] = *(const float4*)(Arow + k);
-#pragma unroll
-            for (int j = 0; j < WN; ++j) bv[g][j] = *(const float4*)(Wrow[j] + k);
-        }
-    }
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-        if (kbeg + 8 * g < kend) {
-            float4 a = av[g];
-            if (PRO == PRO_LN_TANH) {
-                const int k = kbeg + 8 * g + 4 * h;
-                const float4 gg = *(const float4*)(P.ln_g + k);
-                const float4 bb = *(const float4*)(P.ln_b + k);
-                const float sh = -rs * mu;
-                a.x = tanhf(fadd(fmul(fadd(fmul(a.x, rs), sh), gg.x), bb.x));
-                a.y = tanhf(fadd(fmul(fadd(fmul(a.y, rs), sh), gg.y), bb.y));
-                a.z = tanhf(fadd(fmul(fadd(fmul(a.z, rs), sh), gg.z), bb.z));
-                a.w = tanhf(fadd(fmul(fadd(fmul(a.w, rs), sh), gg.w), bb.w));
-            }
-#pragma unroll
-            for (int j = 0; j < WN; ++j) {
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bv[g][j].x, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, bv[g][j].y, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, bv[g][j].z, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, bv[g][j].w, acc[j], 0, 0, 0);
-            }
-        }
-    }
-
-    // partial tile -> LDS [wave][32][LDW]; C/D map: col = lane&31, row = (i&3) + 8*(i>>2) + 4*(lane>>5)
-    float* mys = smem + (size_t)wave * 32 * LDW;
-#pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) mys[((i & 3) + 8 * (i >> 2) + 4 * h) * LDW + 32 * j + r] = acc[j][i];
-    __syncthreads();
-
-    // ---- epilogue: TPR threads per row, each owns 4-column chunks
-    const int nw = nthr >> 6;
-    // threads per row: a power of two (<= 16) so a row's threads are consecutive lanes of one wave and
-    // the xor-shuffle row reductions are exact; surplus threads sit out the epilogue.
-    const int tpr = nthr >= 512 ? 16 : nthr >= 256 ? 8 : nthr >= 128 ? 4 : 2;
-    if (threadIdx.x >= 32 * tpr) return;
-    const int row = threadIdx.x / tpr, q = threadIdx.x % tpr;
-    const int lm = m0 + row;
-    const bool rval = lm < args.M;
-    const int crow = rval ? (args.c_mapped ? map_row(args.cmap, lm) : lm) : 0;
+    const int m0 = blockIdx.x * R, n0 = blockIdx.y * C;
+    if (n0 >= P.N) return;  // uniform over the workgroup
+#ifdef TDMPC_STAMPS
+    unsigned long long st_[6];
+    unsigned long long rt0_ = __builtin_amdgcn_s_memrealtime();
+    STAMP(0);
+#endif
+    const int KS = nthr / (64 * WGM * WGN);
+    const int wm = wave % WGM, wn = (wave / WGM) % WGN, ks = wave / (WGM * WGN);
     const int epi = P.epi;
-    float tsum = 0.f, dsum = 0.f;
-    float* fin = smem;  // reduced tile is written back over wave 0's partial (each chunk has one owner)
-    for (int c = 4 * q; c < BN; c += 4 * tpr) {
-        float4 v = *(const float4*)(smem + row * LDW + c);
-        for (int w = 1; w < nw; ++w) {
-            const float4 u = *(const float4*)(smem + (size_t)w * 32 * LDW + row * LDW + c);
-            v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+
+    // LDS: partial tiles [KS][R][LDC] | bias [C] | dotw [C] | rpart [R][rpart_nt]
+    float* sbias = smem + (size_t)KS * R * LDC;
+    float* sdotw = sbias + C;
+    float* srp = sdotw + C;
+    // prefetch the epilogue's operands now; the loads land while the MFMAs run
+    for (int i = threadIdx.x; i < C / 4; i += nthr) {
+        const int n = n0 + 4 * i;
+        *(float4*)(sbias + 4 * i) = *(const float4*)(P.bias + n);
+        if (epi == EPI_ELU_DOT) *(float4*)(sdotw + 4 * i) = *(const float4*)(P.dotw + n);
+    }
+    if (epi == EPI_LIN_Z && blockIdx.y == 0)
+        for (int i = threadIdx.x; i < R * args.rpart_nt; i += nthr) {
+            const int lm = m0 + i / args.rpart_nt;
+            srp[i] = lm < args.M ? args.rpart[(size_t)lm * args.rpart_nt + i % args.rpart_nt] : 0.f;
         }
-        const int n = n0 + c;
-        const float4 bb = *(const float4*)(P.bias + n);
-        float o[4] = {v.x + bb.x, v.y + bb.y, v.z + bb.z, v.w + bb.w};
-        if (epi == EPI_ELU || epi == EPI_ELU_DOT) {
+
+    // this lane's A rows (TM of them) and W rows (TN)
+    const float* Abase[TM];
+    int arow[TM], env[TM];
+    float mu[TM], rs[TM];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) o[i] = elu1(o[i]);
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + (wm * TM + i) * 32 + r;
+        const int mm = m < args.M ? m : 0;
+        arow[i] = args.a_mapped ? map_row(args.amap, mm) : mm;
+        Abase[i] = P.A.p + (size_t)(arow[i] >> 5) * P.A.ts + (arow[i] & 31) * 4;
+        env[i] = (args.zmode | args.smode) ? arow[i] / args.rows_per_env : 0;
+        mu[i] = 0.f; rs[i] = 1.f;
+        if (PRO == PRO_LN_TANH) {
+            // Chan-combine the producer's per-64-column (mean, M2) into mean and 1/sqrt(var + 1e-5)
+            const float2* st = P.ln_stats + (size_t)mm * P.ln_ld + P.ln_t0;
+            float n = 0.f, mean = 0.f, m2 = 0.f;
+            for (int q = 0; q < P.ln_nt; ++q) {
+                const float2 s = st[q];
+                const float nn = n + 64.f, delta = s.x - mean;
+                mean += delta * 64.f / nn;
+                m2 += s.y + delta * delta * n * 64.f / nn;
+                n = nn;
+            }
+            mu[i] = mean;
+            rs[i] = 1.0f / sqrtf(fmaxf(m2 / n, 0.f) + 1e-5f);
         }
-        if (epi == EPI_ELU_DOT) {
-            const float4 dw = *(const float4*)(P.dotw + n);
-            dsum += o[0] * dw.x + o[1] * dw.y + o[2] * dw.z + o[3] * dw.w;
-            continue;
-        }
-        if (epi == EPI_PI) {
-            // TOLD.pi + TruncatedNormal.sample(clip=0.3) (tdmpc.py:39-45, helper.py:86-96)
-            const int e = lm / args.eps_G, rr = lm % args.eps_G;
-            const float* ep = args.eps + (size_t)e * args.eps_env + args.eps_off + (size_t)rr * args.A;
+    }
+    const float* Wbase = P.W.p + (size_t)((n0 >> 5) + wn * TN) * P.W.ts + r * 4;
+
+    floatx16 acc[TM][TN];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if (n + i < P.N && rval) {
-                    const float muv = tanhf(o[i]);
-                    float x = muv;
-                    if (args.min_std > 0.f) {
-                        const float ee = tclamp(fmul(ep[n + i], args.min_std), -0.3f, 0.3f);
-                        x = tclamp(fadd(muv, ee), args.lo, args.hi);
-                    }
-                    P.C[(size_t)crow * P.ldc + n + i] = x;
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    auto mfma_group = [&](float4 (&a)[TM], const float4 (&b)[TN], int k) {
+        if (PRO == PRO_LN_TANH) {
+            // helper.q: LayerNorm -> Tanh, as ATen computes it: (x * rstd + (-rstd * mean)) * g + b
+            const float4 gg = *(const float4*)(P.ln_g + k);
+            const float4 bb = *(const float4*)(P.ln_b + k);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const float sh = -rs[i] * mu[i];
+                a[i].x = tanh_f(fadd(fmul(fadd(fmul(a[i].x, rs[i]), sh), gg.x), bb.x));
+                a[i].y = tanh_f(fadd(fmul(fadd(fmul(a[i].y, rs[i]), sh), gg.y), bb.y));
+                a[i].z = tanh_f(fadd(fmul(fadd(fmul(a[i].z, rs[i]), sh), gg.z), bb.z));
+                a[i].w = tanh_f(fadd(fmul(fadd(fmul(a[i].w, rs[i]), sh), gg.w), bb.w));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+            }
+    };
+    auto load_group = [&](int g, float4 (&a)[TM], float4 (&b)[TN]) {
+        const int kq = 2 * g + h;  // quad of this lane half within K
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = *(const float4*)(Wbase + (size_t)j * P.W.ts + kq * 128);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = load_a(args, Abase[i], P.A.q0 + kq, arow[i], env[i]);
+    };
+
+    if (!ROLL) {
+        constexpr int NG = KCH / 8;
+        const int g0 = (ks * args.kch) >> 3;
+        const int ng = min(args.kch, args.K - ks * args.kch) >> 3;
+        float4 av[NG][TM], bv[NG][TN];
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+            if (g < ng) load_group(g0 + g, av[g], bv[g]);
+#ifdef TDMPC_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP(1);
+#endif
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+            if (g < ng) mfma_group(av[g], bv[g], 8 * (g0 + g) + 4 * h);
+    } else {
+        constexpr int D = 4;
+        const int ng = args.K >> 3;
+        float4 ra[D][TM], rb[D][TN];
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+            if (d < ng) load_group(d, ra[d], rb[d]);
+#ifdef TDMPC_STAMPS
+        STAMP(1);
+#endif
+        for (int gb = 0; gb < ng; gb += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const int g = gb + d;
+                if (g < ng) {
+                    float4 ta[TM], tb[TN];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) ta[i] = ra[d][i];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) tb[j] = rb[d][j];
+                    if (g + D < ng) load_group(g + D, ra[d], rb[d]);
+                    mfma_group(ta, tb, 8 * g + 4 * h);
                 }
             }
-            continue;
         }
-        if (epi == EPI_LNSTATS) {
-            tsum += (o[0] + o[1]) + (o[2] + o[3]);
-            *(float4*)(fin + row * LDW + c) = make_float4(o[0], o[1], o[2], o[3]);
-        }
-        if (rval) {
-            float* dst = P.C + (size_t)crow * P.ldc + n;
-            if (n + 3 < P.N && epi != EPI_LIN_Z) {
-                *(float4*)dst = make_float4(o[0], o[1], o[2], o[3]);
+    }
+
+    // partial tiles -> LDS [ks][row][col]; C/D map: col = lane&31, row = (e&3) + 8*(e>>2) + 4*(lane>>5)
+    {
+        float* base = smem + (size_t)ks * R * LDC + (size_t)(wm * TM * 32) * LDC + wn * TN * 32;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    base[(size_t)(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * LDC + j * 32 + r] = acc[i][j][e];
+    }
+#ifdef TDMPC_STAMPS
+    STAMP(2);
+#endif
+    __syncthreads();
+#ifdef TDMPC_STAMPS
+    STAMP(3);
+#endif
+
+    // ---- epilogue phase A: thread -> (row, column quads); 32 consecutive lanes own 32 consecutive rows,
+    // so one quad stored by them is 512 contiguous bytes of the panel layout.
+    const bool need_red = epi == EPI_LNSTATS || epi == EPI_ELU_DOT;
+    {
+        const int rows_blk = R / 32;
+        const int row = (threadIdx.x & 31) + 32 * ((threadIdx.x >> 5) % rows_blk);
+        const int cq0 = (threadIdx.x >> 5) / rows_blk, cqs = nthr / R;
+        const int lm = m0 + row;
+        const bool rval = lm < args.M;
+        const int crow = rval ? (args.c_mapped ? map_row(args.cmap, lm) : lm) : 0;
+        float* Cbase = P.C.p ? P.C.p + (size_t)(crow >> 5) * P.C.ts + (crow & 31) * 4 : nullptr;
+        for (int cq = cq0; cq < C / 4; cq += cqs) {
+            const int c = 4 * cq;
+            float4 v = *(const float4*)(smem + (size_t)row * LDC + c);
+            for (int w = 1; w < KS; ++w) {
+                const float4 u = *(const float4*)(smem + ((size_t)w * R + row) * LDC + c);
+                v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+            }
+            const int n = n0 + c;
+            const float4 bb = *(const float4*)(sbias + c);
+            float o[4] = {v.x + bb.x, v.y + bb.y, v.z + bb.z, v.w + bb.w};
+            if (epi == EPI_ELU || epi == EPI_ELU_DOT) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) o[i] = elu_f(o[i]);
+            }
+            if (epi == EPI_PI) {
+                // TOLD.pi + TruncatedNormal.sample(clip=0.3) (tdmpc.py:39-45, helper.py:86-96)
+                const int e = lm / args.eps_G, rr = lm % args.eps_G;
+                const float* ep = args.eps + (size_t)e * args.eps_env + args.eps_off + (size_t)rr * args.A;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float x = 0.f;
+                    if (n + i < P.nvalid && rval) {
+                        const float muv = tanhf(o[i]);
+                        x = muv;
+                        if (args.min_std > 0.f) {
+                            const float ee = tclamp(fmul(ep[n + i], args.min_std), -0.3f, 0.3f);
+                            x = tclamp(fadd(muv, ee), args.lo, args.hi);
+                        }
+                    }
+                    o[i] = x;
+                }
             } else {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    if (n + i < P.N) dst[i] = o[i];
+                    if (n + i >= P.nvalid) o[i] = 0.f;
+            }
+            if (need_red) *(float4*)(smem + (size_t)row * LDC + c) = make_float4(o[0], o[1], o[2], o[3]);
+            if (rval && n < P.nstore)
+                *(float4*)(Cbase + (size_t)(P.C.q0 + (n >> 2)) * 128) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+    }
+    // ---- epilogue phase B: one thread per (row, BW-column block) for the row reductions
+    if (need_red) {
+        __syncthreads();
+        for (int t = threadIdx.x; t < R * NB; t += nthr) {
+            const int row = t % R, blk = t / R;
+            const int lm = m0 + row;
+            if (lm >= args.M) continue;
+            const float* v = smem + (size_t)row * LDC + blk * BW;
+            if (epi == EPI_LNSTATS) {
+                // LayerNorm partial moments of this 64-column slice: (mean, sum of squared deviations)
+                float s = 0.f;
+                for (int c = 0; c < BW; c += 4) {
+                    const float4 x = *(const float4*)(v + c);
+                    s += (x.x + x.y) + (x.z + x.w);
+                }
+                const float mean = s / (float)BW;
+                float m2 = 0.f;
+                for (int c = 0; c < BW; c += 4) {
+                    const float4 x = *(const float4*)(v + c);
+                    const float d0 = x.x - mean, d1 = x.y - mean, d2 = x.z - mean, d3 = x.w - mean;
+                    m2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+                }
+                P.st_out[(size_t)lm * P.st_ld + (n0 / 64) + blk] = make_float2(mean, m2);
+            } else {
+                const float* wv = sdotw + blk * BW;
+                float s = 0.f;
+                for (int c = 0; c < BW; c += 4) {
+                    const float4 x = *(const float4*)(v + c), w4 = *(const float4*)(wv + c);
+                    s += (x.x * w4.x + x.y * w4.y) + (x.z * w4.z + x.w * w4.w);
+                }
+                P.dot_out[(size_t)lm * P.dot_ld + (n0 / BW) + blk] = s;
             }
         }
     }
-    if (epi == EPI_LNSTATS) {
-        // LayerNorm partial moments of this 64-column slice: (mean, sum of squared deviations)
-        for (int off = 1; off < tpr; off <<= 1) tsum += __shfl_xor(tsum, off, 64);
-        const float tmean = tsum / (float)BN;
-        float m2 = 0.f;
-        for (int c = 4 * q; c < BN; c += 4 * tpr) {
-            const float4 v = *(const float4*)(fin + row * LDW + c);
-            const float d0 = v.x - tmean, d1 = v.y - tmean, d2 = v.z - tmean, d3 = v.w - tmean;
-            m2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
-        }
-        for (int off = 1; off < tpr; off <<= 1) m2 += __shfl_xor(m2, off, 64);
-        if (q == 0 && rval) P.st_out[(size_t)lm * P.st_ld + blockIdx.y] = make_float2(tmean, m2);
-    } else if (epi == EPI_ELU_DOT) {
-        for (int off = 1; off < tpr; off <<= 1) dsum += __shfl_xor(dsum, off, 64);
-        if (q == 0 && rval) P.dot_out[(size_t)lm * P.dot_ld + blockIdx.y] = dsum;
-    } else if (epi == EPI_LIN_Z && blockIdx.y == 0 && q == 0 && rval) {
+    if (epi == EPI_LIN_Z && blockIdx.y == 0) {
         // reward head (helper.mlp last Linear, M -> 1) from the partial dots, then
         // G += discount * reward (tdmpc.py:89) with float32(discount) like ATen's scalar mul.
-        const float* rp = args.rpart + (size_t)lm * args.rpart_nt;
-        float s = 0.f;
-        for (int i = 0; i < args.rpart_nt; ++i) s += rp[i];
-        const float rew = s + args.b3r[0];
-        const float dr = fmul(args.disc, rew);
-        args.G[crow] = args.first ? dr : fadd(args.G[crow], dr);
-        if (args.last) args.rlast[crow] = rew;
+        for (int row = threadIdx.x; row < R; row += nthr) {
+            const int lm = m0 + row;
+            if (lm >= args.M) continue;
+            const int crow = args.c_mapped ? map_row(args.cmap, lm) : lm;
+            float s = 0.f;
+            for (int i = 0; i < args.rpart_nt; ++i) s += srp[row * args.rpart_nt + i];
+            const float rew = s + args.b3r[0];
+            const float dr = fmul(args.disc, rew);
+            args.G[crow] = args.first ? dr : fadd(args.G[crow], dr);
+            if (args.last) args.rlast[crow] = rew;
+        }
     }
+#ifdef TDMPC_STAMPS
+    __syncthreads();
+    STAMP(4);
+    if (threadIdx.x == 0 && g_stamps) {
+        const unsigned int slot = atomicAdd(&g_stamp_n, 1u);
+        if (slot >= g_stamp_cap) return;
+        unsigned long long* o = g_stamps + (size_t)slot * 8;
+        o[0] = rt0_; o[1] = st_[0]; o[2] = st_[1]; o[3] = st_[2]; o[4] = st_[3]; o[5] = st_[4];
+        o[6] = blockIdx.x | (blockIdx.y << 16) | ((unsigned long long)blockIdx.z << 32);
+        unsigned int xcc_;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));
+        o[7] = xcc_;
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------ value
 // q_p = w3_p . ELU(LN_p(y_p)) + b3_p (helper.q last layers), G += gamma^H min(q1, q2), nan_to_num
-// (tdmpc.py:91-92). One wave per row.
+// (tdmpc.py:91-92). One workgroup per 32-row panel tile, 16 threads per row; loads unrolled so each
+// thread has all of its operands in flight at once.
 struct ValueArgs {
-    const float* Y; int ldy; const float2* st; int st_ld; int M_;
+    const float* Y; long yts; const float2* st; int st_ld; int M_;
     const float* g2; const float* be2; const float* w3; const float* b3;
     const float* G; float disc; float* value; float* value_out; int rows, T, I, iter;
 };
 
-__global__ void __launch_bounds__(256) value_kernel(const ValueArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= a.rows) return;
-    const int ntile = a.M_ / 64;
-    float q[2];
+__global__ void __launch_bounds__(512) value_kernel(const ValueArgs a) {
+    __shared__ float red[2][16][32];
+    const int tid = threadIdx.x, r = tid & 31, g = tid >> 5;
+    const int row = blockIdx.x * 32 + r;
+    const int rr = row < a.rows ? row : 0;
+    const int ntile = a.M_ / 64, nq = a.M_ / 4;
+    const float* ybase = a.Y + (size_t)(rr >> 5) * a.yts + (rr & 31) * 4;
     for (int p = 0; p < 2; ++p) {
-        const float2* st = a.st + (size_t)row * a.st_ld + p * ntile;
+        const float2* st = a.st + (size_t)rr * a.st_ld + p * ntile;
         float n = 0.f, mean = 0.f, m2 = 0.f;
         for (int i = 0; i < ntile; ++i) {
-            float2 s = st[i];
-            float nb = 64.f, nn = n + nb, delta = s.x - mean;
-            mean += delta * nb / nn;
-            m2 += s.y + delta * delta * n * nb / nn;
+            const float2 s = st[i];
+            const float nn = n + 64.f, delta = s.x - mean;
+            mean += delta * 64.f / nn;
+            m2 += s.y + delta * delta * n * 64.f / nn;
             n = nn;
         }
         const float rs = 1.0f / sqrtf(fmaxf(m2 / n, 0.f) + 1e-5f);
         const float sh = -rs * mean;
-        const float* y = a.Y + (size_t)row * a.ldy + p * a.M_;
-        const float* g = a.g2 + p * a.M_;
-        const float* b = a.be2 + p * a.M_;
-        const float* w = a.w3 + p * a.M_;
+        const float* gp = a.g2 + p * a.M_;
+        const float* bp = a.be2 + p * a.M_;
+        const float* wp = a.w3 + p * a.M_;
         float s = 0.f;
-        for (int c = 4 * lane; c < a.M_; c += 256) {
-            const float4 yv = *(const float4*)(y + c), gv = *(const float4*)(g + c), bv = *(const float4*)(b + c),
-                         wv = *(const float4*)(w + c);
-            s += elu1(fadd(fmul(fadd(fmul(yv.x, rs), sh), gv.x), bv.x)) * wv.x;
-            s += elu1(fadd(fmul(fadd(fmul(yv.y, rs), sh), gv.y), bv.y)) * wv.y;
-            s += elu1(fadd(fmul(fadd(fmul(yv.z, rs), sh), gv.z), bv.z)) * wv.z;
-            s += elu1(fadd(fmul(fadd(fmul(yv.w, rs), sh), gv.w), bv.w)) * wv.w;
+#pragma unroll 8
+        for (int q = g; q < nq; q += 16) {
+            const float4 yv = *(const float4*)(ybase + (size_t)(p * nq + q) * 128);
+            const float4 gv = *(const float4*)(gp + 4 * q), bv = *(const float4*)(bp + 4 * q);
+            const float4 wv = *(const float4*)(wp + 4 * q);
+            s += elu_f(fadd(fmul(fadd(fmul(yv.x, rs), sh), gv.x), bv.x)) * wv.x;
+            s += elu_f(fadd(fmul(fadd(fmul(yv.y, rs), sh), gv.y), bv.y)) * wv.y;
+            s += elu_f(fadd(fmul(fadd(fmul(yv.z, rs), sh), gv.z), bv.z)) * wv.z;
+            s += elu_f(fadd(fmul(fadd(fmul(yv.w, rs), sh), gv.w), bv.w)) * wv.w;
         }
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-        q[p] = s + a.b3[p];
+        red[p][g][r] = s;
     }
-    if (lane == 0) {
-        const float qm = fminf(q[0], q[1]);
-        const float qmin = (q[0] != q[0] || q[1] != q[1]) ? NAN : qm;  // torch.min propagates NaN
-        const float v = nan_to_num(fadd(a.G[row], fmul(a.disc, qmin)));
+    __syncthreads();
+    if (tid < 32 && row < a.rows) {
+        float q[2];
+        for (int p = 0; p < 2; ++p) {
+            float s = 0.f;
+            for (int i = 0; i < 16; ++i) s += red[p][i][r];
+            q[p] = s + a.b3[p];
+        }
+        const float qm = (q[0] != q[0] || q[1] != q[1]) ? NAN : fminf(q[0], q[1]);  // torch.min keeps NaN
+        const float v = nan_to_num(fadd(a.G[row], fmul(a.disc, qm)));
         a.value[row] = v;
         if (a.value_out) a.value_out[((size_t)(row / a.T) * a.I + a.iter) * a.T + row % a.T] = v;
     }
 }
 
 // ------------------------------------------------------------------------------------------------ CEM
-// One workgroup per environment. mode 0: initialise mean/std (tdmpc.py:122-125) and sample iteration 0;
-// mode 1: refit (tdmpc.py:138-149) and sample the next iteration (tdmpc.py:130-132);
-// mode 2: refit and pick the output action (tdmpc.py:152-160).
+// One workgroup (16 waves) per environment, after each iteration's values: top-k (tdmpc.py:138-139),
+// softmax refit (:142-149); on the last iteration the output action (:152-160).
 struct CemArgs {
-    int mode, iter, H, N, P, T, A, K, Kx;
-    float* X; size_t x_stride;          // X_t a-columns hold the candidate actions
+    int final_iter, iter, H, N, P, T, A, K, Kx, Hmax, I;
+    const float* X; size_t x_stride;    // X_t panels: action columns of the pi rows
     const float* value;                 // [B*T]
     const float* rlast;                 // [B*T]
     float* mean; float* stdv;           // [B][Hmax][A]
-    int Hmax;
     const float* eps; long eps_env; long eps_cem_off; long eps_iter; long eps_act_off;
     const double* u;
-    float* prev_mean; int warm, eval_mode;
+    float* prev_mean; int eval_mode;
     float temperature, momentum, omm, std_floor;
     float* action; float* metrics;
-    float* elite_ws; float* score_ws;
-    float* elite_out; float* score_out; float* mean_out; float* std_out; int I;
+    float* elite_out; float* score_out; float* mean_out; float* std_out;
 };
+
+DEVI uint32_t f2ord(float v) {
+    const uint32_t u = __float_as_uint(v);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+DEVI float ord2f(uint32_t o) { return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o); }
+// sort key: ascending key = descending value, then ascending index (torch.topk order for distinct values)
+DEVI unsigned long long topk_key(float v, int i) {
+    return ((unsigned long long)(~f2ord(v)) << 32) | (unsigned)i;
+}
+DEVI float key_value(unsigned long long k) { return ord2f(~(uint32_t)(k >> 32)); }
+
+DEVI unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+    const unsigned lo = __shfl_xor((unsigned)v, m, 64), hi = __shfl_xor((unsigned)(v >> 32), m, 64);
+    return ((unsigned long long)hi << 32) | lo;
+}
+// ascending bitonic sort of one key per lane across the 64 lanes of a wave
+DEVI unsigned long long wave_sort64(unsigned long long key, int lane) {
+    for (int k = 2; k <= 64; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const unsigned long long o = shfl_xor_u64(key, j);
+            const bool up = (lane & k) == 0, lower = (lane & j) == 0;
+            key = (lower == up) ? (key < o ? key : o) : (key > o ? key : o);
+        }
+    return key;
+}
+// lanes hold a bitonic sequence -> ascending
+DEVI unsigned long long wave_clean64(unsigned long long key, int lane) {
+    for (int j = 32; j > 0; j >>= 1) {
+        const unsigned long long o = shfl_xor_u64(key, j);
+        key = ((lane & j) == 0) ? (key < o ? key : o) : (key > o ? key : o);
+    }
+    return key;
+}
+DEVI float wave_sum(float v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
 
 __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int e = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    const int e = blockIdx.x, tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6;
+    const int nwv = nt >> 6;
     const int H = a.H, A = a.A, K = a.K, T = a.T, N = a.N;
-    const int HA = H * A;
-    float* vals = sm;                         // [T]
-    float* EA = vals + rup(T, 4);             // [H][K][A]
-    float* sc = EA + (size_t)H * K * A;       // [K]
-    float* smean = sc + rup(K, 4);            // [HA]
-    float* sstd = smean + rup(HA, 4);         // [HA]
-    int* eidx = (int*)(sstd + rup(HA, 4));    // [K]
-    float* red = (float*)(eidx + rup(K, 4));  // [4]
-    int* jsel_p = (int*)(red + 2);
+    const int HA = H * A, HKA = H * K * A;
+    const int NL = (T + 63) / 64;                           // sorted lists of 64
+    unsigned long long* key = (unsigned long long*)sm;     // [NL*64]
+    float* EA = (float*)(key + (size_t)NL * 64);           // [H][K][A]
+    float* sc = EA + HKA;                                  // [64]
+    float* omean = sc + 64;                                // [HA] mean before the update
+    float* ostd = omean + rup(HA, 4);                      // [HA]
+    float* smean = ostd + rup(HA, 4);                      // [HA]
+    float* sstd = smean + rup(HA, 4);                      // [HA]
+    int* eidx = (int*)(sstd + rup(HA, 4));                 // [64]
+    float* red = (float*)(eidx + 64);                      // [32]
     float* gmean = a.mean + (size_t)e * a.Hmax * A;
     float* gstd = a.stdv + (size_t)e * a.Hmax * A;
+    const float* val = a.value + (size_t)e * T;
 
-    if (a.mode == 0) {
-        for (int i = tid; i < HA; i += nt) {
-            const int t = i / A, c = i % A;
-            float mv = 0.f;
-            if (a.warm && t < H - 1) mv = a.prev_mean[(size_t)e * H * A + (t + 1) * A + c];
-            smean[i] = mv; sstd[i] = 2.f;
-            gmean[i] = mv; gstd[i] = 2.f;
-        }
-    } else {
-        for (int i = tid; i < T; i += nt) vals[i] = a.value[(size_t)e * T + i];
-        __syncthreads();
-        // top-k by rank: rank_i = #{v_j > v_i} + #{j < i : v_j == v_i}; sorted descending like torch.topk.
-        for (int i = tid; i < T; i += nt) {
-            const float vi = vals[i];
-            int rank = 0;
-            for (int j = 0; j < T; ++j) {
-                const float vj = vals[j];
-                rank += (vj > vi) || (vj == vi && j < i);
-            }
-            if (rank < K) eidx[rank] = i;
-        }
-        __syncthreads();
-        for (int i = tid; i < H * K * A; i += nt) {
-            const int t = i / (K * A), k = (i / A) % K, c = i % A;
-            EA[i] = a.X[(size_t)t * a.x_stride + ((size_t)e * T + eidx[k]) * a.Kx + c];
-        }
-        if (tid < K) {
-            const float ev = vals[eidx[tid]], vmax = vals[eidx[0]];
-            sc[tid] = expf(fmul(a.temperature, ev - vmax));
-        }
-        __syncthreads();
-        if (tid == 0) {
-            float s = 0.f;
-            for (int k = 0; k < K; ++k) s += sc[k];
-            red[0] = s;
-        }
-        __syncthreads();
-        if (tid < K) sc[tid] = __fdiv_rn(sc[tid], red[0]);
-        __syncthreads();
-        if (tid == 0) {
-            float s = 0.f;
-            for (int k = 0; k < K; ++k) s += sc[k];
-            red[1] = fadd(s, 1e-9f);
-        }
-        __syncthreads();
-        const float den = red[1];
-        for (int i = tid; i < HA; i += nt) {
-            const int t = i / A, c = i % A;
-            const float* ea = EA + (size_t)t * K * A + c;
-            float s = 0.f;
-            for (int k = 0; k < K; ++k) s = fadd(s, fmul(sc[k], ea[(size_t)k * A]));
-            const float mu = __fdiv_rn(s, den);
-            float v = 0.f;
-            for (int k = 0; k < K; ++k) {
-                const float dd = ea[(size_t)k * A] - mu;
-                v = fadd(v, fmul(sc[k], fmul(dd, dd)));
-            }
-            float sd = sqrtf(__fdiv_rn(v, den));
-            sd = tclamp(sd, a.std_floor, 2.f);
-            const float nm = fadd(fmul(a.momentum, gmean[i]), fmul(a.omm, mu));
-            smean[i] = nm; sstd[i] = sd;
-            gmean[i] = nm; gstd[i] = sd;
-            if (a.mean_out) a.mean_out[((size_t)e * a.I + a.iter) * HA + i] = nm;
-            if (a.std_out) a.std_out[((size_t)e * a.I + a.iter) * HA + i] = sd;
-        }
-        if (a.mode == 2) {
-            for (int i = tid; i < H * K * A; i += nt) {
-                a.elite_ws[(size_t)e * H * K * A + i] = EA[i];
-                if (a.elite_out) a.elite_out[(size_t)e * H * K * A + i] = EA[i];
-            }
-            if (tid < K) {
-                a.score_ws[(size_t)e * K + tid] = sc[tid];
-                if (a.score_out) a.score_out[(size_t)e * K + tid] = sc[tid];
-            }
-        }
+    for (int i = tid; i < HA; i += nt) { omean[i] = gmean[i]; ostd[i] = gstd[i]; }
+    // ---- top-K (K <= 64): each wave sorts 64-key lists, then a merge tree keeps the best 64
+    for (int l = wave; l < NL; l += nwv) {
+        const int i = l * 64 + lane;
+        const unsigned long long k = i < T ? topk_key(val[i], i) : ~0ull;
+        key[(size_t)l * 64 + lane] = wave_sort64(k, lane);
     }
     __syncthreads();
-
-    if (a.mode != 2) {
-        // actions = clamp(mean + std * randn(H,N,A), -1, 1) for the next iteration's rollout rows
-        const int it = a.mode == 0 ? 0 : a.iter + 1;
-        const float* ep = a.eps + (size_t)e * a.eps_env + a.eps_cem_off + (size_t)it * a.eps_iter;
-        const int total = H * N * A;
-        for (int i = tid; i < total; i += nt) {
-            const int t = i / (N * A), n = (i / A) % N, c = i % A;
-            const int hc = t * A + c;
-            const float v = tclamp(fadd(smean[hc], fmul(sstd[hc], ep[i])), -1.f, 1.f);
-            a.X[(size_t)t * a.x_stride + ((size_t)e * T + n) * a.Kx + c] = v;
+    for (int stride = 1; stride < NL; stride <<= 1) {
+        for (int l = wave * 2 * stride; l < NL; l += nwv * 2 * stride) {
+            if (l + stride < NL) {
+                const unsigned long long x = key[(size_t)l * 64 + lane];
+                const unsigned long long y = key[(size_t)(l + stride) * 64 + 63 - lane];
+                key[(size_t)l * 64 + lane] = wave_clean64(x < y ? x : y, lane);
+            }
         }
-        return;
+        __syncthreads();
     }
-    // final pick: j = np.random.choice(K, p=score) -> cdf in float64 (numpy legacy), searchsorted right
+    if (tid < K) eidx[tid] = (int)(key[tid] & 0xffffffffu);
+    __syncthreads();
+    // ---- elite actions: rollout rows re-sampled exactly as the first-layer prologue did; pi rows from X_t
+    const float* ep = a.eps + (size_t)e * a.eps_env + a.eps_cem_off + (size_t)a.iter * a.eps_iter;
+    for (int base = 0; base < HKA; base += 8 * nt) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int idx = base + tid + u * nt;
+            if (idx < HKA) {
+                const int t = idx / (K * A), k = (idx / A) % K, c = idx % A;
+                const int i = eidx[k];
+                v[u] = i < N ? ep[((size_t)t * N + i) * A + c]
+                             : a.X[(size_t)t * a.x_stride + pidx((size_t)e * T + i, c, a.Kx)];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int idx = base + tid + u * nt;
+            if (idx < HKA) {
+                const int t = idx / (K * A), k = (idx / A) % K, c = idx % A;
+                EA[idx] = eidx[k] < N ? tclamp(fadd(omean[t * A + c], fmul(ostd[t * A + c], v[u])), -1.f, 1.f) : v[u];
+            }
+        }
+    }
+    // ---- softmax scores over the elites (one wave)
+    if (wave == 0) {
+        const float v0 = key_value(key[0]);
+        float s = 0.f;
+        if (lane < K) s = expf(fmul(a.temperature, key_value(key[lane]) - v0));
+        const float tot = wave_sum(s);
+        s = lane < K ? __fdiv_rn(s, tot) : 0.f;
+        if (lane < 64) sc[lane] = s;
+        const float tot2 = wave_sum(s);
+        if (lane == 0) red[0] = fadd(tot2, 1e-9f);
+    }
+    __syncthreads();
+    const float den = red[0];
+    for (int i = tid; i < HA; i += nt) {
+        const int t = i / A, c = i % A;
+        const float* ea = EA + (size_t)t * K * A + c;
+        float s = 0.f;
+        for (int k = 0; k < K; ++k) s = fadd(s, fmul(sc[k], ea[(size_t)k * A]));
+        const float mu = __fdiv_rn(s, den);
+        float v = 0.f;
+        for (int k = 0; k < K; ++k) {
+            const float dd = ea[(size_t)k * A] - mu;
+            v = fadd(v, fmul(sc[k], fmul(dd, dd)));
+        }
+        const float sd = tclamp(sqrtf(__fdiv_rn(v, den)), a.std_floor, 2.f);
+        const float nm = fadd(fmul(a.momentum, omean[i]), fmul(a.omm, mu));
+        smean[i] = nm; sstd[i] = sd;
+        gmean[i] = nm; gstd[i] = sd;
+        if (a.mean_out) a.mean_out[((size_t)e * a.I + a.iter) * HA + i] = nm;
+        if (a.std_out) a.std_out[((size_t)e * a.I + a.iter) * HA + i] = sd;
+    }
+    if (!a.final_iter) return;
+    if (a.elite_out)
+        for (int i = tid; i < HKA; i += nt) a.elite_out[(size_t)e * HKA + i] = EA[i];
+    if (a.score_out && tid < K) a.score_out[(size_t)e * K + tid] = sc[tid];
+    // estimate_value's reward.mean() of the last iteration: block reduction over the T rows
+    {
+        float s = 0.f;
+        for (int i = tid; i < T; i += nt) s += a.rlast[(size_t)e * T + i];
+        s = wave_sum(s);
+        if (lane == 0) red[1 + wave] = s;
+    }
+    __syncthreads();
+    // np.random.choice(K, p=score): float64 cdf of the float32 scores, cdf /= cdf[-1], searchsorted right
+    int* jsel = (int*)(red + 20);
     if (tid == 0) {
         double last = 0.0;
         for (int k = 0; k < K; ++k) last += (double)sc[k];
@@ -581,16 +806,16 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
             acc += (double)sc[k];
             if (acc / last > u) { j = k; break; }
         }
-        *jsel_p = j;
+        *jsel = j;
         float rs = 0.f;
-        for (int i = 0; i < T; ++i) rs += a.rlast[(size_t)e * T + i];
+        for (int w = 0; w < nwv; ++w) rs += red[1 + w];
         float cs = 0.f;
         for (int c = 0; c < A; ++c) cs += sstd[c];
-        a.metrics[(size_t)e * 2 + 0] = rs / (float)T;
-        a.metrics[(size_t)e * 2 + 1] = cs / (float)A;
+        a.metrics[(size_t)e * 2 + 0] = rs / (float)T;   // estimate_value's reward.mean() (last iteration)
+        a.metrics[(size_t)e * 2 + 1] = cs / (float)A;   // _std[0].mean()
     }
     __syncthreads();
-    const int j = *jsel_p;
+    const int j = *jsel;
     for (int c = tid; c < A; c += nt) {
         float v = EA[(size_t)j * A + c];
         if (!a.eval_mode) v = fadd(v, fmul(sstd[c], a.eps[(size_t)e * a.eps_env + a.eps_act_off + c]));
@@ -600,55 +825,81 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------ encoder
-// helper.enc, state modality: Linear(obs->E) ELU Linear(E->L) (helper.py:130-132). One wave per output
-// neuron; the workgroup then broadcasts z0 into X_0's latent columns for its slice of the env's T rows.
+// TOLD.h (helper.py:119-133) for one observation per workgroup. Weights are stored transposed ([in][out])
+// so output j's column is read coalesced; each output's dot product is split over several threads whose
+// partial sums meet in LDS, with the loads unrolled. Then the CEM mean/std initialisation
+// (tdmpc.py:122-125).
 struct EncArgs {
-    const float* obs; long obs_stride; int obs_dim, E, L, Lp, Kx, Ap, T, rows_per_blk;
-    const float* w1; const float* b1; const float* w2; const float* b2;
-    float* z0; float* X0;
+    const float* x; long x_stride; int xdim;    // state obs [B][obs_dim] or flat conv features
+    int E, L, Lp;
+    const float* w1t; const float* b1;          // null for pixels (x already the flat features)
+    const float* w2t; const float* b2;
+    float* z0;
+    float* mean; float* stdv; const float* prev_mean; int warm, H, A, Hmax;
 };
 
-__global__ void __launch_bounds__(256) encode_state_kernel(const EncArgs a) {
+// out[j] = sum_k wt[k*nout + j] * in[k] for j < nout, partial sums in part[] (nthr floats)
+DEVI void enc_matvec(const float* wt, const float* in, int nin, int nout, float* part, int tid, int nt) {
+    const int np = nt / nout > 0 ? nt / nout : 1;
+    const int j = tid % nout, p = tid / nout;
+    float s = 0.f;
+    if (p < np && j < nout) {
+#pragma unroll 8
+        for (int k = p; k < nin; k += np) s += wt[(size_t)k * nout + j] * in[k];
+    }
+    if (tid < np * nout) part[tid] = s;
+}
+
+__global__ void __launch_bounds__(1024) encode_kernel(const EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) float es[];
-    const int e = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-    float* x = es;                      // [obs_dim] or [flat]
-    float* hh = x + rup(a.obs_dim, 4);  // [E]
-    float* z = hh + rup(a.E, 4);        // [L]
-    const float* src = a.obs + (size_t)e * a.obs_stride;
-    for (int i = tid; i < a.obs_dim; i += blockDim.x) x[i] = src[i];
+    const int e = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    float* x = es;                       // [xdim]
+    float* hh = x + rup(a.xdim, 4);      // [E]
+    float* part = hh + rup(a.E, 4);      // [nt]
+    const float* src = a.x + (size_t)e * a.x_stride;
+    for (int i = tid; i < a.xdim; i += nt) x[i] = src[i];
     __syncthreads();
-    if (a.w1) {
-        for (int j = wave; j < a.E; j += nw) {
-            const float* wr = a.w1 + (size_t)j * a.obs_dim;
+    const float* hin = x;
+    int E = a.xdim;
+    if (a.w1t) {
+        enc_matvec(a.w1t, x, a.xdim, a.E, part, tid, nt);  // E <= 1024 (check_dims)
+        __syncthreads();
+        if (tid < a.E) {
+            const int np = nt / a.E > 0 ? nt / a.E : 1;
             float s = 0.f;
-            for (int k = lane; k < a.obs_dim; k += 64) s += wr[k] * x[k];
-            for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-            if (lane == 0) hh[j] = elu1(s + a.b1[j]);
+            for (int p = 0; p < np; ++p) s += part[p * a.E + tid];
+            hh[tid] = elu1(s + a.b1[tid]);
         }
         __syncthreads();
-    } else {
-        for (int i = tid; i < a.E; i += blockDim.x) hh[i] = x[i];  // pixel path: flat conv features
-        __syncthreads();
+        hin = hh;
+        E = a.E;
     }
-    for (int j = wave; j < a.L; j += nw) {
-        const float* wr = a.w2 + (size_t)j * a.E;
-        float s = 0.f;
-        for (int k = lane; k < a.E; k += 64) s += wr[k] * hh[k];
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-        if (lane == 0) z[j] = s + a.b2[j];
-    }
+    enc_matvec(a.w2t, hin, E, a.L, part, tid, nt);
     __syncthreads();
-    if (blockIdx.y == 0)
-        for (int i = tid; i < a.L; i += blockDim.x) a.z0[(size_t)e * a.Lp + i] = z[i];
-    const int r0 = blockIdx.y * a.rows_per_blk, r1 = min(r0 + a.rows_per_blk, a.T);
-    for (int i = tid; i < (r1 - r0) * a.L; i += blockDim.x) {
-        const int rr = r0 + i / a.L, c = i % a.L;
-        a.X0[((size_t)e * a.T + rr) * a.Kx + a.Ap + c] = z[c];
+    for (int l = tid; l < a.Lp; l += nt) {
+        float z = 0.f;
+        if (l < a.L) {
+            const int np = nt / a.L > 0 ? nt / a.L : 1;
+            float s = 0.f;
+            for (int p = 0; p < np; ++p) s += part[p * a.L + l];
+            z = s + a.b2[l];
+        }
+        a.z0[(size_t)e * a.Lp + l] = z;
+    }
+    if (a.mean) {
+        const int HA = a.H * a.A;
+        for (int i = tid; i < HA; i += nt) {
+            const int t = i / a.A;
+            float mv = 0.f;
+            if (a.warm && t < a.H - 1) mv = a.prev_mean[(size_t)e * HA + i + a.A];  // mean[:-1] = prev[1:]
+            a.mean[(size_t)e * a.Hmax * a.A + i] = mv;
+            a.stdv[(size_t)e * a.Hmax * a.A + i] = 2.f;
+        }
     }
 }
 
-// Direct 2-D convolution, stride 2, no padding, ReLU; input optionally uint8 scaled by 1/255
-// (NormalizeImg, helper.py:99-106, then nn.Conv2d + nn.ReLU, helper.py:123-127).
+// Direct 2-D convolution, stride 2, no padding, + ReLU; uint8 input scaled by 1/255 (NormalizeImg,
+// helper.py:99-106; conv stack helper.py:123-127).
 __global__ void __launch_bounds__(256) conv_relu_kernel(const void* in, int in_u8, long in_bstride, int cin,
                                                         int hin, float* out, long out_bstride, int cout,
                                                         int hout, int ks, const float* w, const float* b) {
@@ -673,87 +924,130 @@ __global__ void __launch_bounds__(256) conv_relu_kernel(const void* in, int in_u
     out[(size_t)e * out_bstride + idx] = fmaxf(s + b[co], 0.f);
 }
 
-// Actions [B][H][T][A] -> X_t a-columns (tdmpc_estimate_value entry).
-__global__ void scatter_actions_kernel(const float* act, float* X, size_t x_stride, int H, int T, int A, int Kx,
-                                       int B) {
-    const size_t total = (size_t)B * H * T * A;
+// ------------------------------------------------------------------------------------------------ packing
+// dst panel (total `dcols` columns): element (r, dc0 + c) = src[r * sld + sc0 + c], r < rows, c < cols
+__global__ void pack_panel_kernel(const float* src, int sld, int sc0, int rows, int cols, float* dst, int dcols,
+                                  int dc0) {
+    const size_t total = (size_t)rows * cols;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const int c = i % A;
-        const size_t r = (i / A) % T;
-        const int t = (i / ((size_t)A * T)) % H;
-        const size_t e = i / ((size_t)A * T * H);
-        X[(size_t)t * x_stride + (e * T + r) * Kx + c] = act[i];
+        const size_t r = i / cols, c = i % cols;
+        dst[pidx(r, dc0 + c, dcols)] = src[r * sld + sc0 + c];
     }
 }
 
-__global__ void bcast_z_kernel(const float* z0, int L, float* X0, int Kx, int Ap, int T, int B) {
-    const size_t total = (size_t)B * T * L;
+// dst[c * rows + r] = src[r * cols + c]
+__global__ void pack_transpose_kernel(const float* src, int rows, int cols, float* dst) {
+    const size_t total = (size_t)rows * cols;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = i / L;
-        X0[r * Kx + Ap + i % L] = z0[(r / T) * L + i % L];
+        const size_t r = i / cols, c = i % cols;
+        dst[c * rows + r] = src[i];
+    }
+}
+
+// Candidate actions [B][H][T][A] -> X_t panels' action columns (zero pad to Ap) (estimate_value entry).
+__global__ void scatter_actions_kernel(const float* act, float* X, size_t x_stride, int H, int T, int A, int Ap,
+                                       int Kx, int B) {
+    const size_t total = (size_t)B * H * T * Ap;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int c = i % Ap;
+        const size_t r = (i / Ap) % T;
+        const int t = (i / ((size_t)Ap * T)) % H;
+        const size_t e = i / ((size_t)Ap * T * H);
+        const float v = c < A ? act[((e * H + t) * T + r) * A + c] : 0.f;
+        X[(size_t)t * x_stride + pidx(e * T + r, c, Kx)] = v;
     }
 }
 
 __global__ void gather_z_kernel(const float* X, int Kx, int Ap, int L, int rows, float* out) {
     const size_t total = (size_t)rows * L;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x)
-        out[i] = X[(i / L) * Kx + Ap + i % L];
+        out[i] = X[pidx(i / L, Ap + i % L, Kx)];
 }
 
 // ------------------------------------------------------------------------------------------------ host side
-#define HIPCHK(x)                                                                          \
-    do {                                                                                   \
-        hipError_t e_ = (x);                                                               \
-        if (e_ != hipSuccess) {                                                            \
+#define HIPCHK(x)                                                                                 \
+    do {                                                                                          \
+        hipError_t e_ = (x);                                                                      \
+        if (e_ != hipSuccess) {                                                                   \
             snprintf(g_err, sizeof g_err, "%s:%d %s", __FILE__, __LINE__, hipGetErrorString(e_)); \
-            return TDMPC_E_HIP;                                                            \
-        }                                                                                  \
+            return TDMPC_E_HIP;                                                                   \
+        }                                                                                         \
     } while (0)
 
-template <int WN, int PRO, int KCH>
+template <int TM, int TN, int WGM, int WGN, int PRO, int KCH, bool ROLL>
 int set_lds_attr() {
-    HIPCHK(hipFuncSetAttribute((const void*)linear_kernel<WN, PRO, KCH>,
+    HIPCHK(hipFuncSetAttribute((const void*)linear_kernel<TM, TN, WGM, WGN, PRO, KCH, ROLL>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     return 0;
 }
+
+#define FOR_EACH_LINEAR(X)                                                                          \
+    X(1, 1, 1, 1, 0, 32, false) X(1, 1, 1, 1, 0, 64, false) X(1, 1, 1, 1, 0, 128, false)              \
+    X(1, 2, 1, 1, 0, 32, false) X(1, 2, 1, 1, 0, 64, false) X(1, 2, 1, 1, 0, 128, false)              \
+    X(1, 1, 1, 1, 1, 32, false) X(1, 1, 1, 1, 1, 64, false) X(1, 1, 1, 1, 1, 128, false)              \
+    X(1, 2, 1, 1, 1, 32, false) X(1, 2, 1, 1, 1, 64, false) X(1, 2, 1, 1, 1, 128, false)              \
+    X(2, 2, 2, 2, 0, 8, true) X(2, 2, 2, 2, 1, 8, true)
 
 int init_attrs() {
     static int done = 0;
     if (done) return 0;
     int rc = 0;
-    rc |= set_lds_attr<1, 0, 32>(); rc |= set_lds_attr<1, 0, 64>(); rc |= set_lds_attr<1, 0, 128>();
-    rc |= set_lds_attr<2, 0, 32>(); rc |= set_lds_attr<2, 0, 64>(); rc |= set_lds_attr<2, 0, 128>();
-    rc |= set_lds_attr<1, 1, 32>(); rc |= set_lds_attr<1, 1, 64>(); rc |= set_lds_attr<1, 1, 128>();
-    rc |= set_lds_attr<2, 1, 32>(); rc |= set_lds_attr<2, 1, 64>(); rc |= set_lds_attr<2, 1, 128>();
+#define SET_ATTR(TM, TN, WGM, WGN, PRO, KCH, ROLL) rc |= set_lds_attr<TM, TN, WGM, WGN, PRO, KCH, ROLL>();
+    FOR_EACH_LINEAR(SET_ATTR)
+#undef SET_ATTR
     HIPCHK(hipFuncSetAttribute((const void*)cem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (rc) return TDMPC_E_HIP;
     done = 1;
     return 0;
 }
 
-// Diagnostic kernel timer (tdmpc_profile_*): when armed on this thread, every linear_kernel launch whose
-// (WN, PRO, KCH) instance matches is bracketed by HIP events on its stream, and its algorithmic FLOPs
-// (2*M*N*K per problem) are recorded. Used by bench.py for the live roofline of the dominant kernel.
+// Diagnostic kernel timer (tdmpc_profile_*): when armed on this thread, every linear_kernel launch of the
+// selected configuration (cfg id: 1 = latency 32x32 tile, 2 = latency 32x64 tile, 3 = throughput 128x128
+// tile; 0 = any) with K == N == kdim (if kdim > 0) is bracketed by HIP events on its stream, and its
+// algorithmic FLOPs (2*M*N*K per problem) are recorded. bench.py uses it for the dominant kernel's roofline.
 struct Profiler {
-    int armed = 0, wn = 0, pro = 0, kch = 0, n = 0, cap = 0, kdim = 0;
+    int armed = 0, cfg = 0, pro = -1, n = 0, cap = 0, kdim = 0;
     hipEvent_t* ev = nullptr;
     double flops = 0.0;
 };
 thread_local Profiler g_prof;
 
-template <int WN, int PRO, int KCH>
-int launch_lin_t(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
-    const int nw = (a.K + KCH - 1) / KCH;
+// Launch geometry chosen for a linear layer.
+struct LinCfg {
+    int id;      // 1 = LAT1 (32x32, K split), 2 = LAT2 (32x64, K split), 3 = THR (128x128, full K)
+    int C;       // workgroup tile columns
+    int bw;      // row-reduction block width (64 or 32)
+};
+
+int thr_rows() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("TDMPC_THR_ROWS");
+        v = e ? atoi(e) : 2048;
+    }
+    return v;
+}
+
+LinCfg pick_cfg(int M, int nmax, int K, int wn_hint) {
+    if (M >= thr_rows() && nmax >= 256 && K >= 64) return LinCfg{3, 128, 64};
+    if (wn_hint == 2) return LinCfg{2, 64, 64};
+    return LinCfg{1, 32, 32};
+}
+
+template <int TM, int TN, int WGM, int WGN, int PRO, int KCH, bool ROLL>
+int launch_lin_t(const LinArgs& a, int nprob, int nmax, int cfg_id, hipStream_t s) {
+    constexpr int R = 32 * TM * WGM, C = 32 * TN * WGN;
+    const int KS = ROLL ? 1 : (a.K + KCH - 1) / KCH;
     LinArgs b = a;
-    b.kch = KCH;
-    dim3 grid((a.M + 31) / 32, (nmax + 32 * WN - 1) / (32 * WN), nprob);
-    dim3 block(64 * nw);
-    const size_t lds = (size_t)nw * 32 * (32 * WN + 4) * 4;
+    b.kch = ROLL ? a.K : KCH;
+    dim3 grid((a.M + R - 1) / R, (nmax + C - 1) / C, nprob);
+    dim3 block(64 * WGM * WGN * KS);
+    const size_t lds = ((size_t)KS * R * (C + 4) + 2 * C + (size_t)R * std::max(a.rpart_nt, 1)) * 4;
     Profiler& pf = g_prof;
-    const bool prof = pf.armed && pf.wn == WN && pf.pro == PRO && pf.kch == KCH && pf.n + 2 <= pf.cap &&
-                      (pf.kdim == 0 || (a.K == pf.kdim && nmax == pf.kdim));
+    const bool prof = pf.armed && (pf.cfg == 0 || pf.cfg == cfg_id) && (pf.pro < 0 || pf.pro == PRO) &&
+                      pf.n + 2 <= pf.cap && (pf.kdim == 0 || (a.K == pf.kdim && nmax == pf.kdim));
     if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], s));
-    hipLaunchKernelGGL((linear_kernel<WN, PRO, KCH>), grid, block, lds, s, b);
+    hipLaunchKernelGGL((linear_kernel<TM, TN, WGM, WGN, PRO, KCH, ROLL>), grid, block, lds, s, b);
     HIPCHK(hipGetLastError());
     if (prof) {
         HIPCHK(hipEventRecord(pf.ev[pf.n + 1], s));
@@ -763,15 +1057,22 @@ int launch_lin_t(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
     return 0;
 }
 
-// Picks the per-wave K chunk so that a workgroup has at most 8 waves (16 for very wide K).
-int launch_lin(const LinArgs& a, int nprob, int nmax, int wn, int pro, hipStream_t s) {
+// Launch one fused linear layer with the configuration pick_cfg selects.
+int launch_lin(const LinArgs& a, int nprob, int nmax, int wn_hint, int pro, hipStream_t s) {
     if (a.M <= 0) return 0;
+    if (a.K % 8) { snprintf(g_err, sizeof g_err, "bad K %d", a.K); return TDMPC_E_DIMS; }
+    const LinCfg cfg = pick_cfg(a.M, nmax, a.K, wn_hint);
+    if (cfg.id == 3) {
+        if (pro == PRO_PLAIN) return launch_lin_t<2, 2, 2, 2, 0, 8, true>(a, nprob, nmax, 3, s);
+        return launch_lin_t<2, 2, 2, 2, 1, 8, true>(a, nprob, nmax, 3, s);
+    }
     int kch = 32;
     if ((a.K + 31) / 32 > 8) kch = 64;
     if ((a.K + 63) / 64 > 8) kch = 128;
-    if ((a.K + kch - 1) / kch > 8 || a.K % 8) { snprintf(g_err, sizeof g_err, "bad K %d", a.K); return TDMPC_E_DIMS; }
-#define DISPATCH(WN_, PRO_, KCH_) \
-    if (wn == WN_ && pro == PRO_ && kch == KCH_) return launch_lin_t<WN_, PRO_, KCH_>(a, nprob, nmax, s);
+    if ((a.K + kch - 1) / kch > 8) { snprintf(g_err, sizeof g_err, "bad K %d", a.K); return TDMPC_E_DIMS; }
+    const int tn = cfg.id == 2 ? 2 : 1;
+#define DISPATCH(TN_, PRO_, KCH_) \
+    if (tn == TN_ && pro == PRO_ && kch == KCH_) return launch_lin_t<1, TN_, 1, 1, PRO_, KCH_, false>(a, nprob, nmax, cfg.id, s);
     DISPATCH(1, 0, 32) DISPATCH(1, 0, 64) DISPATCH(1, 0, 128)
     DISPATCH(2, 0, 32) DISPATCH(2, 0, 64) DISPATCH(2, 0, 128)
     DISPATCH(1, 1, 32) DISPATCH(1, 1, 64) DISPATCH(1, 1, 128)
@@ -780,8 +1081,14 @@ int launch_lin(const LinArgs& a, int nprob, int nmax, int wn, int pro, hipStream
     return TDMPC_E_DIMS;
 }
 
-LinProb prob0() { LinProb p; memset(&p, 0, sizeof p); return p; }
-LinArgs args0() { LinArgs a; memset(&a, 0, sizeof a); a.amap = {1 << 30, 0, 0}; a.cmap = {1 << 30, 0, 0}; return a; }
+LinArgs args0() {
+    LinArgs a;
+    memset(&a, 0, sizeof a);
+    a.amap = {1 << 30, 0, 0};
+    a.cmap = {1 << 30, 0, 0};
+    a.rows_per_env = 1 << 30;
+    return a;
+}
 
 // The planner's per-call context.
 struct Ctx {
@@ -791,38 +1098,56 @@ struct Ctx {
 };
 
 float* Xt(const Ctx& c, int t) { return c.k.X + (size_t)t * c.k.x_stride; }
+Opnd xop(const Ctx& c, int t, int q0) { return Opnd{Xt(c, t), (long)c.Kx * 32, q0}; }
+Outp xout(const Ctx& c, int t, int q0) { return Outp{Xt(c, t), (long)c.Kx * 32, q0}; }
+Opnd hop(const float* H, const Ctx& c, int q0) { return Opnd{H, (long)2 * c.M * 32, q0}; }
+Outp hout(float* H, const Ctx& c, int q0) { return Outp{H, (long)2 * c.M * 32, q0}; }
+Opnd wop(const Ctx& c, size_t off, int K) { return Opnd{c.pw + off, (long)K * 32, 0}; }
 
-// One TOLD.next step for `rows` logical rows mapped onto X rows (tdmpc.py:34-37 + the G update of :88-90).
-int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last) {
+struct Sampling {  // CEM candidate sampling in the first-layer prologue
+    int on; const float* eps; int iter;
+};
+
+// One TOLD.next step (tdmpc.py:34-37) for `rows` logical rows mapped onto X rows, plus the return update
+// of estimate_value (:88-90). t == 0 reads z0 for every row; `smp` samples the rollout rows' actions.
+int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, Sampling smp) {
     const Layout& w = c.w;
-    const float* pw = c.pw;
+    const int M = c.M;
     int rc;
     {   // h1 = ELU(W1[d;r] [a|z] + b)   (dynamics.0 and reward.0 fused: N = 2M)
         LinArgs a = args0();
         a.M = rows; a.K = c.Kx; a.a_mapped = 1; a.amap = map;
+        a.apq = w.Ap / 4; a.rows_per_env = c.T;
+        a.zmode = t == 0; a.z0 = c.k.z0; a.Lp = w.Lp;
+        if (smp.on) {
+            a.smode = 1; a.mean_t = c.k.mean + t * c.A; a.std_t = c.k.stdv + t * c.A; a.mstride = c.d->max_horizon * c.A;
+            a.seps = smp.eps; a.seps_env = c.eps_env; a.s_rows = c.N;
+            a.seps_off = c.eps_cem_off + (long)smp.iter * c.eps_iter + (long)t * c.N * c.A; a.A = c.A;
+        }
         LinProb& p = a.p[0];
-        p.A = Xt(c, t); p.lda = c.Kx; p.W = pw + w.w1x; p.ldw = c.Kx; p.bias = pw + w.b1x;
-        p.C = c.k.H1; p.ldc = 2 * c.M; p.N = 2 * c.M; p.epi = EPI_ELU;
-        if ((rc = launch_lin(a, 1, 2 * c.M, 2, PRO_PLAIN, c.s))) return rc;
+        p.A = xop(c, t, 0); p.W = wop(c, w.w1x, c.Kx); p.bias = c.pw + w.b1x;
+        p.C = hout(c.k.H1, c, 0); p.N = p.nvalid = p.nstore = 2 * M; p.epi = EPI_ELU;
+        if ((rc = launch_lin(a, 1, 2 * M, 2, PRO_PLAIN, c.s))) return rc;
     }
     {   // h2_d = ELU(W2d h1_d + b); reward partial dots of ELU(W2r h1_r + b) with reward.4.weight
         LinArgs a = args0();
-        a.M = rows; a.K = c.M;
+        a.M = rows; a.K = M;
         LinProb& p0 = a.p[0];
-        p0.A = c.k.H1; p0.lda = 2 * c.M; p0.W = pw + w.w2d; p0.ldw = c.M; p0.bias = pw + w.b2d;
-        p0.C = c.k.H2; p0.ldc = 2 * c.M; p0.N = c.M; p0.epi = EPI_ELU;
+        p0.A = hop(c.k.H1, c, 0); p0.W = wop(c, w.w2d, M); p0.bias = c.pw + w.b2d;
+        p0.C = hout(c.k.H2, c, 0); p0.N = p0.nvalid = p0.nstore = M; p0.epi = EPI_ELU;
         LinProb& p1 = a.p[1];
-        p1.A = c.k.H1 + c.M; p1.lda = 2 * c.M; p1.W = pw + w.w2r; p1.ldw = c.M; p1.bias = pw + w.b2r;
-        p1.N = c.M; p1.epi = EPI_ELU_DOT; p1.dotw = pw + w.w3r; p1.dot_out = c.k.rpart; p1.dot_ld = c.M / 32;
-        if ((rc = launch_lin(a, 2, c.M, 1, PRO_PLAIN, c.s))) return rc;
+        p1.A = hop(c.k.H1, c, M / 4); p1.W = wop(c, w.w2r, M); p1.bias = c.pw + w.b2r;
+        p1.N = p1.nvalid = M; p1.nstore = 0; p1.epi = EPI_ELU_DOT;
+        p1.dotw = c.pw + w.w3r; p1.dot_out = c.k.rpart; p1.dot_ld = M / pick_cfg(rows, M, M, 1).bw;
+        if ((rc = launch_lin(a, 2, M, 1, PRO_PLAIN, c.s))) return rc;
     }
     {   // z' = W3d h2_d + b -> X_{t+1} latent columns; reward = sum(partials) + b; G update
         LinArgs a = args0();
-        a.M = rows; a.K = c.M; a.c_mapped = 1; a.cmap = map;
+        a.M = rows; a.K = M; a.c_mapped = 1; a.cmap = map;
         LinProb& p = a.p[0];
-        p.A = c.k.H2; p.lda = 2 * c.M; p.W = pw + w.w3d; p.ldw = c.M; p.bias = pw + w.b3d;
-        p.C = Xt(c, t + 1) + w.Ap; p.ldc = c.Kx; p.N = w.L; p.epi = EPI_LIN_Z;
-        a.rpart = c.k.rpart; a.rpart_nt = c.M / 32; a.b3r = pw + w.b3r;
+        p.A = hop(c.k.H2, c, 0); p.W = wop(c, w.w3d, M); p.bias = c.pw + w.b3d;
+        p.C = xout(c, t + 1, w.Ap / 4); p.N = w.L; p.nvalid = w.L; p.nstore = w.Lp; p.epi = EPI_LIN_Z;
+        a.rpart = c.k.rpart; a.rpart_nt = M / pick_cfg(rows, M, M, 1).bw; a.b3r = c.pw + w.b3r;
         a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
         if ((rc = launch_lin(a, 1, w.L, 1, PRO_PLAIN, c.s))) return rc;
     }
@@ -833,30 +1158,31 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
 int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps_env, int eps_G, long eps_off,
            float min_std) {
     const Layout& w = c.w;
-    const float* pw = c.pw;
+    const int M = c.M;
     int rc;
     {
         LinArgs a = args0();
         a.M = rows; a.K = w.Lp; a.a_mapped = 1; a.amap = map;
+        a.apq = w.Ap / 4; a.rows_per_env = c.T; a.zmode = t == 0; a.z0 = c.k.z0; a.Lp = w.Lp;
         LinProb& p = a.p[0];
-        p.A = Xt(c, t) + w.Ap; p.lda = c.Kx; p.W = pw + w.wp1; p.ldw = w.Lp; p.bias = pw + w.bp1;
-        p.C = c.k.H1; p.ldc = 2 * c.M; p.N = c.M; p.epi = EPI_ELU;
-        if ((rc = launch_lin(a, 1, c.M, 2, PRO_PLAIN, c.s))) return rc;
+        p.A = xop(c, t, w.Ap / 4); p.W = wop(c, w.wp1, w.Lp); p.bias = c.pw + w.bp1;
+        p.C = hout(c.k.H1, c, 0); p.N = p.nvalid = p.nstore = M; p.epi = EPI_ELU;
+        if ((rc = launch_lin(a, 1, M, 2, PRO_PLAIN, c.s))) return rc;
     }
     {
         LinArgs a = args0();
-        a.M = rows; a.K = c.M;
+        a.M = rows; a.K = M;
         LinProb& p = a.p[0];
-        p.A = c.k.H1; p.lda = 2 * c.M; p.W = pw + w.wp2; p.ldw = c.M; p.bias = pw + w.bp2;
-        p.C = c.k.H2; p.ldc = 2 * c.M; p.N = c.M; p.epi = EPI_ELU;
-        if ((rc = launch_lin(a, 1, c.M, 1, PRO_PLAIN, c.s))) return rc;
+        p.A = hop(c.k.H1, c, 0); p.W = wop(c, w.wp2, M); p.bias = c.pw + w.bp2;
+        p.C = hout(c.k.H2, c, 0); p.N = p.nvalid = p.nstore = M; p.epi = EPI_ELU;
+        if ((rc = launch_lin(a, 1, M, 1, PRO_PLAIN, c.s))) return rc;
     }
     {
         LinArgs a = args0();
-        a.M = rows; a.K = c.M; a.c_mapped = 1; a.cmap = map;
+        a.M = rows; a.K = M; a.c_mapped = 1; a.cmap = map;
         LinProb& p = a.p[0];
-        p.A = c.k.H2; p.lda = 2 * c.M; p.W = pw + w.wp3; p.ldw = c.M; p.bias = pw + w.bp3;
-        p.C = Xt(c, t); p.ldc = c.Kx; p.N = w.A; p.epi = EPI_PI;
+        p.A = hop(c.k.H2, c, 0); p.W = wop(c, w.wp3, M); p.bias = c.pw + w.bp3;
+        p.C = xout(c, t, 0); p.N = w.A; p.nvalid = w.A; p.nstore = w.Ap; p.epi = EPI_PI;
         a.eps = eps; a.eps_G = eps_G; a.eps_env = eps_env; a.eps_off = eps_off; a.A = w.A;
         a.min_std = min_std;
         a.lo = (float)(-1.0 + 1e-6); a.hi = (float)(1.0 - 1e-6);
@@ -867,56 +1193,55 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
 // Terminal value: Q(z_H, pi(z_H)) for all T rows of every env (tdmpc.py:91-92).
 int terminal_q(const Ctx& c, float discH, float* value_out, int I, int iter) {
     const Layout& w = c.w;
-    const float* pw = c.pw;
-    const int rows = c.B * c.T;
+    const int rows = c.B * c.T, M = c.M;
     int rc;
     {   // y1 = Wq1[Q1;Q2] [a|z] + b, with LayerNorm partial moments per 64 columns
         LinArgs a = args0();
         a.M = rows; a.K = c.Kx;
         LinProb& p = a.p[0];
-        p.A = Xt(c, c.H); p.lda = c.Kx; p.W = pw + w.wq1x; p.ldw = c.Kx; p.bias = pw + w.bq1x;
-        p.C = c.k.H1; p.ldc = 2 * c.M; p.N = 2 * c.M; p.epi = EPI_LNSTATS;
-        p.st_out = c.k.st1; p.st_ld = 2 * c.M / 64;
-        if ((rc = launch_lin(a, 1, 2 * c.M, 2, PRO_PLAIN, c.s))) return rc;
+        p.A = xop(c, c.H, 0); p.W = wop(c, w.wq1x, c.Kx); p.bias = c.pw + w.bq1x;
+        p.C = hout(c.k.H1, c, 0); p.N = p.nvalid = p.nstore = 2 * M; p.epi = EPI_LNSTATS;
+        p.st_out = c.k.st1; p.st_ld = 2 * M / 64;
+        if ((rc = launch_lin(a, 1, 2 * M, 2, PRO_PLAIN, c.s))) return rc;
     }
     {   // y2_p = Wq2_p tanh(LN(y1_p)) + b, moments again
         LinArgs a = args0();
-        a.M = rows; a.K = c.M;
+        a.M = rows; a.K = M;
         for (int q = 0; q < 2; ++q) {
             LinProb& p = a.p[q];
-            p.A = c.k.H1 + q * c.M; p.lda = 2 * c.M; p.W = pw + w.wq2 + (size_t)q * c.M * c.M; p.ldw = c.M;
-            p.bias = pw + w.bq2 + q * c.M; p.C = c.k.H2 + q * c.M; p.ldc = 2 * c.M; p.N = c.M;
-            p.epi = EPI_LNSTATS; p.st_out = c.k.st2 + q * (c.M / 64); p.st_ld = 2 * c.M / 64;
-            p.ln_stats = c.k.st1; p.ln_ld = 2 * c.M / 64; p.ln_t0 = q * (c.M / 64); p.ln_nt = c.M / 64;
-            p.ln_g = pw + w.g1 + q * c.M; p.ln_b = pw + w.be1 + q * c.M;
+            p.A = hop(c.k.H1, c, q * M / 4); p.W = wop(c, w.wq2 + (size_t)q * M * M, M);
+            p.bias = c.pw + w.bq2 + q * M; p.C = hout(c.k.H2, c, q * M / 4); p.N = p.nvalid = p.nstore = M;
+            p.epi = EPI_LNSTATS; p.st_out = c.k.st2 + q * (M / 64); p.st_ld = 2 * M / 64;
+            p.ln_stats = c.k.st1; p.ln_ld = 2 * M / 64; p.ln_t0 = q * (M / 64); p.ln_nt = M / 64;
+            p.ln_g = c.pw + w.g1 + q * M; p.ln_b = c.pw + w.be1 + q * M;
         }
-        if ((rc = launch_lin(a, 2, c.M, 2, PRO_LN_TANH, c.s))) return rc;
+        if ((rc = launch_lin(a, 2, M, 2, PRO_LN_TANH, c.s))) return rc;
     }
     {
         ValueArgs v;
-        v.Y = c.k.H2; v.ldy = 2 * c.M; v.st = c.k.st2; v.st_ld = 2 * c.M / 64; v.M_ = c.M;
-        v.g2 = pw + w.g2; v.be2 = pw + w.be2; v.w3 = pw + w.wq3; v.b3 = pw + w.bq3;
+        v.Y = c.k.H2; v.yts = (long)2 * M * 32; v.st = c.k.st2; v.st_ld = 2 * M / 64; v.M_ = M;
+        v.g2 = c.pw + w.g2; v.be2 = c.pw + w.be2; v.w3 = c.pw + w.wq3; v.b3 = c.pw + w.bq3;
         v.G = c.k.G; v.disc = discH; v.value = c.k.value; v.value_out = value_out; v.rows = rows;
         v.T = c.T; v.I = I; v.iter = iter;
-        hipLaunchKernelGGL(value_kernel, dim3((rows + 3) / 4), dim3(256), 0, c.s, v);
+        hipLaunchKernelGGL(value_kernel, dim3((rows + 31) / 32), dim3(512), 0, c.s, v);
         HIPCHK(hipGetLastError());
     }
     return 0;
 }
 
-int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, float* z0_out, int T, float* X0) {
+// TOLD.h for `batch` observations -> z0 [B][Lp]; optionally initialises the CEM mean/std.
+int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, const float* prev_mean, int warm) {
     const Layout& w = c.w;
     const float* pw = c.pw;
     EncArgs a;
     memset(&a, 0, sizeof a);
-    a.L = w.L; a.Lp = w.Lp; a.Kx = w.Kx; a.Ap = w.Ap; a.T = T;
-    a.z0 = z0_out; a.X0 = X0;
+    a.L = w.L; a.Lp = w.Lp; a.z0 = c.k.z0;
     if (w.modality == 0) {
-        a.obs = (const float*)obs; a.obs_dim = w.obs_dim; a.obs_stride = w.obs_dim; a.E = w.E;
-        a.w1 = pw + w.enc_w1; a.b1 = pw + w.enc_b1; a.w2 = pw + w.enc_w2; a.b2 = pw + w.enc_b2;
+        a.x = (const float*)obs; a.x_stride = w.obs_dim; a.xdim = w.obs_dim; a.E = w.E;
+        a.w1t = pw + w.enc_w1t; a.b1 = pw + w.enc_b1; a.w2t = pw + w.enc_w2t; a.b2 = pw + w.enc_b2;
     } else {
         static const int ks[4] = {7, 5, 3, 3};
-        const size_t act = pixel_act_floats(w) / 2;
+        const size_t act = pixel_act_floats(w);
         float* bufs[2] = {c.k.enc_tmp, c.k.enc_tmp + (size_t)batch * act};
         const void* in = obs;
         int in_u8 = obs_is_u8;
@@ -931,15 +1256,15 @@ int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, float* z0_ou
             HIPCHK(hipGetLastError());
             in = out; in_u8 = 0; in_bs = (long)act; cin = w.nch;
         }
-        a.obs = (const float*)in; a.obs_dim = w.flat; a.obs_stride = (long)act;
-        a.E = w.flat; a.w1 = nullptr; a.w2 = pw + w.pl_w; a.b2 = pw + w.pl_b;
+        a.x = (const float*)in; a.x_stride = (long)act; a.xdim = w.flat;
+        a.E = w.flat; a.w1t = nullptr; a.w2t = pw + w.pl_wt; a.b2 = pw + w.pl_b;
     }
-    const int rpb = 64;
-    a.rows_per_blk = rpb;
-    const int chunks = X0 ? (T + rpb - 1) / rpb : 1;
-    if (!X0) a.T = 0;
-    const size_t lds = (rup(a.obs_dim, 4) + rup(a.E, 4) + rup(a.L, 4)) * 4;
-    hipLaunchKernelGGL(encode_state_kernel, dim3(batch, chunks), dim3(256), lds, c.s, a);
+    if (prev_mean) {
+        a.mean = c.k.mean; a.stdv = c.k.stdv; a.prev_mean = prev_mean; a.warm = warm;
+        a.H = c.H; a.A = c.A; a.Hmax = c.d->max_horizon;
+    }
+    const size_t lds = (rup(a.xdim, 4) + rup(std::max(a.E, 1), 4) + 1024) * 4;
+    hipLaunchKernelGGL(encode_kernel, dim3(batch), dim3(1024), lds, c.s, a);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -967,6 +1292,21 @@ int setup_ctx(Ctx& c, const tdmpc_dims* d, const void* packed, void* ws, size_t 
         return TDMPC_E_DIMS;
     }
     return init_attrs();
+}
+
+int launch_pack_panel(const float* src, int sld, int sc0, int rows, int cols, float* dst, int dcols, int dc0,
+                      hipStream_t s) {
+    hipLaunchKernelGGL(pack_panel_kernel, dim3(std::min(1024, (rows * cols + 255) / 256)), dim3(256), 0, s, src, sld,
+                       sc0, rows, cols, dst, dcols, dc0);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int launch_transpose(const float* src, int rows, int cols, float* dst, hipStream_t s) {
+    hipLaunchKernelGGL(pack_transpose_kernel, dim3(std::min(1024, (rows * cols + 255) / 256)), dim3(256), 0, s, src,
+                       rows, cols, dst);
+    HIPCHK(hipGetLastError());
+    return 0;
 }
 
 }  // namespace
@@ -1011,21 +1351,22 @@ int tdmpc_pack_weights(const tdmpc_dims* d, const float* const* t, int32_t n, vo
     if (n != tdmpc_num_param_tensors(d)) return TDMPC_E_DIMS;
     if (bytes < w.total * 4) return TDMPC_E_SIZE;
     if (init_attrs()) return TDMPC_E_HIP;
+    for (int i = 0; i < n; ++i)
+        if (!t[i]) return TDMPC_E_NULL;
     hipStream_t s = (hipStream_t)stream;
     float* pw = (float*)packed;
-    const size_t M = w.M, L = w.L, A = w.A, F = 4;
+    const int M = w.M, L = w.L, A = w.A, F = 4;
+    int rc;
     HIPCHK(hipMemsetAsync(packed, 0, w.total * 4, s));
     auto cp = [&](size_t dst, const float* src, size_t nfl) {
         return hipMemcpyAsync(pw + dst, src, nfl * F, hipMemcpyDeviceToDevice, s);
     };
-    // 2-D copy: rows x cols floats from src (row pitch spitch floats) to dst (pitch dpitch floats)
-    auto cp2 = [&](size_t dst, size_t dpitch, const float* src, size_t spitch, size_t cols, size_t rows) {
-        return hipMemcpy2DAsync(pw + dst, dpitch * F, src, spitch * F, cols * F, rows, hipMemcpyDeviceToDevice, s);
-    };
     int i = 0;
     if (w.modality == 0) {
-        HIPCHK(cp(w.enc_w1, t[i++], (size_t)w.E * w.obs_dim)); HIPCHK(cp(w.enc_b1, t[i++], w.E));
-        HIPCHK(cp(w.enc_w2, t[i++], L * w.E)); HIPCHK(cp(w.enc_b2, t[i++], L));
+        if ((rc = launch_transpose(t[i++], w.E, w.obs_dim, pw + w.enc_w1t, s))) return rc;
+        HIPCHK(cp(w.enc_b1, t[i++], w.E));
+        if ((rc = launch_transpose(t[i++], L, w.E, pw + w.enc_w2t, s))) return rc;
+        HIPCHK(cp(w.enc_b2, t[i++], L));
     } else {
         static const int ks[4] = {7, 5, 3, 3};
         int cin = w.img_c;
@@ -1034,32 +1375,47 @@ int tdmpc_pack_weights(const tdmpc_dims* d, const float* const* t, int32_t n, vo
             HIPCHK(cp(w.cb[c], t[i++], w.nch));
             cin = w.nch;
         }
-        HIPCHK(cp(w.pl_w, t[i++], L * w.flat)); HIPCHK(cp(w.pl_b, t[i++], L));
+        if ((rc = launch_transpose(t[i++], L, w.flat, pw + w.pl_wt, s))) return rc;
+        HIPCHK(cp(w.pl_b, t[i++], L));
     }
-    const size_t KI = L + A;  // reference input width of cat[z, a]
-    // permuted first layer: dst [a | 0 | z | 0]  <-  src [z | a]
-    auto cp_first = [&](size_t dst, const float* src) -> hipError_t {
-        hipError_t e = cp2(dst, w.Kx, src + L, KI, A, M);
-        if (e != hipSuccess) return e;
-        return cp2(dst + w.Ap, w.Kx, src, KI, L, M);
+    const int KI = L + A;  // reference input width of cat[z, a]
+    // first layers: panel [rows][Kx] columns [a | 0 | z | 0] <- reference [z | a]
+    auto first = [&](size_t dst, int row0, int rows, const float* src) -> int {
+        int r;
+        if ((r = launch_pack_panel(src, KI, L, rows, A, pw + dst + (size_t)row0 * w.Kx, w.Kx, 0, s))) return r;
+        return launch_pack_panel(src, KI, 0, rows, L, pw + dst + (size_t)row0 * w.Kx, w.Kx, w.Ap, s);
+    };
+    auto panel = [&](size_t dst, const float* src, int rows, int cols, int dcols) {
+        return launch_pack_panel(src, cols, 0, rows, cols, pw + dst, dcols, 0, s);
     };
     // dynamics: 0.w 0.b 2.w 2.b 4.w 4.b
-    HIPCHK(cp_first(w.w1x, t[i++])); HIPCHK(cp(w.b1x, t[i++], M));
-    HIPCHK(cp(w.w2d, t[i++], M * M)); HIPCHK(cp(w.b2d, t[i++], M));
-    HIPCHK(cp(w.w3d, t[i++], L * M)); HIPCHK(cp(w.b3d, t[i++], L));
+    if ((rc = first(w.w1x, 0, M, t[i++]))) return rc;
+    HIPCHK(cp(w.b1x, t[i++], M));
+    if ((rc = panel(w.w2d, t[i++], M, M, M))) return rc;
+    HIPCHK(cp(w.b2d, t[i++], M));
+    if ((rc = panel(w.w3d, t[i++], L, M, M))) return rc;
+    HIPCHK(cp(w.b3d, t[i++], L));
     // reward
-    HIPCHK(cp_first(w.w1x + M * w.Kx, t[i++])); HIPCHK(cp(w.b1x + M, t[i++], M));
-    HIPCHK(cp(w.w2r, t[i++], M * M)); HIPCHK(cp(w.b2r, t[i++], M));
-    HIPCHK(cp(w.w3r, t[i++], M)); HIPCHK(cp(w.b3r, t[i++], 1));
+    if ((rc = first(w.w1x, M, M, t[i++]))) return rc;
+    HIPCHK(cp(w.b1x + M, t[i++], M));
+    if ((rc = panel(w.w2r, t[i++], M, M, M))) return rc;
+    HIPCHK(cp(w.b2r, t[i++], M));
+    HIPCHK(cp(w.w3r, t[i++], M));
+    HIPCHK(cp(w.b3r, t[i++], 1));
     // pi
-    HIPCHK(cp2(w.wp1, w.Lp, t[i++], L, L, M)); HIPCHK(cp(w.bp1, t[i++], M));
-    HIPCHK(cp(w.wp2, t[i++], M * M)); HIPCHK(cp(w.bp2, t[i++], M));
-    HIPCHK(cp(w.wp3, t[i++], A * M)); HIPCHK(cp(w.bp3, t[i++], A));
+    if ((rc = panel(w.wp1, t[i++], M, L, w.Lp))) return rc;
+    HIPCHK(cp(w.bp1, t[i++], M));
+    if ((rc = panel(w.wp2, t[i++], M, M, M))) return rc;
+    HIPCHK(cp(w.bp2, t[i++], M));
+    if ((rc = panel(w.wp3, t[i++], A, M, M))) return rc;
+    HIPCHK(cp(w.bp3, t[i++], A));
     // Q1, Q2: 0.w 0.b 1.w 1.b 3.w 3.b 4.w 4.b 6.w 6.b
     for (int q = 0; q < 2; ++q) {
-        HIPCHK(cp_first(w.wq1x + q * M * w.Kx, t[i++])); HIPCHK(cp(w.bq1x + q * M, t[i++], M));
+        if ((rc = first(w.wq1x, q * M, M, t[i++]))) return rc;
+        HIPCHK(cp(w.bq1x + q * M, t[i++], M));
         HIPCHK(cp(w.g1 + q * M, t[i++], M)); HIPCHK(cp(w.be1 + q * M, t[i++], M));
-        HIPCHK(cp(w.wq2 + q * M * M, t[i++], M * M)); HIPCHK(cp(w.bq2 + q * M, t[i++], M));
+        if ((rc = panel(w.wq2 + (size_t)q * M * M, t[i++], M, M, M))) return rc;
+        HIPCHK(cp(w.bq2 + q * M, t[i++], M));
         HIPCHK(cp(w.g2 + q * M, t[i++], M)); HIPCHK(cp(w.be2 + q * M, t[i++], M));
         HIPCHK(cp(w.wq3 + q * M, t[i++], M)); HIPCHK(cp(w.bq3 + q, t[i++], 1));
     }
@@ -1074,8 +1430,7 @@ int tdmpc_encode(const tdmpc_dims* d, const void* packed, const void* obs, int32
     int rc = tdmpc_sizes_for(d, &sz);
     if (rc) return rc;
     if ((rc = setup_ctx(c, d, packed, workspace, sz.workspace_bytes, batch, 1, 1, (hipStream_t)stream))) return rc;
-    // z0 written with row stride Lp inside encode; use a compact copy for the caller
-    if ((rc = encode(c, obs, obs_is_u8, batch, c.k.z0, 0, nullptr))) return rc;
+    if ((rc = encode(c, obs, obs_is_u8, batch, nullptr, 0))) return rc;
     HIPCHK(hipMemcpy2DAsync(z0, c.w.L * 4, c.k.z0, c.w.Lp * 4, c.w.L * 4, batch, hipMemcpyDeviceToDevice, c.s));
     return 0;
 }
@@ -1091,51 +1446,46 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     const int H = prm->horizon, I = prm->iterations, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream))) return rc;
     const int N = c.N, P = c.P, T = c.T;
-    // X holds [a|0|z|0] rows; zero the padding once per call (kernels only write real columns)
-    HIPCHK(hipMemsetAsync(c.k.X, 0, (size_t)(H + 1) * c.k.x_stride * 4, c.s));
-    if ((rc = encode(c, obs, obs_is_u8, B, c.k.z0, T, Xt(c, 0)))) return rc;
+    // z0 = h(obs) and mean = 0 (warm: prev_mean shifted), std = 2
+    if ((rc = encode(c, obs, obs_is_u8, B, prev_mean, prm->warm_start))) return rc;
 
-    CemArgs ca;
-    memset(&ca, 0, sizeof ca);
-    ca.H = H; ca.N = N; ca.P = P; ca.T = T; ca.A = c.A; ca.K = d->num_elites; ca.Kx = c.Kx;
-    ca.X = c.k.X; ca.x_stride = c.k.x_stride; ca.value = c.k.value; ca.rlast = c.k.rlast;
-    ca.mean = c.k.mean; ca.stdv = c.k.stdv; ca.Hmax = d->max_horizon;
-    ca.eps = noise; ca.eps_env = c.eps_env; ca.eps_cem_off = c.eps_cem_off; ca.eps_iter = c.eps_iter;
-    ca.eps_act_off = c.eps_act_off; ca.u = u; ca.prev_mean = prev_mean; ca.warm = prm->warm_start;
-    ca.eval_mode = prm->eval_mode; ca.temperature = prm->temperature; ca.momentum = prm->momentum;
-    ca.omm = prm->one_minus_momentum; ca.std_floor = prm->std_floor; ca.action = action; ca.metrics = metrics;
-    ca.elite_ws = c.k.elite; ca.score_ws = c.k.score; ca.elite_out = elite_out; ca.score_out = score_out;
-    ca.mean_out = mean_out; ca.std_out = std_out; ca.I = I;
-    const size_t cem_lds = (rup(T, 4) + (size_t)H * ca.K * c.A + 2 * rup(ca.K, 4) + 2 * rup(H * c.A, 4) + 4) * 4;
-    const int cem_thr = 1024;
-
-    ca.mode = 0;
-    hipLaunchKernelGGL(cem_kernel, dim3(B), dim3(cem_thr), cem_lds, c.s, ca);
-    HIPCHK(hipGetLastError());
-
-    // pi pre-rollout on the P policy rows of every env (tdmpc.py:113-118); their H-step rollout, reward
-    // prefix and z_H are identical in every CEM iteration (same z0, same pi_actions), so they are computed
-    // once here and reused (rows N..T-1 of X_t, G and rlast).
+    // pi pre-rollout on the P policy rows of every env (tdmpc.py:113-118). Their H-step rollout, reward
+    // prefix and z_H are identical in every CEM iteration (same z0, same pi_actions), so they are
+    // computed once here and reused (rows N..T-1 of X_t, G and rlast).
     if (P > 0) {
         const RowMap pm = {P, T, N};
         for (int t = 0; t < H; ++t) {
-            // pi(z_t) -> X_t action cols of pi rows, eps_pi[t]
             if ((rc = policy(c, t, B * P, pm, noise, c.eps_env, P, (long)t * P * c.A, prm->min_std))) return rc;
-            if ((rc = step_next(c, t, B * P, pm, prm->discount_pow[t], t == 0, t == H - 1))) return rc;
+            if ((rc = step_next(c, t, B * P, pm, prm->discount_pow[t], t == 0, t == H - 1, Sampling{0, nullptr, 0})))
+                return rc;
         }
     }
+    CemArgs ca;
+    memset(&ca, 0, sizeof ca);
+    ca.H = H; ca.N = N; ca.P = P; ca.T = T; ca.A = c.A; ca.K = d->num_elites; ca.Kx = c.Kx;
+    ca.Hmax = d->max_horizon; ca.I = I;
+    ca.X = c.k.X; ca.x_stride = c.k.x_stride; ca.value = c.k.value; ca.rlast = c.k.rlast;
+    ca.mean = c.k.mean; ca.stdv = c.k.stdv;
+    ca.eps = noise; ca.eps_env = c.eps_env; ca.eps_cem_off = c.eps_cem_off; ca.eps_iter = c.eps_iter;
+    ca.eps_act_off = c.eps_act_off; ca.u = u; ca.prev_mean = prev_mean;
+    ca.eval_mode = prm->eval_mode; ca.temperature = prm->temperature; ca.momentum = prm->momentum;
+    ca.omm = prm->one_minus_momentum; ca.std_floor = prm->std_floor; ca.action = action; ca.metrics = metrics;
+    ca.elite_out = elite_out; ca.score_out = score_out; ca.mean_out = mean_out; ca.std_out = std_out;
+    const size_t cem_lds = cem_lds_bytes(T, H, ca.K, c.A);
+
     const RowMap rm = {N, T, 0};
     const RowMap all = {T, T, 0};
     for (int i = 0; i < I; ++i) {
         for (int t = 0; t < H; ++t)
-            if ((rc = step_next(c, t, B * N, rm, prm->discount_pow[t], t == 0, t == H - 1))) return rc;
+            if ((rc = step_next(c, t, B * N, rm, prm->discount_pow[t], t == 0, t == H - 1, Sampling{1, noise, i})))
+                return rc;
         if ((rc = policy(c, H, B * T, all, noise, c.eps_env, T, c.eps_cem_off + (long)i * c.eps_iter + c.eps_term_off,
                          prm->min_std)))
             return rc;
         if ((rc = terminal_q(c, prm->discount_pow[H], value_out, I, i))) return rc;
-        ca.mode = (i == I - 1) ? 2 : 1;
+        ca.final_iter = i == I - 1;
         ca.iter = i;
-        hipLaunchKernelGGL(cem_kernel, dim3(B), dim3(cem_thr), cem_lds, c.s, ca);
+        hipLaunchKernelGGL(cem_kernel, dim3(B), dim3(1024), cem_lds, c.s, ca);
         HIPCHK(hipGetLastError());
     }
     return 0;
@@ -1152,15 +1502,15 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
     if (rows != c.T) { snprintf(g_err, sizeof g_err, "rows must equal N+P"); return TDMPC_E_DIMS; }
     const int T = c.T, L = c.w.L;
-    HIPCHK(hipMemsetAsync(c.k.X, 0, (size_t)(H + 1) * c.k.x_stride * 4, c.s));
-    hipLaunchKernelGGL(bcast_z_kernel, dim3(256), dim3(256), 0, c.s, z0, L, Xt(c, 0), c.Kx, c.w.Ap, T, B);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(scatter_actions_kernel, dim3(512), dim3(256), 0, c.s, actions, c.k.X, c.k.x_stride, H, T,
-                       c.A, c.Kx, B);
+    HIPCHK(hipMemsetAsync(c.k.z0, 0, (size_t)B * c.w.Lp * 4, c.s));
+    HIPCHK(hipMemcpy2DAsync(c.k.z0, c.w.Lp * 4, z0, L * 4, L * 4, B, hipMemcpyDeviceToDevice, c.s));
+    hipLaunchKernelGGL(scatter_actions_kernel, dim3(512), dim3(256), 0, c.s, actions, c.k.X, c.k.x_stride, H, T, c.A,
+                       c.w.Ap, c.Kx, B);
     HIPCHK(hipGetLastError());
     const RowMap all = {T, T, 0};
     for (int t = 0; t < H; ++t)
-        if ((rc = step_next(c, t, B * T, all, prm->discount_pow[t], t == 0, t == H - 1))) return rc;
+        if ((rc = step_next(c, t, B * T, all, prm->discount_pow[t], t == 0, t == H - 1, Sampling{0, nullptr, 0})))
+            return rc;
     if (z_last) {
         hipLaunchKernelGGL(gather_z_kernel, dim3(256), dim3(256), 0, c.s, Xt(c, H), c.Kx, c.w.Ap, L, B * T, z_last);
         HIPCHK(hipGetLastError());
@@ -1172,7 +1522,7 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     return 0;
 }
 
-int tdmpc_profile_begin(int32_t wn, int32_t pro, int32_t kch, int32_t kdim, int32_t max_launches) {
+int tdmpc_profile_begin(int32_t cfg, int32_t pro, int32_t kdim, int32_t max_launches) {
     Profiler& pf = g_prof;
     if (pf.ev) {
         for (int i = 0; i < pf.cap; ++i) (void)hipEventDestroy(pf.ev[i]);
@@ -1182,7 +1532,7 @@ int tdmpc_profile_begin(int32_t wn, int32_t pro, int32_t kch, int32_t kdim, int3
     pf.cap = 2 * std::max(1, (int)max_launches);
     pf.ev = (hipEvent_t*)calloc(pf.cap, sizeof(hipEvent_t));
     for (int i = 0; i < pf.cap; ++i) HIPCHK(hipEventCreate(&pf.ev[i]));
-    pf.wn = wn; pf.pro = pro; pf.kch = kch; pf.kdim = kdim; pf.armed = 1;
+    pf.cfg = cfg; pf.pro = pro; pf.kdim = kdim; pf.armed = 1;
     return 0;
 }
 

@@ -1,0 +1,10 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"
+grep -E "passed|failed|FAILED|Error|assert" gpurun_out/pytest_gpu.log | tail -20
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 120 tools/mb/mb_linear 1 && timeout -k 10 120 tools/mb/mb_linear 8
+timeout -k 10 300 rocprofv3 --kernel-trace -T -d gpurun_out/kt6 -o run --output-format csv -- python tools/quick_time.py humanoid-run 1 > gpurun_out/kt6.log 2>&1; echo "kt rc=$?"
+timeout -k 10 300 rocprofv3 --kernel-trace -T -d gpurun_out/kt6b -o run --output-format csv -- python tools/quick_time.py humanoid-run 8 > gpurun_out/kt6b.log 2>&1; echo "kt rc=$?"

@@ -1,0 +1,147 @@
+// Microbenchmark of the planner's kernels in isolation (development tool, not shipped).
+// Includes the library source so the internal launchers can be driven directly.
+#include "../../tdmpc_amd/csrc/tdmpc_kernels.hip"
+
+#include <vector>
+#include <random>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+static float time_it(hipStream_t s, int iters, const std::function<void()>& fn) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) fn();
+    CK(hipEventRecord(a, s));
+    for (int i = 0; i < iters; ++i) fn();
+    CK(hipEventRecord(b, s));
+    CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b));
+    return ms * 1000.f / iters;
+}
+
+int main(int argc, char** argv) {
+    int B = argc > 1 ? atoi(argv[1]) : 1;
+    tdmpc_dims d{};
+    d.modality = 0; d.obs_dim = 67; d.action_dim = 21; d.latent_dim = 100; d.mlp_dim = 512; d.enc_dim = 256;
+    d.num_samples = 512; d.num_pi = 256; d.num_elites = 64; d.max_horizon = 5; d.max_iterations = 6; d.max_batch = B;
+    tdmpc_sizes sz;
+    if (tdmpc_sizes_for(&d, &sz)) { printf("sizes failed\n"); return 1; }
+    void *packed, *ws; float* noise; double* u; float *prev, *act, *met, *obs;
+    CK(hipMalloc(&packed, sz.packed_weight_bytes)); CK(hipMalloc(&ws, sz.workspace_bytes));
+    CK(hipMalloc(&noise, sz.noise_floats_per_env * 4 * B)); CK(hipMalloc(&u, 8 * B));
+    CK(hipMalloc(&prev, 4 * 5 * 21 * B)); CK(hipMalloc(&act, 4 * 21 * B)); CK(hipMalloc(&met, 8 * B));
+    CK(hipMalloc(&obs, 4 * 67 * B));
+    // random packed weights / workspace / noise (values ~ N(0, 1/sqrt(512)))
+    {
+        std::mt19937 g(0); std::normal_distribution<float> nd(0.f, 0.04f);
+        std::vector<float> hw(sz.packed_weight_bytes / 4);
+        for (auto& x : hw) x = nd(g);
+        CK(hipMemcpy(packed, hw.data(), sz.packed_weight_bytes, hipMemcpyHostToDevice));
+        std::vector<float> hn(sz.noise_floats_per_env * B);
+        std::normal_distribution<float> n1(0.f, 1.f);
+        for (auto& x : hn) x = n1(g);
+        CK(hipMemcpy(noise, hn.data(), hn.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemset(ws, 0, sz.workspace_bytes));
+        std::vector<float> ho(67 * B); for (auto& x : ho) x = n1(g);
+        CK(hipMemcpy(obs, ho.data(), ho.size() * 4, hipMemcpyHostToDevice));
+        std::vector<double> hu(B, 0.5); CK(hipMemcpy(u, hu.data(), 8 * B, hipMemcpyHostToDevice));
+        CK(hipMemset(prev, 0, 4 * 5 * 21 * B));
+    }
+    hipStream_t s; CK(hipStreamCreate(&s));
+    tdmpc_plan_params p{};
+    p.horizon = 5; p.iterations = 6; p.batch = B; p.warm_start = 0; p.eval_mode = 0;
+    p.min_std = 0.05f; p.temperature = 0.5f; p.momentum = 0.1f; p.one_minus_momentum = 0.9f; p.std_floor = 0.05f;
+    float dd = 1.f; for (int t = 0; t <= 5; ++t) { p.discount_pow[t] = dd; dd *= 0.99f; }
+    float t_plan = time_it(s, 20, [&] {
+        int rc = tdmpc_plan(&d, &p, packed, obs, 0, noise, u, prev, act, met, nullptr, nullptr, nullptr, nullptr, nullptr,
+                            ws, sz.workspace_bytes, s);
+        if (rc) { printf("plan rc %d %s\n", rc, tdmpc_last_error()); exit(1); }
+    });
+    printf("B=%d full plan: %.1f us\n", B, t_plan);
+    Ctx c;
+    setup_ctx(c, &d, packed, ws, sz.workspace_bytes, B, 5, 6, s);
+    const RowMap rm = {c.N, c.T, 0};
+    const RowMap all = {c.T, c.T, 0};
+    struct Case { const char* name; std::function<void()> fn; };
+    std::vector<Case> cases;
+    // individual layers of one step (rollout rows)
+    cases.push_back({"step_next(t=1) [S1+S2+S3]", [&] { step_next(c, 1, B * c.N, rm, 0.99f, 0, 0, Sampling{1, noise, 0}); }});
+    cases.push_back({"policy(H) [pi1+pi2+pi3]", [&] { policy(c, 5, B * c.T, all, noise, c.eps_env, c.T, 0, 0.05f); }});
+    cases.push_back({"terminal_q [Q1+Q2+value]", [&] { terminal_q(c, 0.95f, nullptr, 6, 0); }});
+    cases.push_back({"encode", [&] { encode(c, obs, 0, B, prev, 0); }});
+    for (auto& cs : cases) printf("%-32s %8.2f us\n", cs.name, time_it(s, 200, cs.fn));
+    // per-layer: S2 only
+    {
+        const Layout& w = c.w; const int M = c.M;
+        LinArgs a = args0();
+        a.M = B * c.N; a.K = M;
+        LinProb& p0 = a.p[0];
+        p0.A = hop(c.k.H1, c, 0); p0.W = wop(c, w.w2d, M); p0.bias = c.pw + w.b2d;
+        p0.C = hout(c.k.H2, c, 0); p0.N = p0.nvalid = p0.nstore = M; p0.epi = EPI_ELU;
+        LinProb& p1 = a.p[1];
+        p1.A = hop(c.k.H1, c, M / 4); p1.W = wop(c, w.w2r, M); p1.bias = c.pw + w.b2r;
+        p1.N = p1.nvalid = M; p1.nstore = 0; p1.epi = EPI_ELU_DOT;
+        p1.dotw = c.pw + w.w3r; p1.dot_out = c.k.rpart; p1.dot_ld = M / 32;
+        printf("%-32s %8.2f us\n", "S2 (WN=1)", time_it(s, 500, [&] { launch_lin(a, 2, M, 1, PRO_PLAIN, s); }));
+        p1.epi = EPI_ELU; p1.C = hout(c.k.H2, c, M / 4); p1.nstore = M;
+        printf("%-32s %8.2f us\n", "S2 (WN=2)", time_it(s, 500, [&] { launch_lin(a, 2, M, 2, PRO_PLAIN, s); }));
+        a.p[0].N = 32;
+        printf("%-32s %8.2f us\n", "1 col tile x 2 (WN=1)", time_it(s, 500, [&] { launch_lin(a, 2, 32, 1, PRO_PLAIN, s); }));
+    }
+#ifdef TDMPC_STAMPS
+    {
+        unsigned long long* dbuf; CK(hipMalloc(&dbuf, 8 * 8 * 8192));
+        unsigned int cap = 8192;
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_cap), &cap, 4));
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dbuf, sizeof(dbuf)));
+        auto run_case = [&](const char* name, const std::function<void()>& fn) {
+            for (int i = 0; i < 5; ++i) fn();
+            CK(hipStreamSynchronize(s));
+            unsigned int zero = 0;
+            CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_n), &zero, 4));
+            fn();
+            CK(hipStreamSynchronize(s));
+            unsigned int n; CK(hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_stamp_n), 4));
+            n = std::min(n, 8192u);
+            std::vector<unsigned long long> h(8 * n);
+            CK(hipMemcpy(h.data(), dbuf, 8 * 8 * n, hipMemcpyDeviceToHost));
+            unsigned long long rtmin = ~0ull, rtmax = 0;
+            double ph[4] = {0, 0, 0, 0}, phmax[4] = {0, 0, 0, 0};
+            int xcc_hist[8] = {0};
+            for (unsigned i = 0; i < n; ++i) {
+                unsigned long long* o = &h[8 * i];
+                rtmin = std::min(rtmin, o[0]); rtmax = std::max(rtmax, o[0]);
+                for (int k = 0; k < 4; ++k) { double d = double(o[2 + k] - o[1 + k]); ph[k] += d; phmax[k] = std::max(phmax[k], d); }
+                xcc_hist[o[7] & 7]++;
+            }
+            printf("%s: %u WGs, start skew %.2f us (100MHz rt), avg cycles: load %.0f mfma %.0f sync %.0f epi %.0f | max %.0f %.0f %.0f %.0f | xcc",
+                   name, n, (rtmax - rtmin) / 100.0, ph[0] / n, ph[1] / n, ph[2] / n, ph[3] / n, phmax[0], phmax[1], phmax[2], phmax[3]);
+            for (int k = 0; k < 8; ++k) printf(" %d", xcc_hist[k]);
+            printf("\n");
+            // xcc of first 16 WGs (blockIdx order)
+            std::vector<std::pair<unsigned long long, unsigned long long>> v;
+            for (unsigned i = 0; i < n; ++i) v.push_back({h[8 * i + 6], h[8 * i + 7]});
+            std::sort(v.begin(), v.end());
+            printf("   blockIdx->xcc:");
+            for (unsigned i = 0; i < std::min(n, 20u); ++i) printf(" %llu:%llu", v[i].first & 0xffff, v[i].second);
+            printf("\n");
+        };
+        const Layout& w = c.w; const int M = c.M;
+        LinArgs a = args0();
+        a.M = B * c.N; a.K = M;
+        LinProb& p0 = a.p[0];
+        p0.A = hop(c.k.H1, c, 0); p0.W = wop(c, w.w2d, M); p0.bias = c.pw + w.b2d;
+        p0.C = hout(c.k.H2, c, 0); p0.N = p0.nvalid = p0.nstore = M; p0.epi = EPI_ELU;
+        a.p[1] = p0;
+        a.p[1].A = hop(c.k.H1, c, M / 4); a.p[1].W = wop(c, w.w2r, M); a.p[1].C = hout(c.k.H2, c, M / 4);
+        run_case("S2 WN=1", [&] { launch_lin(a, 2, M, 1, PRO_PLAIN, s); });
+        run_case("S2 WN=1 again", [&] { launch_lin(a, 2, M, 1, PRO_PLAIN, s); });
+        run_case("S2 WN=2", [&] { launch_lin(a, 2, M, 2, PRO_PLAIN, s); });
+        run_case("S2 1 coltile", [&] { launch_lin(a, 2, 32, 1, PRO_PLAIN, s); });
+        LinArgs b = a; b.K = 128; b.p[0].W = wop(c, w.w2d, 128);  b.p[1].W = wop(c, w.w2r, 128);
+        run_case("S2 K=128", [&] { launch_lin(b, 2, M, 2, PRO_PLAIN, s); });
+    }
+#endif
+    CK(hipStreamSynchronize(s));
+    return 0;
+}
