@@ -284,178 +284,16 @@ DEVI float4 load_a(const LinArgs& args, const float* Abase, int colq, int arow, 
     return *(const float4*)(Abase + (size_t)colq * 128);
 }
 
-// Fused nn.Linear on v_mfma_f32_32x32x2_f32.
-//   Workgroup tile: R = 32*TM*WGM rows x C = 32*TN*WGN columns; waves = WGM*WGN*KS where KS (runtime,
-//   blockDim / (64*WGM*WGN)) splits K into chunks of KCH. Each wave owns a (32*TM) x (32*TN) register tile.
-//   ROLL = false: a wave preloads its whole K chunk (<= KCH/8 groups) -- the latency configuration for
-//   small row counts. ROLL = true: KS = 1 and a 4-deep prefetch ring walks the full K -- the throughput
-//   configuration for large row counts.
-template <int TM, int TN, int WGM, int WGN, int PRO, int KCH, bool ROLL>
-__global__ void __launch_bounds__(512) linear_kernel(const LinArgs args) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int R = 32 * TM * WGM, C = 32 * TN * WGN, LDC = C + 4;
+// Shared epilogue of the linear kernels. smem holds KS partial tiles [KS][R][C+4] (summed here), sbias /
+// sdotw the bias and reward-head weights of this tile's columns, srp the reward partial dots of its rows.
+template <int R, int C>
+DEVI void lin_epilogue(const LinArgs& args, const LinProb& P, float* smem, int KS, int m0, int n0,
+                       const float* sbias, const float* sdotw, const float* srp) {
+    constexpr int LDC = C + 4;
     constexpr int BW = C >= 64 ? 64 : C;     // row-reduction block width
     constexpr int NB = C / BW;
-    const LinProb& P = args.p[blockIdx.z];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nthr = blockDim.x;
-    const int r = lane & 31, h = lane >> 5;
-    const int m0 = blockIdx.x * R, n0 = blockIdx.y * C;
-    if (n0 >= P.N) return;  // uniform over the workgroup
-#ifdef TDMPC_STAMPS
-    unsigned long long st_[6];
-    unsigned long long rt0_ = __builtin_amdgcn_s_memrealtime();
-    STAMP(0);
-#endif
-    const int KS = nthr / (64 * WGM * WGN);
-    const int wm = wave % WGM, wn = (wave / WGM) % WGN, ks = wave / (WGM * WGN);
+    const int nthr = blockDim.x;
     const int epi = P.epi;
-
-    // LDS: partial tiles [KS][R][LDC] | bias [C] | dotw [C] | rpart [R][rpart_nt]
-    float* sbias = smem + (size_t)KS * R * LDC;
-    float* sdotw = sbias + C;
-    float* srp = sdotw + C;
-    // prefetch the epilogue's operands now; the loads land while the MFMAs run
-    for (int i = threadIdx.x; i < C / 4; i += nthr) {
-        const int n = n0 + 4 * i;
-        *(float4*)(sbias + 4 * i) = *(const float4*)(P.bias + n);
-        if (epi == EPI_ELU_DOT) *(float4*)(sdotw + 4 * i) = *(const float4*)(P.dotw + n);
-    }
-    if (epi == EPI_LIN_Z && blockIdx.y == 0)
-        for (int i = threadIdx.x; i < R * args.rpart_nt; i += nthr) {
-            const int lm = m0 + i / args.rpart_nt;
-            srp[i] = lm < args.M ? args.rpart[(size_t)lm * args.rpart_nt + i % args.rpart_nt] : 0.f;
-        }
-
-    // this lane's A rows (TM of them) and W rows (TN)
-    const float* Abase[TM];
-    int arow[TM], env[TM];
-    float mu[TM], rs[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-        const int m = m0 + (wm * TM + i) * 32 + r;
-        const int mm = m < args.M ? m : 0;
-        arow[i] = args.a_mapped ? map_row(args.amap, mm) : mm;
-        Abase[i] = P.A.p + (size_t)(arow[i] >> 5) * P.A.ts + (arow[i] & 31) * 4;
-        env[i] = (args.zmode | args.smode) ? arow[i] / args.rows_per_env : 0;
-        mu[i] = 0.f; rs[i] = 1.f;
-        if (PRO == PRO_LN_TANH) {
-            // Chan-combine the producer's per-64-column (mean, M2) into mean and 1/sqrt(var + 1e-5)
-            const float2* st = P.ln_stats + (size_t)mm * P.ln_ld + P.ln_t0;
-            float n = 0.f, mean = 0.f, m2 = 0.f;
-            for (int q = 0; q < P.ln_nt; ++q) {
-                const float2 s = st[q];
-                const float nn = n + 64.f, delta = s.x - mean;
-                mean += delta * 64.f / nn;
-                m2 += s.y + delta * delta * n * 64.f / nn;
-                n = nn;
-            }
-            mu[i] = mean;
-            rs[i] = 1.0f / sqrtf(fmaxf(m2 / n, 0.f) + 1e-5f);
-        }
-    }
-    const float* Wbase = P.W.p + (size_t)((n0 >> 5) + wn * TN) * P.W.ts + r * 4;
-
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-    auto mfma_group = [&](float4 (&a)[TM], const float4 (&b)[TN], int k) {
-        if (PRO == PRO_LN_TANH) {
-            // helper.q: LayerNorm -> Tanh, as ATen computes it: (x * rstd + (-rstd * mean)) * g + b
-            const float4 gg = *(const float4*)(P.ln_g + k);
-            const float4 bb = *(const float4*)(P.ln_b + k);
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const float sh = -rs[i] * mu[i];
-                a[i].x = tanh_f(fadd(fmul(fadd(fmul(a[i].x, rs[i]), sh), gg.x), bb.x));
-                a[i].y = tanh_f(fadd(fmul(fadd(fmul(a[i].y, rs[i]), sh), gg.y), bb.y));
-                a[i].z = tanh_f(fadd(fmul(fadd(fmul(a[i].z, rs[i]), sh), gg.z), bb.z));
-                a[i].w = tanh_f(fadd(fmul(fadd(fmul(a[i].w, rs[i]), sh), gg.w), bb.w));
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
-            }
-    };
-    auto load_group = [&](int g, float4 (&a)[TM], float4 (&b)[TN]) {
-        const int kq = 2 * g + h;  // quad of this lane half within K
-#pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = *(const float4*)(Wbase + (size_t)j * P.W.ts + kq * 128);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = load_a(args, Abase[i], P.A.q0 + kq, arow[i], env[i]);
-    };
-
-    if (!ROLL) {
-        constexpr int NG = KCH / 8;
-        const int g0 = (ks * args.kch) >> 3;
-        const int ng = min(args.kch, args.K - ks * args.kch) >> 3;
-        float4 av[NG][TM], bv[NG][TN];
-#pragma unroll
-        for (int g = 0; g < NG; ++g)
-            if (g < ng) load_group(g0 + g, av[g], bv[g]);
-#ifdef TDMPC_STAMPS
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        STAMP(1);
-#endif
-#pragma unroll
-        for (int g = 0; g < NG; ++g)
-            if (g < ng) mfma_group(av[g], bv[g], 8 * (g0 + g) + 4 * h);
-    } else {
-        constexpr int D = 4;
-        const int ng = args.K >> 3;
-        float4 ra[D][TM], rb[D][TN];
-#pragma unroll
-        for (int d = 0; d < D; ++d)
-            if (d < ng) load_group(d, ra[d], rb[d]);
-#ifdef TDMPC_STAMPS
-        STAMP(1);
-#endif
-        for (int gb = 0; gb < ng; gb += D) {
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                const int g = gb + d;
-                if (g < ng) {
-                    float4 ta[TM], tb[TN];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) ta[i] = ra[d][i];
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) tb[j] = rb[d][j];
-                    if (g + D < ng) load_group(g + D, ra[d], rb[d]);
-                    mfma_group(ta, tb, 8 * g + 4 * h);
-                }
-            }
-        }
-    }
-
-    // partial tiles -> LDS [ks][row][col]; C/D map: col = lane&31, row = (e&3) + 8*(e>>2) + 4*(lane>>5)
-    {
-        float* base = smem + (size_t)ks * R * LDC + (size_t)(wm * TM * 32) * LDC + wn * TN * 32;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int e = 0; e < 16; ++e)
-                    base[(size_t)(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * LDC + j * 32 + r] = acc[i][j][e];
-    }
-#ifdef TDMPC_STAMPS
-    STAMP(2);
-#endif
-    __syncthreads();
-#ifdef TDMPC_STAMPS
-    STAMP(3);
-#endif
-
     // ---- epilogue phase A: thread -> (row, column quads); 32 consecutive lanes own 32 consecutive rows,
     // so one quad stored by them is 512 contiguous bytes of the panel layout.
     const bool need_red = epi == EPI_LNSTATS || epi == EPI_ELU_DOT;
@@ -557,6 +395,180 @@ __global__ void __launch_bounds__(512) linear_kernel(const LinArgs args) {
             if (args.last) args.rlast[crow] = rew;
         }
     }
+}
+
+// Fused nn.Linear on v_mfma_f32_32x32x2_f32.
+//   Workgroup tile: R = 32*TM*WGM rows x C = 32*TN*WGN columns; waves = WGM*WGN*KS where KS (runtime,
+//   blockDim / (64*WGM*WGN)) splits K into chunks of KCH. Each wave owns a (32*TM) x (32*TN) register tile.
+//   ROLL = false: a wave preloads its whole K chunk (<= KCH/8 groups) -- the latency configuration for
+//   small row counts. ROLL = true: KS = 1 and a 4-deep prefetch ring walks the full K -- the throughput
+//   configuration for large row counts.
+template <int TM, int TN, int WGM, int WGN, int PRO, int KCH, bool ROLL>
+__global__ void __launch_bounds__(512) linear_kernel(const LinArgs args) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int R = 32 * TM * WGM, C = 32 * TN * WGN, LDC = C + 4;
+    const LinProb& P = args.p[blockIdx.z];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nthr = blockDim.x;
+    const int r = lane & 31, h = lane >> 5;
+    const int m0 = blockIdx.x * R, n0 = blockIdx.y * C;
+    if (n0 >= P.N) return;  // uniform over the workgroup
+#ifdef TDMPC_STAMPS
+    unsigned long long st_[6];
+    unsigned long long rt0_ = __builtin_amdgcn_s_memrealtime();
+    STAMP(0);
+#endif
+    const int KS = nthr / (64 * WGM * WGN);
+    const int wm = wave % WGM, wn = (wave / WGM) % WGN, ks = wave / (WGM * WGN);
+    const int epi = P.epi;
+
+    // LDS: partial tiles [KS][R][LDC] | bias [C] | dotw [C] | rpart [R][rpart_nt]
+    float* sbias = smem + (size_t)KS * R * LDC;
+    float* sdotw = sbias + C;
+    float* srp = sdotw + C;
+    // prefetch the epilogue's operands now; the loads land while the MFMAs run
+    for (int i = threadIdx.x; i < C / 4; i += nthr) {
+        const int n = n0 + 4 * i;
+        *(float4*)(sbias + 4 * i) = *(const float4*)(P.bias + n);
+        if (epi == EPI_ELU_DOT) *(float4*)(sdotw + 4 * i) = *(const float4*)(P.dotw + n);
+    }
+    if (epi == EPI_LIN_Z && blockIdx.y == 0)
+        for (int i = threadIdx.x; i < R * args.rpart_nt; i += nthr) {
+            const int lm = m0 + i / args.rpart_nt;
+            srp[i] = lm < args.M ? args.rpart[(size_t)lm * args.rpart_nt + i % args.rpart_nt] : 0.f;
+        }
+
+    // this lane's A rows (TM of them) and W rows (TN)
+    const float* Abase[TM];
+    int arow[TM], env[TM];
+    float mu[TM], rs[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + (wm * TM + i) * 32 + r;
+        const int mm = m < args.M ? m : 0;
+        arow[i] = args.a_mapped ? map_row(args.amap, mm) : mm;
+        Abase[i] = P.A.p + (size_t)(arow[i] >> 5) * P.A.ts + (arow[i] & 31) * 4;
+        env[i] = (args.zmode | args.smode) ? arow[i] / args.rows_per_env : 0;
+        mu[i] = 0.f; rs[i] = 1.f;
+        if (PRO == PRO_LN_TANH) {
+            // Chan-combine the producer's per-64-column (mean, M2) into mean and 1/sqrt(var + 1e-5)
+            const float2* st = P.ln_stats + (size_t)mm * P.ln_ld + P.ln_t0;
+            float n = 0.f, mean = 0.f, m2 = 0.f;
+            for (int q = 0; q < P.ln_nt; ++q) {
+                const float2 s = st[q];
+                const float nn = n + 64.f, delta = s.x - mean;
+                mean += delta * 64.f / nn;
+                m2 += s.y + delta * delta * n * 64.f / nn;
+                n = nn;
+            }
+            mu[i] = mean;
+            rs[i] = 1.0f / sqrtf(fmaxf(m2 / n, 0.f) + 1e-5f);
+        }
+    }
+    const float* Wbase = P.W.p + (size_t)((n0 >> 5) + wn * TN) * P.W.ts + r * 4;
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    auto mfma_group = [&](float4 (&a)[TM], const float4 (&b)[TN], int k) {
+        if (PRO == PRO_LN_TANH) {
+            // helper.q: LayerNorm -> Tanh, as ATen computes it: (x * rstd + (-rstd * mean)) * g + b
+            const float4 gg = *(const float4*)(P.ln_g + k);
+            const float4 bb = *(const float4*)(P.ln_b + k);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const float sh = -rs[i] * mu[i];
+                a[i].x = tanh_f(fadd(fmul(fadd(fmul(a[i].x, rs[i]), sh), gg.x), bb.x));
+                a[i].y = tanh_f(fadd(fmul(fadd(fmul(a[i].y, rs[i]), sh), gg.y), bb.y));
+                a[i].z = tanh_f(fadd(fmul(fadd(fmul(a[i].z, rs[i]), sh), gg.z), bb.z));
+                a[i].w = tanh_f(fadd(fmul(fadd(fmul(a[i].w, rs[i]), sh), gg.w), bb.w));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+            }
+    };
+    auto load_group = [&](int g, float4 (&a)[TM], float4 (&b)[TN]) {
+        const int kq = 2 * g + h;  // quad of this lane half within K
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = *(const float4*)(Wbase + (size_t)j * P.W.ts + kq * 128);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = load_a(args, Abase[i], P.A.q0 + kq, arow[i], env[i]);
+    };
+
+    if constexpr (!ROLL) {
+        constexpr int NG = KCH / 8;
+        const int g0 = (ks * args.kch) >> 3;
+        const int ng = min(args.kch, args.K - ks * args.kch) >> 3;
+        float4 av[NG][TM], bv[NG][TN];
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+            if (g < ng) load_group(g0 + g, av[g], bv[g]);
+#ifdef TDMPC_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP(1);
+#endif
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+            if (g < ng) mfma_group(av[g], bv[g], 8 * (g0 + g) + 4 * h);
+    } else {
+        constexpr int D = 4;
+        const int gbase = (ks * args.kch) >> 3;
+        const int ng = min(args.kch, args.K - ks * args.kch) >> 3;
+        float4 ra[D][TM], rb[D][TN];
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+            if (d < ng) load_group(gbase + d, ra[d], rb[d]);
+#ifdef TDMPC_STAMPS
+        STAMP(1);
+#endif
+        for (int gb = 0; gb < ng; gb += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const int g = gb + d;
+                if (g < ng) {
+                    float4 ta[TM], tb[TN];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) ta[i] = ra[d][i];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) tb[j] = rb[d][j];
+                    if (g + D < ng) load_group(gbase + g + D, ra[d], rb[d]);
+                    mfma_group(ta, tb, 8 * (gbase + g) + 4 * h);
+                }
+            }
+        }
+    }
+
+    // partial tiles -> LDS [ks][row][col]; C/D map: col = lane&31, row = (e&3) + 8*(e>>2) + 4*(lane>>5)
+    {
+        float* base = smem + (size_t)ks * R * LDC + (size_t)(wm * TM * 32) * LDC + wn * TN * 32;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    base[(size_t)(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * LDC + j * 32 + r] = acc[i][j][e];
+    }
+#ifdef TDMPC_STAMPS
+    STAMP(2);
+#endif
+    __syncthreads();
+#ifdef TDMPC_STAMPS
+    STAMP(3);
+#endif
+
+    lin_epilogue<R, C>(args, P, smem, KS, m0, n0, sbias, sdotw, srp);
 #ifdef TDMPC_STAMPS
     __syncthreads();
     STAMP(4);
@@ -571,6 +583,169 @@ __global__ void __launch_bounds__(512) linear_kernel(const LinArgs args) {
         o[7] = xcc_;
     }
 #endif
+}
+
+// Throughput configuration for large row counts: LDS-staged, double-buffered 128x128 output tile.
+// 4 waves in a 2x2 grid, each owning a 64x64 register tile (2x2 MFMA 32x32 tiles), over K tiles of 32.
+// With the panel layout, one K tile of one 32-row block is a contiguous 4 KiB, so a workgroup stages
+// A (4 blocks) and W (4 blocks) with one 1 KiB wave load per block per wave and every fragment read is a
+// conflict-free ds_read_b128. Global traffic per MFMA is half the register-direct kernel's.
+template <int PRO_UNUSED>
+__global__ void __launch_bounds__(256) linear_lds_kernel(const LinArgs args) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int R = 128, C = 128, STAGE = 4096;    // floats per 32-row block x 8 quads... x4 blocks
+    const LinProb& P = args.p[blockIdx.z];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int m0 = blockIdx.x * R, n0 = blockIdx.y * C;
+    if (n0 >= P.N) return;
+    const int epi = P.epi;
+    // LDS: stage buffers [2][A 4096 | W 4096] (aliased by the epilogue tile [128][132] afterwards),
+    // then bias [C], dotw [C], rpart [R][nt]
+    float* sbias = smem + R * (C + 4);
+    float* sdotw = sbias + C;
+    float* srp = sdotw + C;
+    for (int i = tid; i < C / 4; i += 256) {
+        const int n = n0 + 4 * i;
+        *(float4*)(sbias + 4 * i) = *(const float4*)(P.bias + n);
+        if (epi == EPI_ELU_DOT) *(float4*)(sdotw + 4 * i) = *(const float4*)(P.dotw + n);
+    }
+    if (epi == EPI_LIN_Z && blockIdx.y == 0)
+        for (int i = tid; i < R * args.rpart_nt; i += 256) {
+            const int lm = m0 + i / args.rpart_nt;
+            srp[i] = lm < args.M ? args.rpart[(size_t)lm * args.rpart_nt + i % args.rpart_nt] : 0.f;
+        }
+
+    // this thread's staging slots: rows m0 + 32*i + (tid&31) (i < 4), quad (tid>>5) of each K tile
+    const int sq = tid >> 5, sr = tid & 31;
+    const float* Arow[4];
+    int arow[4], env[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + 32 * i + sr;
+        const int mm = m < args.M ? m : 0;
+        arow[i] = args.a_mapped ? map_row(args.amap, mm) : mm;
+        Arow[i] = P.A.p + (size_t)(arow[i] >> 5) * P.A.ts + (arow[i] & 31) * 4;
+        env[i] = (args.zmode | args.smode) ? arow[i] / args.rows_per_env : 0;
+    }
+    const float* Wrow = P.W.p + (size_t)(n0 >> 5) * P.W.ts + sr * 4;
+    const int kq_total = args.K >> 2;
+    auto stage_load = [&](int kt, float4 (&ra)[4], float4 (&rw)[4]) {
+        const int kq = kt * 8 + sq;
+        const bool ok = kq < kq_total;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            ra[i] = ok ? load_a(args, Arow[i], P.A.q0 + kq, arow[i], env[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+            rw[i] = ok ? *(const float4*)(Wrow + (size_t)i * P.W.ts + (size_t)kq * 128) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto stage_store = [&](int buf, const float4 (&ra)[4], const float4 (&rw)[4]) {
+        float* sA = smem + buf * 2 * STAGE;
+        float* sW = sA + STAGE;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            *(float4*)(sA + ((i * 8 + sq) * 32 + sr) * 4) = ra[i];
+            *(float4*)(sW + ((i * 8 + sq) * 32 + sr) * 4) = rw[i];
+        }
+    };
+
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    const int nst = (args.K + 31) >> 5;
+    float4 ra[4], rw[4];
+    stage_load(0, ra, rw);
+    stage_store(0, ra, rw);
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+        const int buf = st & 1;
+        if (st + 1 < nst) stage_load(st + 1, ra, rw);
+        const float* sA = smem + buf * 2 * STAGE;
+        const float* sW = sA + STAGE;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            if (st * 32 + 8 * g < args.K) {
+                float4 a[2], b[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) a[i] = *(const float4*)(sA + (((wm * 2 + i) * 8 + 2 * g + h) * 32 + r) * 4);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) b[j] = *(const float4*)(sW + (((wn * 2 + j) * 8 + 2 * g + h) * 32 + r) * 4);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+                    }
+            }
+        }
+        if (st + 1 < nst) stage_store(buf ^ 1, ra, rw);
+        __syncthreads();
+    }
+    // accumulators -> LDS tile [128][132] (the stage buffers are free after the last barrier)
+    {
+        float* base = smem + (size_t)(wm * 64) * (C + 4) + wn * 64;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    base[(size_t)(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * (C + 4) + j * 32 + r] = acc[i][j][e];
+    }
+    __syncthreads();
+    lin_epilogue<R, C>(args, P, smem, 1, m0, n0, sbias, sdotw, srp);
+}
+
+// ------------------------------------------------------------------------------------------------ LN+tanh
+// a1 = tanh(LayerNorm(y1)) for both Q heads (helper.q: Linear -> LayerNorm -> Tanh), computed once per
+// element from the producer's per-64-column moments, so the next GEMM is a plain one. Grid: (row tiles,
+// 64-column blocks); 32 consecutive lanes own 32 consecutive rows of one panel quad (512 B contiguous).
+struct LnArgs {
+    const float* Y; float* O; long ts; const float2* st; int st_ld; int M_; int rows;
+    const float* g; const float* b;
+};
+
+__global__ void __launch_bounds__(256) ln_tanh_kernel(const LnArgs a) {
+    const int r = threadIdx.x & 31, g = threadIdx.x >> 5;
+    const int row = blockIdx.x * 32 + r;
+    if (row >= a.rows) return;
+    const int c0 = blockIdx.y * 64;            // 64-column block, inside one head (M % 64 == 0)
+    const int p = c0 / a.M_;
+    const int ntile = a.M_ / 64;
+    const float2* st = a.st + (size_t)row * a.st_ld + p * ntile;
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+    for (int i = 0; i < ntile; ++i) {
+        const float2 s = st[i];
+        const float nn = n + 64.f, delta = s.x - mean;
+        mean += delta * 64.f / nn;
+        m2 += s.y + delta * delta * n * 64.f / nn;
+        n = nn;
+    }
+    const float rs = 1.0f / sqrtf(fmaxf(m2 / n, 0.f) + 1e-5f);
+    const float sh = -rs * mean;
+    const size_t base = (size_t)(row >> 5) * a.ts + (row & 31) * 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int c = c0 + 4 * (g + 8 * i);
+        const float4 y = *(const float4*)(a.Y + base + (size_t)(c >> 2) * 128);
+        const float4 gg = *(const float4*)(a.g + c), bb = *(const float4*)(a.b + c);
+        float4 o;
+        // ATen LayerNorm: (x * rstd + (-rstd * mean)) * gamma + beta
+        o.x = tanh_f(fadd(fmul(fadd(fmul(y.x, rs), sh), gg.x), bb.x));
+        o.y = tanh_f(fadd(fmul(fadd(fmul(y.y, rs), sh), gg.y), bb.y));
+        o.z = tanh_f(fadd(fmul(fadd(fmul(y.z, rs), sh), gg.z), bb.z));
+        o.w = tanh_f(fadd(fmul(fadd(fmul(y.w, rs), sh), gg.w), bb.w));
+        *(float4*)(a.O + base + (size_t)(c >> 2) * 128) = o;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------ value
@@ -986,7 +1161,8 @@ int set_lds_attr() {
     X(1, 2, 1, 1, 0, 32, false) X(1, 2, 1, 1, 0, 64, false) X(1, 2, 1, 1, 0, 128, false)              \
     X(1, 1, 1, 1, 1, 32, false) X(1, 1, 1, 1, 1, 64, false) X(1, 1, 1, 1, 1, 128, false)              \
     X(1, 2, 1, 1, 1, 32, false) X(1, 2, 1, 1, 1, 64, false) X(1, 2, 1, 1, 1, 128, false)              \
-    X(2, 2, 2, 2, 0, 8, true) X(2, 2, 2, 2, 1, 8, true)
+    X(2, 2, 2, 2, 0, 1, true) X(2, 2, 2, 2, 1, 1, true) X(2, 2, 2, 2, 0, 2, true) X(2, 2, 2, 2, 1, 2, true) \
+    X(2, 1, 2, 2, 0, 1, true) X(2, 1, 2, 2, 0, 2, true) X(1, 2, 4, 2, 0, 1, true)
 
 int init_attrs() {
     static int done = 0;
@@ -996,6 +1172,8 @@ int init_attrs() {
     FOR_EACH_LINEAR(SET_ATTR)
 #undef SET_ATTR
     HIPCHK(hipFuncSetAttribute((const void*)cem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024));
     if (rc) return TDMPC_E_HIP;
     done = 1;
     return 0;
@@ -1028,8 +1206,23 @@ int thr_rows() {
     return v;
 }
 
+// throughput tile variant (development knob TDMPC_THR_VARIANT): 0 = LDS-staged 128x128 (default),
+// register-direct: 5 = 128x128 4 waves, 1 = 128x128 8 waves (K split in 2), 2 = 128x64 4 waves,
+// 3 = 128x64 8 waves (K split), 4 = 128x128 8 waves (32x64 each)
+int thr_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("TDMPC_THR_VARIANT");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+
 LinCfg pick_cfg(int M, int nmax, int K, int wn_hint) {
-    if (M >= thr_rows() && nmax >= 256 && K >= 64) return LinCfg{3, 128, 64};
+    if (M >= thr_rows() && nmax >= 256 && K >= 64) {
+        const int v = thr_variant();
+        return LinCfg{3, (v == 2 || v == 3) ? 64 : 128, 64};
+    }
     if (wn_hint == 2) return LinCfg{2, 64, 64};
     return LinCfg{1, 32, 32};
 }
@@ -1037,9 +1230,10 @@ LinCfg pick_cfg(int M, int nmax, int K, int wn_hint) {
 template <int TM, int TN, int WGM, int WGN, int PRO, int KCH, bool ROLL>
 int launch_lin_t(const LinArgs& a, int nprob, int nmax, int cfg_id, hipStream_t s) {
     constexpr int R = 32 * TM * WGM, C = 32 * TN * WGN;
-    const int KS = ROLL ? 1 : (a.K + KCH - 1) / KCH;
+    // ROLL: KCH is the number of K splits (1 or 2), each wave group rolls over K/KCH
+    const int KS = ROLL ? KCH : (a.K + KCH - 1) / KCH;
     LinArgs b = a;
-    b.kch = ROLL ? a.K : KCH;
+    b.kch = ROLL ? (int)rup((a.K + KCH - 1) / KCH, 8) : KCH;
     dim3 grid((a.M + R - 1) / R, (nmax + C - 1) / C, nprob);
     dim3 block(64 * WGM * WGN * KS);
     const size_t lds = ((size_t)KS * R * (C + 4) + 2 * C + (size_t)R * std::max(a.rpart_nt, 1)) * 4;
@@ -1057,14 +1251,41 @@ int launch_lin_t(const LinArgs& a, int nprob, int nmax, int cfg_id, hipStream_t 
     return 0;
 }
 
+int launch_lds(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
+    constexpr int R = 128, C = 128;
+    dim3 grid((a.M + R - 1) / R, (nmax + C - 1) / C, nprob);
+    const size_t lds = ((size_t)R * (C + 4) + 2 * C + (size_t)R * std::max(a.rpart_nt, 1)) * 4;
+    Profiler& pf = g_prof;
+    const bool prof = pf.armed && (pf.cfg == 0 || pf.cfg == 3) && (pf.pro <= 0) && pf.n + 2 <= pf.cap &&
+                      (pf.kdim == 0 || (a.K == pf.kdim && nmax == pf.kdim));
+    if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], s));
+    hipLaunchKernelGGL(linear_lds_kernel<0>, grid, dim3(256), lds, s, a);
+    HIPCHK(hipGetLastError());
+    if (prof) {
+        HIPCHK(hipEventRecord(pf.ev[pf.n + 1], s));
+        pf.n += 2;
+        for (int q = 0; q < nprob; ++q) pf.flops += 2.0 * a.M * std::min(a.p[q].N, nmax) * a.K;
+    }
+    return 0;
+}
+
 // Launch one fused linear layer with the configuration pick_cfg selects.
 int launch_lin(const LinArgs& a, int nprob, int nmax, int wn_hint, int pro, hipStream_t s) {
     if (a.M <= 0) return 0;
     if (a.K % 8) { snprintf(g_err, sizeof g_err, "bad K %d", a.K); return TDMPC_E_DIMS; }
     const LinCfg cfg = pick_cfg(a.M, nmax, a.K, wn_hint);
     if (cfg.id == 3) {
-        if (pro == PRO_PLAIN) return launch_lin_t<2, 2, 2, 2, 0, 8, true>(a, nprob, nmax, 3, s);
-        return launch_lin_t<2, 2, 2, 2, 1, 8, true>(a, nprob, nmax, 3, s);
+        const int v = thr_variant();
+        if (v == 0 && pro == PRO_PLAIN) return launch_lds(a, nprob, nmax, s);
+        if (pro == PRO_PLAIN) {
+            if (v == 1) return launch_lin_t<2, 2, 2, 2, 0, 2, true>(a, nprob, nmax, 3, s);
+            if (v == 2) return launch_lin_t<2, 1, 2, 2, 0, 1, true>(a, nprob, nmax, 3, s);
+            if (v == 3) return launch_lin_t<2, 1, 2, 2, 0, 2, true>(a, nprob, nmax, 3, s);
+            if (v == 4) return launch_lin_t<1, 2, 4, 2, 0, 1, true>(a, nprob, nmax, 3, s);
+            return launch_lin_t<2, 2, 2, 2, 0, 1, true>(a, nprob, nmax, 3, s);
+        }
+        if (v == 1) return launch_lin_t<2, 2, 2, 2, 1, 2, true>(a, nprob, nmax, 3, s);
+        return launch_lin_t<2, 2, 2, 2, 1, 1, true>(a, nprob, nmax, 3, s);
     }
     int kch = 32;
     if ((a.K + 31) / 32 > 8) kch = 64;
@@ -1195,7 +1416,7 @@ int terminal_q(const Ctx& c, float discH, float* value_out, int I, int iter) {
     const Layout& w = c.w;
     const int rows = c.B * c.T, M = c.M;
     int rc;
-    {   // y1 = Wq1[Q1;Q2] [a|z] + b, with LayerNorm partial moments per 64 columns
+    {   // y1 = Wq1[Q1;Q2] [a|z] + b -> H1, with LayerNorm partial moments per 64 columns
         LinArgs a = args0();
         a.M = rows; a.K = c.Kx;
         LinProb& p = a.p[0];
@@ -1204,22 +1425,27 @@ int terminal_q(const Ctx& c, float discH, float* value_out, int I, int iter) {
         p.st_out = c.k.st1; p.st_ld = 2 * M / 64;
         if ((rc = launch_lin(a, 1, 2 * M, 2, PRO_PLAIN, c.s))) return rc;
     }
-    {   // y2_p = Wq2_p tanh(LN(y1_p)) + b, moments again
+    {   // a1 = tanh(LN(y1)) -> H2
+        LnArgs l;
+        l.Y = c.k.H1; l.O = c.k.H2; l.ts = (long)2 * M * 32; l.st = c.k.st1; l.st_ld = 2 * M / 64; l.M_ = M;
+        l.rows = rows; l.g = c.pw + w.g1; l.b = c.pw + w.be1;
+        hipLaunchKernelGGL(ln_tanh_kernel, dim3((rows + 31) / 32, 2 * M / 64), dim3(256), 0, c.s, l);
+        HIPCHK(hipGetLastError());
+    }
+    {   // y2_p = Wq2_p a1_p + b -> H1, moments again
         LinArgs a = args0();
         a.M = rows; a.K = M;
         for (int q = 0; q < 2; ++q) {
             LinProb& p = a.p[q];
-            p.A = hop(c.k.H1, c, q * M / 4); p.W = wop(c, w.wq2 + (size_t)q * M * M, M);
-            p.bias = c.pw + w.bq2 + q * M; p.C = hout(c.k.H2, c, q * M / 4); p.N = p.nvalid = p.nstore = M;
+            p.A = hop(c.k.H2, c, q * M / 4); p.W = wop(c, w.wq2 + (size_t)q * M * M, M);
+            p.bias = c.pw + w.bq2 + q * M; p.C = hout(c.k.H1, c, q * M / 4); p.N = p.nvalid = p.nstore = M;
             p.epi = EPI_LNSTATS; p.st_out = c.k.st2 + q * (M / 64); p.st_ld = 2 * M / 64;
-            p.ln_stats = c.k.st1; p.ln_ld = 2 * M / 64; p.ln_t0 = q * (M / 64); p.ln_nt = M / 64;
-            p.ln_g = c.pw + w.g1 + q * M; p.ln_b = c.pw + w.be1 + q * M;
         }
-        if ((rc = launch_lin(a, 2, M, 2, PRO_LN_TANH, c.s))) return rc;
+        if ((rc = launch_lin(a, 2, M, 2, PRO_PLAIN, c.s))) return rc;
     }
     {
         ValueArgs v;
-        v.Y = c.k.H2; v.yts = (long)2 * M * 32; v.st = c.k.st2; v.st_ld = 2 * M / 64; v.M_ = M;
+        v.Y = c.k.H1; v.yts = (long)2 * M * 32; v.st = c.k.st2; v.st_ld = 2 * M / 64; v.M_ = M;
         v.g2 = c.pw + w.g2; v.be2 = c.pw + w.be2; v.w3 = c.pw + w.wq3; v.b3 = c.pw + w.bq3;
         v.G = c.k.G; v.disc = discH; v.value = c.k.value; v.value_out = value_out; v.rows = rows;
         v.T = c.T; v.I = I; v.iter = iter;
