@@ -3,20 +3,25 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config humanoid-run] [--envs-per-gpu B]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
-A "step" is one planning call: one full TDMPC.plan (N=512 candidates, H=5, 6 CEM iterations, the
-pi pre-rollout, final elite choice) for each of the B environments a GPU owns. Inputs (observations, weights)
-are synthetic and resident on the device; noise is drawn on the device inside the timed region.
+Workload (BASELINE.json configs[2], the north-star target): humanoid-run, N=512 candidates, H=5, 6 CEM
+iterations, mixture 0.5 (P=256 pi trajectories, T=768 rows), K=64 elites, latent 100 (cfgs/tasks/humanoid.yaml:6),
+fp32. A "step" is one planning call for the B environments a GPU owns: B complete, independent TDMPC.plan
+computations (each env its own observation, noise, CEM state and elite choice; bitwise identical to B separate
+single-env calls, tests/test_gpu_plan.py::test_batched_equals_single). The default B = 8 is the vectorised-env
+sharding of BASELINE.json configs[3] ("8 per GPU"); the single-env drop-in path (B = 1, one plan() per call,
+latency-bound) is timed in the same run and reported under "single_env".
 
-Multi-GPU: environments are independent units; each rank plans its own B envs with its own
-weight replica. With --envs-per-gpu > 1 (the vectorised-env config) every step ends with one RCCL
-all-gather of the per-env results ([B, A+2]: action + reward-mean + std) so every rank holds the whole
-vectorised env batch; with one env per GPU the ranks are independent replicas (no collective).
+Multi-GPU: environments are independent units, so every rank plans its own B envs on its own
+weight replica (weak scaling) and each step ends with one RCCL all-gather over xGMI of the per-env results
+([B, A+2]: action, reward mean, std) so that every rank holds the whole vectorised batch.
 
-Rank 0 prints ONE JSON line (the driver's contract), including
-  roofline     : the dominant kernel (linear_kernel<1,0,64>: every hidden 512x512 Linear) -- algorithmic
-                 FLOPs per launch / its average launch time, HIP events on its stream over the timed region;
-  cpu_baseline : the oracle's CPU restatement of the reference plan() (bit-exact to the reference, see
-                 tests/test_oracle.py) timed on this host's cores over a bounded sample.
+Rank 0 prints ONE JSON line with, besides the driver's contract fields,
+  roofline     : the dominant kernel class (the hidden M x M Linear layers: 2 x 5 per CEM iteration + pi's)
+                 -- algorithmic FLOPs per launch / average launch time, HIP events around every launch on its
+                 stream over a timed replay of the same steps; traffic from profiles/pmc_traffic.json (rocprofv3
+                 PMC FETCH_SIZE x2 + WRITE_SIZE per launch, MI355X_MICROARCH.md §HBM correction) when present;
+  cpu_baseline : the oracle's CPU restatement of the reference plan() (pinned bit-exact to the reference's own
+                 outputs, tests/test_oracle.py) timed on this host's cores over a bounded sample.
 """
 from __future__ import annotations
 
@@ -39,13 +44,13 @@ from tdmpc_amd.tdmpc import TDMPC  # noqa: E402
 from tdmpc_amd.told import synthetic_state_dict  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector peak (spec)
-DOMINANT = (1, 0, 64)      # linear_kernel<WN=1, PRO_PLAIN, KCH=64>: the M x M hidden layers
 
 
 def plan_flops(cfg, executed: bool) -> float:
     """Algorithmic FLOPs of one plan-step: 2*[P*H*(pi+d+R) + I*T*(H*(d+R) + pi + 2Q) + enc].
-    executed=True counts what this build runs: the pi rows' H-step rollout is computed once per plan
-    (identical in every CEM iteration) so per iteration only N rows are rolled out."""
+    executed=True counts what this build runs: the pi rows' H-step rollout is identical in every CEM
+    iteration (same z0, same pi actions), so it is computed once per plan and only N rows are rolled out
+    per iteration."""
     L, A, M, E = cfg.latent_dim, cfg.action_dim, cfg.mlp_dim, cfg.enc_dim
     N = cfg.num_samples
     P = int(cfg.mixture_coef * N)
@@ -55,7 +60,7 @@ def plan_flops(cfg, executed: bool) -> float:
     pi = L * M + M * M + M * A
     Q = (L + A) * M + M * M + M
     if cfg.modality == "pixels":
-        enc = 0  # conv encoder counted separately below
+        enc = 0
         s, c, ch = cfg.img_size, 3 * cfg.frame_stack, cfg.num_channels
         for k in (7, 5, 3, 3):
             so = (s - k) // 2 + 1
@@ -79,8 +84,8 @@ def synthetic_obs(cfg, B, seed=0):
 
 
 def cpu_baseline(cfg, budget_s: float):
-    """Time the oracle (CPU restatement of the reference plan(), pinned bit-exact to the reference's golden
-    vectors) on this host: 2 warm-up calls, then calls until `budget_s` of CPU work (>= 5 calls)."""
+    """Time the oracle (CPU restatement of the reference plan(), bit-exact to the reference's golden vectors)
+    on this host: 2 warm-up calls, then calls until `budget_s` seconds of CPU work (>= 5 calls), median."""
     from oracle import tdmpc_ref
     threads = int(os.environ.get("TDMPC_CPU_THREADS", min(16, os.cpu_count() or 1)))
     torch.set_num_threads(threads)
@@ -89,14 +94,14 @@ def cpu_baseline(cfg, budget_s: float):
     obs = synthetic_obs(cfg, 1)[0]
     step = 10**6
     times = []
-    for i in range(2 + 200):
+    for i in range(2 + 400):
         nb = tdmpc_ref.draw_noise(cfg, step, False)
         t = time.perf_counter()
         tdmpc_ref.plan(told, cfg, st, obs, nb, eval_mode=False, step=step, t0=(i == 0))
         dt = time.perf_counter() - t
         if i >= 2:
             times.append(dt)
-        if i >= 6 and sum(times) > budget_s:
+        if len(times) >= 5 and sum(times) > budget_s:
             break
     med = float(np.median(times))
     cpu_model = ""
@@ -108,8 +113,34 @@ def cpu_baseline(cfg, budget_s: float):
     except OSError:
         pass
     return {"value": round(1.0 / med, 3), "unit": "plan-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{len(times)} plan() calls of {cfg.task} N={cfg.num_samples} H={cfg.horizon} "
-                      f"I={cfg.iterations} after 2 warm-up (median), torch CPU fp32, {cpu_model}"}
+            "sample": f"{len(times)} plan() calls ({sum(times):.1f} s) of {cfg.task} N={cfg.num_samples} "
+                      f"H={cfg.horizon} I={cfg.iterations} L={cfg.latent_dim} after 2 warm-up, median; "
+                      f"torch CPU fp32, {threads} threads, {cpu_model}"}
+
+
+def make_agent(cfg, B, rng, graph, seed):
+    torch.manual_seed(seed)
+    agent = TDMPC(cfg, max_batch=B, rng=rng, graph=graph)
+    agent.model.load_state_dict(synthetic_state_dict(cfg, 0))
+    agent.std = 0.05   # trained-regime value of std_schedule
+    return agent
+
+
+def time_steps(step_fn, warmup, steps, dist):
+    for i in range(warmup):
+        step_fn(i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step_fn(warmup + i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
 
 
 def main():
@@ -118,12 +149,13 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="humanoid-run")
-    ap.add_argument("--envs-per-gpu", type=int, default=1)
+    ap.add_argument("--envs-per-gpu", type=int, default=8)
     ap.add_argument("--rng", default="fused", choices=["fused", "reference"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-single", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -139,39 +171,20 @@ def main():
     cfg = bench_cfg(args.config)
     cfg.device = f"cuda:{local}"
     B = args.envs_per_gpu
-    torch.manual_seed(1 + rank)
+    graph = not args.no_graph
     np.random.seed(2 + rank)
-    agent = TDMPC(cfg, max_batch=B, rng=args.rng, graph=not args.no_graph)
-    agent.model.load_state_dict(synthetic_state_dict(cfg, 0))
-    agent.std = 0.05
-    obs_np = synthetic_obs(cfg, B, seed=rank)
-    obs = torch.from_numpy(obs_np).to(dev)
+    agent = make_agent(cfg, B, args.rng, graph, 1 + rank)
+    obs = torch.from_numpy(synthetic_obs(cfg, B, seed=rank)).to(dev)
     step = 10**6
-    gather_buf = None
-    if dist is not None and B > 1:
-        gather_buf = torch.empty(world, B, cfg.action_dim + 2, device=dev)
+    gather_buf = torch.empty(world, B, cfg.action_dim + 2, device=dev) if dist is not None else None
 
-    def one_step(i):
-        a, m = agent.plan_batch(obs, step=step, t0=(i % 100 == 0), sync_metrics=False)
+    def one_step(i, ag=agent, ob=obs):
+        a, m = ag.plan_batch(ob, step=step, t0=(i % 100 == 0), sync_metrics=False)
         if gather_buf is not None:
-            local_res = torch.cat([a, m], dim=1)
-            dist.all_gather_into_tensor(gather_buf, local_res)
+            dist.all_gather_into_tensor(gather_buf, torch.cat([a, m], dim=1))
         return a
 
-    for i in range(args.warmup):
-        one_step(i)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        one_step(args.warmup + i)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed = time_steps(one_step, args.warmup, args.steps, dist)
     if dist is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -179,34 +192,38 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
 
-    # ---- roofline of the dominant kernel: HIP events around every launch of it, eager replay of the same
-    # steps (graph replay cannot carry events), same stream the kernel runs on.
+    # ---- roofline of the dominant kernel class: HIP events around each launch, eager replay of the same
+    # steps on the same stream (graph replays cannot carry the events)
     roof = None
     if not args.no_roofline:
         L = _lib.lib()
-        steps_r = max(3, min(args.steps, 10))
-        graph_state = agent.graph
         agent.graph = False
         one_step(0)
         torch.cuda.synchronize()
-        _lib.check(L.tdmpc_profile_begin(0, 0, cfg.mlp_dim, 4096), "profile_begin")
-        for i in range(steps_r):
+        n_r = max(3, min(args.steps, 10))
+        _lib.check(L.tdmpc_profile_begin(0, 0, cfg.mlp_dim, 8192), "profile_begin")
+        for i in range(n_r):
             one_step(1 + i)
         n, ms, fl = C.c_int32(), C.c_double(), C.c_double()
         _lib.check(L.tdmpc_profile_end(C.byref(n), C.byref(ms), C.byref(fl)), "profile_end")
-        agent.graph = graph_state
+        agent.graph = graph
         avg_s = ms.value / max(n.value, 1) * 1e-3
         per_launch = fl.value / max(n.value, 1)
         achieved = per_launch / avg_s / 1e12
+        thr = B * cfg.num_samples >= int(os.environ.get("TDMPC_THR_ROWS", "2048"))
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                "kernel": "linear_kernel<1,0,64> (hidden MxM Linear, fp32 MFMA 32x32x2)",
-                "launches": n.value, "avg_launch_us": round(avg_s * 1e6, 3),
-                "flops_per_launch": per_launch}
+                "kernel": ("linear_lds_kernel (128x128 LDS-staged tile)" if thr else
+                           "linear_kernel<1,1,1,1> (32x32 tile, 8-way K split)") +
+                          f": hidden {cfg.mlp_dim}x{cfg.mlp_dim} Linear + ELU, fp32 v_mfma_f32_32x32x2_f32",
+                "launches": n.value, "avg_launch_us": round(avg_s * 1e6, 3), "flops_per_launch": per_launch}
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
-                roof["traffic"] = json.load(open(pmc)).get(args.config)
+                t = json.load(open(pmc)).get(f"{args.config}/B{B}")
+                if t:
+                    roof["traffic"] = t.get("hbm_bytes_per_launch")
+                    roof["traffic_source"] = t.get("source")
             except (OSError, ValueError):
                 pass
 
@@ -215,6 +232,16 @@ def main():
     plan_roof = {"flop_per_plan_step_algorithmic": fl_alg, "flop_per_plan_step_executed": fl_exec,
                  "tflops_per_gpu_algorithmic": round(value / world * fl_alg / 1e12, 3),
                  "frac_of_fp32_peak": round(value / world * min(fl_alg, fl_exec) / 1e12 / FP32_PEAK_TFLOPS, 4)}
+
+    single = None
+    if not args.no_single and world == 1:
+        a1 = make_agent(cfg, 1, args.rng, graph, 7)
+        o1 = obs[:1].clone()
+        ks = max(10, args.steps // 2)
+        el1 = time_steps(lambda i: a1.plan_batch(o1, step=step, t0=(i % 100 == 0), sync_metrics=False),
+                         3, ks, None)
+        single = {"value": round(ks / el1, 3), "unit": "plan-steps/s", "ms_per_step": round(el1 / ks * 1e3, 4),
+                  "note": "one env per plan() call (the drop-in TDMPC.plan path), same GPU, same run"}
 
     cpu = None
     if rank == 0 and not args.no_cpu and world == 1:
@@ -226,19 +253,22 @@ def main():
             "value": round(value, 3), "unit": "plan-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-            "data": "synthetic (seeded N(0,1/fan_in) TOLD weights, N(0,1) obs; noise drawn on device)",
+            "data": "synthetic: seeded N(0,1/fan_in) TOLD weights, N(0,1) observations, noise drawn on device",
             "config": {"workload": f"{args.config}: TDMPC.plan N={cfg.num_samples} H={cfg.horizon} "
-                                   f"iters={cfg.iterations} L={cfg.latent_dim} A={cfg.action_dim}",
+                                   f"iters={cfg.iterations} mixture={cfg.mixture_coef} K={cfg.num_elites} "
+                                   f"L={cfg.latent_dim} A={cfg.action_dim}, {B} envs per GPU",
                        "envs_per_gpu": B, "global_envs": B * world,
-                       "parallelism": f"env-shard x{world}" + (" + rccl all-gather" if gather_buf is not None
-                                                               else " (independent replicas)"),
-                       "rng": args.rng, "hip_graph": not args.no_graph},
+                       "parallelism": f"env-shard x{world}" + (" + rccl all-gather" if world > 1 else ""),
+                       "rng": args.rng, "hip_graph": graph},
             "roofline": roof,
             "plan_roofline": plan_roof,
+            "single_env": single,
             "cpu_baseline": cpu,
         }
         if cpu:
             out["speedup_vs_cpu"] = round(value / world / cpu["value"], 2)
+            if single:
+                out["single_env"]["speedup_vs_cpu"] = round(single["value"] / cpu["value"], 2)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

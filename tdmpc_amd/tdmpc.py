@@ -66,15 +66,20 @@ class HipPlanner:
         else:
             self.obs_buf = torch.zeros(max_batch, cfg.obs_shape[0], dtype=torch.float32, device=dev)
         self._packed_key = None
+        self._packed_model = None
+        self._packed_params = []
         self._graphs = {}
 
     # ------------------------------------------------------------------ weights
     def pack(self, model: TOLD):
         """Pack TOLD parameters when any of them changed (in-place updates bump tensor versions)."""
+        if self._packed_key is not None and self._packed_model is model:
+            key = tuple((p.data_ptr(), p._version) for p in self._packed_params)
+            if key == self._packed_key:
+                return
         params = list(model.state_dict().values())
+        self._packed_model, self._packed_params = model, params
         key = tuple((p.data_ptr(), p._version) for p in params)
-        if key == self._packed_key:
-            return
         params = [p.detach().to(self.device, torch.float32).contiguous() for p in params]
         n = self.L.tdmpc_num_param_tensors(C.byref(self.dims))
         if n != len(params):
@@ -315,10 +320,11 @@ class TDMPC:
             for e, nb in enumerate(noise):
                 pl.load_noise(e, H, I, nb.eps_pi, nb.eps_cem, nb.eps_term, nb.eps_act)
                 us.append(float(nb.u))
-        else:
-            us = list(np.random.random_sample(B)) if self.rng == "fused" else \
-                [float(np.random.random_sample()) for _ in range(B)]
-        pl.u[:B].copy_(torch.tensor(us, dtype=torch.float64))
+            pl.u[:B].copy_(torch.tensor(us, dtype=torch.float64))
+        elif self.rng == "reference":
+            # np.random.choice's uniform, drawn on the host from numpy's global generator (tdmpc.py:153)
+            pl.u[:B].copy_(torch.tensor([float(np.random.random_sample()) for _ in range(B)],
+                                        dtype=torch.float64))
 
         def device_work():
             if noise is None:
@@ -327,6 +333,7 @@ class TDMPC:
                         pl.draw_reference_torch(e, H, I, eval_mode)
                 else:
                     pl.noise_view(H, I, B).normal_()
+                    pl.u[:B].uniform_()
             pl.launch(prm, obs_u8, trace)
 
         if self.graph and noise is None and trace is None:
