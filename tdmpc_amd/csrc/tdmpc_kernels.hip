@@ -585,101 +585,112 @@ __global__ void __launch_bounds__(512) linear_kernel(const LinArgs args) {
 #endif
 }
 
-// Throughput configuration for large row counts: LDS-staged, double-buffered 128x128 output tile.
-// 4 waves in a 2x2 grid, each owning a 64x64 register tile (2x2 MFMA 32x32 tiles), over K tiles of 32.
-// With the panel layout, one K tile of one 32-row block is a contiguous 4 KiB, so a workgroup stages
-// A (4 blocks) and W (4 blocks) with one 1 KiB wave load per block per wave and every fragment read is a
-// conflict-free ds_read_b128. Global traffic per MFMA is half the register-direct kernel's.
-template <int PRO_UNUSED>
-__global__ void __launch_bounds__(256) linear_lds_kernel(const LinArgs args) {
+// Throughput configuration for large row counts: LDS-staged, double-buffered output tile of 128 rows x
+// C = 32*TN*WGN columns over K tiles of 32. WGM x WGN waves (2x2 or 2x4), each owning a (32*TM) x (32*TN)
+// register tile. With the panel layout one K tile of one 32-row block is a contiguous 4 KiB, so staging is
+// 1 KiB wave loads and every fragment read is a conflict-free ds_read_b128; global traffic per MFMA is
+// shared by the whole workgroup.
+template <int TM, int TN, int WGM, int WGN>
+__global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArgs args) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int R = 128, C = 128, STAGE = 4096;    // floats per 32-row block x 8 quads... x4 blocks
+    constexpr int R = 32 * TM * WGM, C = 32 * TN * WGN, NT = 64 * WGM * WGN;
+    constexpr int RB = R / 32, CB = C / 32;            // 32-row / 32-col blocks
+    constexpr int SA = RB * 1024, SW = CB * 1024;      // floats per stage (8 quads x 32 x 4 per block)
+    constexpr int CA = RB * 256 / NT, CW = CB * 256 / NT;   // 16-B chunks per thread per stage
+    static_assert(R == 128, "throughput tile is 128 rows");
     const LinProb& P = args.p[blockIdx.z];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int wm = wave & 1, wn = wave >> 1;
+    const int wm = wave % WGM, wn = wave / WGM;
     const int m0 = blockIdx.x * R, n0 = blockIdx.y * C;
     if (n0 >= P.N) return;
     const int epi = P.epi;
-    // LDS: stage buffers [2][A 4096 | W 4096] (aliased by the epilogue tile [128][132] afterwards),
-    // then bias [C], dotw [C], rpart [R][nt]
-    float* sbias = smem + R * (C + 4);
+    // LDS: stage buffers [2][SA + SW] aliased by the epilogue tile [R][C+4]; then bias, dotw, rpart
+    constexpr int BUF = SA + SW;
+    constexpr int EPI_F = R * (C + 4);
+    constexpr int BODY = 2 * BUF > EPI_F ? 2 * BUF : EPI_F;
+    float* sbias = smem + BODY;
     float* sdotw = sbias + C;
     float* srp = sdotw + C;
-    for (int i = tid; i < C / 4; i += 256) {
+    for (int i = tid; i < C / 4; i += NT) {
         const int n = n0 + 4 * i;
         *(float4*)(sbias + 4 * i) = *(const float4*)(P.bias + n);
         if (epi == EPI_ELU_DOT) *(float4*)(sdotw + 4 * i) = *(const float4*)(P.dotw + n);
     }
     if (epi == EPI_LIN_Z && blockIdx.y == 0)
-        for (int i = tid; i < R * args.rpart_nt; i += 256) {
+        for (int i = tid; i < R * args.rpart_nt; i += NT) {
             const int lm = m0 + i / args.rpart_nt;
             srp[i] = lm < args.M ? args.rpart[(size_t)lm * args.rpart_nt + i % args.rpart_nt] : 0.f;
         }
 
-    // this thread's staging slots: rows m0 + 32*i + (tid&31) (i < 4), quad (tid>>5) of each K tile
-    const int sq = tid >> 5, sr = tid & 31;
-    const float* Arow[4];
-    int arow[4], env[4];
+    // staging slots: chunk c = tid + i*NT of a stage -> block c>>8, quad (c>>5)&7, row c&31
+    const float* Asrc[CA];
+    int arow[CA], env[CA];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int m = m0 + 32 * i + sr;
+    for (int i = 0; i < CA; ++i) {
+        const int cidx = tid + i * NT;
+        const int m = m0 + (cidx >> 8) * 32 + (cidx & 31);
         const int mm = m < args.M ? m : 0;
         arow[i] = args.a_mapped ? map_row(args.amap, mm) : mm;
-        Arow[i] = P.A.p + (size_t)(arow[i] >> 5) * P.A.ts + (arow[i] & 31) * 4;
+        Asrc[i] = P.A.p + (size_t)(arow[i] >> 5) * P.A.ts + (arow[i] & 31) * 4;
         env[i] = (args.zmode | args.smode) ? arow[i] / args.rows_per_env : 0;
     }
-    const float* Wrow = P.W.p + (size_t)(n0 >> 5) * P.W.ts + sr * 4;
+    const float* Wsrc = P.W.p + (size_t)(n0 >> 5) * P.W.ts;
     const int kq_total = args.K >> 2;
-    auto stage_load = [&](int kt, float4 (&ra)[4], float4 (&rw)[4]) {
-        const int kq = kt * 8 + sq;
-        const bool ok = kq < kq_total;
+    auto stage_load = [&](int kt, float4 (&ra)[CA], float4 (&rw)[CW]) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            ra[i] = ok ? load_a(args, Arow[i], P.A.q0 + kq, arow[i], env[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
-            rw[i] = ok ? *(const float4*)(Wrow + (size_t)i * P.W.ts + (size_t)kq * 128) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = 0; i < CA; ++i) {
+            const int cidx = tid + i * NT;
+            const int kq = kt * 8 + ((cidx >> 5) & 7);
+            ra[i] = kq < kq_total ? load_a(args, Asrc[i], P.A.q0 + kq, arow[i], env[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < CW; ++i) {
+            const int cidx = tid + i * NT;
+            const int kq = kt * 8 + ((cidx >> 5) & 7);
+            rw[i] = kq < kq_total ? *(const float4*)(Wsrc + (size_t)(cidx >> 8) * P.W.ts + (size_t)kq * 128 + (cidx & 31) * 4)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
-    auto stage_store = [&](int buf, const float4 (&ra)[4], const float4 (&rw)[4]) {
-        float* sA = smem + buf * 2 * STAGE;
-        float* sW = sA + STAGE;
+    auto stage_store = [&](int buf, const float4 (&ra)[CA], const float4 (&rw)[CW]) {
+        float* sA = smem + buf * BUF;
+        float* sW = sA + SA;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            *(float4*)(sA + ((i * 8 + sq) * 32 + sr) * 4) = ra[i];
-            *(float4*)(sW + ((i * 8 + sq) * 32 + sr) * 4) = rw[i];
-        }
+        for (int i = 0; i < CA; ++i) *(float4*)(sA + (tid + i * NT) * 4) = ra[i];
+#pragma unroll
+        for (int i = 0; i < CW; ++i) *(float4*)(sW + (tid + i * NT) * 4) = rw[i];
     };
 
-    floatx16 acc[2][2];
+    floatx16 acc[TM][TN];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
     const int nst = (args.K + 31) >> 5;
-    float4 ra[4], rw[4];
+    float4 ra[CA], rw[CW];
     stage_load(0, ra, rw);
     stage_store(0, ra, rw);
     __syncthreads();
     for (int st = 0; st < nst; ++st) {
         const int buf = st & 1;
         if (st + 1 < nst) stage_load(st + 1, ra, rw);
-        const float* sA = smem + buf * 2 * STAGE;
-        const float* sW = sA + STAGE;
+        const float* sA = smem + buf * BUF;
+        const float* sW = sA + SA;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             if (st * 32 + 8 * g < args.K) {
-                float4 a[2], b[2];
+                float4 a[TM], b[TN];
 #pragma unroll
-                for (int i = 0; i < 2; ++i) a[i] = *(const float4*)(sA + (((wm * 2 + i) * 8 + 2 * g + h) * 32 + r) * 4);
+                for (int i = 0; i < TM; ++i) a[i] = *(const float4*)(sA + (((wm * TM + i) * 8 + 2 * g + h) * 32 + r) * 4);
 #pragma unroll
-                for (int j = 0; j < 2; ++j) b[j] = *(const float4*)(sW + (((wn * 2 + j) * 8 + 2 * g + h) * 32 + r) * 4);
+                for (int j = 0; j < TN; ++j) b[j] = *(const float4*)(sW + (((wn * TN + j) * 8 + 2 * g + h) * 32 + r) * 4);
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < TM; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
+                    for (int j = 0; j < TN; ++j) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
@@ -690,13 +701,13 @@ __global__ void __launch_bounds__(256) linear_lds_kernel(const LinArgs args) {
         if (st + 1 < nst) stage_store(buf ^ 1, ra, rw);
         __syncthreads();
     }
-    // accumulators -> LDS tile [128][132] (the stage buffers are free after the last barrier)
+    // accumulators -> LDS tile [R][C+4] (the stage buffers are free after the last barrier)
     {
-        float* base = smem + (size_t)(wm * 64) * (C + 4) + wn * 64;
+        float* base = smem + (size_t)(wm * TM * 32) * (C + 4) + wn * TN * 32;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int e = 0; e < 16; ++e)
                     base[(size_t)(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * (C + 4) + j * 32 + r] = acc[i][j][e];
@@ -708,19 +719,18 @@ __global__ void __launch_bounds__(256) linear_lds_kernel(const LinArgs args) {
 // ------------------------------------------------------------------------------------------------ LN+tanh
 // a1 = tanh(LayerNorm(y1)) for both Q heads (helper.q: Linear -> LayerNorm -> Tanh), computed once per
 // element from the producer's per-64-column moments, so the next GEMM is a plain one. Grid: (row tiles,
-// 64-column blocks); 32 consecutive lanes own 32 consecutive rows of one panel quad (512 B contiguous).
+// Q head); 32 consecutive lanes own 32 consecutive rows of one panel quad (512 B contiguous).
 struct LnArgs {
     const float* Y; float* O; long ts; const float2* st; int st_ld; int M_; int rows;
     const float* g; const float* b;
 };
 
-__global__ void __launch_bounds__(256) ln_tanh_kernel(const LnArgs a) {
-    const int r = threadIdx.x & 31, g = threadIdx.x >> 5;
+__global__ void __launch_bounds__(512) ln_tanh_kernel(const LnArgs a) {
+    const int r = threadIdx.x & 31, g = threadIdx.x >> 5;   // 16 threads per row
     const int row = blockIdx.x * 32 + r;
     if (row >= a.rows) return;
-    const int c0 = blockIdx.y * 64;            // 64-column block, inside one head (M % 64 == 0)
-    const int p = c0 / a.M_;
-    const int ntile = a.M_ / 64;
+    const int p = blockIdx.y;                                 // Q head
+    const int ntile = a.M_ / 64, nq = a.M_ / 4;
     const float2* st = a.st + (size_t)row * a.st_ld + p * ntile;
     float n = 0.f, mean = 0.f, m2 = 0.f;
     for (int i = 0; i < ntile; ++i) {
@@ -733,9 +743,9 @@ __global__ void __launch_bounds__(256) ln_tanh_kernel(const LnArgs a) {
     const float rs = 1.0f / sqrtf(fmaxf(m2 / n, 0.f) + 1e-5f);
     const float sh = -rs * mean;
     const size_t base = (size_t)(row >> 5) * a.ts + (row & 31) * 4;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int c = c0 + 4 * (g + 8 * i);
+#pragma unroll 8
+    for (int q = g; q < nq; q += 16) {
+        const int c = p * a.M_ + 4 * q;
         const float4 y = *(const float4*)(a.Y + base + (size_t)(c >> 2) * 128);
         const float4 gg = *(const float4*)(a.g + c), bb = *(const float4*)(a.b + c);
         float4 o;
@@ -1172,7 +1182,11 @@ int init_attrs() {
     FOR_EACH_LINEAR(SET_ATTR)
 #undef SET_ATTR
     HIPCHK(hipFuncSetAttribute((const void*)cem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<2, 2, 2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<2, 1, 2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<2, 1, 2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                160 * 1024));
     if (rc) return TDMPC_E_HIP;
     done = 1;
@@ -1251,15 +1265,19 @@ int launch_lin_t(const LinArgs& a, int nprob, int nmax, int cfg_id, hipStream_t 
     return 0;
 }
 
-int launch_lds(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
-    constexpr int R = 128, C = 128;
+template <int TM, int TN, int WGM, int WGN>
+int launch_lds_t(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
+    constexpr int R = 32 * TM * WGM, C = 32 * TN * WGN;
+    constexpr int BUF = (R / 32) * 1024 + (C / 32) * 1024;
+    constexpr int EPI_F = R * (C + 4);
+    constexpr int BODY = 2 * BUF > EPI_F ? 2 * BUF : EPI_F;
     dim3 grid((a.M + R - 1) / R, (nmax + C - 1) / C, nprob);
-    const size_t lds = ((size_t)R * (C + 4) + 2 * C + (size_t)R * std::max(a.rpart_nt, 1)) * 4;
+    const size_t lds = ((size_t)BODY + 2 * C + (size_t)R * std::max(a.rpart_nt, 1)) * 4;
     Profiler& pf = g_prof;
     const bool prof = pf.armed && (pf.cfg == 0 || pf.cfg == 3) && (pf.pro <= 0) && pf.n + 2 <= pf.cap &&
                       (pf.kdim == 0 || (a.K == pf.kdim && nmax == pf.kdim));
     if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], s));
-    hipLaunchKernelGGL(linear_lds_kernel<0>, grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN>), grid, dim3(64 * WGM * WGN), lds, s, a);
     HIPCHK(hipGetLastError());
     if (prof) {
         HIPCHK(hipEventRecord(pf.ev[pf.n + 1], s));
@@ -1267,6 +1285,24 @@ int launch_lds(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
         for (int q = 0; q < nprob; ++q) pf.flops += 2.0 * a.M * std::min(a.p[q].N, nmax) * a.K;
     }
     return 0;
+}
+
+int lds_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("TDMPC_LDS_VARIANT");
+        v = e ? atoi(e) : 1;
+    }
+    return v;
+}
+
+// LDS-staged throughput tile: variant 0 = 128x128 with 4 waves (64x64 each), 1 = 128x128 with 8 waves
+// (64x32 each, 2 waves per SIMD), 2 = 128x64 with 4 waves (64x32 each) for mid-size row counts.
+int launch_lds(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
+    const int ctiles128 = (nmax + 127) / 128, rtiles = (a.M + 127) / 128;
+    if (rtiles * ctiles128 * nprob < 192) return launch_lds_t<2, 1, 2, 2>(a, nprob, nmax, s);
+    if (lds_variant() == 0) return launch_lds_t<2, 2, 2, 2>(a, nprob, nmax, s);
+    return launch_lds_t<2, 1, 2, 4>(a, nprob, nmax, s);
 }
 
 // Launch one fused linear layer with the configuration pick_cfg selects.
@@ -1429,7 +1465,7 @@ int terminal_q(const Ctx& c, float discH, float* value_out, int I, int iter) {
         LnArgs l;
         l.Y = c.k.H1; l.O = c.k.H2; l.ts = (long)2 * M * 32; l.st = c.k.st1; l.st_ld = 2 * M / 64; l.M_ = M;
         l.rows = rows; l.g = c.pw + w.g1; l.b = c.pw + w.be1;
-        hipLaunchKernelGGL(ln_tanh_kernel, dim3((rows + 31) / 32, 2 * M / 64), dim3(256), 0, c.s, l);
+        hipLaunchKernelGGL(ln_tanh_kernel, dim3((rows + 31) / 32, 2), dim3(512), 0, c.s, l);
         HIPCHK(hipGetLastError());
     }
     {   // y2_p = Wq2_p a1_p + b -> H1, moments again
