@@ -40,6 +40,7 @@ sys.path.insert(0, REPO)
 
 from tdmpc_amd import _lib  # noqa: E402
 from tdmpc_amd.config import bench_cfg  # noqa: E402
+from tdmpc_amd.parallel import EnvShardedPlanner  # noqa: E402
 from tdmpc_amd.tdmpc import TDMPC  # noqa: E402
 from tdmpc_amd.told import synthetic_state_dict  # noqa: E402
 
@@ -174,15 +175,14 @@ def main():
     graph = not args.no_graph
     np.random.seed(2 + rank)
     agent = make_agent(cfg, B, args.rng, graph, 1 + rank)
-    obs = torch.from_numpy(synthetic_obs(cfg, B, seed=rank)).to(dev)
+    # the global vectorised batch (identical on every rank); each rank plans its contiguous shard
+    global_obs = torch.from_numpy(synthetic_obs(cfg, B * world, seed=0)).to(dev)
+    sharded = EnvShardedPlanner(B * world, cfg.action_dim, agent=agent)
+    obs = sharded.local_obs(global_obs)
     step = 10**6
-    gather_buf = torch.empty(world, B, cfg.action_dim + 2, device=dev) if dist is not None else None
 
-    def one_step(i, ag=agent, ob=obs):
-        a, m = ag.plan_batch(ob, step=step, t0=(i % 100 == 0), sync_metrics=False)
-        if gather_buf is not None:
-            dist.all_gather_into_tensor(gather_buf, torch.cat([a, m], dim=1))
-        return a
+    def one_step(i):
+        return sharded.plan(global_obs, step, t0=(i % 100 == 0))
 
     elapsed = time_steps(one_step, args.warmup, args.steps, dist)
     if dist is not None:
@@ -258,7 +258,7 @@ def main():
                                    f"iters={cfg.iterations} mixture={cfg.mixture_coef} K={cfg.num_elites} "
                                    f"L={cfg.latent_dim} A={cfg.action_dim}, {B} envs per GPU",
                        "envs_per_gpu": B, "global_envs": B * world,
-                       "parallelism": f"env-shard x{world}" + (" + rccl all-gather" if world > 1 else ""),
+                       "parallelism": f"env-shard x{world}" + (" + rccl all-gather of [envs, A+2]" if world > 1 else ""),
                        "rng": args.rng, "hip_graph": graph},
             "roofline": roof,
             "plan_roofline": plan_roof,

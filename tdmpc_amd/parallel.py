@@ -1,0 +1,79 @@
+"""Vectorised-env planning sharded over the GPUs of one node.
+
+Environments are independent units, so a global batch of E = world * B envs is split into contiguous shards:
+rank r owns envs [r*B, (r+1)*B), plans them with its own TDMPC (a full weight replica) and one collective --
+an all-gather of the per-env results [B, A+2] = (action, reward mean, std) -- gives every rank the whole
+vectorised batch. There is no collective inside planning: the only exchange is ~(A+2)*4 bytes per env per
+step, latency-bound over xGMI (RCCL picks its one-shot algorithm at this size). Weight replicas are kept in sync
+by broadcasting the TOLD parameters from one rank (after loading a checkpoint or a learner update).
+
+The reference has no distributed code (its only parallelism is Ray Tune trial scheduling,
+src/train_multi_experiments.py:144-170); this module is the MI355X-native equivalent for the vectorised
+configuration BASELINE.json names ("dog-run, 64 vectorised envs sharded 8-per-GPU across 8xMI355X").
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(n_envs: int, rank: int, world: int):
+    """Contiguous, balanced shard [lo, hi) of `n_envs` envs for `rank` (first n_envs % world ranks get one more)."""
+    base, extra = divmod(n_envs, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+class EnvShardedPlanner:
+    """Plans this rank's shard of a global env batch and all-gathers every env's result.
+
+    plan_fn(obs_shard, step, t0) -> (actions [b, A], metrics [b, 2]) runs on this rank's device; by default it is
+    `agent.plan_batch(..., sync_metrics=False)` of a `tdmpc_amd.TDMPC`. Shards must be equal-sized (the
+    all-gather is a single fixed-size collective); `n_envs % world == 0` is required."""
+
+    def __init__(self, n_envs: int, action_dim: int, agent=None, plan_fn: Optional[Callable] = None,
+                 group=None, device=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if n_envs % self.world:
+            raise ValueError(f"{n_envs} envs do not split evenly over {self.world} ranks")
+        self.n_envs, self.A = n_envs, action_dim
+        self.lo, self.hi = shard_bounds(n_envs, self.rank, self.world)
+        self.agent = agent
+        if plan_fn is None:
+            if agent is None:
+                raise ValueError("need an agent or a plan_fn")
+            plan_fn = lambda obs, step, t0: agent.plan_batch(obs, step=step, t0=t0, sync_metrics=False)  # noqa
+        self.plan_fn = plan_fn
+        self.device = torch.device(device) if device is not None else (
+            agent.device if agent is not None else torch.device("cpu"))
+        b = self.hi - self.lo
+        self._local = torch.empty(b, action_dim + 2, device=self.device)
+        self._all = torch.empty(self.world * b, action_dim + 2, device=self.device)
+
+    def local_obs(self, global_obs):
+        return global_obs[self.lo:self.hi]
+
+    @torch.no_grad()
+    def plan(self, global_obs, step, t0=True):
+        """Plan this rank's envs of `global_obs` ([n_envs, ...]) and return every env's (actions, metrics)."""
+        a, m = self.plan_fn(self.local_obs(global_obs), step, t0)
+        self._local[:, :self.A].copy_(a)
+        self._local[:, self.A:].copy_(m)
+        if self.world > 1:
+            dist.all_gather_into_tensor(self._all, self._local, group=self.group)
+            res = self._all
+        else:
+            res = self._local
+        return res[:, :self.A], res[:, self.A:]
+
+    @torch.no_grad()
+    def broadcast_weights(self, model: torch.nn.Module, src: int = 0):
+        """Make every rank's TOLD replica equal to rank `src`'s (after a checkpoint load or an update)."""
+        if self.world == 1:
+            return
+        for p in model.state_dict().values():
+            dist.broadcast(p, src=src, group=self.group)
