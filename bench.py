@@ -201,7 +201,7 @@ def main():
         one_step(0)
         torch.cuda.synchronize()
         n_r = max(3, min(args.steps, 10))
-        _lib.check(L.tdmpc_profile_begin(0, 0, cfg.mlp_dim, 8192), "profile_begin")
+        _lib.check(L.tdmpc_profile_begin(0, 0, cfg.mlp_dim, B * cfg.num_samples, 8192), "profile_begin")
         for i in range(n_r):
             one_step(1 + i)
         n, ms, fl = C.c_int32(), C.c_double(), C.c_double()
@@ -210,12 +210,13 @@ def main():
         avg_s = ms.value / max(n.value, 1) * 1e-3
         per_launch = fl.value / max(n.value, 1)
         achieved = per_launch / avg_s / 1e12
-        thr = B * cfg.num_samples >= int(os.environ.get("TDMPC_THR_ROWS", "2048"))
+        thr = B * cfg.num_samples >= int(os.environ.get("TDMPC_THR_ROWS", "4096"))
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                "kernel": ("linear_lds_kernel (128x128 LDS-staged tile)" if thr else
-                           "linear_kernel<1,1,1,1> (32x32 tile, 8-way K split)") +
-                          f": hidden {cfg.mlp_dim}x{cfg.mlp_dim} Linear + ELU, fp32 v_mfma_f32_32x32x2_f32",
+                "kernel": ("linear_lds_kernel<2,1,2,4,32> (128x128 LDS-staged tile)" if thr else
+                           "linear_kernel<1,2,1,1,0,64> (32x64 tile, 8-way K split)") +
+                          f": CEM rollout layer 2 (dynamics + reward hidden {cfg.mlp_dim}x{cfg.mlp_dim} Linear + "
+                          f"ELU, {B * cfg.num_samples} rows x 2 problems), fp32 v_mfma_f32_32x32x2_f32",
                 "launches": n.value, "avg_launch_us": round(avg_s * 1e6, 3), "flops_per_launch": per_launch}
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define TDMPC_ABI_VERSION 1
+#define TDMPC_ABI_VERSION 2
 
 #define TDMPC_OK 0
 #define TDMPC_E_DIMS (-1)     /* unsupported or inconsistent dims / params */
@@ -140,11 +140,12 @@ int tdmpc_estimate_value(const tdmpc_dims* dims, const tdmpc_plan_params* params
 /* Diagnostic kernel timer for the roofline report (bench.py). Arms a per-thread recorder: every later
  * linear_kernel launch issued from this thread with launch configuration `cfg` (1 = latency 32x32 tile,
  * 2 = latency 32x64 tile, 3 = throughput 128x128 tile, 0 = any) and prologue `pro` (0 plain, 1 LayerNorm,
- * -1 any) -- restricted to K == N == kdim when kdim > 0 (the hidden kdim x kdim layers) -- is bracketed by
+ * -1 any) -- restricted to K == N == kdim when kdim > 0 (the hidden kdim x kdim layers) and to launches over
+ * exactly `rows` rows when rows > 0 (e.g. batch * num_samples: the CEM rollout layers) -- is bracketed by
  * HIP events on its stream (at most max_launches). tdmpc_profile_end waits for the events and returns the launch count,
  * the summed kernel time in ms and the summed algorithmic FLOPs (2*M*N*K per GEMM problem). Eager use
  * only (the events are not graph-capturable). */
-int tdmpc_profile_begin(int32_t cfg, int32_t pro, int32_t kdim, int32_t max_launches);
+int tdmpc_profile_begin(int32_t cfg, int32_t pro, int32_t kdim, int32_t rows, int32_t max_launches);
 int tdmpc_profile_end(int32_t* launches, double* total_ms, double* flops);
 
 /* Last HIP error string seen by this thread (for diagnostics). */

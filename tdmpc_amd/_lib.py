@@ -61,12 +61,12 @@ def lib():
     L.tdmpc_estimate_value.argtypes = [C.POINTER(Dims), C.POINTER(PlanParams), vp, vp, vp, vp, i32, vp, vp,
                                        vp, vp, sz, vp]
     L.tdmpc_last_error.restype = C.c_char_p
-    L.tdmpc_profile_begin.argtypes = [i32, i32, i32, i32]
+    L.tdmpc_profile_begin.argtypes = [i32, i32, i32, i32, i32]
     L.tdmpc_profile_end.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_double), C.POINTER(C.c_double)]
     for name in EXPORTED:
         if not hasattr(L, name):
             raise RuntimeError(f"{LIB_PATH} does not export {name}")
-    if L.tdmpc_abi_version() != 1:
+    if L.tdmpc_abi_version() != 2:
         raise RuntimeError("libtdmpc_hip ABI version mismatch")
     _LIB = L
     return L

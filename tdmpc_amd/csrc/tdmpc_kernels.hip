@@ -49,6 +49,22 @@ __device__ unsigned int g_stamp_cap;
         __builtin_amdgcn_sched_barrier(0);                                                            \
         st_[slot] = t_;                                                                               \
     } while (0)
+// Record of one workgroup: [realtime start, 5 phase stamps (shader clock), block ids, xcc | realtime span << 8]
+#define STAMP_RECORD()                                                                                \
+    do {                                                                                              \
+        if (threadIdx.x == 0 && g_stamps) {                                                           \
+            const unsigned long long rt1_ = __builtin_amdgcn_s_memrealtime();                         \
+            const unsigned int slot = atomicAdd(&g_stamp_n, 1u);                                      \
+            if (slot < g_stamp_cap) {                                                                 \
+                unsigned long long* o = g_stamps + (size_t)slot * 8;                                  \
+                o[0] = rt0_; o[1] = st_[0]; o[2] = st_[1]; o[3] = st_[2]; o[4] = st_[3]; o[5] = st_[4]; \
+                o[6] = blockIdx.x | (blockIdx.y << 16) | ((unsigned long long)blockIdx.z << 32);      \
+                unsigned int xcc_;                                                                    \
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                   \
+                o[7] = (xcc_ & 0xff) | ((rt1_ - rt0_) << 8);                                          \
+            }                                                                                         \
+        }                                                                                             \
+    } while (0)
 #else
 #define STAMP(slot) do {} while (0)
 #endif
@@ -302,10 +318,12 @@ DEVI void lin_epilogue(const LinArgs& args, const LinProb& P, float* smem, int K
         const int row = (threadIdx.x & 31) + 32 * ((threadIdx.x >> 5) % rows_blk);
         const int cq0 = (threadIdx.x >> 5) / rows_blk, cqs = nthr / R;
         const int lm = m0 + row;
+        // threads past the last full row sweep (nthr % R) idle in this phase
+        const bool active = (int)threadIdx.x < cqs * R;
         const bool rval = lm < args.M;
         const int crow = rval ? (args.c_mapped ? map_row(args.cmap, lm) : lm) : 0;
         float* Cbase = P.C.p ? P.C.p + (size_t)(crow >> 5) * P.C.ts + (crow & 31) * 4 : nullptr;
-        for (int cq = cq0; cq < C / 4; cq += cqs) {
+        for (int cq = active ? cq0 : C / 4; cq < C / 4; cq += cqs) {
             const int c = 4 * cq;
             float4 v = *(const float4*)(smem + (size_t)row * LDC + c);
             for (int w = 1; w < KS; ++w) {
@@ -572,38 +590,37 @@ __global__ void __launch_bounds__(512) linear_kernel(const LinArgs args) {
 #ifdef TDMPC_STAMPS
     __syncthreads();
     STAMP(4);
-    if (threadIdx.x == 0 && g_stamps) {
-        const unsigned int slot = atomicAdd(&g_stamp_n, 1u);
-        if (slot >= g_stamp_cap) return;
-        unsigned long long* o = g_stamps + (size_t)slot * 8;
-        o[0] = rt0_; o[1] = st_[0]; o[2] = st_[1]; o[3] = st_[2]; o[4] = st_[3]; o[5] = st_[4];
-        o[6] = blockIdx.x | (blockIdx.y << 16) | ((unsigned long long)blockIdx.z << 32);
-        unsigned int xcc_;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));
-        o[7] = xcc_;
-    }
+    STAMP_RECORD();
 #endif
 }
+
+DEVI float f4c(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
 // Throughput configuration for large row counts: LDS-staged, double-buffered output tile of 128 rows x
 // C = 32*TN*WGN columns over K tiles of 32. WGM x WGN waves (2x2 or 2x4), each owning a (32*TM) x (32*TN)
 // register tile. With the panel layout one K tile of one 32-row block is a contiguous 4 KiB, so staging is
 // 1 KiB wave loads and every fragment read is a conflict-free ds_read_b128; global traffic per MFMA is
 // shared by the whole workgroup.
-template <int TM, int TN, int WGM, int WGN>
+template <int TM, int TN, int WGM, int WGN, int KT, bool FK>
 __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArgs args) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int R = 32 * TM * WGM, C = 32 * TN * WGN, NT = 64 * WGM * WGN;
     constexpr int RB = R / 32, CB = C / 32;            // 32-row / 32-col blocks
-    constexpr int SA = RB * 1024, SW = CB * 1024;      // floats per stage (8 quads x 32 x 4 per block)
-    constexpr int CA = RB * 256 / NT, CW = CB * 256 / NT;   // 16-B chunks per thread per stage
-    static_assert(R == 128, "throughput tile is 128 rows");
+    constexpr int KQ = KT / 4;                         // k quads per stage
+    constexpr int SA = RB * KQ * 128, SW = CB * KQ * 128;   // floats per stage (KQ quads x 32 x 4 per block)
+    constexpr int CA = RB * KQ * 32 / NT, CW = CB * KQ * 32 / NT;   // 16-B chunks per thread per stage
+    static_assert(CA * NT == RB * KQ * 32 && CW * NT == CB * KQ * 32, "stage does not split over the threads");
     const LinProb& P = args.p[blockIdx.z];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int wm = wave % WGM, wn = wave / WGM;
     const int m0 = blockIdx.x * R, n0 = blockIdx.y * C;
     if (n0 >= P.N) return;
+#ifdef TDMPC_STAMPS
+    unsigned long long st_[5];
+    const unsigned long long rt0_ = __builtin_amdgcn_s_memrealtime();
+    STAMP(0);
+#endif
     const int epi = P.epi;
     // LDS: stage buffers [2][SA + SW] aliased by the epilogue tile [R][C+4]; then bias, dotw, rpart
     constexpr int BUF = SA + SW;
@@ -623,13 +640,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArg
             srp[i] = lm < args.M ? args.rpart[(size_t)lm * args.rpart_nt + i % args.rpart_nt] : 0.f;
         }
 
-    // staging slots: chunk c = tid + i*NT of a stage -> block c>>8, quad (c>>5)&7, row c&31
+    // staging slots: chunk c = tid + i*NT of a stage -> block c / (32*KQ), quad (c>>5) % KQ, row c&31
     const float* Asrc[CA];
     int arow[CA], env[CA];
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
         const int cidx = tid + i * NT;
-        const int m = m0 + (cidx >> 8) * 32 + (cidx & 31);
+        const int m = m0 + (cidx / (32 * KQ)) * 32 + (cidx & 31);
         const int mm = m < args.M ? m : 0;
         arow[i] = args.a_mapped ? map_row(args.amap, mm) : mm;
         Asrc[i] = P.A.p + (size_t)(arow[i] >> 5) * P.A.ts + (arow[i] & 31) * 4;
@@ -638,18 +655,19 @@ __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArg
     const float* Wsrc = P.W.p + (size_t)(n0 >> 5) * P.W.ts;
     const int kq_total = args.K >> 2;
     auto stage_load = [&](int kt, float4 (&ra)[CA], float4 (&rw)[CW]) {
+        // FK (K a multiple of KT): every chunk is in range, no guards
 #pragma unroll
         for (int i = 0; i < CA; ++i) {
             const int cidx = tid + i * NT;
-            const int kq = kt * 8 + ((cidx >> 5) & 7);
-            ra[i] = kq < kq_total ? load_a(args, Asrc[i], P.A.q0 + kq, arow[i], env[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const int kq = kt * KQ + ((cidx >> 5) % KQ);
+            ra[i] = (FK || kq < kq_total) ? load_a(args, Asrc[i], P.A.q0 + kq, arow[i], env[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
             const int cidx = tid + i * NT;
-            const int kq = kt * 8 + ((cidx >> 5) & 7);
-            rw[i] = kq < kq_total ? *(const float4*)(Wsrc + (size_t)(cidx >> 8) * P.W.ts + (size_t)kq * 128 + (cidx & 31) * 4)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+            const int kq = kt * KQ + ((cidx >> 5) % KQ);
+            rw[i] = (FK || kq < kq_total) ? *(const float4*)(Wsrc + (size_t)(cidx / (32 * KQ)) * P.W.ts + (size_t)kq * 128 + (cidx & 31) * 4)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
     auto stage_store = [&](int buf, const float4 (&ra)[CA], const float4 (&rw)[CW]) {
@@ -669,38 +687,66 @@ __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArg
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-    const int nst = (args.K + 31) >> 5;
+    const int nst = (args.K + KT - 1) / KT;
     float4 ra[CA], rw[CW];
     stage_load(0, ra, rw);
     stage_store(0, ra, rw);
     __syncthreads();
+#ifdef TDMPC_STAMPS
+    STAMP(1);
+#endif
     for (int st = 0; st < nst; ++st) {
         const int buf = st & 1;
         if (st + 1 < nst) stage_load(st + 1, ra, rw);
         const float* sA = smem + buf * BUF;
         const float* sW = sA + SA;
+        if constexpr (FK) {
+            // K is a multiple of KT: all fragments of the tile first, then the MFMAs of the independent
+            // accumulators interleaved k-step by k-step
+            float4 a[KT / 8][TM], b[KT / 8][TN];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            if (st * 32 + 8 * g < args.K) {
-                float4 a[TM], b[TN];
+            for (int g = 0; g < KT / 8; ++g) {
 #pragma unroll
-                for (int i = 0; i < TM; ++i) a[i] = *(const float4*)(sA + (((wm * TM + i) * 8 + 2 * g + h) * 32 + r) * 4);
+                for (int i = 0; i < TM; ++i) a[g][i] = *(const float4*)(sA + (((wm * TM + i) * KQ + 2 * g + h) * 32 + r) * 4);
 #pragma unroll
-                for (int j = 0; j < TN; ++j) b[j] = *(const float4*)(sW + (((wn * TN + j) * 8 + 2 * g + h) * 32 + r) * 4);
+                for (int j = 0; j < TN; ++j) b[g][j] = *(const float4*)(sW + (((wn * TN + j) * KQ + 2 * g + h) * 32 + r) * 4);
+            }
 #pragma unroll
-                for (int i = 0; i < TM; ++i)
+            for (int g = 0; g < KT / 8; ++g)
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
-                    }
+                for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(a[g][i], kk), f4c(b[g][j], kk), acc[i][j], 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int g = 0; g < KT / 8; ++g) {
+                if (st * KT + 8 * g < args.K) {
+                    float4 a[TM], b[TN];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) a[i] = *(const float4*)(sA + (((wm * TM + i) * KQ + 2 * g + h) * 32 + r) * 4);
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) b[j] = *(const float4*)(sW + (((wn * TN + j) * KQ + 2 * g + h) * 32 + r) * 4);
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) {
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+                        }
+                }
             }
         }
         if (st + 1 < nst) stage_store(buf ^ 1, ra, rw);
         __syncthreads();
     }
+#ifdef TDMPC_STAMPS
+    STAMP(2);
+#endif
     // accumulators -> LDS tile [R][C+4] (the stage buffers are free after the last barrier)
     {
         float* base = smem + (size_t)(wm * TM * 32) * (C + 4) + wn * TN * 32;
@@ -713,7 +759,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArg
                     base[(size_t)(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * (C + 4) + j * 32 + r] = acc[i][j][e];
     }
     __syncthreads();
+#ifdef TDMPC_STAMPS
+    STAMP(3);
+#endif
     lin_epilogue<R, C>(args, P, smem, 1, m0, n0, sbias, sdotw, srp);
+#ifdef TDMPC_STAMPS
+    __syncthreads();
+    STAMP(4);
+    STAMP_RECORD();
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------ LN+tanh
@@ -1182,12 +1236,13 @@ int init_attrs() {
     FOR_EACH_LINEAR(SET_ATTR)
 #undef SET_ATTR
     HIPCHK(hipFuncSetAttribute((const void*)cem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<2, 2, 2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+#define LDS_ATTR(...) \
+    HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<__VA_ARGS__, true>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                               160 * 1024));                                                                   \
+    HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<__VA_ARGS__, false>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<2, 1, 2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<2, 1, 2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               160 * 1024));
+    LDS_ATTR(2, 2, 2, 2, 32) LDS_ATTR(2, 1, 2, 4, 32) LDS_ATTR(3, 1, 2, 4, 32) LDS_ATTR(1, 1, 2, 2, 32) LDS_ATTR(2, 1, 2, 4, 64) LDS_ATTR(2, 1, 2, 2, 32)
+#undef LDS_ATTR
     if (rc) return TDMPC_E_HIP;
     done = 1;
     return 0;
@@ -1195,10 +1250,10 @@ int init_attrs() {
 
 // Diagnostic kernel timer (tdmpc_profile_*): when armed on this thread, every linear_kernel launch of the
 // selected configuration (cfg id: 1 = latency 32x32 tile, 2 = latency 32x64 tile, 3 = throughput 128x128
-// tile; 0 = any) with K == N == kdim (if kdim > 0) is bracketed by HIP events on its stream, and its
+// tile; 0 = any) with K == N == kdim (if kdim > 0) and M == rows (if rows > 0) is bracketed by HIP events on its stream, and its
 // algorithmic FLOPs (2*M*N*K per problem) are recorded. bench.py uses it for the dominant kernel's roofline.
 struct Profiler {
-    int armed = 0, cfg = 0, pro = -1, n = 0, cap = 0, kdim = 0;
+    int armed = 0, cfg = 0, pro = -1, n = 0, cap = 0, kdim = 0, rows = 0;
     hipEvent_t* ev = nullptr;
     double flops = 0.0;
 };
@@ -1215,7 +1270,7 @@ int thr_rows() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("TDMPC_THR_ROWS");
-        v = e ? atoi(e) : 2048;
+        v = e ? atoi(e) : 4096;
     }
     return v;
 }
@@ -1232,12 +1287,16 @@ int thr_variant() {
     return v;
 }
 
-LinCfg pick_cfg(int M, int nmax, int K, int wn_hint) {
+// Tile choice by shape (tools/mb/mb_linear.hip "sweep" on MI355X): the LDS-staged throughput tiles from
+// thr_rows() rows on; below that the K-split latency tiles, 32x64 where K and N are wide enough to feed
+// its 8 waves (512x512 hidden layers from 512 rows, the 100-wide latent layer from 2048 rows) or where the
+// epilogue needs 64-column row blocks (wide64: LayerNorm moments are kept per 64 columns).
+LinCfg pick_cfg(int M, int nmax, int K, int wide64) {
     if (M >= thr_rows() && nmax >= 256 && K >= 64) {
         const int v = thr_variant();
         return LinCfg{3, (v == 2 || v == 3) ? 64 : 128, 64};
     }
-    if (wn_hint == 2) return LinCfg{2, 64, 64};
+    if (wide64 || (nmax >= 256 ? (K >= 256 && M >= 512) : M >= 2048)) return LinCfg{2, 64, 64};
     return LinCfg{1, 32, 32};
 }
 
@@ -1253,7 +1312,8 @@ int launch_lin_t(const LinArgs& a, int nprob, int nmax, int cfg_id, hipStream_t 
     const size_t lds = ((size_t)KS * R * (C + 4) + 2 * C + (size_t)R * std::max(a.rpart_nt, 1)) * 4;
     Profiler& pf = g_prof;
     const bool prof = pf.armed && (pf.cfg == 0 || pf.cfg == cfg_id) && (pf.pro < 0 || pf.pro == PRO) &&
-                      pf.n + 2 <= pf.cap && (pf.kdim == 0 || (a.K == pf.kdim && nmax == pf.kdim));
+                      pf.n + 2 <= pf.cap && (pf.kdim == 0 || (a.K == pf.kdim && nmax == pf.kdim)) &&
+                      (pf.rows == 0 || a.M == pf.rows);
     if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], s));
     hipLaunchKernelGGL((linear_kernel<TM, TN, WGM, WGN, PRO, KCH, ROLL>), grid, block, lds, s, b);
     HIPCHK(hipGetLastError());
@@ -1265,19 +1325,22 @@ int launch_lin_t(const LinArgs& a, int nprob, int nmax, int cfg_id, hipStream_t 
     return 0;
 }
 
-template <int TM, int TN, int WGM, int WGN>
+template <int TM, int TN, int WGM, int WGN, int KT>
 int launch_lds_t(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
     constexpr int R = 32 * TM * WGM, C = 32 * TN * WGN;
-    constexpr int BUF = (R / 32) * 1024 + (C / 32) * 1024;
+    constexpr int BUF = (R / 32 + C / 32) * KT * 32;
     constexpr int EPI_F = R * (C + 4);
     constexpr int BODY = 2 * BUF > EPI_F ? 2 * BUF : EPI_F;
     dim3 grid((a.M + R - 1) / R, (nmax + C - 1) / C, nprob);
     const size_t lds = ((size_t)BODY + 2 * C + (size_t)R * std::max(a.rpart_nt, 1)) * 4;
     Profiler& pf = g_prof;
     const bool prof = pf.armed && (pf.cfg == 0 || pf.cfg == 3) && (pf.pro <= 0) && pf.n + 2 <= pf.cap &&
-                      (pf.kdim == 0 || (a.K == pf.kdim && nmax == pf.kdim));
+                      (pf.kdim == 0 || (a.K == pf.kdim && nmax == pf.kdim)) && (pf.rows == 0 || a.M == pf.rows);
     if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], s));
-    hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN>), grid, dim3(64 * WGM * WGN), lds, s, a);
+    if (a.K % KT == 0)
+        hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, true>), grid, dim3(64 * WGM * WGN), lds, s, a);
+    else
+        hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, false>), grid, dim3(64 * WGM * WGN), lds, s, a);
     HIPCHK(hipGetLastError());
     if (prof) {
         HIPCHK(hipEventRecord(pf.ev[pf.n + 1], s));
@@ -1285,6 +1348,18 @@ int launch_lds_t(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
         for (int q = 0; q < nprob; ++q) pf.flops += 2.0 * a.M * std::min(a.p[q].N, nmax) * a.K;
     }
     return 0;
+}
+
+int num_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            n = v;
+        else
+            n = 256;
+    }
+    return n;
 }
 
 int lds_variant() {
@@ -1296,20 +1371,35 @@ int lds_variant() {
     return v;
 }
 
-// LDS-staged throughput tile: variant 0 = 128x128 with 4 waves (64x64 each), 1 = 128x128 with 8 waves
-// (64x32 each, 2 waves per SIMD), 2 = 128x64 with 4 waves (64x32 each) for mid-size row counts.
+// LDS-staged throughput tiles: 128x128 with 8 waves (64x32 each, 2 waves per SIMD) by default, 192x128
+// (8 waves of 96x32) or 64x64 (4 waves of 32x32) when the work per CU says so; TDMPC_LDS_VARIANT=0 selects
+// the 4-wave 128x128 tile, 2 the 128x128 tile with K tiles of 64 (both kept for comparison).
 int launch_lds(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
     const int ctiles128 = (nmax + 127) / 128, rtiles = (a.M + 127) / 128;
-    if (rtiles * ctiles128 * nprob < 192) return launch_lds_t<2, 1, 2, 2>(a, nprob, nmax, s);
-    if (lds_variant() == 0) return launch_lds_t<2, 2, 2, 2>(a, nprob, nmax, s);
-    return launch_lds_t<2, 1, 2, 4>(a, nprob, nmax, s);
+    {   // Tile by the work of the busiest CU: ceil(WGs / CUs) x tile area, over the tile's efficiency.
+        // 192x128 when 128x128 would need a second, partly idle round (6144 rows x 2 problems: 256 WGs
+        // instead of 384); 64x64 (4 waves, 4 resident per CU) when 128x128 leaves CUs idle.
+        const int cus = num_cus();
+        const long w128 = (long)rtiles * ctiles128 * nprob, w192 = (long)((a.M + 191) / 192) * ctiles128 * nprob;
+        const long w64 = (long)((a.M + 63) / 64) * ((nmax + 63) / 64) * nprob;
+        const double c128 = (double)((w128 + cus - 1) / cus) * 128 * 128;
+        const double c192 = (double)((w192 + cus - 1) / cus) * 192 * 128 / 1.05;
+        const long r64 = (w64 + cus - 1) / cus;
+        const double c64 = (double)r64 * 64 * 64 / (r64 >= 2 ? 0.8 : 0.4);
+        if (c192 < c128 && c192 <= c64) return launch_lds_t<3, 1, 2, 4, 32>(a, nprob, nmax, s);
+        if (c64 < c128) return launch_lds_t<1, 1, 2, 2, 32>(a, nprob, nmax, s);
+    }
+    const int v = lds_variant();
+    if (v == 0) return launch_lds_t<2, 2, 2, 2, 32>(a, nprob, nmax, s);
+    if (v == 2) return launch_lds_t<2, 1, 2, 4, 64>(a, nprob, nmax, s);
+    return launch_lds_t<2, 1, 2, 4, 32>(a, nprob, nmax, s);
 }
 
 // Launch one fused linear layer with the configuration pick_cfg selects.
-int launch_lin(const LinArgs& a, int nprob, int nmax, int wn_hint, int pro, hipStream_t s) {
+int launch_lin(const LinArgs& a, int nprob, int nmax, int wide64, int pro, hipStream_t s) {
     if (a.M <= 0) return 0;
     if (a.K % 8) { snprintf(g_err, sizeof g_err, "bad K %d", a.K); return TDMPC_E_DIMS; }
-    const LinCfg cfg = pick_cfg(a.M, nmax, a.K, wn_hint);
+    const LinCfg cfg = pick_cfg(a.M, nmax, a.K, wide64);
     if (cfg.id == 3) {
         const int v = thr_variant();
         if (v == 0 && pro == PRO_PLAIN) return launch_lds(a, nprob, nmax, s);
@@ -1384,7 +1474,7 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         LinProb& p = a.p[0];
         p.A = xop(c, t, 0); p.W = wop(c, w.w1x, c.Kx); p.bias = c.pw + w.b1x;
         p.C = hout(c.k.H1, c, 0); p.N = p.nvalid = p.nstore = 2 * M; p.epi = EPI_ELU;
-        if ((rc = launch_lin(a, 1, 2 * M, 2, PRO_PLAIN, c.s))) return rc;
+        if ((rc = launch_lin(a, 1, 2 * M, 0, PRO_PLAIN, c.s))) return rc;
     }
     {   // h2_d = ELU(W2d h1_d + b); reward partial dots of ELU(W2r h1_r + b) with reward.4.weight
         LinArgs a = args0();
@@ -1395,8 +1485,8 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         LinProb& p1 = a.p[1];
         p1.A = hop(c.k.H1, c, M / 4); p1.W = wop(c, w.w2r, M); p1.bias = c.pw + w.b2r;
         p1.N = p1.nvalid = M; p1.nstore = 0; p1.epi = EPI_ELU_DOT;
-        p1.dotw = c.pw + w.w3r; p1.dot_out = c.k.rpart; p1.dot_ld = M / pick_cfg(rows, M, M, 1).bw;
-        if ((rc = launch_lin(a, 2, M, 1, PRO_PLAIN, c.s))) return rc;
+        p1.dotw = c.pw + w.w3r; p1.dot_out = c.k.rpart; p1.dot_ld = M / pick_cfg(rows, M, M, 0).bw;
+        if ((rc = launch_lin(a, 2, M, 0, PRO_PLAIN, c.s))) return rc;
     }
     {   // z' = W3d h2_d + b -> X_{t+1} latent columns; reward = sum(partials) + b; G update
         LinArgs a = args0();
@@ -1404,9 +1494,9 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         LinProb& p = a.p[0];
         p.A = hop(c.k.H2, c, 0); p.W = wop(c, w.w3d, M); p.bias = c.pw + w.b3d;
         p.C = xout(c, t + 1, w.Ap / 4); p.N = w.L; p.nvalid = w.L; p.nstore = w.Lp; p.epi = EPI_LIN_Z;
-        a.rpart = c.k.rpart; a.rpart_nt = M / pick_cfg(rows, M, M, 1).bw; a.b3r = c.pw + w.b3r;
+        a.rpart = c.k.rpart; a.rpart_nt = M / pick_cfg(rows, M, M, 0).bw; a.b3r = c.pw + w.b3r;
         a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
-        if ((rc = launch_lin(a, 1, w.L, 1, PRO_PLAIN, c.s))) return rc;
+        if ((rc = launch_lin(a, 1, w.L, 0, PRO_PLAIN, c.s))) return rc;
     }
     return 0;
 }
@@ -1424,7 +1514,7 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
         LinProb& p = a.p[0];
         p.A = xop(c, t, w.Ap / 4); p.W = wop(c, w.wp1, w.Lp); p.bias = c.pw + w.bp1;
         p.C = hout(c.k.H1, c, 0); p.N = p.nvalid = p.nstore = M; p.epi = EPI_ELU;
-        if ((rc = launch_lin(a, 1, M, 2, PRO_PLAIN, c.s))) return rc;
+        if ((rc = launch_lin(a, 1, M, 0, PRO_PLAIN, c.s))) return rc;
     }
     {
         LinArgs a = args0();
@@ -1432,7 +1522,7 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
         LinProb& p = a.p[0];
         p.A = hop(c.k.H1, c, 0); p.W = wop(c, w.wp2, M); p.bias = c.pw + w.bp2;
         p.C = hout(c.k.H2, c, 0); p.N = p.nvalid = p.nstore = M; p.epi = EPI_ELU;
-        if ((rc = launch_lin(a, 1, M, 1, PRO_PLAIN, c.s))) return rc;
+        if ((rc = launch_lin(a, 1, M, 0, PRO_PLAIN, c.s))) return rc;
     }
     {
         LinArgs a = args0();
@@ -1443,7 +1533,7 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
         a.eps = eps; a.eps_G = eps_G; a.eps_env = eps_env; a.eps_off = eps_off; a.A = w.A;
         a.min_std = min_std;
         a.lo = (float)(-1.0 + 1e-6); a.hi = (float)(1.0 - 1e-6);
-        return launch_lin(a, 1, w.A, 1, PRO_PLAIN, c.s);
+        return launch_lin(a, 1, w.A, 0, PRO_PLAIN, c.s);
     }
 }
 
@@ -1459,7 +1549,7 @@ int terminal_q(const Ctx& c, float discH, float* value_out, int I, int iter) {
         p.A = xop(c, c.H, 0); p.W = wop(c, w.wq1x, c.Kx); p.bias = c.pw + w.bq1x;
         p.C = hout(c.k.H1, c, 0); p.N = p.nvalid = p.nstore = 2 * M; p.epi = EPI_LNSTATS;
         p.st_out = c.k.st1; p.st_ld = 2 * M / 64;
-        if ((rc = launch_lin(a, 1, 2 * M, 2, PRO_PLAIN, c.s))) return rc;
+        if ((rc = launch_lin(a, 1, 2 * M, 1, PRO_PLAIN, c.s))) return rc;
     }
     {   // a1 = tanh(LN(y1)) -> H2
         LnArgs l;
@@ -1477,7 +1567,7 @@ int terminal_q(const Ctx& c, float discH, float* value_out, int I, int iter) {
             p.bias = c.pw + w.bq2 + q * M; p.C = hout(c.k.H1, c, q * M / 4); p.N = p.nvalid = p.nstore = M;
             p.epi = EPI_LNSTATS; p.st_out = c.k.st2 + q * (M / 64); p.st_ld = 2 * M / 64;
         }
-        if ((rc = launch_lin(a, 2, M, 2, PRO_PLAIN, c.s))) return rc;
+        if ((rc = launch_lin(a, 2, M, 1, PRO_PLAIN, c.s))) return rc;
     }
     {
         ValueArgs v;
@@ -1711,14 +1801,17 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     // z0 = h(obs) and mean = 0 (warm: prev_mean shifted), std = 2
     if ((rc = encode(c, obs, obs_is_u8, B, prev_mean, prm->warm_start))) return rc;
 
-    // pi pre-rollout on the P policy rows of every env (tdmpc.py:113-118). Their H-step rollout, reward
-    // prefix and z_H are identical in every CEM iteration (same z0, same pi_actions), so they are
-    // computed once here and reused (rows N..T-1 of X_t, G and rlast).
+    // pi pre-rollout (tdmpc.py:113-118) fused with CEM iteration 0: at each step t the policy rows get
+    // pi(z_t) first, then ONE TOLD.next launch advances all T rows of every env (rollout rows with the
+    // sampled candidates, pi rows with their pi actions). The pi rows' rollout, reward prefix and z_H are
+    // identical in every CEM iteration (same z0, same pi actions), so later iterations only roll out the N
+    // sampled rows and reuse rows N..T-1 of X_t, G and rlast.
+    const RowMap all = {T, T, 0};
     if (P > 0) {
         const RowMap pm = {P, T, N};
         for (int t = 0; t < H; ++t) {
             if ((rc = policy(c, t, B * P, pm, noise, c.eps_env, P, (long)t * P * c.A, prm->min_std))) return rc;
-            if ((rc = step_next(c, t, B * P, pm, prm->discount_pow[t], t == 0, t == H - 1, Sampling{0, nullptr, 0})))
+            if ((rc = step_next(c, t, B * T, all, prm->discount_pow[t], t == 0, t == H - 1, Sampling{1, noise, 0})))
                 return rc;
         }
     }
@@ -1736,11 +1829,11 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     const size_t cem_lds = cem_lds_bytes(T, H, ca.K, c.A);
 
     const RowMap rm = {N, T, 0};
-    const RowMap all = {T, T, 0};
     for (int i = 0; i < I; ++i) {
-        for (int t = 0; t < H; ++t)
-            if ((rc = step_next(c, t, B * N, rm, prm->discount_pow[t], t == 0, t == H - 1, Sampling{1, noise, i})))
-                return rc;
+        if (i > 0 || P == 0)
+            for (int t = 0; t < H; ++t)
+                if ((rc = step_next(c, t, B * N, rm, prm->discount_pow[t], t == 0, t == H - 1, Sampling{1, noise, i})))
+                    return rc;
         if ((rc = policy(c, H, B * T, all, noise, c.eps_env, T, c.eps_cem_off + (long)i * c.eps_iter + c.eps_term_off,
                          prm->min_std)))
             return rc;
@@ -1784,7 +1877,7 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     return 0;
 }
 
-int tdmpc_profile_begin(int32_t cfg, int32_t pro, int32_t kdim, int32_t max_launches) {
+int tdmpc_profile_begin(int32_t cfg, int32_t pro, int32_t kdim, int32_t rows, int32_t max_launches) {
     Profiler& pf = g_prof;
     if (pf.ev) {
         for (int i = 0; i < pf.cap; ++i) (void)hipEventDestroy(pf.ev[i]);
@@ -1794,7 +1887,7 @@ int tdmpc_profile_begin(int32_t cfg, int32_t pro, int32_t kdim, int32_t max_laun
     pf.cap = 2 * std::max(1, (int)max_launches);
     pf.ev = (hipEvent_t*)calloc(pf.cap, sizeof(hipEvent_t));
     for (int i = 0; i < pf.cap; ++i) HIPCHK(hipEventCreate(&pf.ev[i]));
-    pf.cfg = cfg; pf.pro = pro; pf.kdim = kdim; pf.armed = 1;
+    pf.cfg = cfg; pf.pro = pro; pf.kdim = kdim; pf.rows = rows; pf.armed = 1;
     return 0;
 }
 
