@@ -596,12 +596,12 @@ __global__ void __launch_bounds__(512) linear_kernel(const LinArgs args) {
 
 DEVI float f4c(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
-// Throughput configuration for large row counts: LDS-staged, double-buffered output tile of 128 rows x
-// C = 32*TN*WGN columns over K tiles of 32. WGM x WGN waves (2x2 or 2x4), each owning a (32*TM) x (32*TN)
+// Throughput configuration for large row counts: LDS-staged (three stage buffers) output tile of
+// R = 32*TM*WGM rows x C = 32*TN*WGN columns over K tiles of KT. WGM x WGN waves (2x2 or 2x4), each owning a (32*TM) x (32*TN)
 // register tile. With the panel layout one K tile of one 32-row block is a contiguous 4 KiB, so staging is
 // 1 KiB wave loads and every fragment read is a conflict-free ds_read_b128; global traffic per MFMA is
 // shared by the whole workgroup.
-template <int TM, int TN, int WGM, int WGN, int KT, bool FK>
+template <int TM, int TN, int WGM, int WGN, int KT, bool FK, bool AG>
 __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArgs args) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int R = 32 * TM * WGM, C = 32 * TN * WGN, NT = 64 * WGM * WGN;
@@ -622,10 +622,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArg
     STAMP(0);
 #endif
     const int epi = P.epi;
-    // LDS: stage buffers [2][SA + SW] aliased by the epilogue tile [R][C+4]; then bias, dotw, rpart
+    // LDS: stage buffers [3][SA + SW] aliased by the epilogue tile [R][C+4]; then bias, dotw, rpart
     constexpr int BUF = SA + SW;
     constexpr int EPI_F = R * (C + 4);
-    constexpr int BODY = 2 * BUF > EPI_F ? 2 * BUF : EPI_F;
+    constexpr int BODY = 3 * BUF > EPI_F ? 3 * BUF : EPI_F;
     float* sbias = smem + BODY;
     float* sdotw = sbias + C;
     float* srp = sdotw + C;
@@ -652,22 +652,31 @@ __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArg
         Asrc[i] = P.A.p + (size_t)(arow[i] >> 5) * P.A.ts + (arow[i] & 31) * 4;
         env[i] = (args.zmode | args.smode) ? arow[i] / args.rows_per_env : 0;
     }
-    const float* Wsrc = P.W.p + (size_t)(n0 >> 5) * P.W.ts;
+    // per-chunk W pointers (chunk c: column block c / (32*KQ), quad (c>>5) % KQ, column c&31 of the block)
+    const float* Wsrc[CW];
+#pragma unroll
+    for (int i = 0; i < CW; ++i) {
+        const int cidx = tid + i * NT;
+        Wsrc[i] = P.W.p + (size_t)((n0 >> 5) + cidx / (32 * KQ)) * P.W.ts + ((cidx >> 5) % KQ) * 128 + (cidx & 31) * 4;
+    }
     const int kq_total = args.K >> 2;
+    // AG: the A operand may be sampled (smode) or broadcast from z0 (zmode) -- load_a; else a plain panel load
     auto stage_load = [&](int kt, float4 (&ra)[CA], float4 (&rw)[CW]) {
         // FK (K a multiple of KT): every chunk is in range, no guards
 #pragma unroll
         for (int i = 0; i < CA; ++i) {
             const int cidx = tid + i * NT;
             const int kq = kt * KQ + ((cidx >> 5) % KQ);
-            ra[i] = (FK || kq < kq_total) ? load_a(args, Asrc[i], P.A.q0 + kq, arow[i], env[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (FK || kq < kq_total)
+                ra[i] = AG ? load_a(args, Asrc[i], P.A.q0 + kq, arow[i], env[i])
+                           : *(const float4*)(Asrc[i] + (size_t)(P.A.q0 + kq) * 128);
+            else
+                ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
-            const int cidx = tid + i * NT;
-            const int kq = kt * KQ + ((cidx >> 5) % KQ);
-            rw[i] = (FK || kq < kq_total) ? *(const float4*)(Wsrc + (size_t)(cidx / (32 * KQ)) * P.W.ts + (size_t)kq * 128 + (cidx & 31) * 4)
-                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+            const int kq = kt * KQ + (((tid + i * NT) >> 5) % KQ);
+            rw[i] = (FK || kq < kq_total) ? *(const float4*)(Wsrc[i] + (size_t)kt * KQ * 128) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
     auto stage_store = [&](int buf, const float4 (&ra)[CA], const float4 (&rw)[CW]) {
@@ -687,63 +696,73 @@ __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArg
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
+    // Three LDS stage buffers: while the MFMAs of stage st run, the fragments of stage st+1 (complete since
+    // the previous barrier) are already being read into registers and stage st+2 is in flight from global
+    // memory; it lands in the buffer stage st-1 used. One barrier per stage, and no MFMA ever waits on an
+    // LDS read issued after a barrier. A partial last K tile is zero-filled, so every stage runs all KT/8
+    // fragment groups (adding exact zero products).
+    constexpr int NG = KT / 8;
+    float4 fa0[NG][TM], fb0[NG][TN], fa1[NG][TM], fb1[NG][TN];
+    auto frag_load = [&](int buf, float4 (&fa)[NG][TM], float4 (&fb)[NG][TN]) {
+        const float* sA = smem + buf * BUF;
+        const float* sW = sA + SA;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) fa[g][i] = *(const float4*)(sA + (((wm * TM + i) * KQ + 2 * g + h) * 32 + r) * 4);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) fb[g][j] = *(const float4*)(sW + (((wn * TN + j) * KQ + 2 * g + h) * 32 + r) * 4);
+        }
+    };
+    auto mfma_stage = [&](const float4 (&fa)[NG][TM], const float4 (&fb)[NG][TN]) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(fa[g][i], kk), f4c(fb[g][j], kk), acc[i][j], 0, 0, 0);
+    };
+    // Global loads run two stages ahead of their LDS store: stage st+3 is requested during stage st into one
+    // register set while the other set (stage st+2, requested a stage earlier) is written to LDS at its end,
+    // so each load has ~2 stages (~4 us) to arrive from HBM.
     const int nst = (args.K + KT - 1) / KT;
-    float4 ra[CA], rw[CW];
-    stage_load(0, ra, rw);
-    stage_store(0, ra, rw);
+    float4 ra0[CA], rw0[CW], ra1[CA], rw1[CW];
+    stage_load(0, ra0, rw0);
+    if (nst > 1) stage_load(1, ra1, rw1);
+    stage_store(0, ra0, rw0);
+    if (nst > 1) stage_store(1, ra1, rw1);
+    if (nst > 2) stage_load(2, ra0, rw0);
     __syncthreads();
 #ifdef TDMPC_STAMPS
     STAMP(1);
 #endif
-    for (int st = 0; st < nst; ++st) {
-        const int buf = st & 1;
-        if (st + 1 < nst) stage_load(st + 1, ra, rw);
-        const float* sA = smem + buf * BUF;
-        const float* sW = sA + SA;
-        if constexpr (FK) {
-            // K is a multiple of KT: all fragments of the tile first, then the MFMAs of the independent
-            // accumulators interleaved k-step by k-step
-            float4 a[KT / 8][TM], b[KT / 8][TN];
-#pragma unroll
-            for (int g = 0; g < KT / 8; ++g) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i) a[g][i] = *(const float4*)(sA + (((wm * TM + i) * KQ + 2 * g + h) * 32 + r) * 4);
-#pragma unroll
-                for (int j = 0; j < TN; ++j) b[g][j] = *(const float4*)(sW + (((wn * TN + j) * KQ + 2 * g + h) * 32 + r) * 4);
-            }
-#pragma unroll
-            for (int g = 0; g < KT / 8; ++g)
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-#pragma unroll
-                        for (int j = 0; j < TN; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(a[g][i], kk), f4c(b[g][j], kk), acc[i][j], 0, 0, 0);
-        } else {
-#pragma unroll
-            for (int g = 0; g < KT / 8; ++g) {
-                if (st * KT + 8 * g < args.K) {
-                    float4 a[TM], b[TN];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) a[i] = *(const float4*)(sA + (((wm * TM + i) * KQ + 2 * g + h) * 32 + r) * 4);
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) b[j] = *(const float4*)(sW + (((wn * TN + j) * KQ + 2 * g + h) * 32 + r) * 4);
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-#pragma unroll
-                        for (int j = 0; j < TN; ++j) {
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
-                        }
-                }
-            }
-        }
-        if (st + 1 < nst) stage_store(buf ^ 1, ra, rw);
+    frag_load(0, fa0, fb0);
+    // drain the LDS counter here: otherwise the loop header merges these reads' pending state and the
+    // waitcnt pass makes the first MFMAs of every iteration wait on the next stage's fragment reads
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), vmcnt/expcnt unconstrained
+    int bnext = 1, bfill = 2;   // buffers of stages st+1 and st+2
+    auto iter = [&](int st, const float4 (&fac)[NG][TM], const float4 (&fbc)[NG][TN], float4 (&fan)[NG][TM],
+                    float4 (&fbn)[NG][TN], float4 (&ral)[CA], float4 (&rwl)[CW], const float4 (&ras)[CA],
+                    const float4 (&rws)[CW]) {
+        // unconditional (past the end: the last stage again, never stored) so that the vmcnt wait before
+        // the store below can leave exactly this stage's loads in flight
+        stage_load(min(st + 3, nst - 1), ral, rwl);
+        if (st + 1 < nst) frag_load(bnext, fan, fbn);
+        mfma_stage(fac, fbc);
+        if (st + 2 < nst) stage_store(bfill, ras, rws);
         __syncthreads();
+        bnext = bfill;
+        bfill = bfill == 2 ? 0 : bfill + 1;
+    };
+    int st = 0;
+    for (; st + 1 < nst; st += 2) {
+        iter(st, fa0, fb0, fa1, fb1, ra1, rw1, ra0, rw0);
+        iter(st + 1, fa1, fb1, fa0, fb0, ra0, rw0, ra1, rw1);
     }
+    if (st < nst) iter(st, fa0, fb0, fa1, fb1, ra1, rw1, ra0, rw0);
 #ifdef TDMPC_STAMPS
     STAMP(2);
 #endif
@@ -1236,13 +1255,14 @@ int init_attrs() {
     FOR_EACH_LINEAR(SET_ATTR)
 #undef SET_ATTR
     HIPCHK(hipFuncSetAttribute((const void*)cem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+#define LDS_ATTR1(...) \
+    HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<__VA_ARGS__>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 #define LDS_ATTR(...) \
-    HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<__VA_ARGS__, true>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                               160 * 1024));                                                                   \
-    HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<__VA_ARGS__, false>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                               160 * 1024));
-    LDS_ATTR(2, 2, 2, 2, 32) LDS_ATTR(2, 1, 2, 4, 32) LDS_ATTR(3, 1, 2, 4, 32) LDS_ATTR(1, 1, 2, 2, 32) LDS_ATTR(2, 1, 2, 4, 64) LDS_ATTR(2, 1, 2, 2, 32)
+    LDS_ATTR1(__VA_ARGS__, true, false) LDS_ATTR1(__VA_ARGS__, true, true) LDS_ATTR1(__VA_ARGS__, false, false) \
+    LDS_ATTR1(__VA_ARGS__, false, true)
+    LDS_ATTR(2, 2, 2, 2, 32) LDS_ATTR(2, 1, 2, 4, 32) LDS_ATTR(3, 1, 2, 4, 32) LDS_ATTR(1, 1, 2, 2, 32) LDS_ATTR(2, 1, 2, 2, 32)
 #undef LDS_ATTR
+#undef LDS_ATTR1
     if (rc) return TDMPC_E_HIP;
     done = 1;
     return 0;
@@ -1330,17 +1350,19 @@ int launch_lds_t(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
     constexpr int R = 32 * TM * WGM, C = 32 * TN * WGN;
     constexpr int BUF = (R / 32 + C / 32) * KT * 32;
     constexpr int EPI_F = R * (C + 4);
-    constexpr int BODY = 2 * BUF > EPI_F ? 2 * BUF : EPI_F;
+    constexpr int BODY = 3 * BUF > EPI_F ? 3 * BUF : EPI_F;
     dim3 grid((a.M + R - 1) / R, (nmax + C - 1) / C, nprob);
     const size_t lds = ((size_t)BODY + 2 * C + (size_t)R * std::max(a.rpart_nt, 1)) * 4;
     Profiler& pf = g_prof;
     const bool prof = pf.armed && (pf.cfg == 0 || pf.cfg == 3) && (pf.pro <= 0) && pf.n + 2 <= pf.cap &&
                       (pf.kdim == 0 || (a.K == pf.kdim && nmax == pf.kdim)) && (pf.rows == 0 || a.M == pf.rows);
     if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], s));
-    if (a.K % KT == 0)
-        hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, true>), grid, dim3(64 * WGM * WGN), lds, s, a);
-    else
-        hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, false>), grid, dim3(64 * WGM * WGN), lds, s, a);
+    const dim3 block(64 * WGM * WGN);
+    const bool fk = a.K % KT == 0, ag = a.smode || a.zmode;
+    if (fk && !ag) hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, true, false>), grid, block, lds, s, a);
+    else if (fk) hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, true, true>), grid, block, lds, s, a);
+    else if (!ag) hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, false, false>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, false, true>), grid, block, lds, s, a);
     HIPCHK(hipGetLastError());
     if (prof) {
         HIPCHK(hipEventRecord(pf.ev[pf.n + 1], s));
@@ -1373,7 +1395,7 @@ int lds_variant() {
 
 // LDS-staged throughput tiles: 128x128 with 8 waves (64x32 each, 2 waves per SIMD) by default, 192x128
 // (8 waves of 96x32) or 64x64 (4 waves of 32x32) when the work per CU says so; TDMPC_LDS_VARIANT=0 selects
-// the 4-wave 128x128 tile, 2 the 128x128 tile with K tiles of 64 (both kept for comparison).
+// the 4-wave 128x128 tile (kept for comparison).
 int launch_lds(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
     const int ctiles128 = (nmax + 127) / 128, rtiles = (a.M + 127) / 128;
     {   // Tile by the work of the busiest CU: ceil(WGs / CUs) x tile area, over the tile's efficiency.
@@ -1391,7 +1413,6 @@ int launch_lds(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
     }
     const int v = lds_variant();
     if (v == 0) return launch_lds_t<2, 2, 2, 2, 32>(a, nprob, nmax, s);
-    if (v == 2) return launch_lds_t<2, 1, 2, 4, 64>(a, nprob, nmax, s);
     return launch_lds_t<2, 1, 2, 4, 32>(a, nprob, nmax, s);
 }
 

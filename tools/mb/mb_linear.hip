@@ -80,9 +80,9 @@ int main(int argc, char** argv) {
         Ctx c;
         if (setup_ctx(c, &d, packed, ws, sz.workspace_bytes, B, 5, 6, s)) { printf("ctx failed\n"); return 1; }
         init_attrs();
-#define ATTR(...) CK(hipFuncSetAttribute((const void*)linear_lds_kernel<__VA_ARGS__, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)); \
-                  CK(hipFuncSetAttribute((const void*)linear_lds_kernel<__VA_ARGS__, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        ATTR(1, 1, 2, 2, 32) ATTR(1, 2, 2, 2, 32) ATTR(1, 1, 2, 4, 32) ATTR(2, 1, 2, 4, 64) ATTR(1, 2, 2, 4, 32)
+#define ATTR1(...) CK(hipFuncSetAttribute((const void*)linear_lds_kernel<__VA_ARGS__>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+#define ATTR(...) ATTR1(__VA_ARGS__, true, false) ATTR1(__VA_ARGS__, true, true) ATTR1(__VA_ARGS__, false, false) ATTR1(__VA_ARGS__, false, true)
+        ATTR(1, 1, 2, 2, 32) ATTR(1, 2, 2, 2, 32) ATTR(1, 1, 2, 4, 32) ATTR(1, 2, 2, 4, 32)
 #undef ATTR
         const Layout& w = c.w; const int M = c.M;
         struct Shape { const char* name; int rows, n, k, nprob; size_t woff; };
@@ -119,7 +119,6 @@ int main(int argc, char** argv) {
                 run("lds 64x128 4w", [&] { return launch_lds_t<1, 2, 2, 2, 32>(a, np, nm, s); });
                 run("lds 64x128 8w", [&] { return launch_lds_t<1, 1, 2, 4, 32>(a, np, nm, s); });
                 if (nm % 256 == 0) run("lds 64x256 8w", [&] { return launch_lds_t<1, 2, 2, 4, 32>(a, np, nm, s); });
-                run("lds 128x128 8w kt64", [&] { return launch_lds_t<2, 1, 2, 4, 64>(a, np, nm, s); });
             }
             if (sh.k <= 1024) {
                 const int kch = sh.k > 256 ? 64 : 32;
