@@ -262,43 +262,13 @@ struct LinArgs {
     int M, K, kch;
     int a_mapped, c_mapped;
     RowMap amap, cmap;
-    // A-operand sources for first-layer inputs x = [a|z] (column quads < apq are the action part)
-    int apq, rows_per_env;
-    int zmode;                    // z part from z0[env][Lp] (t = 0: every row starts at h(obs))
-    const float* z0; int Lp;
-    int smode;                    // action part of rows with (row % rows_per_env) < s_rows sampled:
-    int s_rows;                   //   clamp(mean_t + std_t * eps, -1, 1)
-    const float* mean_t; const float* std_t; int mstride;
-    const float* seps; long seps_env; long seps_off; int A;
+    int A;                        // action dim (EPI_PI noise rows)
     // EPI_LIN_Z: reward head + return
     const float* rpart; int rpart_nt; const float* b3r;
     float* G; float* rlast; float disc; int first, last;
     // EPI_PI
     const float* eps; int eps_G; long eps_env; long eps_off; float min_std, lo, hi;
 };
-
-// A operand quad (4 consecutive k of one row) for first-layer / plain inputs.
-DEVI float4 load_a(const LinArgs& args, const float* Abase, int colq, int arow, int env) {
-    if (args.smode && colq < args.apq) {
-        const int n = arow % args.rows_per_env;
-        if (n < args.s_rows) {
-            // CEM candidates (tdmpc.py:130-132): clamp(mean + std * randn, -1, 1), mul then add
-            const float* ep = args.seps + (size_t)env * args.seps_env + args.seps_off + (size_t)n * args.A;
-            const float* mt = args.mean_t + (size_t)env * args.mstride;
-            const float* sd = args.std_t + (size_t)env * args.mstride;
-            float v[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int c = colq * 4 + i;
-                v[i] = c < args.A ? tclamp(fadd(mt[c], fmul(sd[c], ep[c])), -1.f, 1.f) : 0.f;
-            }
-            return make_float4(v[0], v[1], v[2], v[3]);
-        }
-    }
-    if (args.zmode && colq >= args.apq)
-        return *(const float4*)(args.z0 + (size_t)env * args.Lp + (colq - args.apq) * 4);
-    return *(const float4*)(Abase + (size_t)colq * 128);
-}
 
 // Shared epilogue of the linear kernels. smem holds KS partial tiles [KS][R][C+4] (summed here), sbias /
 // sdotw the bias and reward-head weights of this tile's columns, srp the reward partial dots of its rows.
@@ -457,7 +427,7 @@ __global__ void __launch_bounds__(512) linear_kernel(const LinArgs args) {
 
     // this lane's A rows (TM of them) and W rows (TN)
     const float* Abase[TM];
-    int arow[TM], env[TM];
+    int arow[TM];
     float mu[TM], rs[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -465,7 +435,6 @@ __global__ void __launch_bounds__(512) linear_kernel(const LinArgs args) {
         const int mm = m < args.M ? m : 0;
         arow[i] = args.a_mapped ? map_row(args.amap, mm) : mm;
         Abase[i] = P.A.p + (size_t)(arow[i] >> 5) * P.A.ts + (arow[i] & 31) * 4;
-        env[i] = (args.zmode | args.smode) ? arow[i] / args.rows_per_env : 0;
         mu[i] = 0.f; rs[i] = 1.f;
         if (PRO == PRO_LN_TANH) {
             // Chan-combine the producer's per-64-column (mean, M2) into mean and 1/sqrt(var + 1e-5)
@@ -521,7 +490,7 @@ __global__ void __launch_bounds__(512) linear_kernel(const LinArgs args) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) b[j] = *(const float4*)(Wbase + (size_t)j * P.W.ts + kq * 128);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = load_a(args, Abase[i], P.A.q0 + kq, arow[i], env[i]);
+        for (int i = 0; i < TM; ++i) a[i] = *(const float4*)(Abase[i] + (size_t)(P.A.q0 + kq) * 128);
     };
 
     if constexpr (!ROLL) {
@@ -601,7 +570,7 @@ DEVI float f4c(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k 
 // register tile. With the panel layout one K tile of one 32-row block is a contiguous 4 KiB, so staging is
 // 1 KiB wave loads and every fragment read is a conflict-free ds_read_b128; global traffic per MFMA is
 // shared by the whole workgroup.
-template <int TM, int TN, int WGM, int WGN, int KT, bool FK, bool AG>
+template <int TM, int TN, int WGM, int WGN, int KT, bool FK>
 __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArgs args) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int R = 32 * TM * WGM, C = 32 * TN * WGN, NT = 64 * WGM * WGN;
@@ -642,15 +611,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArg
 
     // staging slots: chunk c = tid + i*NT of a stage -> block c / (32*KQ), quad (c>>5) % KQ, row c&31
     const float* Asrc[CA];
-    int arow[CA], env[CA];
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
         const int cidx = tid + i * NT;
         const int m = m0 + (cidx / (32 * KQ)) * 32 + (cidx & 31);
         const int mm = m < args.M ? m : 0;
-        arow[i] = args.a_mapped ? map_row(args.amap, mm) : mm;
-        Asrc[i] = P.A.p + (size_t)(arow[i] >> 5) * P.A.ts + (arow[i] & 31) * 4;
-        env[i] = (args.zmode | args.smode) ? arow[i] / args.rows_per_env : 0;
+        const int arow = args.a_mapped ? map_row(args.amap, mm) : mm;
+        Asrc[i] = P.A.p + (size_t)(arow >> 5) * P.A.ts + (arow & 31) * 4 + (size_t)P.A.q0 * 128;
     }
     // per-chunk W pointers (chunk c: column block c / (32*KQ), quad (c>>5) % KQ, column c&31 of the block)
     const float* Wsrc[CW];
@@ -660,18 +627,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArg
         Wsrc[i] = P.W.p + (size_t)((n0 >> 5) + cidx / (32 * KQ)) * P.W.ts + ((cidx >> 5) % KQ) * 128 + (cidx & 31) * 4;
     }
     const int kq_total = args.K >> 2;
-    // AG: the A operand may be sampled (smode) or broadcast from z0 (zmode) -- load_a; else a plain panel load
     auto stage_load = [&](int kt, float4 (&ra)[CA], float4 (&rw)[CW]) {
         // FK (K a multiple of KT): every chunk is in range, no guards
 #pragma unroll
         for (int i = 0; i < CA; ++i) {
             const int cidx = tid + i * NT;
             const int kq = kt * KQ + ((cidx >> 5) % KQ);
-            if (FK || kq < kq_total)
-                ra[i] = AG ? load_a(args, Asrc[i], P.A.q0 + kq, arow[i], env[i])
-                           : *(const float4*)(Asrc[i] + (size_t)(P.A.q0 + kq) * 128);
-            else
-                ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            ra[i] = (FK || kq < kq_total) ? *(const float4*)(Asrc[i] + (size_t)kq * 128) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int i = 0; i < CW; ++i) {
@@ -891,6 +853,56 @@ __global__ void __launch_bounds__(512) value_kernel(const ValueArgs a) {
     }
 }
 
+
+// ------------------------------------------------------------------------------------------------ prep
+// Fills X before a CEM iteration's rollout: the sampled candidates of the N rollout rows for every step,
+// actions = clamp(mean + std * randn, -1, 1) (tdmpc.py:130-132, multiply then add like ATen), and -- before
+// the first iteration -- the latent columns of X_0 for all T rows with z0 = h(obs) (tdmpc.py:126-127: every
+// trajectory starts at the encoded observation). One float4 panel quad per thread, consecutive threads on
+// consecutive rows (512-byte runs of the panel layout).
+struct PrepArgs {
+    float* X; size_t x_stride; int Kx, apq, lpq;
+    int B, N, T, H, A;
+    const float* mean; const float* stdv; int mstride;   // [B][Hmax][A]
+    const float* eps; long eps_env; long eps_off;        // candidate noise [H][N][A] at eps_off per env
+    const float* z0;                                     // [B][Lp] or null (no broadcast)
+    long n_zq, n_sq;                                     // work items: z quads, sample quads
+};
+
+__global__ void __launch_bounds__(256) prep_kernel(const PrepArgs a) {
+    const long total = a.n_zq + a.n_sq;
+    for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
+        if (it < a.n_zq) {
+            // (e, q, row) with row fastest: X_0[e*T + row] latent quad q = z0[e][4q..4q+3]
+            const int row = (int)(it % a.T);
+            const long r2 = it / a.T;
+            const int q = (int)(r2 % a.lpq), e = (int)(r2 / a.lpq);
+            const int gr = e * a.T + row;
+            *(float4*)(a.X + (size_t)(gr >> 5) * a.Kx * 32 + (size_t)(a.apq + q) * 128 + (gr & 31) * 4) =
+                *(const float4*)(a.z0 + (size_t)e * a.lpq * 4 + q * 4);
+        } else {
+            // (e, t, q, n) with n fastest
+            long r2 = it - a.n_zq;
+            const int n = (int)(r2 % a.N); r2 /= a.N;
+            const int q = (int)(r2 % a.apq); r2 /= a.apq;
+            const int t = (int)(r2 % a.H);
+            const int e = (int)(r2 / a.H);
+            const float* mt = a.mean + (size_t)e * a.mstride + (size_t)t * a.A;
+            const float* sd = a.stdv + (size_t)e * a.mstride + (size_t)t * a.A;
+            const float* ep = a.eps + (size_t)e * a.eps_env + a.eps_off + ((size_t)t * a.N + n) * a.A;
+            float v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int cc = q * 4 + k;
+                v[k] = cc < a.A ? tclamp(fadd(mt[cc], fmul(sd[cc], ep[cc])), -1.f, 1.f) : 0.f;
+            }
+            const int gr = e * a.T + n;
+            *(float4*)(a.X + (size_t)t * a.x_stride + (size_t)(gr >> 5) * a.Kx * 32 + (size_t)q * 128 + (gr & 31) * 4) =
+                make_float4(v[0], v[1], v[2], v[3]);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------ CEM
 // One workgroup (16 waves) per environment, after each iteration's values: top-k (tdmpc.py:138-139),
 // softmax refit (:142-149); on the last iteration the output action (:152-160).
@@ -957,8 +969,7 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
     float* EA = (float*)(key + (size_t)NL * 64);           // [H][K][A]
     float* sc = EA + HKA;                                  // [64]
     float* omean = sc + 64;                                // [HA] mean before the update
-    float* ostd = omean + rup(HA, 4);                      // [HA]
-    float* smean = ostd + rup(HA, 4);                      // [HA]
+    float* smean = omean + 2 * rup(HA, 4);                 // [HA] (one [HA] slot unused)
     float* sstd = smean + rup(HA, 4);                      // [HA]
     int* eidx = (int*)(sstd + rup(HA, 4));                 // [64]
     float* red = (float*)(eidx + 64);                      // [32]
@@ -966,7 +977,7 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
     float* gstd = a.stdv + (size_t)e * a.Hmax * A;
     const float* val = a.value + (size_t)e * T;
 
-    for (int i = tid; i < HA; i += nt) { omean[i] = gmean[i]; ostd[i] = gstd[i]; }
+    for (int i = tid; i < HA; i += nt) omean[i] = gmean[i];
     // ---- top-K (K <= 64): each wave sorts 64-key lists, then a merge tree keeps the best 64
     for (int l = wave; l < NL; l += nwv) {
         const int i = l * 64 + lane;
@@ -986,8 +997,7 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
     }
     if (tid < K) eidx[tid] = (int)(key[tid] & 0xffffffffu);
     __syncthreads();
-    // ---- elite actions: rollout rows re-sampled exactly as the first-layer prologue did; pi rows from X_t
-    const float* ep = a.eps + (size_t)e * a.eps_env + a.eps_cem_off + (size_t)a.iter * a.eps_iter;
+    // ---- elite actions from X_t (sampled rows: prep_kernel; pi rows: the pi pre-rollout)
     for (int base = 0; base < HKA; base += 8 * nt) {
         float v[8];
 #pragma unroll
@@ -995,18 +1005,13 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
             const int idx = base + tid + u * nt;
             if (idx < HKA) {
                 const int t = idx / (K * A), k = (idx / A) % K, c = idx % A;
-                const int i = eidx[k];
-                v[u] = i < N ? ep[((size_t)t * N + i) * A + c]
-                             : a.X[(size_t)t * a.x_stride + pidx((size_t)e * T + i, c, a.Kx)];
+                v[u] = a.X[(size_t)t * a.x_stride + pidx((size_t)e * T + eidx[k], c, a.Kx)];
             }
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int idx = base + tid + u * nt;
-            if (idx < HKA) {
-                const int t = idx / (K * A), k = (idx / A) % K, c = idx % A;
-                EA[idx] = eidx[k] < N ? tclamp(fadd(omean[t * A + c], fmul(ostd[t * A + c], v[u])), -1.f, 1.f) : v[u];
-            }
+            if (idx < HKA) EA[idx] = v[u];
         }
     }
     // ---- softmax scores over the elites (one wave)
@@ -1257,10 +1262,8 @@ int init_attrs() {
     HIPCHK(hipFuncSetAttribute((const void*)cem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 #define LDS_ATTR1(...) \
     HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<__VA_ARGS__>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-#define LDS_ATTR(...) \
-    LDS_ATTR1(__VA_ARGS__, true, false) LDS_ATTR1(__VA_ARGS__, true, true) LDS_ATTR1(__VA_ARGS__, false, false) \
-    LDS_ATTR1(__VA_ARGS__, false, true)
-    LDS_ATTR(2, 2, 2, 2, 32) LDS_ATTR(2, 1, 2, 4, 32) LDS_ATTR(3, 1, 2, 4, 32) LDS_ATTR(1, 1, 2, 2, 32) LDS_ATTR(2, 1, 2, 2, 32)
+#define LDS_ATTR(...) LDS_ATTR1(__VA_ARGS__, true) LDS_ATTR1(__VA_ARGS__, false)
+    LDS_ATTR(2, 2, 2, 2, 32) LDS_ATTR(2, 1, 2, 4, 32) LDS_ATTR(3, 1, 2, 4, 32) LDS_ATTR(1, 1, 2, 2, 32)
 #undef LDS_ATTR
 #undef LDS_ATTR1
     if (rc) return TDMPC_E_HIP;
@@ -1358,11 +1361,8 @@ int launch_lds_t(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
                       (pf.kdim == 0 || (a.K == pf.kdim && nmax == pf.kdim)) && (pf.rows == 0 || a.M == pf.rows);
     if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], s));
     const dim3 block(64 * WGM * WGN);
-    const bool fk = a.K % KT == 0, ag = a.smode || a.zmode;
-    if (fk && !ag) hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, true, false>), grid, block, lds, s, a);
-    else if (fk) hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, true, true>), grid, block, lds, s, a);
-    else if (!ag) hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, false, false>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, false, true>), grid, block, lds, s, a);
+    if (a.K % KT == 0) hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, true>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((linear_lds_kernel<TM, TN, WGM, WGN, KT, false>), grid, block, lds, s, a);
     HIPCHK(hipGetLastError());
     if (prof) {
         HIPCHK(hipEventRecord(pf.ev[pf.n + 1], s));
@@ -1454,7 +1454,6 @@ LinArgs args0() {
     memset(&a, 0, sizeof a);
     a.amap = {1 << 30, 0, 0};
     a.cmap = {1 << 30, 0, 0};
-    a.rows_per_env = 1 << 30;
     return a;
 }
 
@@ -1472,26 +1471,15 @@ Opnd hop(const float* H, const Ctx& c, int q0) { return Opnd{H, (long)2 * c.M * 
 Outp hout(float* H, const Ctx& c, int q0) { return Outp{H, (long)2 * c.M * 32, q0}; }
 Opnd wop(const Ctx& c, size_t off, int K) { return Opnd{c.pw + off, (long)K * 32, 0}; }
 
-struct Sampling {  // CEM candidate sampling in the first-layer prologue
-    int on; const float* eps; int iter;
-};
-
 // One TOLD.next step (tdmpc.py:34-37) for `rows` logical rows mapped onto X rows, plus the return update
-// of estimate_value (:88-90). t == 0 reads z0 for every row; `smp` samples the rollout rows' actions.
-int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, Sampling smp) {
+// of estimate_value (:88-90). X_t holds the rows' [a|z] (prep_kernel wrote the sampled actions and z0).
+int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last) {
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
     {   // h1 = ELU(W1[d;r] [a|z] + b)   (dynamics.0 and reward.0 fused: N = 2M)
         LinArgs a = args0();
         a.M = rows; a.K = c.Kx; a.a_mapped = 1; a.amap = map;
-        a.apq = w.Ap / 4; a.rows_per_env = c.T;
-        a.zmode = t == 0; a.z0 = c.k.z0; a.Lp = w.Lp;
-        if (smp.on) {
-            a.smode = 1; a.mean_t = c.k.mean + t * c.A; a.std_t = c.k.stdv + t * c.A; a.mstride = c.d->max_horizon * c.A;
-            a.seps = smp.eps; a.seps_env = c.eps_env; a.s_rows = c.N;
-            a.seps_off = c.eps_cem_off + (long)smp.iter * c.eps_iter + (long)t * c.N * c.A; a.A = c.A;
-        }
         LinProb& p = a.p[0];
         p.A = xop(c, t, 0); p.W = wop(c, w.w1x, c.Kx); p.bias = c.pw + w.b1x;
         p.C = hout(c.k.H1, c, 0); p.N = p.nvalid = p.nstore = 2 * M; p.epi = EPI_ELU;
@@ -1531,7 +1519,6 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
     {
         LinArgs a = args0();
         a.M = rows; a.K = w.Lp; a.a_mapped = 1; a.amap = map;
-        a.apq = w.Ap / 4; a.rows_per_env = c.T; a.zmode = t == 0; a.z0 = c.k.z0; a.Lp = w.Lp;
         LinProb& p = a.p[0];
         p.A = xop(c, t, w.Ap / 4); p.W = wop(c, w.wp1, w.Lp); p.bias = c.pw + w.bp1;
         p.C = hout(c.k.H1, c, 0); p.N = p.nvalid = p.nstore = M; p.epi = EPI_ELU;
@@ -1559,6 +1546,26 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
 }
 
 // Terminal value: Q(z_H, pi(z_H)) for all T rows of every env (tdmpc.py:91-92).
+// prep_kernel launch: candidates of CEM iteration `iter` for all H steps (if noise) and, with z0, the
+// latent columns of X_0 for every row.
+int prep(const Ctx& c, const float* noise, int iter, const float* z0) {
+    PrepArgs a;
+    memset(&a, 0, sizeof a);
+    a.X = c.k.X; a.x_stride = c.k.x_stride; a.Kx = c.Kx; a.apq = c.w.Ap / 4; a.lpq = c.w.Lp / 4;
+    a.B = c.B; a.N = c.N; a.T = c.T; a.H = c.H; a.A = c.A;
+    a.mean = c.k.mean; a.stdv = c.k.stdv; a.mstride = c.d->max_horizon * c.A;
+    a.eps = noise; a.eps_env = c.eps_env; a.eps_off = c.eps_cem_off + (long)iter * c.eps_iter;
+    a.z0 = z0;
+    a.n_zq = z0 ? (long)c.B * a.lpq * c.T : 0;
+    a.n_sq = noise ? (long)c.B * c.H * a.apq * c.N : 0;
+    const long total = a.n_zq + a.n_sq;
+    if (!total) return 0;
+    const int blocks = (int)std::min<long>((total + 255) / 256, 2048);
+    hipLaunchKernelGGL(prep_kernel, dim3(blocks), dim3(256), 0, c.s, a);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 int terminal_q(const Ctx& c, float discH, float* value_out, int I, int iter) {
     const Layout& w = c.w;
     const int rows = c.B * c.T, M = c.M;
@@ -1821,6 +1828,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     const int N = c.N, P = c.P, T = c.T;
     // z0 = h(obs) and mean = 0 (warm: prev_mean shifted), std = 2
     if ((rc = encode(c, obs, obs_is_u8, B, prev_mean, prm->warm_start))) return rc;
+    if ((rc = prep(c, noise, 0, c.k.z0))) return rc;
 
     // pi pre-rollout (tdmpc.py:113-118) fused with CEM iteration 0: at each step t the policy rows get
     // pi(z_t) first, then ONE TOLD.next launch advances all T rows of every env (rollout rows with the
@@ -1832,7 +1840,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
         const RowMap pm = {P, T, N};
         for (int t = 0; t < H; ++t) {
             if ((rc = policy(c, t, B * P, pm, noise, c.eps_env, P, (long)t * P * c.A, prm->min_std))) return rc;
-            if ((rc = step_next(c, t, B * T, all, prm->discount_pow[t], t == 0, t == H - 1, Sampling{1, noise, 0})))
+            if ((rc = step_next(c, t, B * T, all, prm->discount_pow[t], t == 0, t == H - 1)))
                 return rc;
         }
     }
@@ -1851,9 +1859,10 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
 
     const RowMap rm = {N, T, 0};
     for (int i = 0; i < I; ++i) {
+        if (i > 0 && (rc = prep(c, noise, i, nullptr))) return rc;
         if (i > 0 || P == 0)
             for (int t = 0; t < H; ++t)
-                if ((rc = step_next(c, t, B * N, rm, prm->discount_pow[t], t == 0, t == H - 1, Sampling{1, noise, i})))
+                if ((rc = step_next(c, t, B * N, rm, prm->discount_pow[t], t == 0, t == H - 1)))
                     return rc;
         if ((rc = policy(c, H, B * T, all, noise, c.eps_env, T, c.eps_cem_off + (long)i * c.eps_iter + c.eps_term_off,
                          prm->min_std)))
@@ -1883,9 +1892,10 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     hipLaunchKernelGGL(scatter_actions_kernel, dim3(512), dim3(256), 0, c.s, actions, c.k.X, c.k.x_stride, H, T, c.A,
                        c.w.Ap, c.Kx, B);
     HIPCHK(hipGetLastError());
+    if ((rc = prep(c, nullptr, 0, c.k.z0))) return rc;
     const RowMap all = {T, T, 0};
     for (int t = 0; t < H; ++t)
-        if ((rc = step_next(c, t, B * T, all, prm->discount_pow[t], t == 0, t == H - 1, Sampling{0, nullptr, 0})))
+        if ((rc = step_next(c, t, B * T, all, prm->discount_pow[t], t == 0, t == H - 1)))
             return rc;
     if (z_last) {
         hipLaunchKernelGGL(gather_z_kernel, dim3(256), dim3(256), 0, c.s, Xt(c, H), c.Kx, c.w.Ap, L, B * T, z_last);

@@ -81,7 +81,7 @@ int main(int argc, char** argv) {
         if (setup_ctx(c, &d, packed, ws, sz.workspace_bytes, B, 5, 6, s)) { printf("ctx failed\n"); return 1; }
         init_attrs();
 #define ATTR1(...) CK(hipFuncSetAttribute((const void*)linear_lds_kernel<__VA_ARGS__>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-#define ATTR(...) ATTR1(__VA_ARGS__, true, false) ATTR1(__VA_ARGS__, true, true) ATTR1(__VA_ARGS__, false, false) ATTR1(__VA_ARGS__, false, true)
+#define ATTR(...) ATTR1(__VA_ARGS__, true) ATTR1(__VA_ARGS__, false)
         ATTR(1, 1, 2, 2, 32) ATTR(1, 2, 2, 2, 32) ATTR(1, 1, 2, 4, 32) ATTR(1, 2, 2, 4, 32)
 #undef ATTR
         const Layout& w = c.w; const int M = c.M;
@@ -147,7 +147,7 @@ int main(int argc, char** argv) {
     struct Case { const char* name; std::function<void()> fn; };
     std::vector<Case> cases;
     // individual layers of one step (rollout rows)
-    cases.push_back({"step_next(t=1) [S1+S2+S3]", [&] { step_next(c, 1, B * c.N, rm, 0.99f, 0, 0, Sampling{1, noise, 0}); }});
+    cases.push_back({"step_next(t=1) [S1+S2+S3]", [&] { step_next(c, 1, B * c.N, rm, 0.99f, 0, 0); }});
     cases.push_back({"policy(H) [pi1+pi2+pi3]", [&] { policy(c, 5, B * c.T, all, noise, c.eps_env, c.T, 0, 0.05f); }});
     cases.push_back({"terminal_q [Q1+Q2+value]", [&] { terminal_q(c, 0.95f, nullptr, 6, 0); }});
     cases.push_back({"encode", [&] { encode(c, obs, 0, B, prev, 0); }});
