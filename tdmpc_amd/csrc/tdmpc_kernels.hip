@@ -591,23 +591,17 @@ __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArg
     STAMP(0);
 #endif
     const int epi = P.epi;
-    // LDS: stage buffers [3][SA + SW] aliased by the epilogue tile [R][C+4]; then bias, dotw, rpart
+    // LDS: stage buffers [3][SA + SW]; bias [C]; dotw [C]; per-row 32-column partials [R][C/32] (float2)
     constexpr int BUF = SA + SW;
-    constexpr int EPI_F = R * (C + 4);
-    constexpr int BODY = 3 * BUF > EPI_F ? 3 * BUF : EPI_F;
+    constexpr int BODY = 3 * BUF;
     float* sbias = smem + BODY;
     float* sdotw = sbias + C;
-    float* srp = sdotw + C;
+    float2* spart = (float2*)(sdotw + C);
     for (int i = tid; i < C / 4; i += NT) {
         const int n = n0 + 4 * i;
         *(float4*)(sbias + 4 * i) = *(const float4*)(P.bias + n);
         if (epi == EPI_ELU_DOT) *(float4*)(sdotw + 4 * i) = *(const float4*)(P.dotw + n);
     }
-    if (epi == EPI_LIN_Z && blockIdx.y == 0)
-        for (int i = tid; i < R * args.rpart_nt; i += NT) {
-            const int lm = m0 + i / args.rpart_nt;
-            srp[i] = lm < args.M ? args.rpart[(size_t)lm * args.rpart_nt + i % args.rpart_nt] : 0.f;
-        }
 
     // staging slots: chunk c = tid + i*NT of a stage -> block c / (32*KQ), quad (c>>5) % KQ, row c&31
     const float* Asrc[CA];
@@ -685,7 +679,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArg
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(fa[g][i], kk), f4c(fb[g][j], kk), acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(fb[g][j], kk), f4c(fa[g][i], kk), acc[i][j], 0, 0, 0);
     };
     // Global loads run two stages ahead of their LDS store: stage st+3 is requested during stage st into one
     // register set while the other set (stage st+2, requested a stage earlier) is written to LDS at its end,
@@ -728,22 +722,87 @@ __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArg
 #ifdef TDMPC_STAMPS
     STAMP(2);
 #endif
-    // accumulators -> LDS tile [R][C+4] (the stage buffers are free after the last barrier)
-    {
-        float* base = smem + (size_t)(wm * TM * 32) * (C + 4) + wn * TN * 32;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int e = 0; e < 16; ++e)
-                    base[(size_t)(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * (C + 4) + j * 32 + r] = acc[i][j][e];
-    }
-    __syncthreads();
+    // Register epilogue. The MFMA operands are swapped (W fragment first), so acc[i][j] holds the transposed
+    // 32x32 block: lane (r, h) owns activation row (wm*TM + i)*32 + r and, for q = 0..3, the four consecutive
+    // output columns (wn*TN + j)*32 + 8q + 4h + 0..3 -- one float4 panel quad per q, and 32 lanes store one
+    // quad of 32 consecutive rows = 512 contiguous bytes. Row reductions (reward-head dot, LayerNorm moments)
+    // meet the other half-wave through a lane swap and the other 32-column block through LDS.
 #ifdef TDMPC_STAMPS
     STAMP(3);
 #endif
-    lin_epilogue<R, C>(args, P, smem, 1, m0, n0, sbias, sdotw, srp);
+    {
+        const int cq0 = n0 >> 2;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int lrow = (wm * TM + i) * 32 + r;
+            const int lm = m0 + lrow;
+            const bool rval = lm < args.M;
+            const int crow = rval ? (args.c_mapped ? map_row(args.cmap, lm) : lm) : 0;
+            float* Cbase = P.C.p ? P.C.p + (size_t)(crow >> 5) * P.C.ts + (crow & 31) * 4 : nullptr;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int cb = (wn * TN + j) * 32;        // column block within the tile
+                float v[16];
+                float s1 = 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int c = cb + 8 * q + 4 * h;
+                    const float4 bb = *(const float4*)(sbias + c);
+                    float o[4] = {acc[i][j][4 * q] + bb.x, acc[i][j][4 * q + 1] + bb.y, acc[i][j][4 * q + 2] + bb.z,
+                                  acc[i][j][4 * q + 3] + bb.w};
+                    if (epi == EPI_ELU || epi == EPI_ELU_DOT) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) o[k] = elu_f(o[k]);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (n0 + c + k >= P.nvalid) o[k] = 0.f;
+                        v[4 * q + k] = o[k];
+                    }
+                    if (rval && n0 + c < P.nstore)
+                        *(float4*)(Cbase + (size_t)(P.C.q0 + cq0 + (c >> 2)) * 128) = make_float4(o[0], o[1], o[2], o[3]);
+                    if (epi == EPI_ELU_DOT) {
+                        const float4 w4 = *(const float4*)(sdotw + c);
+                        s1 += (o[0] * w4.x + o[1] * w4.y) + (o[2] * w4.z + o[3] * w4.w);
+                    } else if (epi == EPI_LNSTATS) {
+                        s1 += (o[0] + o[1]) + (o[2] + o[3]);
+                    }
+                }
+                if (epi == EPI_ELU_DOT) {
+                    const float tot = s1 + __shfl_xor(s1, 32);
+                    if (h == 0) spart[lrow * (C / 32) + (wn * TN + j)] = make_float2(tot, 0.f);
+                } else if (epi == EPI_LNSTATS) {
+                    // (mean, M2) of the 32 columns of this block
+                    const float mean = (s1 + __shfl_xor(s1, 32)) * (1.f / 32.f);
+                    float m2 = 0.f;
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) {
+                        const float d = v[k] - mean;
+                        m2 += d * d;
+                    }
+                    m2 += __shfl_xor(m2, 32);
+                    if (h == 0) spart[lrow * (C / 32) + (wn * TN + j)] = make_float2(mean, m2);
+                }
+            }
+        }
+        if (epi == EPI_ELU_DOT || epi == EPI_LNSTATS) {
+            // pairs of 32-column blocks -> the per-64-column outputs (dot partials / Chan-combined moments)
+            __syncthreads();
+            for (int t = tid; t < R * (C / 64); t += NT) {
+                const int row = t % R, b = t / R;
+                const int lm = m0 + row;
+                if (lm >= args.M) continue;
+                const float2 x = spart[row * (C / 32) + 2 * b], y = spart[row * (C / 32) + 2 * b + 1];
+                if (epi == EPI_ELU_DOT) {
+                    P.dot_out[(size_t)lm * P.dot_ld + (n0 / 64) + b] = x.x + y.x;
+                } else {
+                    const float delta = y.x - x.x;
+                    P.st_out[(size_t)lm * P.st_ld + (n0 / 64) + b] =
+                        make_float2(x.x + 0.5f * delta, x.y + y.y + delta * delta * 16.f);
+                }
+            }
+        }
+    }
 #ifdef TDMPC_STAMPS
     __syncthreads();
     STAMP(4);
@@ -1352,10 +1411,14 @@ template <int TM, int TN, int WGM, int WGN, int KT>
 int launch_lds_t(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
     constexpr int R = 32 * TM * WGM, C = 32 * TN * WGN;
     constexpr int BUF = (R / 32 + C / 32) * KT * 32;
-    constexpr int EPI_F = R * (C + 4);
-    constexpr int BODY = 3 * BUF > EPI_F ? 3 * BUF : EPI_F;
+    static_assert(C % 64 == 0, "row reductions work on 64-column blocks");
     dim3 grid((a.M + R - 1) / R, (nmax + C - 1) / C, nprob);
-    const size_t lds = ((size_t)BODY + 2 * C + (size_t)R * std::max(a.rpart_nt, 1)) * 4;
+    for (int q = 0; q < nprob; ++q)
+        if (a.p[q].epi != EPI_ELU && a.p[q].epi != EPI_ELU_DOT && a.p[q].epi != EPI_LNSTATS) {
+            snprintf(g_err, sizeof g_err, "LDS tile: unsupported epilogue %d", a.p[q].epi);
+            return TDMPC_E_DIMS;
+        }
+    const size_t lds = ((size_t)3 * BUF + 2 * C + (size_t)R * (C / 32) * 2) * 4;
     Profiler& pf = g_prof;
     const bool prof = pf.armed && (pf.cfg == 0 || pf.cfg == 3) && (pf.pro <= 0) && pf.n + 2 <= pf.cap &&
                       (pf.kdim == 0 || (a.K == pf.kdim && nmax == pf.kdim)) && (pf.rows == 0 || a.M == pf.rows);
