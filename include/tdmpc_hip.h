@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define TDMPC_ABI_VERSION 2
+#define TDMPC_ABI_VERSION 3
 
 #define TDMPC_OK 0
 #define TDMPC_E_DIMS (-1)     /* unsupported or inconsistent dims / params */
@@ -66,7 +66,13 @@ typedef struct tdmpc_plan_params {
     float one_minus_momentum; /* float32(1 - momentum) computed in float64 like Python does */
     float std_floor;       /* self.std: lower clamp of the CEM std (tdmpc.py:148) */
     float discount_pow[17];/* float32(discount**t) for t = 0..H, the running Python-float product */
+    int32_t path;          /* kernel path: 0 = auto by row count, 1 = layered GEMMs only, 2 = row-block chain
+                              kernels wherever the shape allows (results agree within the fp32 tolerance) */
 } tdmpc_plan_params;
+
+#define TDMPC_PATH_AUTO 0
+#define TDMPC_PATH_LAYERED 1
+#define TDMPC_PATH_CHAIN 2
 
 /* Byte sizes the caller must allocate (all 256-byte aligned). */
 typedef struct tdmpc_sizes {

@@ -11,6 +11,9 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libtdmpc_hip.so")
 
+ABI_VERSION = 3
+PATHS = {"auto": 0, "layered": 1, "chain": 2}
+
 EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc_num_param_tensors",
             "tdmpc_pack_weights", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_last_error",
             "tdmpc_profile_begin", "tdmpc_profile_end")
@@ -27,7 +30,7 @@ class PlanParams(C.Structure):
                 ("warm_start", C.c_int32), ("eval_mode", C.c_int32),
                 ("min_std", C.c_float), ("temperature", C.c_float), ("momentum", C.c_float),
                 ("one_minus_momentum", C.c_float), ("std_floor", C.c_float),
-                ("discount_pow", C.c_float * 17)]
+                ("discount_pow", C.c_float * 17), ("path", C.c_int32)]
 
 
 class Sizes(C.Structure):
@@ -66,7 +69,7 @@ def lib():
     for name in EXPORTED:
         if not hasattr(L, name):
             raise RuntimeError(f"{LIB_PATH} does not export {name}")
-    if L.tdmpc_abi_version() != 2:
+    if L.tdmpc_abi_version() != ABI_VERSION:
         raise RuntimeError("libtdmpc_hip ABI version mismatch")
     _LIB = L
     return L

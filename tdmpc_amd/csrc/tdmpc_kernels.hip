@@ -147,6 +147,7 @@ struct Work {
     float* G;        // [B*T] discounted return so far
     float* rlast;    // [B*T] reward at t = H-1
     float* value;    // [B*T]
+    float* qv;       // [2][xrows] Q-head outputs of the chain path
     float* z0;       // [B][Lp] dense
     float* mean;     // [B][Hmax][A]
     float* stdv;     // [B][Hmax][A]
@@ -178,6 +179,7 @@ void make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k) {
     k->G = (float*)take(B * T * 4);
     k->rlast = (float*)take(B * T * 4);
     k->value = (float*)take(B * T * 4);
+    k->qv = (float*)take(2 * (size_t)k->xrows * 4);
     k->z0 = (float*)take(B * w.Lp * 4);
     k->mean = (float*)take(B * H * w.A * 4);
     k->stdv = (float*)take(B * H * w.A * 4);
@@ -810,6 +812,371 @@ __global__ void __launch_bounds__(64 * WGM * WGN) linear_lds_kernel(const LinArg
 #endif
 }
 
+// ------------------------------------------------------------------------------------------------ chain
+// Row-block MLP chain: one workgroup carries 32 candidate rows through a whole TOLD head -- Linear(K1 -> M)
+// + activation, Linear(M -> M) + activation and the head's last layer -- with the hidden activations held in
+// LDS ([M/4][32][4], the panel layout of one 32-row block) and never written to HBM. 8 waves; in the two
+// M-wide layers wave w owns output columns [w*32*TN, (w+1)*32*TN) and streams its own weight-panel columns
+// from L2 straight into registers (a D-deep ring of 1 KiB wave loads; the 1-3 MB of a head's weights are
+// read by every workgroup and stay L2-resident), while the A fragments -- the block's activations -- are
+// conflict-free ds_read_b128 shared by all waves. Per FLOP this reads as many bytes as a 128x128-tiled GEMM
+// (32 rows reuse each weight fragment), but a rollout step is one launch instead of three and the
+// 2 x 16 MB of hidden activations per step never leave the CU.
+//   CH_STEP  TOLD.next (tdmpc.py:34-37) + the return update (:88-90); blockIdx.y = 0 dynamics (z' into
+//            X_{t+1}), 1 reward (reward-head dot, G += gamma^t r).
+//   CH_PI    TOLD.pi + TruncatedNormal sample (tdmpc.py:39-45, helper.py:86-96) -> X_t action columns.
+//   CH_Q     helper.q (helper.py:197-201): Linear, LayerNorm, Tanh, Linear, LayerNorm, ELU, Linear(M -> 1);
+//            blockIdx.y = Q head; writes q_p per row (min, gamma^H and nan_to_num: qvalue()).
+enum { CH_STEP = 0, CH_PI = 1, CH_Q = 2 };
+
+struct ChainProb {
+    const float* W1; const float* b1;    // panel [M][K1], bias [M]
+    const float* W2; const float* b2;    // panel [M][M], bias [M]
+    const float* g1; const float* be1; const float* g2; const float* be2;  // CH_Q LayerNorm affines [M]
+    const float* w3v; const float* b3v;  // reward / Q last layer: dense [M] + bias [1]
+};
+
+struct ChainArgs {
+    ChainProb p[2];
+    int rows, M, K1, q1;                 // logical rows; hidden width; first-layer K and its X quad offset
+    int hfl;                             // floats of the LDS activation block (max(K1, M) * 32)
+    RowMap amap;                         // logical row -> X row (input and output)
+    const float* X; long x_ts;           // X_t panel (input)
+    // last layer of dynamics / pi: panel [n3][M] + bias -> Xo quads [out_q0, out_q0 + nstore/4)
+    const float* W3; const float* b3; int n3, nvalid, nstore;
+    float* Xo; int out_q0;
+    // CH_STEP reward: G update (EPI_LIN_Z of the layered path)
+    float* G; float* rlast; float disc; int first, last;
+    // CH_PI: TruncatedNormal noise
+    const float* eps; int eps_G; long eps_env; long eps_off; float min_std, lo, hi; int A;
+    // CH_Q: q_p of row x at q[p * q_ld + x]
+    float* q; int q_ld;
+};
+
+// acc[j] += W(block j) . A over k groups [g0, g1). A: LDS block [K/4][32][4]; Wp: the wave's first weight-panel
+// block, already offset by the lane's (h, r); blocks wbs floats apart. W rides a D-deep register ring, A is
+// read one group ahead.
+template <int TN, int D>
+DEVI void chain_gemm(floatx16 (&acc)[TN], const float* sA, const float* Wp, long wbs, int g0, int g1, int r,
+                     int h) {
+    // Every load is issued unconditionally (past the end: the last group again, never used) so that the
+    // number of loads in flight is the same at every MFMA and the wait before group g's MFMAs is
+    // vmcnt((D-1)*TN), not a drain.
+    const int gl = g1 - 1;
+    float4 wr[D][TN];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) wr[d][j] = *(const float4*)(Wp + j * wbs + (size_t)min(g0 + d, gl) * 256);
+    const float* ap = sA + (h * 32 + r) * 4;
+    float4 an = *(const float4*)(ap + (size_t)g0 * 256);
+    int gb = g0;
+    for (; gb + D <= g1; gb += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int g = gb + d;
+            const float4 av = an;
+            an = *(const float4*)(ap + (size_t)min(g + 1, gl) * 256);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(wr[d][j], kk), f4c(av, kk), acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) wr[d][j] = *(const float4*)(Wp + j * wbs + (size_t)min(g + D, gl) * 256);
+            // keep each group's refill right behind its MFMAs (the scheduler would otherwise cluster the
+            // chunk's loads at its end and shrink the prefetch distance to one group)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // tail (< D groups): their weights are already in the ring
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) {
+        if (gb + d < g1) {
+            const float4 av = an;
+            an = *(const float4*)(ap + (size_t)min(gb + d + 1, gl) * 256);
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(wr[d][j], kk), f4c(av, kk), acc[j], 0, 0, 0);
+        }
+    }
+}
+
+// Row mean and 1/sqrt(var + 1e-5) over the M columns of the block's rows (biased variance, two passes),
+// from each lane's TN*16 values of row r: per-wave partials through red0 / red1 ([8][32] each).
+template <int TN>
+DEVI void chain_row_moments(const float (&v)[TN * 16], float* red0, float* red1, int wave, int r, int h, int M,
+                            float& mean, float& rstd) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TN * 16; ++i) s += v[i];
+    s += __shfl_xor(s, 32);
+    if (h == 0) red0[wave * 32 + r] = s;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) tot += red0[w * 32 + r];
+    mean = tot / (float)M;
+    float m2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < TN * 16; ++i) {
+        const float d = v[i] - mean;
+        m2 += d * d;
+    }
+    m2 += __shfl_xor(m2, 32);
+    if (h == 0) red1[wave * 32 + r] = m2;
+    __syncthreads();
+    float tot2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) tot2 += red1[w * 32 + r];
+    rstd = 1.0f / sqrtf(fmaxf(tot2 / (float)M, 0.f) + 1e-5f);
+}
+
+template <int MODE, int TN>
+__global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int D = 4;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int pb = blockIdx.y;
+    const ChainProb& P = a.p[pb];
+    const int M = a.M;
+    const int m0 = blockIdx.x * 32;
+    float* sH = smem;                       // activation block [max(K1, M)/4][32][4]
+    float* red0 = smem + a.hfl;             // [8][32]
+    float* red1 = red0 + 256;               // [8][32]
+    const int lo = h * 128 + r * 4;         // lane offset inside a weight-panel k group
+    const int cw0 = wave * TN;              // first 32-column block of this wave in the M-wide layers
+
+    // ---- the block's input rows: X quads [q1, q1 + K1/4), 32 consecutive lanes = 32 rows of one quad
+    for (int i = tid; i < (a.K1 >> 2) * 32; i += 512) {
+        const int row = i & 31, q = i >> 5;
+        const int lm = m0 + row;
+        const int xr = map_row(a.amap, lm < a.rows ? lm : 0);
+        ((float4*)sH)[i] = *(const float4*)(a.X + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.q1 + q) * 128 + (xr & 31) * 4);
+    }
+    __syncthreads();
+
+    // ---- layer 1: [32 x K1] . W1^T -> [32 x M]
+    floatx16 acc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    chain_gemm<TN, D>(acc, sH, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3, r, h);
+    __syncthreads();   // every wave is done with the input tile: sH becomes h1
+    {
+        float v[TN * 16];
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int c = (cw0 + j) * 32 + 8 * q + 4 * h;
+                const float4 bb = *(const float4*)(P.b1 + c);
+                v[j * 16 + 4 * q + 0] = acc[j][4 * q + 0] + bb.x;
+                v[j * 16 + 4 * q + 1] = acc[j][4 * q + 1] + bb.y;
+                v[j * 16 + 4 * q + 2] = acc[j][4 * q + 2] + bb.z;
+                v[j * 16 + 4 * q + 3] = acc[j][4 * q + 3] + bb.w;
+            }
+        if (MODE == CH_Q) {
+            float mean, rs;
+            chain_row_moments<TN>(v, red0, red1, wave, r, h, M, mean, rs);
+            const float sh = -rs * mean;
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int c = (cw0 + j) * 32 + 8 * q + 4 * h;
+                    const float4 gg = *(const float4*)(P.g1 + c), bb = *(const float4*)(P.be1 + c);
+                    float* x = v + j * 16 + 4 * q;
+                    // ATen LayerNorm: (x * rstd + (-rstd * mean)) * gamma + beta, then Tanh
+                    x[0] = tanh_f(fadd(fmul(fadd(fmul(x[0], rs), sh), gg.x), bb.x));
+                    x[1] = tanh_f(fadd(fmul(fadd(fmul(x[1], rs), sh), gg.y), bb.y));
+                    x[2] = tanh_f(fadd(fmul(fadd(fmul(x[2], rs), sh), gg.z), bb.z));
+                    x[3] = tanh_f(fadd(fmul(fadd(fmul(x[3], rs), sh), gg.w), bb.w));
+                }
+        } else {
+#pragma unroll
+            for (int i = 0; i < TN * 16; ++i) v[i] = elu_f(v[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int cq = (cw0 + j) * 8 + 2 * q + h;
+                *(float4*)(sH + (cq * 32 + r) * 4) =
+                    make_float4(v[j * 16 + 4 * q], v[j * 16 + 4 * q + 1], v[j * 16 + 4 * q + 2], v[j * 16 + 4 * q + 3]);
+            }
+    }
+    __syncthreads();
+
+    // ---- layer 2: [32 x M] . W2^T -> [32 x M]
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    chain_gemm<TN, D>(acc, sH, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3, r, h);
+    float v[TN * 16];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int c = (cw0 + j) * 32 + 8 * q + 4 * h;
+            const float4 bb = *(const float4*)(P.b2 + c);
+            v[j * 16 + 4 * q + 0] = acc[j][4 * q + 0] + bb.x;
+            v[j * 16 + 4 * q + 1] = acc[j][4 * q + 1] + bb.y;
+            v[j * 16 + 4 * q + 2] = acc[j][4 * q + 2] + bb.z;
+            v[j * 16 + 4 * q + 3] = acc[j][4 * q + 3] + bb.w;
+        }
+    const bool head_dot = MODE == CH_Q || (MODE == CH_STEP && pb == 1);
+    if (head_dot) {
+        // reward / Q last layer Linear(M -> 1) on the row: per-wave partial dots, then one lane per row
+        if (MODE == CH_Q) {
+            float mean, rs;
+            chain_row_moments<TN>(v, red0, red1, wave, r, h, M, mean, rs);
+            const float sh = -rs * mean;
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int c = (cw0 + j) * 32 + 8 * q + 4 * h;
+                    const float4 gg = *(const float4*)(P.g2 + c), bb = *(const float4*)(P.be2 + c);
+                    float* x = v + j * 16 + 4 * q;
+                    x[0] = fadd(fmul(fadd(fmul(x[0], rs), sh), gg.x), bb.x);
+                    x[1] = fadd(fmul(fadd(fmul(x[1], rs), sh), gg.y), bb.y);
+                    x[2] = fadd(fmul(fadd(fmul(x[2], rs), sh), gg.z), bb.z);
+                    x[3] = fadd(fmul(fadd(fmul(x[3], rs), sh), gg.w), bb.w);
+                }
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int c = (cw0 + j) * 32 + 8 * q + 4 * h;
+                const float4 w4 = *(const float4*)(P.w3v + c);
+                const float* x = v + j * 16 + 4 * q;
+                s += (elu_f(x[0]) * w4.x + elu_f(x[1]) * w4.y) + (elu_f(x[2]) * w4.z + elu_f(x[3]) * w4.w);
+            }
+        s += __shfl_xor(s, 32);
+        if (h == 0) red0[wave * 32 + r] = s;
+        __syncthreads();
+        if (tid < 32) {
+            const int lm = m0 + tid;
+            if (lm < a.rows) {
+                const int xr = map_row(a.amap, lm);
+                float tot = 0.f;
+#pragma unroll
+                for (int w = 0; w < 8; ++w) tot += red0[w * 32 + tid];
+                const float o = tot + P.b3v[0];
+                if (MODE == CH_Q) {
+                    a.q[(size_t)pb * a.q_ld + xr] = o;
+                } else {
+                    // G += discount * reward (tdmpc.py:89), float32(discount) like ATen's scalar mul
+                    const float dr = fmul(a.disc, o);
+                    a.G[xr] = a.first ? dr : fadd(a.G[xr], dr);
+                    if (a.last) a.rlast[xr] = o;
+                }
+            }
+        }
+        return;
+    }
+    // dynamics / pi: h2 = ELU(y2) back into the activation block once every wave is done reading h1
+#pragma unroll
+    for (int i = 0; i < TN * 16; ++i) v[i] = elu_f(v[i]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int cq = (cw0 + j) * 8 + 2 * q + h;
+            *(float4*)(sH + (cq * 32 + r) * 4) =
+                make_float4(v[j * 16 + 4 * q], v[j * 16 + 4 * q + 1], v[j * 16 + 4 * q + 2], v[j * 16 + 4 * q + 3]);
+        }
+    __syncthreads();
+
+    // ---- layer 3: [32 x M] . W3^T -> [32 x n3] as items (32-column block, K part): narrow heads split K
+    // over up to 4 waves (one per SIMD); partial tiles meet in the activation block after the reads.
+    const int nb3 = a.n3 >> 5;
+    const int ks = nb3 >= 4 ? 1 : 4 / nb3;
+    const int items = nb3 * ks;
+    const int gper = (M >> 3) / ks;
+    floatx16 a3a[1], a3b[1];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { a3a[0][e] = 0.f; a3b[0][e] = 0.f; }
+    if (wave < items) {
+        const int blk = wave / ks, kp = wave % ks;
+        chain_gemm<1, D>(a3a, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
+    }
+    if (wave + 8 < items) {
+        const int blk = (wave + 8) / ks, kp = (wave + 8) % ks;
+        chain_gemm<1, D>(a3b, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (wave < items)
+            *(float4*)(sH + (size_t)wave * 1024 + ((2 * q + h) * 32 + r) * 4) =
+                make_float4(a3a[0][4 * q], a3a[0][4 * q + 1], a3a[0][4 * q + 2], a3a[0][4 * q + 3]);
+        if (wave + 8 < items)
+            *(float4*)(sH + (size_t)(wave + 8) * 1024 + ((2 * q + h) * 32 + r) * 4) =
+                make_float4(a3b[0][4 * q], a3b[0][4 * q + 1], a3b[0][4 * q + 2], a3b[0][4 * q + 3]);
+    }
+    __syncthreads();
+    for (int i = tid; i < (a.nstore >> 2) * 32; i += 512) {
+        const int row = i & 31, cq = i >> 5;
+        const int lm = m0 + row;
+        if (lm >= a.rows) continue;
+        const int blk = cq >> 3, qi = cq & 7;
+        float4 s = *(const float4*)(sH + (size_t)(blk * ks) * 1024 + (qi * 32 + row) * 4);
+        for (int kp = 1; kp < ks; ++kp) {
+            const float4 u = *(const float4*)(sH + (size_t)(blk * ks + kp) * 1024 + (qi * 32 + row) * 4);
+            s.x += u.x; s.y += u.y; s.z += u.z; s.w += u.w;
+        }
+        const int c = 4 * cq;
+        const float4 bb = *(const float4*)(a.b3 + c);
+        float o[4] = {s.x + bb.x, s.y + bb.y, s.z + bb.z, s.w + bb.w};
+        const int xr = map_row(a.amap, lm);
+        if (MODE == CH_PI) {
+            // TOLD.pi + TruncatedNormal.sample(clip=0.3) (tdmpc.py:39-45, helper.py:86-96)
+            const int e = lm / a.eps_G, rr = lm % a.eps_G;
+            const float* ep = a.eps + (size_t)e * a.eps_env + a.eps_off + (size_t)rr * a.A;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float x = 0.f;
+                if (c + k < a.nvalid) {
+                    const float muv = tanhf(o[k]);
+                    x = muv;
+                    if (a.min_std > 0.f) {
+                        const float ee = tclamp(fmul(ep[c + k], a.min_std), -0.3f, 0.3f);
+                        x = tclamp(fadd(muv, ee), a.lo, a.hi);
+                    }
+                }
+                o[k] = x;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (c + k >= a.nvalid) o[k] = 0.f;
+        }
+        *(float4*)(a.Xo + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.out_q0 + cq) * 128 + (xr & 31) * 4) =
+            make_float4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+// estimate_value's terminal combination (tdmpc.py:91-92): G + gamma^H min(Q1, Q2), nan_to_num.
+DEVI float qvalue(float G, float q1, float q2, float discH) {
+    const float qm = (q1 != q1 || q2 != q2) ? NAN : fminf(q1, q2);   // torch.min keeps NaN
+    return nan_to_num(fadd(G, fmul(discH, qm)));
+}
+
+__global__ void qvalue_kernel(const float* G, const float* q, int q_ld, float discH, float* value, int rows) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < rows) value[i] = qvalue(G[i], q[i], q[q_ld + i], discH);
+}
+
 // ------------------------------------------------------------------------------------------------ LN+tanh
 // a1 = tanh(LayerNorm(y1)) for both Q heads (helper.q: Linear -> LayerNorm -> Tanh), computed once per
 // element from the producer's per-64-column moments, so the next GEMM is a plain one. Grid: (row tiles,
@@ -968,7 +1335,9 @@ __global__ void __launch_bounds__(256) prep_kernel(const PrepArgs a) {
 struct CemArgs {
     int final_iter, iter, H, N, P, T, A, K, Kx, Hmax, I;
     const float* X; size_t x_stride;    // X_t panels: action columns of the pi rows
-    const float* value;                 // [B*T]
+    const float* value;                 // [B*T] (layered path: value_kernel's output)
+    const float* G; const float* qv; int q_ld; float discH;   // chain path: value = qvalue(G, q1, q2)
+    float* value_out;                   // optional [B][I][T]
     const float* rlast;                 // [B*T]
     float* mean; float* stdv;           // [B][Hmax][A]
     const float* eps; long eps_env; long eps_cem_off; long eps_iter; long eps_act_off;
@@ -1040,7 +1409,17 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
     // ---- top-K (K <= 64): each wave sorts 64-key lists, then a merge tree keeps the best 64
     for (int l = wave; l < NL; l += nwv) {
         const int i = l * 64 + lane;
-        const unsigned long long k = i < T ? topk_key(val[i], i) : ~0ull;
+        float v = 0.f;
+        if (i < T) {
+            if (a.qv) {
+                const size_t x = (size_t)e * T + i;
+                v = qvalue(a.G[x], a.qv[x], a.qv[a.q_ld + x], a.discH);
+                if (a.value_out) a.value_out[((size_t)e * a.I + a.iter) * T + i] = v;
+            } else {
+                v = val[i];
+            }
+        }
+        const unsigned long long k = i < T ? topk_key(v, i) : ~0ull;
         key[(size_t)l * 64 + lane] = wave_sort64(k, lane);
     }
     __syncthreads();
@@ -1325,6 +1704,12 @@ int init_attrs() {
     LDS_ATTR(2, 2, 2, 2, 32) LDS_ATTR(2, 1, 2, 4, 32) LDS_ATTR(3, 1, 2, 4, 32) LDS_ATTR(1, 1, 2, 2, 32)
 #undef LDS_ATTR
 #undef LDS_ATTR1
+#define CHAIN_ATTR(MODE, TN) \
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<MODE, TN>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CHAIN_ATTR(CH_STEP, 1) CHAIN_ATTR(CH_STEP, 2) CHAIN_ATTR(CH_STEP, 4)
+    CHAIN_ATTR(CH_PI, 1) CHAIN_ATTR(CH_PI, 2) CHAIN_ATTR(CH_PI, 4)
+    CHAIN_ATTR(CH_Q, 1) CHAIN_ATTR(CH_Q, 2) CHAIN_ATTR(CH_Q, 4)
+#undef CHAIN_ATTR
     if (rc) return TDMPC_E_HIP;
     done = 1;
     return 0;
@@ -1512,6 +1897,48 @@ int launch_lin(const LinArgs& a, int nprob, int nmax, int wide64, int pro, hipSt
     return TDMPC_E_DIMS;
 }
 
+// ---- chain path (chain_kernel): on the auto path used for launches of at least chain_wgs() workgroups
+// (32-row blocks x problems; TDMPC_CHAIN_WGS, default 128, 0 disables): one chain workgroup takes ~50 us
+// whatever the row count, so with fewer workgroups than about half the CUs the layered GEMMs, whose K-split
+// tiles spread the same rows over more CUs, finish first (tools/mb/mb_linear.hip "chain" on MI355X:
+// 2048 pi rows 45 us chain vs 37 us layered; 4096 x 2 step rows 55 vs 69; 512 x 2 step rows 54 vs 23).
+int chain_wgs() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("TDMPC_CHAIN_WGS");
+        v = e ? atoi(e) : 128;
+    }
+    return v;
+}
+
+// Shapes the chain kernel supports: M = 256 * TN (TN = 1, 2, 4); the last layer's (block, K-part) items
+// (<= 16) fit the activation block as 32x32 partial tiles.
+bool chain_shape_ok(const Layout& w) {
+    const int M = w.M;
+    if (M % 256 || M / 256 > 4 || M / 256 == 3) return false;
+    const size_t hfl = (size_t)std::max(w.Kx, M) * 32;
+    for (int n3 : {w.Lr, w.Ar}) {
+        const int nb3 = n3 / 32, ks = nb3 >= 4 ? 1 : 4 / nb3, items = nb3 * ks;
+        if (items > 16 || (size_t)items * 1024 > hfl || (M / 8) % ks) return false;
+    }
+    return (hfl + 512) * 4 <= 160 * 1024;
+}
+
+int launch_chain(int mode, const ChainArgs& a, int nprob, hipStream_t s) {
+    if (a.rows <= 0) return 0;
+    const size_t lds = ((size_t)a.hfl + 512) * 4;
+    const dim3 grid((a.rows + 31) / 32, nprob), block(512);
+    const int tn = a.M / 256;
+#define CHAIN_LAUNCH(MODE, TN) \
+    if (mode == MODE && tn == TN) { hipLaunchKernelGGL((chain_kernel<MODE, TN>), grid, block, lds, s, a); HIPCHK(hipGetLastError()); return 0; }
+    CHAIN_LAUNCH(CH_STEP, 1) CHAIN_LAUNCH(CH_STEP, 2) CHAIN_LAUNCH(CH_STEP, 4)
+    CHAIN_LAUNCH(CH_PI, 1) CHAIN_LAUNCH(CH_PI, 2) CHAIN_LAUNCH(CH_PI, 4)
+    CHAIN_LAUNCH(CH_Q, 1) CHAIN_LAUNCH(CH_Q, 2) CHAIN_LAUNCH(CH_Q, 4)
+#undef CHAIN_LAUNCH
+    snprintf(g_err, sizeof g_err, "chain: unsupported mode %d / M %d", mode, a.M);
+    return TDMPC_E_DIMS;
+}
+
 LinArgs args0() {
     LinArgs a;
     memset(&a, 0, sizeof a);
@@ -1524,10 +1951,24 @@ LinArgs args0() {
 struct Ctx {
     const tdmpc_dims* d; Layout w; Work k; const float* pw; hipStream_t s;
     int B, N, P, T, H, A, M, Kx;
+    int path;        // TDMPC_PATH_*
     long eps_env, eps_cem_off, eps_iter, eps_term_off, eps_act_off;
 };
 
 float* Xt(const Ctx& c, int t) { return c.k.X + (size_t)t * c.k.x_stride; }
+bool use_chain(const Ctx& c, int rows, int nprob) {
+    if (c.path == TDMPC_PATH_LAYERED || !chain_shape_ok(c.w)) return false;
+    return c.path == TDMPC_PATH_CHAIN || (chain_wgs() > 0 && (rows + 31) / 32 * nprob >= chain_wgs());
+}
+
+ChainArgs chain0(const Ctx& c, int rows, RowMap map, int t, int K1, int q1) {
+    ChainArgs a;
+    memset(&a, 0, sizeof a);
+    a.rows = rows; a.M = c.M; a.K1 = K1; a.q1 = q1; a.amap = map;
+    a.hfl = std::max(c.Kx, c.M) * 32;
+    a.X = Xt(c, t); a.x_ts = (long)c.Kx * 32;
+    return a;
+}
 Opnd xop(const Ctx& c, int t, int q0) { return Opnd{Xt(c, t), (long)c.Kx * 32, q0}; }
 Outp xout(const Ctx& c, int t, int q0) { return Outp{Xt(c, t), (long)c.Kx * 32, q0}; }
 Opnd hop(const float* H, const Ctx& c, int q0) { return Opnd{H, (long)2 * c.M * 32, q0}; }
@@ -1540,6 +1981,18 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
+    if (use_chain(c, rows, 2)) {
+        ChainArgs a = chain0(c, rows, map, t, c.Kx, 0);
+        ChainProb& d = a.p[0];
+        d.W1 = c.pw + w.w1x; d.b1 = c.pw + w.b1x; d.W2 = c.pw + w.w2d; d.b2 = c.pw + w.b2d;
+        ChainProb& r = a.p[1];
+        r.W1 = c.pw + w.w1x + (size_t)M * c.Kx; r.b1 = c.pw + w.b1x + M; r.W2 = c.pw + w.w2r; r.b2 = c.pw + w.b2r;
+        r.w3v = c.pw + w.w3r; r.b3v = c.pw + w.b3r;
+        a.W3 = c.pw + w.w3d; a.b3 = c.pw + w.b3d; a.n3 = w.Lr; a.nvalid = w.L; a.nstore = w.Lp;
+        a.Xo = Xt(c, t + 1); a.out_q0 = w.Ap / 4;
+        a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
+        return launch_chain(CH_STEP, a, 2, c.s);
+    }
     {   // h1 = ELU(W1[d;r] [a|z] + b)   (dynamics.0 and reward.0 fused: N = 2M)
         LinArgs a = args0();
         a.M = rows; a.K = c.Kx; a.a_mapped = 1; a.amap = map;
@@ -1579,6 +2032,16 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
+    if (use_chain(c, rows, 1)) {
+        ChainArgs a = chain0(c, rows, map, t, w.Lp, w.Ap / 4);
+        ChainProb& p = a.p[0];
+        p.W1 = c.pw + w.wp1; p.b1 = c.pw + w.bp1; p.W2 = c.pw + w.wp2; p.b2 = c.pw + w.bp2;
+        a.W3 = c.pw + w.wp3; a.b3 = c.pw + w.bp3; a.n3 = w.Ar; a.nvalid = w.A; a.nstore = w.Ap;
+        a.Xo = Xt(c, t); a.out_q0 = 0;
+        a.eps = eps; a.eps_G = eps_G; a.eps_env = eps_env; a.eps_off = eps_off; a.A = w.A;
+        a.min_std = min_std; a.lo = (float)(-1.0 + 1e-6); a.hi = (float)(1.0 - 1e-6);
+        return launch_chain(CH_PI, a, 1, c.s);
+    }
     {
         LinArgs a = args0();
         a.M = rows; a.K = w.Lp; a.a_mapped = 1; a.amap = map;
@@ -1633,6 +2096,20 @@ int terminal_q(const Ctx& c, float discH, float* value_out, int I, int iter) {
     const Layout& w = c.w;
     const int rows = c.B * c.T, M = c.M;
     int rc;
+    if (use_chain(c, rows, 2)) {
+        // q_p per row into k.qv; the value combination happens where it is consumed (cem_kernel / qvalue_kernel)
+        ChainArgs a = chain0(c, rows, RowMap{1 << 30, 0, 0}, c.H, c.Kx, 0);
+        for (int q = 0; q < 2; ++q) {
+            ChainProb& p = a.p[q];
+            p.W1 = c.pw + w.wq1x + (size_t)q * M * c.Kx; p.b1 = c.pw + w.bq1x + q * M;
+            p.g1 = c.pw + w.g1 + q * M; p.be1 = c.pw + w.be1 + q * M;
+            p.W2 = c.pw + w.wq2 + (size_t)q * M * M; p.b2 = c.pw + w.bq2 + q * M;
+            p.g2 = c.pw + w.g2 + q * M; p.be2 = c.pw + w.be2 + q * M;
+            p.w3v = c.pw + w.wq3 + q * M; p.b3v = c.pw + w.bq3 + q;
+        }
+        a.q = c.k.qv; a.q_ld = c.k.xrows;
+        return launch_chain(CH_Q, a, 2, c.s);
+    }
     {   // y1 = Wq1[Q1;Q2] [a|z] + b -> H1, with LayerNorm partial moments per 64 columns
         LinArgs a = args0();
         a.M = rows; a.K = c.Kx;
@@ -1722,7 +2199,7 @@ int setup_ctx(Ctx& c, const tdmpc_dims* d, const void* packed, void* ws, size_t 
     if (ws_bytes < probe.total) { snprintf(g_err, sizeof g_err, "workspace too small"); return TDMPC_E_SIZE; }
     make_work(d, c.w, (char*)ws, &c.k);
     c.pw = (const float*)packed; c.s = s;
-    c.B = batch; c.N = d->num_samples; c.P = d->num_pi; c.T = c.N + c.P; c.H = H;
+    c.B = batch; c.N = d->num_samples; c.P = d->num_pi; c.T = c.N + c.P; c.H = H; c.path = TDMPC_PATH_AUTO;
     c.A = c.w.A; c.M = c.w.M; c.Kx = c.w.Kx;
     const long A = c.A;
     c.eps_cem_off = (long)H * c.P * A;
@@ -1888,6 +2365,8 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     int rc;
     const int H = prm->horizon, I = prm->iterations, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream))) return rc;
+    if (prm->path < 0 || prm->path > 2) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T;
     // z0 = h(obs) and mean = 0 (warm: prev_mean shifted), std = 2
     if ((rc = encode(c, obs, obs_is_u8, B, prev_mean, prm->warm_start))) return rc;
@@ -1918,6 +2397,9 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     ca.eval_mode = prm->eval_mode; ca.temperature = prm->temperature; ca.momentum = prm->momentum;
     ca.omm = prm->one_minus_momentum; ca.std_floor = prm->std_floor; ca.action = action; ca.metrics = metrics;
     ca.elite_out = elite_out; ca.score_out = score_out; ca.mean_out = mean_out; ca.std_out = std_out;
+    if (use_chain(c, B * T, 2)) {   // terminal_q leaves q1, q2 per row; cem_kernel forms the values
+        ca.G = c.k.G; ca.qv = c.k.qv; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H]; ca.value_out = value_out;
+    }
     const size_t cem_lds = cem_lds_bytes(T, H, ca.K, c.A);
 
     const RowMap rm = {N, T, 0};
@@ -1948,6 +2430,8 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
+    if (prm->path < 0 || prm->path > 2) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    c.path = prm->path;
     if (rows != c.T) { snprintf(g_err, sizeof g_err, "rows must equal N+P"); return TDMPC_E_DIMS; }
     const int T = c.T, L = c.w.L;
     HIPCHK(hipMemsetAsync(c.k.z0, 0, (size_t)B * c.w.Lp * 4, c.s));
@@ -1966,6 +2450,11 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     }
     if ((rc = policy(c, H, B * T, all, eps_term, (long)T * c.A, T, 0, prm->min_std))) return rc;
     if ((rc = terminal_q(c, prm->discount_pow[H], nullptr, 1, 0))) return rc;
+    if (use_chain(c, B * T, 2)) {
+        hipLaunchKernelGGL(qvalue_kernel, dim3((B * T + 255) / 256), dim3(256), 0, c.s, c.k.G, c.k.qv, c.k.xrows,
+                           prm->discount_pow[H], c.k.value, B * T);
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipMemcpyAsync(value, c.k.value, (size_t)B * T * 4, hipMemcpyDeviceToDevice, c.s));
     HIPCHK(hipMemcpyAsync(reward_last, c.k.rlast, (size_t)B * T * 4, hipMemcpyDeviceToDevice, c.s));
     return 0;

@@ -12,6 +12,8 @@ Extensions beyond the reference API:
     all envs stacked), with per-env state (`_prev_mean` per env).
   * `rng="fused"` draws all of a call's Gaussian noise with one generator call instead of the reference's
     18 separate draws (same distribution, different stream); `graph=True` replays the call from a HIP graph.
+  * `path` picks the kernel family: "auto" (by row count), "layered" (one fused GEMM per Linear) or "chain"
+    (one row-block kernel per TOLD head); all agree within the fp32 parity tolerance.
 """
 from __future__ import annotations
 
@@ -39,8 +41,11 @@ def _discount_pows(discount: float, H: int):
 class HipPlanner:
     """Owns the device buffers of one planner instance and calls the C ABI."""
 
-    def __init__(self, cfg, max_batch: int = 1, device=None):
+    def __init__(self, cfg, max_batch: int = 1, device=None, path: str = "auto"):
         self.cfg = cfg
+        if path not in _lib.PATHS:
+            raise ValueError(f"path must be one of {sorted(_lib.PATHS)}")
+        self.path = path
         self.device = torch.device(device or "cuda")
         self.L = _lib.lib()
         self.dims = _lib.dims_from_cfg(cfg, max_batch=max_batch)
@@ -154,6 +159,7 @@ class HipPlanner:
         p.momentum = float(cfg.momentum)
         p.one_minus_momentum = float(1 - cfg.momentum)
         p.std_floor = float(std_floor)
+        p.path = _lib.PATHS[self.path]
         for t, v in enumerate(_discount_pows(cfg.discount, H)):
             p.discount_pow[t] = v
         return p
@@ -222,7 +228,7 @@ class HipPlanner:
 class TDMPC:
     """Drop-in for the reference `TDMPC` planning interface (tdmpc.py:53-163)."""
 
-    def __init__(self, cfg, max_batch: int = 1, rng: str = "reference", graph: bool = False):
+    def __init__(self, cfg, max_batch: int = 1, rng: str = "reference", graph: bool = False, path: str = "auto"):
         self.cfg = cfg
         self.device = torch.device(cfg.device)
         self.std = linear_schedule(cfg.std_schedule, 0)      # tdmpc.py:59
@@ -234,7 +240,7 @@ class TDMPC:
             raise ValueError(rng)
         self.rng = rng
         self.graph = graph
-        self.planner = HipPlanner(cfg, max_batch=max_batch, device=self.device)
+        self.planner = HipPlanner(cfg, max_batch=max_batch, device=self.device, path=path)
         self._has_prev = np.zeros(max_batch, dtype=bool)
         self._prev_H = np.zeros(max_batch, dtype=np.int64)
 

@@ -22,8 +22,11 @@ pytestmark = pytest.mark.gpu
 RTOL, ATOL = 1e-4, 1e-5
 
 
-def _agent(cfg, wseed, B=1):
-    agent = TDMPC(cfg, max_batch=B)
+PATHS = ["layered", "chain"]
+
+
+def _agent(cfg, wseed, B=1, path="auto"):
+    agent = TDMPC(cfg, max_batch=B, path=path)
     agent.model.load_state_dict(synthetic_state_dict(cfg, wseed))
     agent.std = 0.05
     return agent
@@ -59,12 +62,13 @@ def _compare_iterations(gpu_vals, ref_vals, K):
     return True
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name", case_names())
-def test_plan_matches_reference_golden(name):
+def test_plan_matches_reference_golden(name, path):
     """Replay every golden call (reference outputs recorded from /root/reference's TDMPC.plan) on the GPU
-    with the very same noise."""
+    with the very same noise, on both kernel paths."""
     cfg, wseed, d = load_case(name)
-    agent = _agent(cfg, wseed)
+    agent = _agent(cfg, wseed, path=path)
     for ci in range(int(d["ncalls"])):
         step, t0, ev = [int(x) for x in d[f"c{ci}_call"]]
         nb = call_noise(d, ci)
@@ -91,10 +95,11 @@ def test_plan_matches_reference_golden(name):
     ("humanoid", dict(num_samples=512, num_elites=64, latent_dim=512)),
     ("dog", dict(num_samples=512, num_elites=64)),
 ])
-def test_estimate_value_fullsize(task, ov):
-    """TDMPC.estimate_value at BASELINE sizes (T=768, H=5) vs the oracle's CPU fp32 TOLD."""
+@pytest.mark.parametrize("path", PATHS)
+def test_estimate_value_fullsize(task, ov, path):
+    """TDMPC.estimate_value at BASELINE sizes (T=768, H=5) vs the oracle's CPU fp32 TOLD, both kernel paths."""
     cfg = make_cfg(task, **ov)
-    agent = _agent(cfg, 7)
+    agent = _agent(cfg, 7, path=path)
     pl = agent.planner
     pl.pack(agent.model)
     H, T, A, L = 5, pl.T, cfg.action_dim, cfg.latent_dim
@@ -133,14 +138,15 @@ def test_encoder(task, ov):
     assert _close(z, zr, atol=1e-5, rtol=1e-4).all(), np.abs(z - zr).max()
 
 
-def test_batched_equals_single():
+@pytest.mark.parametrize("path", PATHS)
+def test_batched_equals_single(path):
     """plan_batch over B envs: an env's result does not depend on its slot in the batch (bitwise, permuted
     envs), and equals a single-env plan of it up to the GEMM tile's summation order (tile shapes are chosen
     by row count, tdmpc_kernels.hip pick_cfg, so B=1 and B=3 may accumulate in different orders)."""
     cfg = make_cfg("humanoid", num_samples=128, num_elites=16, iterations=3)
     B = 3
-    agent_b = _agent(cfg, 5, B=B)
-    agent_1 = _agent(cfg, 5, B=1)
+    agent_b = _agent(cfg, 5, B=B, path=path)
+    agent_1 = _agent(cfg, 5, B=1, path=path)
     rs = np.random.RandomState(1)
     obs = rs.standard_normal((B, cfg.obs_shape[0])).astype(np.float32)
     torch.manual_seed(0)
@@ -185,11 +191,12 @@ def test_reference_rng_order_on_device():
     assert torch.equal(buf[lay["act_off"]:lay["act_off"] + A], nb.eps_act)
 
 
-def test_plan_fullsize_vs_oracle():
+@pytest.mark.parametrize("path", PATHS)
+def test_plan_fullsize_vs_oracle(path):
     """Full humanoid-run plan (N=512, H=5, 6 iterations, T=768): GPU vs oracle on identical noise, warm
     start on the second call."""
     cfg = make_cfg("humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5)
-    agent = _agent(cfg, 9)
+    agent = _agent(cfg, 9, path=path)
     told = tdmpc_ref.RefTOLD(synthetic_state_dict(cfg, 9), cfg)
     st = tdmpc_ref.PlanState(0.05)
     rs = np.random.RandomState(2)
@@ -208,3 +215,29 @@ def test_plan_fullsize_vs_oracle():
         np.testing.assert_allclose(a[0].cpu().numpy(), ra.numpy(), atol=2e-5, rtol=0)
         np.testing.assert_allclose(tr["mean"][0, -1].cpu().numpy(), rtr["mean"][-1].numpy(), atol=2e-5, rtol=0)
         np.testing.assert_allclose(tr["std"][0, -1].cpu().numpy(), rtr["std"][-1].numpy(), atol=2e-5, rtol=0)
+
+
+def test_bench_batch_vs_oracle():
+    """The bench workload's shape: 8 humanoid envs in one plan_batch call (auto path: the row-block chain
+    kernels at 4096 / 6144 rows), every env against the oracle on its own noise."""
+    cfg = make_cfg("humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5)
+    B = 8
+    agent = _agent(cfg, 13, B=B)
+    told = tdmpc_ref.RefTOLD(synthetic_state_dict(cfg, 13), cfg)
+    rs = np.random.RandomState(3)
+    obs = rs.standard_normal((B, cfg.obs_shape[0])).astype(np.float32)
+    torch.manual_seed(6)
+    np.random.seed(6)
+    noises = [tdmpc_ref.draw_noise(cfg, 10**6, False) for _ in range(B)]
+    tr = {}
+    a, m = agent._plan_envs(obs, False, 10**6, [True] * B, trace=tr, noise=noises)
+    compared = 0
+    for e in range(B):
+        st = tdmpc_ref.PlanState(0.05)
+        rtr = {}
+        ra, rm = tdmpc_ref.plan(told, cfg, st, obs[e], noises[e], eval_mode=False, step=10**6, t0=True, trace=rtr)
+        ref_vals = torch.stack(rtr["value"]).squeeze(-1).numpy()
+        if _compare_iterations(tr["value"][e].cpu().numpy(), ref_vals, cfg.num_elites):
+            np.testing.assert_allclose(a[e].cpu().numpy(), ra.numpy(), atol=2e-5, rtol=0)
+            compared += 1
+    assert compared >= B // 2, "too many near-tie elite swaps to compare actions"

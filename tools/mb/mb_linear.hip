@@ -134,24 +134,40 @@ int main(int argc, char** argv) {
         CK(hipStreamSynchronize(s));
         return 0;
     }
-    float t_plan = time_it(s, 20, [&] {
-        int rc = tdmpc_plan(&d, &p, packed, obs, 0, noise, u, prev, act, met, nullptr, nullptr, nullptr, nullptr, nullptr,
-                            ws, sz.workspace_bytes, s);
-        if (rc) { printf("plan rc %d %s\n", rc, tdmpc_last_error()); exit(1); }
-    });
-    printf("B=%d full plan: %.1f us\n", B, t_plan);
+    for (int path = 0; path <= 2; ++path) {
+        p.path = path;
+        float t_plan = time_it(s, 20, [&] {
+            int rc = tdmpc_plan(&d, &p, packed, obs, 0, noise, u, prev, act, met, nullptr, nullptr, nullptr, nullptr,
+                                nullptr, ws, sz.workspace_bytes, s);
+            if (rc) { printf("plan rc %d %s\n", rc, tdmpc_last_error()); exit(1); }
+        });
+        printf("B=%d full plan (path %d): %.1f us\n", B, path, t_plan);
+    }
+    p.path = 0;
     Ctx c;
     setup_ctx(c, &d, packed, ws, sz.workspace_bytes, B, 5, 6, s);
     const RowMap rm = {c.N, c.T, 0};
     const RowMap all = {c.T, c.T, 0};
     struct Case { const char* name; std::function<void()> fn; };
     std::vector<Case> cases;
-    // individual layers of one step (rollout rows)
-    cases.push_back({"step_next(t=1) [S1+S2+S3]", [&] { step_next(c, 1, B * c.N, rm, 0.99f, 0, 0); }});
-    cases.push_back({"policy(H) [pi1+pi2+pi3]", [&] { policy(c, 5, B * c.T, all, noise, c.eps_env, c.T, 0, 0.05f); }});
-    cases.push_back({"terminal_q [Q1+Q2+value]", [&] { terminal_q(c, 0.95f, nullptr, 6, 0); }});
+    // one rollout step / terminal heads on each path
+    for (int path = 1; path <= 2; ++path) {
+        const char* pn = path == 1 ? "layered" : "chain";
+        static char nm[8][64];
+        snprintf(nm[path * 3 - 3], 64, "step_next N rows (%s)", pn);
+        snprintf(nm[path * 3 - 2], 64, "policy T rows (%s)", pn);
+        snprintf(nm[path * 3 - 1], 64, "terminal_q T rows (%s)", pn);
+        cases.push_back({nm[path * 3 - 3], [&, path] { c.path = path; step_next(c, 1, B * c.N, rm, 0.99f, 0, 0); }});
+        cases.push_back({nm[path * 3 - 2], [&, path] { c.path = path; policy(c, 5, B * c.T, all, noise, c.eps_env, c.T, 0, 0.05f); }});
+        cases.push_back({nm[path * 3 - 1], [&, path] { c.path = path; terminal_q(c, 0.95f, nullptr, 6, 0); }});
+    }
+    cases.push_back({"step_next T rows (chain)", [&] { c.path = 2; step_next(c, 1, B * c.T, all, 0.99f, 0, 0); }});
+    cases.push_back({"policy P rows (chain)", [&] { c.path = 2; policy(c, 1, B * c.P, RowMap{c.P, c.T, c.N}, noise, c.eps_env, c.P, 0, 0.05f); }});
+    cases.push_back({"policy P rows (layered)", [&] { c.path = 1; policy(c, 1, B * c.P, RowMap{c.P, c.T, c.N}, noise, c.eps_env, c.P, 0, 0.05f); }});
     cases.push_back({"encode", [&] { encode(c, obs, 0, B, prev, 0); }});
     for (auto& cs : cases) printf("%-32s %8.2f us\n", cs.name, time_it(s, 200, cs.fn));
+    c.path = 0;
+    if (argc > 2 && !strcmp(argv[2], "chain")) return 0;
     // per-layer: S2 only
     {
         const Layout& w = c.w; const int M = c.M;
