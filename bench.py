@@ -16,10 +16,11 @@ weight replica (weak scaling) and each step ends with one RCCL all-gather over x
 ([B, A+2]: action, reward mean, std) so that every rank holds the whole vectorised batch.
 
 Rank 0 prints ONE JSON line with, besides the driver's contract fields,
-  roofline     : the dominant kernel class (the hidden M x M Linear layers: 2 x 5 per CEM iteration + pi's)
-                 -- algorithmic FLOPs per launch / average launch time, HIP events around every launch on its
-                 stream over a timed replay of the same steps; traffic from profiles/pmc_traffic.json (rocprofv3
-                 PMC FETCH_SIZE x2 + WRITE_SIZE per launch, MI355X_MICROARCH.md §HBM correction) when present;
+  roofline     : the dominant kernel -- the CEM rollout step (TOLD.next over the B*N candidate rows, 5 launches
+                 per iteration): algorithmic FLOPs per launch / average launch time, HIP events around every
+                 launch on its stream over an eager replay of the same steps; traffic from
+                 profiles/pmc_traffic.json (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE per launch,
+                 MI355X_MICROARCH.md §HBM correction) when present;
   cpu_baseline : the oracle's CPU restatement of the reference plan() (pinned bit-exact to the reference's own
                  outputs, tests/test_oracle.py) timed on this host's cores over a bounded sample.
 """
@@ -201,27 +202,46 @@ def main():
         one_step(0)
         torch.cuda.synchronize()
         n_r = max(3, min(args.steps, 10))
-        _lib.check(L.tdmpc_profile_begin(0, 0, cfg.mlp_dim, B * cfg.num_samples, 8192), "profile_begin")
-        for i in range(n_r):
-            one_step(1 + i)
-        n, ms, fl = C.c_int32(), C.c_double(), C.c_double()
-        _lib.check(L.tdmpc_profile_end(C.byref(n), C.byref(ms), C.byref(fl)), "profile_end")
+
+        def timed(cfg_id, pro, kdim, rows):
+            _lib.check(L.tdmpc_profile_begin(cfg_id, pro, kdim, rows, 8192), "profile_begin")
+            for i in range(n_r):
+                one_step(1 + i)
+            n, ms, fl = C.c_int32(), C.c_double(), C.c_double()
+            _lib.check(L.tdmpc_profile_end(C.byref(n), C.byref(ms), C.byref(fl)), "profile_end")
+            return n.value, ms.value, fl.value
+
+        rows = B * cfg.num_samples
+        M, Lt, A = cfg.mlp_dim, cfg.latent_dim, cfg.action_dim
+        # dominant kernel: the CEM rollout step (TOLD.next, 5 of every iteration's launches, ~half the time).
+        # Row-block chain kernel when the auto path picks it (>= 128 workgroups), else the layered hidden GEMM.
+        n, ms, fl = timed(4, -1, 0, rows)
+        if n > 0:
+            kernel = (f"chain_kernel<CH_STEP> (TOLD.next: dynamics + reward heads, 32-row blocks, hidden "
+                      f"activations in LDS, weights streamed from L2; {rows} rows x 2 heads per launch), "
+                      f"fp32 v_mfma_f32_32x32x2_f32")
+            kx = A + Lt
+            alg_bytes = 4.0 * (rows * (kx + Lt + 2) + 2 * M * kx + 2 * M * M + M * Lt + M)
+            pmc_key = f"{args.config}/B{B}/chain_step"
+        else:
+            n, ms, fl = timed(0, 0, M, rows)
+            kernel = (f"linear_lds_kernel (128x128 LDS-staged tile): CEM rollout layer 2 (dynamics + reward "
+                      f"hidden {M}x{M} Linear + ELU, {rows} rows x 2 problems), fp32 v_mfma_f32_32x32x2_f32")
+            alg_bytes = 4.0 * (rows * 2 * M + 2 * M * M + rows * M)
+            pmc_key = f"{args.config}/B{B}"
         agent.graph = graph
-        avg_s = ms.value / max(n.value, 1) * 1e-3
-        per_launch = fl.value / max(n.value, 1)
+        avg_s = ms / max(n, 1) * 1e-3
+        per_launch = fl / max(n, 1)
         achieved = per_launch / avg_s / 1e12
-        thr = B * cfg.num_samples >= int(os.environ.get("TDMPC_THR_ROWS", "4096"))
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                "kernel": ("linear_lds_kernel<2,1,2,4,32> (128x128 LDS-staged tile)" if thr else
-                           "linear_kernel<1,2,1,1,0,64> (32x64 tile, 8-way K split)") +
-                          f": CEM rollout layer 2 (dynamics + reward hidden {cfg.mlp_dim}x{cfg.mlp_dim} Linear + "
-                          f"ELU, {B * cfg.num_samples} rows x 2 problems), fp32 v_mfma_f32_32x32x2_f32",
-                "launches": n.value, "avg_launch_us": round(avg_s * 1e6, 3), "flops_per_launch": per_launch}
+                "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None, "kernel": kernel,
+                "launches": n, "avg_launch_us": round(avg_s * 1e6, 3), "flops_per_launch": per_launch,
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "hbm_gbs_algorithmic": round(alg_bytes / avg_s / 1e9, 1)}
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
-                t = json.load(open(pmc)).get(f"{args.config}/B{B}")
+                t = json.load(open(pmc)).get(pmc_key)
                 if t:
                     roof["traffic"] = t.get("hbm_bytes_per_launch")
                     roof["traffic_source"] = t.get("source")

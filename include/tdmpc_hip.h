@@ -144,13 +144,16 @@ int tdmpc_estimate_value(const tdmpc_dims* dims, const tdmpc_plan_params* params
                          void* workspace, size_t workspace_bytes, void* stream);
 
 /* Diagnostic kernel timer for the roofline report (bench.py). Arms a per-thread recorder: every later
- * linear_kernel launch issued from this thread with launch configuration `cfg` (1 = latency 32x32 tile,
- * 2 = latency 32x64 tile, 3 = throughput 128x128 tile, 0 = any) and prologue `pro` (0 plain, 1 LayerNorm,
- * -1 any) -- restricted to K == N == kdim when kdim > 0 (the hidden kdim x kdim layers) and to launches over
- * exactly `rows` rows when rows > 0 (e.g. batch * num_samples: the CEM rollout layers) -- is bracketed by
- * HIP events on its stream (at most max_launches). tdmpc_profile_end waits for the events and returns the launch count,
- * the summed kernel time in ms and the summed algorithmic FLOPs (2*M*N*K per GEMM problem). Eager use
- * only (the events are not graph-capturable). */
+ * launch issued from this thread that matches is bracketed by HIP events on its stream (at most
+ * max_launches).
+ *   cfg 0..3: linear_kernel / linear_lds_kernel launches of tile configuration `cfg` (1 = latency 32x32,
+ *     2 = latency 32x64, 3 = throughput LDS tile, 0 = any) and prologue `pro` (0 plain, 1 LayerNorm, -1 any),
+ *     restricted to K == N == kdim when kdim > 0 (the hidden kdim x kdim layers);
+ *   cfg 4 / 5 / 6: chain_kernel launches of the TOLD.next step / pi / Q heads;
+ * in both cases restricted to launches over exactly `rows` rows when rows > 0 (e.g. batch * num_samples:
+ * the CEM rollout). tdmpc_profile_end waits for the events and returns the launch count, the summed kernel
+ * time in ms and the summed algorithmic FLOPs (2*M*N*K per GEMM problem; for a chain launch 2 * rows * the
+ * head's MACs per row at the real, unpadded widths). Eager use only (events are not graph-capturable). */
 int tdmpc_profile_begin(int32_t cfg, int32_t pro, int32_t kdim, int32_t rows, int32_t max_launches);
 int tdmpc_profile_end(int32_t* launches, double* total_ms, double* flops);
 

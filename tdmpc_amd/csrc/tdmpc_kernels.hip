@@ -853,21 +853,27 @@ struct ChainArgs {
     float* q; int q_ld;
 };
 
-// acc[j] += W(block j) . A over k groups [g0, g1). A: LDS block [K/4][32][4]; Wp: the wave's first weight-panel
-// block, already offset by the lane's (h, r); blocks wbs floats apart. W rides a D-deep register ring, A is
-// read one group ahead.
+// Weight ring: D k groups x TN 1-KiB wave loads of the weight panel in flight. ring_fill issues the first D
+// groups (callers issue it early: before the input staging or the previous layer's epilogue, so that the
+// ~1 us L2 latency under load hides behind that work); ring_run then walks groups [g0, g1):
+// acc[j] += W(block j) . A, A from the LDS block [K/4][32][4] one group ahead, W refilled D groups ahead.
+// Wp is the wave's first weight-panel block, already offset by the lane's (h, r); blocks wbs floats apart.
 template <int TN, int D>
-DEVI void chain_gemm(floatx16 (&acc)[TN], const float* sA, const float* Wp, long wbs, int g0, int g1, int r,
-                     int h) {
-    // Every load is issued unconditionally (past the end: the last group again, never used) so that the
-    // number of loads in flight is the same at every MFMA and the wait before group g's MFMAs is
-    // vmcnt((D-1)*TN), not a drain.
+DEVI void ring_fill(float4 (&wr)[D][TN], const float* Wp, long wbs, int g0, int g1) {
     const int gl = g1 - 1;
-    float4 wr[D][TN];
 #pragma unroll
     for (int d = 0; d < D; ++d)
 #pragma unroll
         for (int j = 0; j < TN; ++j) wr[d][j] = *(const float4*)(Wp + j * wbs + (size_t)min(g0 + d, gl) * 256);
+}
+
+template <int TN, int D>
+DEVI void ring_run(floatx16 (&acc)[TN], float4 (&wr)[D][TN], const float* sA, const float* Wp, long wbs, int g0,
+                   int g1, int r, int h) {
+    // Every refill is issued unconditionally (past the end: the last group again, never used) so that the
+    // number of loads in flight is the same at every MFMA and the wait before group g's MFMAs is
+    // vmcnt((D-1)*TN), not a drain.
+    const int gl = g1 - 1;
     const float* ap = sA + (h * 32 + r) * 4;
     float4 an = *(const float4*)(ap + (size_t)g0 * 256);
     int gb = g0;
@@ -935,10 +941,60 @@ DEVI void chain_row_moments(const float (&v)[TN * 16], float* red0, float* red1,
     rstd = 1.0f / sqrtf(fmaxf(tot2 / (float)M, 0.f) + 1e-5f);
 }
 
+// LDS floats of the chain kernel's per-head parameter vectors (after the activation block and red0/red1).
+__host__ __device__ inline int chain_param_floats(int mode, int M, int n3) {
+    return mode == CH_Q ? 7 * M : 3 * M + n3;
+}
+
+// bias (+ LayerNorm affine + activation) of a layer's register tile, in place: v = act(acc + b)
+template <int TN>
+DEVI void chain_bias(float (&v)[TN * 16], const floatx16 (&acc)[TN], const float* sb, int cw0, int h) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 bb = *(const float4*)(sb + (cw0 + j) * 32 + 8 * q + 4 * h);
+            v[j * 16 + 4 * q + 0] = acc[j][4 * q + 0] + bb.x;
+            v[j * 16 + 4 * q + 1] = acc[j][4 * q + 1] + bb.y;
+            v[j * 16 + 4 * q + 2] = acc[j][4 * q + 2] + bb.z;
+            v[j * 16 + 4 * q + 3] = acc[j][4 * q + 3] + bb.w;
+        }
+}
+
+// ATen LayerNorm on the tile: (x * rstd + (-rstd * mean)) * gamma + beta
+template <int TN>
+DEVI void chain_ln(float (&v)[TN * 16], float rs, float sh, const float* sg, const float* sbe, int cw0, int h) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int c = (cw0 + j) * 32 + 8 * q + 4 * h;
+            const float4 gg = *(const float4*)(sg + c), bb = *(const float4*)(sbe + c);
+            float* x = v + j * 16 + 4 * q;
+            x[0] = fadd(fmul(fadd(fmul(x[0], rs), sh), gg.x), bb.x);
+            x[1] = fadd(fmul(fadd(fmul(x[1], rs), sh), gg.y), bb.y);
+            x[2] = fadd(fmul(fadd(fmul(x[2], rs), sh), gg.z), bb.z);
+            x[3] = fadd(fmul(fadd(fmul(x[3], rs), sh), gg.w), bb.w);
+        }
+}
+
+// the tile into the activation block (panel quads; lanes of one quad write 512 contiguous bytes)
+template <int TN>
+DEVI void chain_store_lds(float* sH, const float (&v)[TN * 16], int cw0, int r, int h) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int cq = (cw0 + j) * 8 + 2 * q + h;
+            *(float4*)(sH + (cq * 32 + r) * 4) =
+                make_float4(v[j * 16 + 4 * q], v[j * 16 + 4 * q + 1], v[j * 16 + 4 * q + 2], v[j * 16 + 4 * q + 3]);
+        }
+}
+
 template <int MODE, int TN>
 __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int D = 4;
+    constexpr int D = 4, D3 = 8;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     const int pb = blockIdx.y;
     const ChainProb& P = a.p[pb];
@@ -947,15 +1003,58 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
     float* sH = smem;                       // activation block [max(K1, M)/4][32][4]
     float* red0 = smem + a.hfl;             // [8][32]
     float* red1 = red0 + 256;               // [8][32]
+    float* sp = red1 + 256;                 // parameter vectors (chain_param_floats)
+    float* sb1 = sp;
+    float* sb2 = sp + M;
+    float* sw3 = sp + 2 * M;                // reward / Q head weights
+    float* sb3 = sp + 3 * M;                // dynamics / pi last-layer bias [n3]
+    float* sg1 = sp + 3 * M;                // CH_Q LayerNorm affines
+    float* sbe1 = sp + 4 * M;
+    float* sg2 = sp + 5 * M;
+    float* sbe2 = sp + 6 * M;
     const int lo = h * 128 + r * 4;         // lane offset inside a weight-panel k group
     const int cw0 = wave * TN;              // first 32-column block of this wave in the M-wide layers
+    const bool head_dot = MODE == CH_Q || (MODE == CH_STEP && pb == 1);
+#ifdef TDMPC_STAMPS
+    unsigned long long st_[5];
+    const unsigned long long rt0_ = __builtin_amdgcn_s_memrealtime();
+    STAMP(0);
+#endif
 
-    // ---- the block's input rows: X quads [q1, q1 + K1/4), 32 consecutive lanes = 32 rows of one quad
+    // ---- layer-1 weights in flight first, then the block's input rows (X quads [q1, q1 + K1/4); 32
+    // consecutive lanes = 32 rows of one quad) and the parameter vectors
+    float4 wr[D][TN];
+    ring_fill<TN, D>(wr, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3);
     for (int i = tid; i < (a.K1 >> 2) * 32; i += 512) {
         const int row = i & 31, q = i >> 5;
         const int lm = m0 + row;
         const int xr = map_row(a.amap, lm < a.rows ? lm : 0);
         ((float4*)sH)[i] = *(const float4*)(a.X + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.q1 + q) * 128 + (xr & 31) * 4);
+    }
+    for (int i = tid; i < M / 4; i += 512) {
+        ((float4*)sb1)[i] = ((const float4*)P.b1)[i];
+        ((float4*)sb2)[i] = ((const float4*)P.b2)[i];
+        if (head_dot) ((float4*)sw3)[i] = ((const float4*)P.w3v)[i];
+        if (MODE == CH_Q) {
+            ((float4*)sg1)[i] = ((const float4*)P.g1)[i];
+            ((float4*)sbe1)[i] = ((const float4*)P.be1)[i];
+            ((float4*)sg2)[i] = ((const float4*)P.g2)[i];
+            ((float4*)sbe2)[i] = ((const float4*)P.be2)[i];
+        }
+    }
+    if (!head_dot)
+        for (int i = tid; i < a.n3 / 4; i += 512) ((float4*)sb3)[i] = ((const float4*)a.b3)[i];
+    // early operands of the last stage: the running return (reward WG) / the policy noise (pi)
+    float g_old = 0.f;
+    if (MODE == CH_STEP && pb == 1 && tid < 32 && !a.first && m0 + tid < a.rows)
+        g_old = a.G[map_row(a.amap, m0 + tid)];
+    float eps4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (MODE == CH_PI && tid < (a.nstore >> 2) * 32 && m0 + (tid & 31) < a.rows) {
+        const int lm = m0 + (tid & 31), c = 4 * (tid >> 5);
+        const int e = lm / a.eps_G, rr = lm % a.eps_G;
+        const float* ep = a.eps + (size_t)e * a.eps_env + a.eps_off + (size_t)rr * a.A;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) eps4[k] = c + k < a.nvalid ? ep[c + k] : 0.f;
     }
     __syncthreads();
 
@@ -965,98 +1064,66 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
     for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    chain_gemm<TN, D>(acc, sH, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3, r, h);
+    ring_run<TN, D>(acc, wr, sH, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3, r, h);
+    // layer-2 weights in flight during the epilogue
+    ring_fill<TN, D>(wr, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3);
     __syncthreads();   // every wave is done with the input tile: sH becomes h1
+#ifdef TDMPC_STAMPS
+    STAMP(1);
+#endif
     {
         float v[TN * 16];
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int c = (cw0 + j) * 32 + 8 * q + 4 * h;
-                const float4 bb = *(const float4*)(P.b1 + c);
-                v[j * 16 + 4 * q + 0] = acc[j][4 * q + 0] + bb.x;
-                v[j * 16 + 4 * q + 1] = acc[j][4 * q + 1] + bb.y;
-                v[j * 16 + 4 * q + 2] = acc[j][4 * q + 2] + bb.z;
-                v[j * 16 + 4 * q + 3] = acc[j][4 * q + 3] + bb.w;
-            }
+        chain_bias<TN>(v, acc, sb1, cw0, h);
         if (MODE == CH_Q) {
             float mean, rs;
             chain_row_moments<TN>(v, red0, red1, wave, r, h, M, mean, rs);
-            const float sh = -rs * mean;
+            chain_ln<TN>(v, rs, -rs * mean, sg1, sbe1, cw0, h);
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int c = (cw0 + j) * 32 + 8 * q + 4 * h;
-                    const float4 gg = *(const float4*)(P.g1 + c), bb = *(const float4*)(P.be1 + c);
-                    float* x = v + j * 16 + 4 * q;
-                    // ATen LayerNorm: (x * rstd + (-rstd * mean)) * gamma + beta, then Tanh
-                    x[0] = tanh_f(fadd(fmul(fadd(fmul(x[0], rs), sh), gg.x), bb.x));
-                    x[1] = tanh_f(fadd(fmul(fadd(fmul(x[1], rs), sh), gg.y), bb.y));
-                    x[2] = tanh_f(fadd(fmul(fadd(fmul(x[2], rs), sh), gg.z), bb.z));
-                    x[3] = tanh_f(fadd(fmul(fadd(fmul(x[3], rs), sh), gg.w), bb.w));
-                }
+            for (int i = 0; i < TN * 16; ++i) v[i] = tanh_f(v[i]);
         } else {
 #pragma unroll
             for (int i = 0; i < TN * 16; ++i) v[i] = elu_f(v[i]);
         }
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int cq = (cw0 + j) * 8 + 2 * q + h;
-                *(float4*)(sH + (cq * 32 + r) * 4) =
-                    make_float4(v[j * 16 + 4 * q], v[j * 16 + 4 * q + 1], v[j * 16 + 4 * q + 2], v[j * 16 + 4 * q + 3]);
-            }
+        chain_store_lds<TN>(sH, v, cw0, r, h);
     }
     __syncthreads();
+#ifdef TDMPC_STAMPS
+    STAMP(2);
+#endif
 
     // ---- layer 2: [32 x M] . W2^T -> [32 x M]
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    chain_gemm<TN, D>(acc, sH, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3, r, h);
+    ring_run<TN, D>(acc, wr, sH, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3, r, h);
+#ifdef TDMPC_STAMPS
+    STAMP(3);
+#endif
+    // layer-3 work items (32-column block, K part): narrow heads split K over all 8 waves (2 per SIMD)
+    const int nb3 = a.n3 >> 5;
+    const int ks = nb3 >= 8 ? 1 : 8 / nb3;
+    const int items = nb3 * ks;
+    const int gper = (M >> 3) / ks;
+    float4 w3r[D3][1];
+    if (!head_dot && wave < items)
+        ring_fill<1, D3>(w3r, a.W3 + (size_t)(wave / ks) * M * 32 + lo, (long)M * 32, (wave % ks) * gper,
+                         (wave % ks + 1) * gper);
     float v[TN * 16];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int c = (cw0 + j) * 32 + 8 * q + 4 * h;
-            const float4 bb = *(const float4*)(P.b2 + c);
-            v[j * 16 + 4 * q + 0] = acc[j][4 * q + 0] + bb.x;
-            v[j * 16 + 4 * q + 1] = acc[j][4 * q + 1] + bb.y;
-            v[j * 16 + 4 * q + 2] = acc[j][4 * q + 2] + bb.z;
-            v[j * 16 + 4 * q + 3] = acc[j][4 * q + 3] + bb.w;
-        }
-    const bool head_dot = MODE == CH_Q || (MODE == CH_STEP && pb == 1);
+    chain_bias<TN>(v, acc, sb2, cw0, h);
     if (head_dot) {
         // reward / Q last layer Linear(M -> 1) on the row: per-wave partial dots, then one lane per row
         if (MODE == CH_Q) {
             float mean, rs;
             chain_row_moments<TN>(v, red0, red1, wave, r, h, M, mean, rs);
-            const float sh = -rs * mean;
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int c = (cw0 + j) * 32 + 8 * q + 4 * h;
-                    const float4 gg = *(const float4*)(P.g2 + c), bb = *(const float4*)(P.be2 + c);
-                    float* x = v + j * 16 + 4 * q;
-                    x[0] = fadd(fmul(fadd(fmul(x[0], rs), sh), gg.x), bb.x);
-                    x[1] = fadd(fmul(fadd(fmul(x[1], rs), sh), gg.y), bb.y);
-                    x[2] = fadd(fmul(fadd(fmul(x[2], rs), sh), gg.z), bb.z);
-                    x[3] = fadd(fmul(fadd(fmul(x[3], rs), sh), gg.w), bb.w);
-                }
+            chain_ln<TN>(v, rs, -rs * mean, sg2, sbe2, cw0, h);
         }
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int c = (cw0 + j) * 32 + 8 * q + 4 * h;
-                const float4 w4 = *(const float4*)(P.w3v + c);
+                const float4 w4 = *(const float4*)(sw3 + (cw0 + j) * 32 + 8 * q + 4 * h);
                 const float* x = v + j * 16 + 4 * q;
                 s += (elu_f(x[0]) * w4.x + elu_f(x[1]) * w4.y) + (elu_f(x[2]) * w4.z + elu_f(x[3]) * w4.w);
             }
@@ -1076,43 +1143,37 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
                 } else {
                     // G += discount * reward (tdmpc.py:89), float32(discount) like ATen's scalar mul
                     const float dr = fmul(a.disc, o);
-                    a.G[xr] = a.first ? dr : fadd(a.G[xr], dr);
+                    a.G[xr] = a.first ? dr : fadd(g_old, dr);
                     if (a.last) a.rlast[xr] = o;
                 }
             }
         }
+#ifdef TDMPC_STAMPS
+        __syncthreads();
+        STAMP(4);
+        STAMP_RECORD();
+#endif
         return;
     }
     // dynamics / pi: h2 = ELU(y2) back into the activation block once every wave is done reading h1
 #pragma unroll
     for (int i = 0; i < TN * 16; ++i) v[i] = elu_f(v[i]);
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int cq = (cw0 + j) * 8 + 2 * q + h;
-            *(float4*)(sH + (cq * 32 + r) * 4) =
-                make_float4(v[j * 16 + 4 * q], v[j * 16 + 4 * q + 1], v[j * 16 + 4 * q + 2], v[j * 16 + 4 * q + 3]);
-        }
+    chain_store_lds<TN>(sH, v, cw0, r, h);
     __syncthreads();
 
-    // ---- layer 3: [32 x M] . W3^T -> [32 x n3] as items (32-column block, K part): narrow heads split K
-    // over up to 4 waves (one per SIMD); partial tiles meet in the activation block after the reads.
-    const int nb3 = a.n3 >> 5;
-    const int ks = nb3 >= 4 ? 1 : 4 / nb3;
-    const int items = nb3 * ks;
-    const int gper = (M >> 3) / ks;
+    // ---- layer 3: [32 x M] . W3^T -> [32 x n3]; partial tiles meet in the activation block after the reads
     floatx16 a3a[1], a3b[1];
 #pragma unroll
     for (int e = 0; e < 16; ++e) { a3a[0][e] = 0.f; a3b[0][e] = 0.f; }
     if (wave < items) {
         const int blk = wave / ks, kp = wave % ks;
-        chain_gemm<1, D>(a3a, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
+        ring_run<1, D3>(a3a, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
     }
     if (wave + 8 < items) {
         const int blk = (wave + 8) / ks, kp = (wave + 8) % ks;
-        chain_gemm<1, D>(a3b, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
+        ring_fill<1, D3>(w3r, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper);
+        ring_run<1, D3>(a3b, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
     }
     __syncthreads();
 #pragma unroll
@@ -1136,13 +1197,12 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
             s.x += u.x; s.y += u.y; s.z += u.z; s.w += u.w;
         }
         const int c = 4 * cq;
-        const float4 bb = *(const float4*)(a.b3 + c);
+        const float4 bb = *(const float4*)(sb3 + c);
         float o[4] = {s.x + bb.x, s.y + bb.y, s.z + bb.z, s.w + bb.w};
         const int xr = map_row(a.amap, lm);
         if (MODE == CH_PI) {
-            // TOLD.pi + TruncatedNormal.sample(clip=0.3) (tdmpc.py:39-45, helper.py:86-96)
-            const int e = lm / a.eps_G, rr = lm % a.eps_G;
-            const float* ep = a.eps + (size_t)e * a.eps_env + a.eps_off + (size_t)rr * a.A;
+            // TOLD.pi + TruncatedNormal.sample(clip=0.3) (tdmpc.py:39-45, helper.py:86-96); this thread's noise
+            // was loaded at kernel start (i == tid: nstore/4 * 32 <= 512 items)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 float x = 0.f;
@@ -1150,7 +1210,7 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
                     const float muv = tanhf(o[k]);
                     x = muv;
                     if (a.min_std > 0.f) {
-                        const float ee = tclamp(fmul(ep[c + k], a.min_std), -0.3f, 0.3f);
+                        const float ee = tclamp(fmul(eps4[k], a.min_std), -0.3f, 0.3f);
                         x = tclamp(fadd(muv, ee), a.lo, a.hi);
                     }
                 }
@@ -1164,6 +1224,11 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
         *(float4*)(a.Xo + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.out_q0 + cq) * 128 + (xr & 31) * 4) =
             make_float4(o[0], o[1], o[2], o[3]);
     }
+#ifdef TDMPC_STAMPS
+    __syncthreads();
+    STAMP(4);
+    STAMP_RECORD();
+#endif
 }
 
 // estimate_value's terminal combination (tdmpc.py:91-92): G + gamma^H min(Q1, Q2), nan_to_num.
@@ -1918,19 +1983,44 @@ bool chain_shape_ok(const Layout& w) {
     if (M % 256 || M / 256 > 4 || M / 256 == 3) return false;
     const size_t hfl = (size_t)std::max(w.Kx, M) * 32;
     for (int n3 : {w.Lr, w.Ar}) {
-        const int nb3 = n3 / 32, ks = nb3 >= 4 ? 1 : 4 / nb3, items = nb3 * ks;
+        const int nb3 = n3 / 32, ks = nb3 >= 8 ? 1 : 8 / nb3, items = nb3 * ks;
         if (items > 16 || (size_t)items * 1024 > hfl || (M / 8) % ks) return false;
     }
-    return (hfl + 512) * 4 <= 160 * 1024;
+    // the pi noise is prefetched one quad per thread: Ap/4 * 32 <= 512
+    if (w.Ap / 4 * 32 > 512) return false;
+    const int pmax = std::max(chain_param_floats(CH_Q, M, 0), chain_param_floats(CH_STEP, M, std::max(w.Lr, w.Ar)));
+    return (hfl + 512 + pmax) * 4 <= 160 * 1024;
+}
+
+// Algorithmic MACs per row of a chain launch (with the real widths, not the padded ones):
+// CH_STEP d + R = 2 (K1 M + M^2) + M L + M, CH_PI K1 M + M^2 + M A, CH_Q 2 (K1 M + M^2 + M).
+double chain_macs_per_row(int mode, const ChainArgs& a, int nprob) {
+    const double K1 = a.K1, M = a.M;
+    if (mode == CH_STEP) return 2 * (K1 * M + M * M) + M * a.nvalid + M;
+    if (mode == CH_PI) return K1 * M + M * M + M * a.nvalid;
+    return nprob * (K1 * M + M * M + M);
 }
 
 int launch_chain(int mode, const ChainArgs& a, int nprob, hipStream_t s) {
     if (a.rows <= 0) return 0;
-    const size_t lds = ((size_t)a.hfl + 512) * 4;
+    const size_t lds = ((size_t)a.hfl + 512 + chain_param_floats(mode, a.M, a.n3)) * 4;
     const dim3 grid((a.rows + 31) / 32, nprob), block(512);
     const int tn = a.M / 256;
+    // diagnostic timer (tdmpc_profile_begin cfg 4 + mode): HIP events around matching chain launches
+    Profiler& pf = g_prof;
+    const bool prof = pf.armed && pf.cfg == 4 + mode && pf.n + 2 <= pf.cap && (pf.rows == 0 || a.rows == pf.rows);
+    if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], s));
 #define CHAIN_LAUNCH(MODE, TN) \
-    if (mode == MODE && tn == TN) { hipLaunchKernelGGL((chain_kernel<MODE, TN>), grid, block, lds, s, a); HIPCHK(hipGetLastError()); return 0; }
+    if (mode == MODE && tn == TN) { \
+        hipLaunchKernelGGL((chain_kernel<MODE, TN>), grid, block, lds, s, a); \
+        HIPCHK(hipGetLastError()); \
+        if (prof) { \
+            HIPCHK(hipEventRecord(pf.ev[pf.n + 1], s)); \
+            pf.n += 2; \
+            pf.flops += 2.0 * a.rows * chain_macs_per_row(mode, a, nprob); \
+        } \
+        return 0; \
+    }
     CHAIN_LAUNCH(CH_STEP, 1) CHAIN_LAUNCH(CH_STEP, 2) CHAIN_LAUNCH(CH_STEP, 4)
     CHAIN_LAUNCH(CH_PI, 1) CHAIN_LAUNCH(CH_PI, 2) CHAIN_LAUNCH(CH_PI, 4)
     CHAIN_LAUNCH(CH_Q, 1) CHAIN_LAUNCH(CH_Q, 2) CHAIN_LAUNCH(CH_Q, 4)

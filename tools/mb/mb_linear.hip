@@ -75,6 +75,18 @@ int main(int argc, char** argv) {
         printf("s2loop B=%d rows=%d launches=%d\n", B, a.M, s2n);
         return 0;
     }
+    if (argc > 2 && !strcmp(argv[2], "chainloop")) {
+        // only the chain rollout step over the B*N candidate rows, n times (PMC passes)
+        Ctx c;
+        if (setup_ctx(c, &d, packed, ws, sz.workspace_bytes, B, 5, 6, s)) { printf("ctx failed\n"); return 1; }
+        c.path = 2;
+        const RowMap rmc = {c.N, c.T, 0};
+        for (int i = 0; i < s2n; ++i)
+            if (step_next(c, 1, B * c.N, rmc, 0.99f, 0, 0)) { printf("launch failed %s\n", tdmpc_last_error()); return 1; }
+        CK(hipStreamSynchronize(s));
+        printf("chainloop B=%d rows=%d launches=%d\n", B, B * c.N, s2n);
+        return 0;
+    }
     if (argc > 2 && !strcmp(argv[2], "sweep")) {
         // tile-shape sweep over the planner's GEMM shapes (rows x N x K x problems), plain ELU epilogue
         Ctx c;
@@ -192,7 +204,7 @@ int main(int argc, char** argv) {
         unsigned int cap = 8192;
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_cap), &cap, 4));
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dbuf, sizeof(dbuf)));
-        auto run_case = [&](const char* name, const std::function<void()>& fn) {
+        auto run_case = [&](const char* name, const std::function<void()>& fn, int ysel = -1) {
             for (int i = 0; i < 5; ++i) fn();
             CK(hipStreamSynchronize(s));
             unsigned int zero = 0;
@@ -203,6 +215,12 @@ int main(int argc, char** argv) {
             n = std::min(n, 8192u);
             std::vector<unsigned long long> h(8 * n);
             CK(hipMemcpy(h.data(), dbuf, 8 * 8 * n, hipMemcpyDeviceToHost));
+            if (ysel >= 0) {   // keep the workgroups with blockIdx.y == ysel
+                unsigned m = 0;
+                for (unsigned i = 0; i < n; ++i)
+                    if ((int)((h[8 * i + 6] >> 16) & 0xffff) == ysel) { for (int k = 0; k < 8; ++k) h[8 * m + k] = h[8 * i + k]; ++m; }
+                n = m;
+            }
             unsigned long long rtmin = ~0ull, rtmax = 0;
             double ph[4] = {0, 0, 0, 0}, phmax[4] = {0, 0, 0, 0};
             int xcc_hist[8] = {0};
@@ -242,6 +260,14 @@ int main(int argc, char** argv) {
         run_case("S2 lds 128x128 K=128", [&] { launch_lds_t<2, 1, 2, 4, 32>(b, 2, M, s); });
         LinArgs e = a; e.M = B * c.T;
         run_case("S2 all rows lds 192x128", [&] { launch_lds_t<3, 1, 2, 4, 32>(e, 2, M, s); });
+        const RowMap rmc = {c.N, c.T, 0};
+        const RowMap allc = {c.T, c.T, 0};
+        c.path = 2;
+        run_case("chain step dyn (N rows)", [&] { step_next(c, 1, B * c.N, rmc, 0.99f, 0, 0); }, 0);
+        run_case("chain step rew (N rows)", [&] { step_next(c, 1, B * c.N, rmc, 0.99f, 0, 0); }, 1);
+        run_case("chain pi (T rows)", [&] { policy(c, 5, B * c.T, allc, noise, c.eps_env, c.T, 0, 0.05f); });
+        run_case("chain Q (T rows)", [&] { terminal_q(c, 0.95f, nullptr, 6, 0); }, 0);
+        c.path = 0;
     }
 #endif
     CK(hipStreamSynchronize(s));
