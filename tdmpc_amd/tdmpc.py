@@ -38,6 +38,16 @@ def _discount_pows(discount: float, H: int):
     return out
 
 
+def load_checkpoint(fp, model, model_target, device="cpu"):
+    """Load a reference checkpoint -- `{'model': sd, 'model_target': sd}` as written by the reference's
+    `TDMPC.save` (tdmpc.py:68-81; logger.py:126-133 saves `agent.state_dict()` the same way) -- into TOLD
+    modules with the reference's key names. Loaded with weights_only=True (nothing in the file executes) and
+    strict key matching; the planner repacks the new tensors on its next call."""
+    d = torch.load(fp, map_location=device, weights_only=True)
+    model.load_state_dict(d["model"])
+    model_target.load_state_dict(d["model_target"])
+
+
 class HipPlanner:
     """Owns the device buffers of one planner instance and calls the C ABI."""
 
@@ -252,9 +262,7 @@ class TDMPC:
         torch.save(self.state_dict(), fp)
 
     def load(self, fp):
-        d = torch.load(fp, map_location=self.device, weights_only=True)
-        self.model.load_state_dict(d["model"])
-        self.model_target.load_state_dict(d["model_target"])
+        load_checkpoint(fp, self.model, self.model_target, self.device)
 
     @property
     def _prev_mean(self):

@@ -28,6 +28,10 @@ def _enc(cfg) -> nn.Sequential:
         s = cfg.img_size
         for k in (7, 5, 3, 3):
             s = (s - k) // 2 + 1
+        # the reference sizes the flatten by running the convs on torch.randn(C, S, S) (helper.py:28-31,
+        # :129): draw (and drop) the same tensor so the default init of the layers built after it consumes
+        # torch's generator exactly as in the reference (seeded inits then agree bit for bit)
+        torch.randn(c, cfg.img_size, cfg.img_size)
         layers += [nn.Flatten(), nn.Linear(nc * s * s, cfg.latent_dim)]
         return nn.Sequential(*layers)
     return nn.Sequential(nn.Linear(cfg.obs_shape[0], cfg.enc_dim), nn.ELU(),

@@ -76,7 +76,9 @@ def _worker_body(rank, world, port, obs, out_q):
         model.load_state_dict(synthetic_state_dict(cfg, 3 if rank == 0 else 4))
         pl.broadcast_weights(model, src=0)
         same = all(torch.equal(v, synthetic_state_dict(cfg, 3)[k]) for k, v in model.state_dict().items())
-        out_q.put((rank, a.clone(), m.clone(), same))
+        # numpy, not tensors: torch's queue shares tensor storage through file descriptors that vanish when
+        # this worker exits before the parent has received them
+        out_q.put((rank, a.numpy().copy(), m.numpy().copy(), same))
     finally:
         dist.destroy_process_group()
 
@@ -107,5 +109,5 @@ def test_sharded_plan_gloo_world2():
     a_ref, m_ref = _oracle_plan_fn(cfg, sd, 0)(obs, 10**6, True)
     for rank, a, m, same in res:
         assert same, f"rank {rank} weights not synchronised"
-        assert torch.equal(a, a_ref), rank
-        assert torch.equal(m, m_ref), rank
+        assert torch.equal(torch.from_numpy(a), a_ref), rank
+        assert torch.equal(torch.from_numpy(m), m_ref), rank
