@@ -120,6 +120,64 @@ def cpu_baseline(cfg, budget_s: float):
                       f"torch CPU fp32, {threads} threads, {cpu_model}"}
 
 
+def replay_bench(cfg, dev, cpu=True, reps=200):
+    """one prioritized-replay sample() (batch 512, H+1 = 6-step windows) from a buffer of the
+    task's capacity (train_steps 500000 / action_repeat 2 = 250k transitions, 500-step episodes), random
+    priorities, on the device (tdmpc_amd.replay) -- with replacement (buffer not yet full, the common case) and
+    without (full). CPU baseline: the oracle's restatement of the reference sample() (torch CPU + numpy choice,
+    1 process) on the same buffer contents."""
+    from types import SimpleNamespace
+    from tdmpc_amd.replay import ReplayBuffer
+    L, cap, B, H = 500, 250_000, 512, 5
+    obs_dim, A = cfg.obs_shape[0], cfg.action_dim
+    rc = SimpleNamespace(device=str(dev), modality="state", obs_shape=(obs_dim,), action_dim=A, episode_length=L,
+                         train_steps=cap, max_buffer_size=10**6, batch_size=B, horizon=H, env_horizon=H,
+                         per_alpha=0.6, per_beta=0.4, frame_stack=1)
+    rs = np.random.RandomState(0)
+    ep = SimpleNamespace(obs=torch.from_numpy(rs.standard_normal((L + 1, obs_dim)).astype(np.float32)),
+                         action=torch.from_numpy(rs.uniform(-1, 1, (L, A)).astype(np.float32)),
+                         reward=torch.from_numpy(rs.standard_normal(L).astype(np.float32)))
+    out = {"config": f"capacity {cap}, batch {B}, window H+1={H + 1}, obs {obs_dim}, A {A}, alpha 0.6, beta 0.4"}
+    for full in (False, True):
+        buf = ReplayBuffer(rc, latent_plan=True)
+        for _ in range(cap // L if full else cap // L - 1):
+            buf.add(ep)
+        total = cap if full else buf.idx
+        buf.update_priorities(torch.from_numpy(rs.randint(0, total, 50_000)),
+                              torch.from_numpy(rs.exponential(1.0, (50_000, 1)).astype(np.float32)))
+        for _ in range(5):
+            buf.sample()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(reps):
+            buf.sample()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / reps
+        key = "without_replacement" if full else "with_replacement"
+        # algorithmic HBM bytes: priorities read, p**alpha write + read, probs write, float64 cdf write, window gather
+        alg = total * (4 + 8 + 4 + 8) + B * (H + 2) * (obs_dim + A + 1) * 4
+        out[key] = {"value": round(1.0 / dt, 1), "unit": "samples/s", "us_per_sample": round(dt * 1e6, 2),
+                    "total": total, "hbm_gbs_algorithmic": round(alg / dt / 1e9, 1)}
+        if cpu:
+            from oracle.replay_ref import RefReplay
+            ref = RefReplay(SimpleNamespace(modality="state", obs_shape=(obs_dim,), action_dim=A, episode_length=L,
+                                            capacity=cap, batch_size=B, horizon=H, per_alpha=0.6, per_beta=0.4))
+            ref._obs = buf._obs.cpu()
+            ref._last_obs = buf._last_obs.cpu()
+            ref._action, ref._reward = buf._action.cpu(), buf._reward.cpu()
+            ref._priorities, ref._full, ref.idx = buf._priorities.cpu(), full, buf.idx
+            n, t0 = 0, time.perf_counter()
+            while n < 5 or time.perf_counter() - t0 < 3.0:
+                ref.sample(np.random.random_sample(4 * B))
+                n += 1
+            cdt = (time.perf_counter() - t0) / n
+            out[key]["cpu_baseline"] = {"value": round(1.0 / cdt, 2), "unit": "samples/s", "kind": "port",
+                                        "cores": torch.get_num_threads(),
+                                        "sample": f"{n} oracle sample() calls (torch CPU + numpy choice)"}
+            out[key]["speedup_vs_cpu"] = round(cdt / dt, 1)
+    return out
+
+
 def make_agent(cfg, B, rng, graph, seed):
     torch.manual_seed(seed)
     agent = TDMPC(cfg, max_batch=B, rng=rng, graph=graph)
@@ -158,6 +216,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-single", action="store_true")
+    ap.add_argument("--no-replay", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -264,6 +323,10 @@ def main():
         single = {"value": round(ks / el1, 3), "unit": "plan-steps/s", "ms_per_step": round(el1 / ks * 1e3, 4),
                   "note": "one env per plan() call (the drop-in TDMPC.plan path), same GPU, same run"}
 
+    replay = None
+    if not args.no_replay and world == 1:
+        replay = replay_bench(cfg, dev, cpu=not args.no_cpu)
+
     cpu = None
     if rank == 0 and not args.no_cpu and world == 1:
         cpu = cpu_baseline(cfg, args.cpu_budget)
@@ -284,6 +347,7 @@ def main():
             "roofline": roof,
             "plan_roofline": plan_roof,
             "single_env": single,
+            "replay_sampler": replay,
             "cpu_baseline": cpu,
         }
         if cpu:

@@ -16,7 +16,10 @@ PATHS = {"auto": 0, "layered": 1, "chain": 2}
 
 EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc_num_param_tensors",
             "tdmpc_pack_weights", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_last_error",
-            "tdmpc_profile_begin", "tdmpc_profile_end")
+            "tdmpc_profile_begin", "tdmpc_profile_end",
+            # include/tdmpc_replay.h
+            "tdmpc_replay_workspace_bytes", "tdmpc_replay_add_priorities", "tdmpc_replay_update_priorities",
+            "tdmpc_replay_sample")
 
 
 class Dims(C.Structure):
@@ -31,6 +34,16 @@ class PlanParams(C.Structure):
                 ("min_std", C.c_float), ("temperature", C.c_float), ("momentum", C.c_float),
                 ("one_minus_momentum", C.c_float), ("std_floor", C.c_float),
                 ("discount_pow", C.c_float * 17), ("path", C.c_int32)]
+
+
+class ReplayDims(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("modality", "obs_dim", "img_hw", "frame_stack", "action_dim",
+                                         "episode_length", "capacity", "horizon", "batch_size")]
+
+
+class ReplayStore(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("last_obs", C.c_void_p), ("action", C.c_void_p), ("reward", C.c_void_p),
+                ("priorities", C.c_void_p)]
 
 
 class Sizes(C.Structure):
@@ -66,6 +79,12 @@ def lib():
     L.tdmpc_last_error.restype = C.c_char_p
     L.tdmpc_profile_begin.argtypes = [i32, i32, i32, i32, i32]
     L.tdmpc_profile_end.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.tdmpc_replay_workspace_bytes.argtypes = [C.POINTER(ReplayDims)]
+    L.tdmpc_replay_workspace_bytes.restype = sz
+    L.tdmpc_replay_add_priorities.argtypes = [C.POINTER(ReplayDims), vp, i32, i32, vp, sz, vp]
+    L.tdmpc_replay_update_priorities.argtypes = [C.POINTER(ReplayDims), vp, vp, vp, i32, C.c_float, vp]
+    L.tdmpc_replay_sample.argtypes = [C.POINTER(ReplayDims), C.POINTER(ReplayStore), i32, i32, C.c_float,
+                                      C.c_float, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
     for name in EXPORTED:
         if not hasattr(L, name):
             raise RuntimeError(f"{LIB_PATH} does not export {name}")

@@ -11,7 +11,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "tdmpc_kernels.hip")
+SRCS = [os.path.join(HERE, "csrc", "tdmpc_kernels.hip"), os.path.join(HERE, "csrc", "replay_kernels.hip")]
 OUT = os.path.join(HERE, "libtdmpc_hip.so")
 ARCH = os.environ.get("TDMPC_OFFLOAD_ARCH", "gfx950")
 
@@ -24,12 +24,12 @@ def hipcc() -> str:
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
-    deps = [SRC, os.path.join(REPO, "include", "tdmpc_hip.h")]
+    deps = SRCS + [os.path.join(REPO, "include", "tdmpc_hip.h"), os.path.join(REPO, "include", "tdmpc_replay.h")]
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
     tmp = OUT + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(REPO, "include"), "-o", tmp, SRC]
+           "-I", os.path.join(REPO, "include"), "-o", tmp] + SRCS
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -2321,6 +2321,11 @@ int launch_transpose(const float* src, int rows, int cols, float* dst, hipStream
 
 }  // namespace
 
+namespace tdmpc_internal {
+// error text for tdmpc_last_error() from the other translation units of the library (replay_kernels.hip)
+void set_error(const char* msg) { snprintf(g_err, sizeof g_err, "%s", msg); }
+}  // namespace tdmpc_internal
+
 // ================================================================================================ C ABI
 extern "C" {
 

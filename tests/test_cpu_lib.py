@@ -14,14 +14,18 @@ HEADER = "include/tdmpc_hip.h"
 
 def _declared():
     import os
-    src = open(os.path.join(os.path.dirname(os.path.dirname(__file__)), HEADER)).read()
-    return sorted(set(re.findall(r"^(?:int|size_t|const char\*)\s+(tdmpc_\w+)\(", src, re.M)))
+    root = os.path.dirname(os.path.dirname(__file__))
+    names = set()
+    for hdr in (HEADER, "include/tdmpc_replay.h"):
+        src = open(os.path.join(root, hdr)).read()
+        names |= set(re.findall(r"^(?:int|size_t|const char\*)\s+(tdmpc_\w+)\(", src, re.M))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():
     L = _lib.lib()
     names = _declared()
-    assert "tdmpc_plan" in names and len(names) >= 8
+    assert "tdmpc_plan" in names and "tdmpc_replay_sample" in names and len(names) >= 12
     for n in names:
         assert hasattr(L, n), n
     assert L.tdmpc_abi_version() == _lib.ABI_VERSION == 3
