@@ -178,6 +178,63 @@ def replay_bench(cfg, dev, cpu=True, reps=200):
     return out
 
 
+def learner_bench(cfg, dev, cpu=True, reps=30):
+    """TDMPC.update (batch 512, horizon 5, the task's TOLD) fed by the device replay buffer
+    (50k transitions): HIP-graph replay of the whole update vs the same update issued eagerly (the reference's
+    execution model on a GPU), and the oracle restatement of the reference update on the host CPU."""
+    from types import SimpleNamespace
+    from tdmpc_amd.replay import ReplayBuffer
+    lcfg = bench_cfg(args_config_for_learner(cfg), batch_size=512)
+    lcfg.device = str(dev)
+    L = 500
+    rc = SimpleNamespace(**{**vars(lcfg), "train_steps": 50_000, "max_buffer_size": 10**6, "episode_length": L,
+                            "env_horizon": lcfg.horizon})
+    rs = np.random.RandomState(0)
+    O, A = lcfg.obs_shape[0], lcfg.action_dim
+    ep = SimpleNamespace(obs=torch.from_numpy(rs.standard_normal((L + 1, O)).astype(np.float32)),
+                         action=torch.from_numpy(rs.uniform(-1, 1, (L, A)).astype(np.float32)),
+                         reward=torch.from_numpy(rs.standard_normal(L).astype(np.float32)))
+    out = {"config": f"{lcfg.task}: batch {lcfg.batch_size}, horizon {lcfg.horizon}, latent {lcfg.latent_dim}, "
+                     f"mlp {lcfg.mlp_dim}, replay 50k transitions"}
+    for mode, warm in (("graph", 3), ("eager", 10**9)):
+        agent = TDMPC(lcfg)
+        agent.model.load_state_dict(synthetic_state_dict(lcfg, 0))
+        agent.model_target.load_state_dict(synthetic_state_dict(lcfg, 1))
+        agent.learner(graph=True, warmup=warm)
+        buf = ReplayBuffer(rc, latent_plan=True)
+        for _ in range(50_000 // L - 1):
+            buf.add(ep)
+        for i in range(5):
+            agent.update(buf, i + 1, sync_metrics=False)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for i in range(reps):
+            agent.update(buf, 6 + i, sync_metrics=False)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / reps
+        out[mode] = {"value": round(1.0 / dt, 1), "unit": "updates/s", "ms_per_update": round(dt * 1e3, 3)}
+    out["graph_speedup_vs_eager"] = round(out["eager"]["ms_per_update"] / out["graph"]["ms_per_update"], 2)
+    if cpu:
+        from oracle.learner_ref import RefLearner
+        ref = RefLearner(lcfg, synthetic_state_dict(lcfg, 0), synthetic_state_dict(lcfg, 1))
+        b = tuple(x.cpu() for x in buf.sample())
+        n, t0 = 0, time.perf_counter()
+        while n < 2 or time.perf_counter() - t0 < 5.0:
+            ref.update(b, n + 1)
+            n += 1
+        cdt = (time.perf_counter() - t0) / n
+        out["cpu_baseline"] = {"value": round(1.0 / cdt, 2), "unit": "updates/s", "kind": "port",
+                               "cores": torch.get_num_threads(),
+                               "sample": f"{n} oracle update() calls (reference math on torch CPU)"}
+        out["speedup_vs_cpu"] = round(cdt / out["graph"]["ms_per_update"] * 1e3, 1)
+    return out
+
+
+def args_config_for_learner(cfg):
+    return {"humanoid": "humanoid-run", "cheetah": "cheetah-run", "dog": "dog-run",
+            "cartpole": "cartpole-swingup"}.get(cfg.task, "humanoid-run")
+
+
 def make_agent(cfg, B, rng, graph, seed):
     torch.manual_seed(seed)
     agent = TDMPC(cfg, max_batch=B, rng=rng, graph=graph)
@@ -217,6 +274,7 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-single", action="store_true")
     ap.add_argument("--no-replay", action="store_true")
+    ap.add_argument("--no-learner", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -327,6 +385,10 @@ def main():
     if not args.no_replay and world == 1:
         replay = replay_bench(cfg, dev, cpu=not args.no_cpu)
 
+    learner = None
+    if not args.no_learner and world == 1 and cfg.modality == "state":
+        learner = learner_bench(cfg, dev, cpu=not args.no_cpu)
+
     cpu = None
     if rank == 0 and not args.no_cpu and world == 1:
         cpu = cpu_baseline(cfg, args.cpu_budget)
@@ -348,6 +410,7 @@ def main():
             "plan_roofline": plan_roof,
             "single_env": single,
             "replay_sampler": replay,
+            "learner": learner,
             "cpu_baseline": cpu,
         }
         if cpu:

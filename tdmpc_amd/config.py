@@ -32,7 +32,19 @@ DEFAULTS = dict(
     enc_dim=256,                 # :72
     mlp_dim=512,                 # :73
     latent_dim=50,               # :74
-    lr=1e-3,                     # :60 (unused by plan, kept for TDMPC.__init__ parity)
+    # learning (TDMPC.update / update_pi / ReplayBuffer, tdmpc.py:165-245, helper.py:434-534)
+    lr=1e-3,                     # :64
+    batch_size=512,              # :27
+    max_buffer_size=1000000,     # :28
+    rho=1.0,                     # :37
+    reward_coef=0.5,             # :32
+    value_coef=0.1,              # :33
+    consistency_coef=0.5,        # :34
+    per_alpha=0.6,               # :40
+    per_beta=0.4,                # :41
+    grad_clip_norm=10,           # :42
+    update_freq=2,               # :43
+    tau=0.01,                    # :44
     # pixels.yaml
     frame_stack=3,               # cfgs/pixels.yaml:2
     num_channels=32,             # cfgs/pixels.yaml:3

@@ -1,0 +1,185 @@
+"""The TD-MPC learner on the GPU: `TDMPC.update / update_pi / _td_target`.
+
+Reference: /root/reference/src/algorithm/tdmpc.py:165-245 (+ helper.py:19-26 mse / l1, 48-52 ema, 71-96
+TruncatedNormal, 250-283 RandomShiftsAug). The math is the reference's, op for op (the oracle restatement
+oracle/learner_ref.py is pinned bit-exact to the reference on the CPU; tests/test_learner.py holds this
+against it within the fp32 tolerance stated there), including the reference's quirks: the IS-weighted mean
+broadcasts total_loss [B, 1] against weights [B] to [B, B]; the TD target uses the ONLINE encoder and policy
+with the target Q; the policy update re-samples TruncatedNormal noise.
+
+What is MI355X-specific is how it runs. A reference update is ~1,500 small kernel launches issued one by one
+from Python with seven host syncs (`.item()` metrics, the host-side replay choice). Here, after `warmup`
+eager updates (which also create Adam's state), one whole update -- the device replay sample
+(tdmpc_amd.replay), encoder / dynamics / reward / Q forward over the horizon, the TD targets, backward,
+grad-norm clipping, Adam (capturable, foreach), the priority write-back, the policy update -- is captured
+into ONE HIP graph per (buffer fill, EMA) shape and replayed: no Python in the loop, no host sync, the RNG
+(philox, graph-safe) advancing exactly as the eager calls would. The EMA of the target is one foreach lerp.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+METRICS = ("consistency_loss", "reward_loss", "value_loss", "pi_loss", "total_loss", "weighted_loss", "grad_norm")
+
+
+class RandomShiftsAug(torch.nn.Module):
+    """helper.py:250-283: random-shift augmentation of pixel observations (identity for state)."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        self.pad = int(cfg.img_size / 21) if cfg.modality == "pixels" else None
+
+    def forward(self, x):
+        if not self.pad:
+            return x
+        shape_len = len(x.size())
+        if shape_len == 5:
+            t, n, c, hh, ww = x.size()
+            x = x.reshape(t * n, c, hh, ww)
+        n_stacked, c, hh, ww = x.size()
+        padding = tuple([self.pad] * 4)
+        x = F.pad(x, padding, "replicate")
+        eps = 1.0 / (hh + 2 * self.pad)
+        arange = torch.linspace(-1.0 + eps, 1.0 - eps, hh + 2 * self.pad, device=x.device, dtype=x.dtype)[:hh]
+        arange = arange.unsqueeze(0).repeat(hh, 1).unsqueeze(2)
+        base_grid = torch.cat([arange, arange.transpose(1, 0)], dim=2)
+        base_grid = base_grid.unsqueeze(0).repeat(n_stacked, 1, 1, 1)
+        shift = torch.randint(0, 2 * self.pad + 1, size=(n_stacked, 1, 1, 2), device=x.device, dtype=x.dtype)
+        shift *= 2.0 / (hh + 2 * self.pad)
+        grid = base_grid + shift
+        shifted = F.grid_sample(x, grid, padding_mode="zeros", align_corners=False)
+        if shape_len == 5:
+            shifted = shifted.reshape(t, n, c, hh, ww)
+        return shifted
+
+
+def _mse(pred, target):
+    return F.mse_loss(pred, target, reduction="none")
+
+
+def _l1(pred, target):
+    return F.l1_loss(pred, target, reduction="none")
+
+
+class Learner:
+    """Owns the optimisers and (in graph mode) the captured update graphs of one TDMPC agent."""
+
+    def __init__(self, agent, graph: bool = True, warmup: int = 3):
+        self.agent = agent
+        self.cfg = agent.cfg
+        self.graph = graph
+        self.warmup = warmup
+        model = agent.model
+        self.params = list(model.parameters())
+        self.pi_params = list(model._pi.parameters())
+        self.target_params = list(agent.model_target.parameters())
+        # tdmpc.py:62-63 (Adam over all TOLD parameters; the policy's own Adam, both at cfg.lr)
+        agent.optim = torch.optim.Adam(self.params, lr=self.cfg.lr, capturable=graph, foreach=True)
+        agent.pi_optim = torch.optim.Adam(self.pi_params, lr=self.cfg.lr, capturable=graph, foreach=True)
+        self.calls = 0
+        self._graphs = {}
+
+    # ------------------------------------------------------------------ reference math
+    @torch.no_grad()
+    def td_target(self, next_obs, reward, eps=None):
+        """tdmpc.py:184-190."""
+        a, cfg = self.agent, self.cfg
+        next_z = a.model.h(next_obs)
+        return reward + cfg.discount * torch.min(*a.model_target.Q(next_z, a.model.pi(next_z, cfg.min_std, eps=eps)))
+
+    def update_pi(self, zs, eps=None):
+        """tdmpc.py:165-182 -> pi_loss (tensor)."""
+        a, cfg = self.agent, self.cfg
+        a.pi_optim.zero_grad(set_to_none=True)
+        a.model.track_q_grad(False)
+        pi_loss = 0
+        for t, z in enumerate(zs):
+            act = a.model.pi(z, cfg.min_std, eps=None if eps is None else eps[t])
+            q = torch.min(*a.model.Q(z, act))
+            pi_loss += -q.mean() * (cfg.rho ** t)
+        pi_loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.pi_params, cfg.grad_clip_norm, error_if_nonfinite=False, foreach=True)
+        a.pi_optim.step()
+        a.model.track_q_grad(True)
+        return pi_loss.detach()
+
+    def step(self, buffer, noise=None):
+        """One TDMPC.update without the EMA (tdmpc.py:192-241) -> metrics tensor [7] (METRICS order).
+        noise: optional list of 2H+1 [B, A] TruncatedNormal draws (H for the TD targets, H+1 for update_pi)."""
+        a, cfg = self.agent, self.cfg
+        H = cfg.horizon
+        obs, next_obses, action, reward, idxs, weights = buffer.sample()
+        a.optim.zero_grad(set_to_none=True)
+        z = a.model.h(a.aug(obs))
+        zs = [z.detach()]
+        consistency_loss, reward_loss, value_loss, priority_loss = 0, 0, 0, 0
+        for t in range(H):
+            Q1, Q2 = a.model.Q(z, action[t])
+            z, reward_pred = a.model.next(z, action[t])
+            with torch.no_grad():
+                next_obs = a.aug(next_obses[t])
+                next_z = a.model_target.h(next_obs)
+                td_target = self.td_target(next_obs, reward[t], eps=None if noise is None else noise[t])
+            zs.append(z.detach())
+            rho = cfg.rho ** t
+            consistency_loss += rho * torch.mean(_mse(z, next_z), dim=1, keepdim=True)
+            reward_loss += rho * _mse(reward_pred, reward[t])
+            value_loss += rho * (_mse(Q1, td_target) + _mse(Q2, td_target))
+            priority_loss += rho * (_l1(Q1, td_target) + _l1(Q2, td_target))
+        total_loss = cfg.consistency_coef * consistency_loss.clamp(max=1e4) + \
+            cfg.reward_coef * reward_loss.clamp(max=1e4) + \
+            cfg.value_coef * value_loss.clamp(max=1e4)
+        weighted_loss = (total_loss * weights).mean()
+        weighted_loss.register_hook(lambda grad: grad * (1 / H))
+        weighted_loss.backward()
+        grad_norm = torch.nn.utils.clip_grad_norm_(self.params, cfg.grad_clip_norm, error_if_nonfinite=False,
+                                                   foreach=True)
+        a.optim.step()
+        buffer.update_priorities(idxs, priority_loss.clamp(max=1e4).detach())
+        pi_loss = self.update_pi(zs, eps=None if noise is None else noise[H:])
+        return torch.stack([consistency_loss.mean(), reward_loss.mean(), value_loss.mean(), pi_loss,
+                            total_loss.mean(), weighted_loss.mean(), grad_norm]).detach()
+
+    @torch.no_grad()
+    def ema(self):
+        """helper.py:48-52: target <- lerp(target, model, tau)."""
+        torch._foreach_lerp_(self.target_params, self.params, self.cfg.tau)
+
+    # ------------------------------------------------------------------ graph driver
+    def _capturable(self, buffer):
+        return self.graph and getattr(buffer, "graph_safe", False)
+
+    def update(self, buffer, step, noise=None):
+        """TDMPC.update semantics -> metrics tensor [7] on the device (no sync)."""
+        self.agent.model.train()
+        if noise is not None or not self._capturable(buffer) or self.calls < self.warmup:
+            if self._capturable(buffer) and self.calls == self.warmup - 1:
+                # the last warm-up runs on a side stream, as graph capture requires of lazily created state
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    m = self.step(buffer, noise)
+                torch.cuda.current_stream().wait_stream(s)
+            else:
+                m = self.step(buffer, noise)
+        else:
+            key = (buffer.idx, buffer._full)
+            g = self._graphs.get(key)
+            if g is None:
+                if len(self._graphs) >= 2:   # the buffer grew: drop the stale captures
+                    self._graphs.clear()
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    out = self.step(buffer)
+                g = self._graphs[key] = (graph, out)
+                # capture recorded the kernels without running them: run this call's update
+            g[0].replay()
+            m = g[1]
+        self.calls += 1
+        if step % self.cfg.update_freq == 0:
+            self.ema()
+        self.agent.model.eval()
+        # parameters changed in place (a graph replay does not bump tensor versions): repack for planning
+        self.agent.planner._packed_key = None
+        return m

@@ -24,6 +24,8 @@ from . import _lib
 
 
 class ReplayBuffer:
+    graph_safe = True   # sample() / update_priorities() are sync-free and capturable (tdmpc_amd.learner)
+
     def __init__(self, cfg, latent_plan: bool = False):
         self.cfg = deepcopy(cfg)
         self.device = torch.device(cfg.device)

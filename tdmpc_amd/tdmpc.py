@@ -5,7 +5,8 @@ constructor argument (a cfg namespace), attributes (`cfg`, `device`, `std`, `mod
 `_prev_mean`), `plan(obs, eval_mode=False, step=None, t0=True) -> (action tensor [A], metrics dict)`,
 `state_dict / save / load`. Planning runs entirely in the HIP library (libtdmpc_hip.so, include/tdmpc_hip.h):
 Python only draws the random numbers (in the reference's order, from torch's and numpy's global generators)
-and launches one `tdmpc_plan` call. The learner (`update`, `update_pi`) is outside this round's scope.
+and launches one `tdmpc_plan` call. `update` / `update_pi` / `_td_target` (the learner) run on the GPU in
+tdmpc_amd/learner.py, replayed from a HIP graph.
 
 Extensions beyond the reference API:
   * `plan_batch(obs[B], ...)` plans B independent environments in one call (one launch sequence, rows of
@@ -251,6 +252,10 @@ class TDMPC:
         self.rng = rng
         self.graph = graph
         self.planner = HipPlanner(cfg, max_batch=max_batch, device=self.device, path=path)
+        from .learner import RandomShiftsAug
+        self.aug = RandomShiftsAug(cfg)                       # tdmpc.py:64
+        self._learner = None
+        self.optim = self.pi_optim = None                     # created with the learner (tdmpc.py:62-63)
         self._has_prev = np.zeros(max_batch, dtype=bool)
         self._prev_H = np.zeros(max_batch, dtype=np.int64)
 
@@ -263,6 +268,33 @@ class TDMPC:
 
     def load(self, fp):
         load_checkpoint(fp, self.model, self.model_target, self.device)
+
+    # ------------------------------------------------------------------ learner (tdmpc.py:165-245)
+    def learner(self, graph: bool = True, warmup: int = 3):
+        """The GPU learner (tdmpc_amd/learner.py), created on first use with its Adam optimisers."""
+        if self._learner is None:
+            from .learner import Learner
+            self._learner = Learner(self, graph=graph, warmup=warmup)
+        return self._learner
+
+    def update(self, replay_buffer, step, sync_metrics: bool = True, noise=None):
+        """tdmpc.py:192-245: one TOLD + policy update from `replay_buffer.sample()`. Returns the reference's
+        metrics dict (one host sync), or the metrics tensor [7] when sync_metrics=False. With a
+        tdmpc_amd.replay.ReplayBuffer the update is replayed from a HIP graph after a few eager warm-ups."""
+        from .learner import METRICS
+        self.std = linear_schedule(self.cfg.std_schedule, step)   # tdmpc.py:197
+        m = self.learner().update(replay_buffer, step, noise=noise)
+        if not sync_metrics:
+            return m
+        return {k: float(v) for k, v in zip(METRICS, m.double().cpu().tolist())}
+
+    def update_pi(self, zs):
+        """tdmpc.py:165-182."""
+        return float(self.learner().update_pi(zs))
+
+    def _td_target(self, next_obs, reward):
+        """tdmpc.py:184-190."""
+        return self.learner().td_target(next_obs, reward)
 
     @property
     def _prev_mean(self):

@@ -76,7 +76,14 @@ class TOLD(nn.Module):
                 m[-1].weight.data.fill_(0)
                 m[-1].bias.data.fill_(0)
 
-    # Eager forms of the four heads (tdmpc.py:30-50); not used by the HIP planner.
+    def track_q_grad(self, enable=True):
+        """tdmpc.py:25-28 (helper.set_requires_grad on Q1, Q2)."""
+        for m in (self._Q1, self._Q2):
+            for p in m.parameters():
+                p.requires_grad_(enable)
+
+    # Eager forms of the heads (tdmpc.py:30-50): the learner (tdmpc_amd/learner.py) differentiates through
+    # them; the HIP planner does not use them.
     def h(self, obs):
         if self.cfg.modality == "pixels":
             obs = obs / 255.0
@@ -89,6 +96,30 @@ class TOLD(nn.Module):
     def Q(self, z, a):
         x = torch.cat([z, a], dim=-1)
         return self._Q1(x), self._Q2(x)
+
+    def pi(self, z, std=0, eps=None):
+        """tdmpc.py:39-45: tanh(pi(z)), plus a TruncatedNormal(mu, std).sample(clip=0.3) when std > 0
+        (`eps`: the N(0, 1) draw to use instead of drawing one -- parity tests)."""
+        mu = torch.tanh(self._pi(z))
+        if std > 0:
+            return truncated_normal_sample(mu, torch.ones_like(mu) * std, clip=0.3, noise=eps)
+        return mu
+
+
+def truncated_normal_sample(loc, scale, clip=None, low=-1.0, high=1.0, eps=1e-6, noise=None):
+    """helper.TruncatedNormal.sample (helper.py:71-96): eps ~ N(0, 1) drawn like torch.distributions'
+    `_standard_normal` (an empty tensor filled by normal_), scaled, clipped to +-clip, added to loc, then
+    clamped to (low + eps, high - eps) with a straight-through gradient."""
+    if noise is None:
+        noise = torch.empty(loc.shape, dtype=loc.dtype, device=loc.device).normal_()
+    else:
+        noise = noise.to(loc.device, loc.dtype).clone()
+    noise *= scale
+    if clip is not None:
+        noise = torch.clamp(noise, -clip, clip)
+    x = loc + noise
+    clamped = torch.clamp(x, low + eps, high - eps)
+    return x - x.detach() + clamped.detach()
 
 
 def _orthogonal_init(m):
