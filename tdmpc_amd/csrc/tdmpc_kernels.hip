@@ -2182,24 +2182,29 @@ int prep(const Ctx& c, const float* noise, int iter, const float* z0) {
     return 0;
 }
 
+// helper.q for both heads over `rows` rows of X_H mapped by `map`, on the chain kernel: q_p per row into k.qv
+// (the value combination happens where it is consumed: cem_kernel / qvalue_kernel).
+int q_chain(const Ctx& c, int rows, RowMap map) {
+    const Layout& w = c.w;
+    const int M = c.M;
+    ChainArgs a = chain0(c, rows, map, c.H, c.Kx, 0);
+    for (int q = 0; q < 2; ++q) {
+        ChainProb& p = a.p[q];
+        p.W1 = c.pw + w.wq1x + (size_t)q * M * c.Kx; p.b1 = c.pw + w.bq1x + q * M;
+        p.g1 = c.pw + w.g1 + q * M; p.be1 = c.pw + w.be1 + q * M;
+        p.W2 = c.pw + w.wq2 + (size_t)q * M * M; p.b2 = c.pw + w.bq2 + q * M;
+        p.g2 = c.pw + w.g2 + q * M; p.be2 = c.pw + w.be2 + q * M;
+        p.w3v = c.pw + w.wq3 + q * M; p.b3v = c.pw + w.bq3 + q;
+    }
+    a.q = c.k.qv; a.q_ld = c.k.xrows;
+    return launch_chain(CH_Q, a, 2, c.s);
+}
+
 int terminal_q(const Ctx& c, float discH, float* value_out, int I, int iter) {
     const Layout& w = c.w;
     const int rows = c.B * c.T, M = c.M;
     int rc;
-    if (use_chain(c, rows, 2)) {
-        // q_p per row into k.qv; the value combination happens where it is consumed (cem_kernel / qvalue_kernel)
-        ChainArgs a = chain0(c, rows, RowMap{1 << 30, 0, 0}, c.H, c.Kx, 0);
-        for (int q = 0; q < 2; ++q) {
-            ChainProb& p = a.p[q];
-            p.W1 = c.pw + w.wq1x + (size_t)q * M * c.Kx; p.b1 = c.pw + w.bq1x + q * M;
-            p.g1 = c.pw + w.g1 + q * M; p.be1 = c.pw + w.be1 + q * M;
-            p.W2 = c.pw + w.wq2 + (size_t)q * M * M; p.b2 = c.pw + w.bq2 + q * M;
-            p.g2 = c.pw + w.g2 + q * M; p.be2 = c.pw + w.be2 + q * M;
-            p.w3v = c.pw + w.wq3 + q * M; p.b3v = c.pw + w.bq3 + q;
-        }
-        a.q = c.k.qv; a.q_ld = c.k.xrows;
-        return launch_chain(CH_Q, a, 2, c.s);
-    }
+    if (use_chain(c, rows, 2)) return q_chain(c, rows, RowMap{1 << 30, 0, 0});
     {   // y1 = Wq1[Q1;Q2] [a|z] + b -> H1, with LayerNorm partial moments per 64 columns
         LinArgs a = args0();
         a.M = rows; a.K = c.Kx;
@@ -2473,8 +2478,9 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     // identical in every CEM iteration (same z0, same pi actions), so later iterations only roll out the N
     // sampled rows and reuse rows N..T-1 of X_t, G and rlast.
     const RowMap all = {T, T, 0};
+    const RowMap pm = {P, T, N};
+    const RowMap rm = {N, T, 0};
     if (P > 0) {
-        const RowMap pm = {P, T, N};
         for (int t = 0; t < H; ++t) {
             if ((rc = policy(c, t, B * P, pm, noise, c.eps_env, P, (long)t * P * c.A, prm->min_std))) return rc;
             if ((rc = step_next(c, t, B * T, all, prm->discount_pow[t], t == 0, t == H - 1)))
@@ -2497,7 +2503,6 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     }
     const size_t cem_lds = cem_lds_bytes(T, H, ca.K, c.A);
 
-    const RowMap rm = {N, T, 0};
     for (int i = 0; i < I; ++i) {
         if (i > 0 && (rc = prep(c, noise, i, nullptr))) return rc;
         if (i > 0 || P == 0)

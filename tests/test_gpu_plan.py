@@ -241,3 +241,24 @@ def test_bench_batch_vs_oracle():
             np.testing.assert_allclose(a[e].cpu().numpy(), ra.numpy(), atol=2e-5, rtol=0)
             compared += 1
     assert compared >= B // 2, "too many near-tie elite swaps to compare actions"
+
+
+def test_graph_replay_equals_eager_batched():
+    """B=8 humanoid through a captured HIP graph (the bench's mode: chain kernels on two streams, the side
+    stream joining the capture through events) equals the same calls issued eagerly, bitwise."""
+    cfg = make_cfg("humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5)
+    B = 8
+    obs = np.random.RandomState(4).standard_normal((B, cfg.obs_shape[0])).astype(np.float32)
+    outs = []
+    for graph in (True, False):
+        agent = TDMPC(cfg, max_batch=B, rng="fused", graph=graph)
+        agent.model.load_state_dict(synthetic_state_dict(cfg, 2))
+        agent.std = 0.05
+        torch.manual_seed(11)
+        res = []
+        for call in range(3):
+            a, m = agent.plan_batch(obs, step=10**6, t0=(call == 0), sync_metrics=False)
+            res.append((a.clone(), m.clone()))
+        outs.append(res)
+    for (a1, m1), (a2, m2) in zip(*outs):
+        assert torch.equal(a1, a2) and torch.equal(m1, m2)
