@@ -230,6 +230,51 @@ def learner_bench(cfg, dev, cpu=True, reps=30):
     return out
 
 
+def icem_bench(cfg, dev, cpu=True, steps=20):
+    """the iCEM planner (TdICemSimMlp.plan) on the same task and N / H / iterations / K as the
+    headline, iCEM defaults (N shrinking by 1.25 per iteration, 25 % of the elites reused, coloured noise), one
+    env per call (the drop-in path), vs the oracle restatement of the reference planner on the host CPU."""
+    from tdmpc_amd.icem import TdICEM
+    icfg = bench_cfg(args_config_for_learner(cfg))
+    icfg.device = str(dev)
+    agent = TdICEM(icfg)
+    agent.model.load_state_dict(synthetic_state_dict(icfg, 0, enc_norm=True))
+    agent.std = 0.05
+    obs = synthetic_obs(icfg, 1)[0]
+    step = 10**6
+    for i in range(3):
+        agent.plan(obs, step=step, t0=(i == 0))
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for i in range(steps):
+        agent.plan(obs, step=step, t0=False)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / steps
+    out = {"config": f"{icfg.task}: N={icfg.num_samples} (x1/{icfg.factor_decrease_num} per iteration) H={icfg.horizon} "
+                     f"iters={icfg.iterations} K={icfg.num_elites} reuse={agent.E_max} elites, 1 env per call, "
+                     "noise drawn in the reference's order (host numpy coloured noise included)",
+           "value": round(1.0 / dt, 2), "unit": "plan-steps/s", "ms_per_step": round(dt * 1e3, 3)}
+    if cpu:
+        from oracle import icem_ref
+        from oracle.tdmpc_ref import RefTOLD
+        told = RefTOLD(synthetic_state_dict(icfg, 0, enc_norm=True), icfg)
+        st = icem_ref.IcemState(0.05)
+        times = []
+        for i in range(40):
+            nz = icem_ref.draw_icem_noise(icfg, st, step, i == 0, False)
+            t0 = time.perf_counter()
+            icem_ref.plan(told, icfg, st, obs, nz, eval_mode=False, step=step, t0=(i == 0))
+            times.append(time.perf_counter() - t0)
+            if i >= 3 and sum(times[2:]) > 6.0:
+                break
+        med = float(np.median(times[2:]))
+        out["cpu_baseline"] = {"value": round(1.0 / med, 2), "unit": "plan-steps/s", "kind": "port",
+                               "cores": torch.get_num_threads(),
+                               "sample": f"{len(times) - 2} oracle iCEM plan() calls after 2 warm-up, median"}
+        out["speedup_vs_cpu"] = round(med / dt, 1)
+    return out
+
+
 def args_config_for_learner(cfg):
     return {"humanoid": "humanoid-run", "cheetah": "cheetah-run", "dog": "dog-run",
             "cartpole": "cartpole-swingup"}.get(cfg.task, "humanoid-run")
@@ -275,6 +320,7 @@ def main():
     ap.add_argument("--no-single", action="store_true")
     ap.add_argument("--no-replay", action="store_true")
     ap.add_argument("--no-learner", action="store_true")
+    ap.add_argument("--no-icem", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -389,6 +435,10 @@ def main():
     if not args.no_learner and world == 1 and cfg.modality == "state":
         learner = learner_bench(cfg, dev, cpu=not args.no_cpu)
 
+    icem = None
+    if not args.no_icem and world == 1 and cfg.modality == "state":
+        icem = icem_bench(cfg, dev, cpu=not args.no_cpu)
+
     cpu = None
     if rank == 0 and not args.no_cpu and world == 1:
         cpu = cpu_baseline(cfg, args.cpu_budget)
@@ -411,6 +461,7 @@ def main():
             "single_env": single,
             "replay_sampler": replay,
             "learner": learner,
+            "icem": icem,
             "cpu_baseline": cpu,
         }
         if cpu:

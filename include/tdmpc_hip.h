@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define TDMPC_ABI_VERSION 3
+#define TDMPC_ABI_VERSION 4
 
 #define TDMPC_OK 0
 #define TDMPC_E_DIMS (-1)     /* unsupported or inconsistent dims / params */
@@ -51,6 +51,9 @@ typedef struct tdmpc_dims {
     int32_t max_horizon;   /* largest H any call will use (workspace is sized for it) */
     int32_t max_iterations;/* largest cfg.iterations any call will use */
     int32_t max_batch;     /* largest number of environments planned per call */
+    int32_t enc_norm;      /* state encoder: 0 = Linear-ELU-Linear (helper.enc, helper.py:130-132); 1 = with a
+                              LayerNorm after the first Linear (helper.dmlab_enc_norm for state with
+                              norm_type 'ln', helper.py:156-166: the iCEM agent's cfg.normalize) */
 } tdmpc_dims;
 
 /* Per-call scalars (tdmpc.py:106-149). */
@@ -97,7 +100,8 @@ size_t tdmpc_noise_floats(const tdmpc_dims* dims, int32_t horizon, int32_t itera
 
 /* Number of parameter tensors tdmpc_pack_weights expects: the reference state_dict order
  * (TOLD, tdmpc.py:9-23): _encoder.*, _dynamics.{0,2,4}.{weight,bias}, _reward.{0,2,4}.*, _pi.{0,2,4}.*,
- * _Q1.{0,1,3,4,6}.*, _Q2.{0,1,3,4,6}.*  (state encoder: 4 tensors; pixel encoder: 10). */
+ * _Q1.{0,1,3,4,6}.*, _Q2.{0,1,3,4,6}.*  (state encoder: 4 tensors, 6 with enc_norm -- 0.w 0.b 1.w 1.b 3.w
+ * 3.b --; pixel encoder: 10). */
 int tdmpc_num_param_tensors(const tdmpc_dims* dims);
 
 /* Pack the TOLD parameters (device pointers, reference state_dict order, fp32, contiguous nn.Linear
@@ -129,6 +133,43 @@ int tdmpc_plan(const tdmpc_dims* dims, const tdmpc_plan_params* params, const vo
                float* prev_mean, float* action, float* metrics,
                float* elite_out, float* score_out, float* value_out, float* mean_out, float* std_out,
                void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- iCEM planner: TdICemSimMlp.plan, /root/reference/src/algorithm/
+ * tdmpc_icem_similarity_mlp.py:160-265, on the chain kernels. Per-iteration candidate counts shrink
+ * (N_i = max(2K, int(N_{i-1} / factor))), a fraction of the elites is reused (shifted in time from the previous
+ * plan in the first iteration, carried over from the previous iteration afterwards), the last iteration's
+ * sample 0 is the CEM mean, and the sample noise is the caller's (white / pink / brown thirds, coloured noise
+ * from the powerlaw-PSD generator, drawn in the reference's order). Row layout per env: [sampled | reused] at
+ * rows [0, N_i + E_i), the P0 policy rollouts at rows [N + K, N + K + P0) (dims.num_pi is the largest P0). */
+typedef struct tdmpc_icem_params {
+    int32_t horizon, iterations, batch, warm_start, eval_mode;
+    int32_t has_elites;       /* the elite buffer holds the previous plan's elites (hasattr(self, '_elite_actions')) */
+    int32_t elite_horizon;    /* their horizon: H, or H - 1 right after the horizon schedule grew */
+    int32_t n_pi0;            /* P0 = int(mixture_coef * num_samples): policy rollouts of the pre-rollout */
+    int32_t n_samples[16];    /* N_i (n_samples[0] == dims.num_samples) */
+    int32_t n_pi[16];         /* P_i = int(mixture_coef * N_i) */
+    int32_t n_elite[16];      /* E_i reused elite trajectories (0 when none) */
+    int64_t samp_off[16];     /* per-env noise offsets (floats): iteration i's sample noise [H][N_i][A] */
+    int64_t term_off[16];     /*   iteration i's terminal policy noise [N_i + E_i + P_i][A] */
+    int64_t reuse_off;        /*   the reused elites' fresh coloured sequence [H][E_0][A] (first iteration) */
+    int64_t pi_off;           /*   the pre-rollout policy noise [H][P0][A] */
+    int64_t act_off;          /*   the final action noise [A] */
+    int64_t env_stride;       /* floats per env noise stream */
+    float min_std, temperature, momentum, one_minus_momentum, std_floor, init_std;
+    float discount_pow[17];
+} tdmpc_icem_params;
+
+/* Sizes for tdmpc_plan_icem (the workspace holds N + K + num_pi rows per env). */
+int tdmpc_icem_sizes_for(const tdmpc_dims* dims, tdmpc_sizes* out);
+
+/*   elites   [batch, max_horizon, K, A] in/out: the previous plan's elites (read when has_elites), then every
+ *            iteration's (`self._elite_actions`)
+ *   value_out [batch, iterations, N + K + num_pi] optional: iteration i's values of its T_i candidates
+ *   other arguments as tdmpc_plan. */
+int tdmpc_plan_icem(const tdmpc_dims* dims, const tdmpc_icem_params* params, const void* packed,
+                    const void* obs, int32_t obs_is_u8, const float* noise, const double* u, float* prev_mean,
+                    float* elites, float* action, float* metrics, float* value_out, float* mean_out,
+                    float* std_out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Building blocks of tdmpc_plan, exposed for unit parity tests (each is one part of the reference):
  * rollout values for explicit candidate action sequences -- TDMPC.estimate_value (tdmpc.py:83-92) for

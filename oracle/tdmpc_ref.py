@@ -113,8 +113,12 @@ class RefTOLD:
                 x = F.relu(F.conv2d(x, self.sd[f"_encoder.{i}.weight"], self.sd[f"_encoder.{i}.bias"], stride=2))
             x = x.view(x.size(0), -1)
             return self._lin(x, "_encoder.10")
-        x = F.elu(self._lin(obs, "_encoder.0"))
-        return self._lin(x, "_encoder.2")
+        x = self._lin(obs, "_encoder.0")
+        if "_encoder.3.weight" in self.sd:
+            # helper.dmlab_enc_norm, state, norm_type 'ln' (helper.py:156-166): Linear, LayerNorm, ELU, Linear
+            x = F.layer_norm(x, (x.shape[-1],), self.sd["_encoder.1.weight"], self.sd["_encoder.1.bias"], 1e-5)
+            return self._lin(F.elu(x), "_encoder.3")
+        return self._lin(F.elu(x), "_encoder.2")
 
     def next(self, z, a):
         x = torch.cat([z, a], dim=-1)

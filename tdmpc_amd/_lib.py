@@ -11,12 +11,12 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libtdmpc_hip.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 PATHS = {"auto": 0, "layered": 1, "chain": 2}
 
 EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc_num_param_tensors",
             "tdmpc_pack_weights", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_last_error",
-            "tdmpc_profile_begin", "tdmpc_profile_end",
+            "tdmpc_profile_begin", "tdmpc_profile_end", "tdmpc_icem_sizes_for", "tdmpc_plan_icem",
             # include/tdmpc_replay.h
             "tdmpc_replay_workspace_bytes", "tdmpc_replay_add_priorities", "tdmpc_replay_update_priorities",
             "tdmpc_replay_sample")
@@ -25,7 +25,8 @@ EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc
 class Dims(C.Structure):
     _fields_ = [(n, C.c_int32) for n in (
         "modality", "obs_dim", "img_c", "img_hw", "num_channels", "action_dim", "latent_dim", "mlp_dim",
-        "enc_dim", "num_samples", "num_pi", "num_elites", "max_horizon", "max_iterations", "max_batch")]
+        "enc_dim", "num_samples", "num_pi", "num_elites", "max_horizon", "max_iterations", "max_batch",
+        "enc_norm")]
 
 
 class PlanParams(C.Structure):
@@ -34,6 +35,16 @@ class PlanParams(C.Structure):
                 ("min_std", C.c_float), ("temperature", C.c_float), ("momentum", C.c_float),
                 ("one_minus_momentum", C.c_float), ("std_floor", C.c_float),
                 ("discount_pow", C.c_float * 17), ("path", C.c_int32)]
+
+
+class IcemParams(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("horizon", "iterations", "batch", "warm_start", "eval_mode", "has_elites",
+                                         "elite_horizon", "n_pi0")] + \
+               [("n_samples", C.c_int32 * 16), ("n_pi", C.c_int32 * 16), ("n_elite", C.c_int32 * 16),
+                ("samp_off", C.c_int64 * 16), ("term_off", C.c_int64 * 16)] + \
+               [(n, C.c_int64) for n in ("reuse_off", "pi_off", "act_off", "env_stride")] + \
+               [(n, C.c_float) for n in ("min_std", "temperature", "momentum", "one_minus_momentum", "std_floor",
+                                         "init_std")] + [("discount_pow", C.c_float * 17)]
 
 
 class ReplayDims(C.Structure):
@@ -79,6 +90,9 @@ def lib():
     L.tdmpc_last_error.restype = C.c_char_p
     L.tdmpc_profile_begin.argtypes = [i32, i32, i32, i32, i32]
     L.tdmpc_profile_end.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.tdmpc_icem_sizes_for.argtypes = [C.POINTER(Dims), C.POINTER(Sizes)]
+    L.tdmpc_plan_icem.argtypes = [C.POINTER(Dims), C.POINTER(IcemParams), vp, vp, i32, vp, vp, vp, vp, vp, vp,
+                                  vp, vp, vp, vp, sz, vp]
     L.tdmpc_replay_workspace_bytes.argtypes = [C.POINTER(ReplayDims)]
     L.tdmpc_replay_workspace_bytes.restype = sz
     L.tdmpc_replay_add_priorities.argtypes = [C.POINTER(ReplayDims), vp, i32, i32, vp, sz, vp]
@@ -100,7 +114,7 @@ def check(rc: int, what: str):
         raise RuntimeError(f"{what} failed with code {rc}: {msg}")
 
 
-def dims_from_cfg(cfg, max_batch: int = 1, max_horizon=None, max_iterations=None) -> Dims:
+def dims_from_cfg(cfg, max_batch: int = 1, max_horizon=None, max_iterations=None, enc_norm: bool = False) -> Dims:
     d = Dims()
     pixels = cfg.modality == "pixels"
     d.modality = 1 if pixels else 0
@@ -118,6 +132,7 @@ def dims_from_cfg(cfg, max_batch: int = 1, max_horizon=None, max_iterations=None
     d.max_horizon = int(max_horizon or cfg.horizon)
     d.max_iterations = int(max_iterations or cfg.iterations)
     d.max_batch = int(max_batch)
+    d.enc_norm = int(bool(enc_norm))
     return d
 
 

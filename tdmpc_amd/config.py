@@ -45,6 +45,15 @@ DEFAULTS = dict(
     grad_clip_norm=10,           # :42
     update_freq=2,               # :43
     tau=0.01,                    # :44
+    # iCEM planner (TdICemSimMlp, tdmpc_icem_similarity_mlp.py; cfgs/default.yaml)
+    factor_decrease_num=1.25,    # :20
+    shift_elites_over_time=True, # :21
+    fraction_elites_reused=0.25, # :22
+    keep_previous_elites=True,   # :23
+    noise_beta=2.5,              # :24
+    regularization_schedule="linear(0.05, 0.5, 1, 5000)",  # :47 (mixture_coef substituted)
+    normalize=True,              # :97 (DSSM encoder: helper.dmlab_enc_norm; TOLD ignores it)
+    norm_type="ln",              # :98
     # pixels.yaml
     frame_stack=3,               # cfgs/pixels.yaml:2
     num_channels=32,             # cfgs/pixels.yaml:3
@@ -62,10 +71,13 @@ TASK_DIMS = {
 
 # cfgs/tasks/{domain}.yaml overrides of keys the planner reads.
 TASK_OVERRIDES = {
-    "humanoid": dict(latent_dim=100),   # cfgs/tasks/humanoid.yaml:6 (iterations:3 / num_samples:4 are
+    "humanoid": dict(latent_dim=100,    # cfgs/tasks/humanoid.yaml:6 (iterations:3 / num_samples:4 are
                                         # overridden by BASELINE.json's N=512, iters=6)
-    "dog": dict(latent_dim=100),        # cfgs/tasks/dog.yaml:4
-    "cartpole": dict(),                 # cfgs/tasks/cartpole.yaml: action_repeat only
+                     regularization_schedule="linear(0.05, 0.5, 1, 50000)",     # :9
+                     batch_size=512, lr=1e-3),                                    # :7
+    "dog": dict(latent_dim=100, batch_size=2048, lr=3e-4),                        # cfgs/tasks/dog.yaml:4-6
+    "cartpole": dict(regularization_schedule="linear(0.05, 0.5, 10000, 2500)",  # cfgs/tasks/cartpole.yaml:3
+                     lr=3e-4),                                                    # :4
 }
 
 # The BASELINE.json configs (name -> overrides). N/H/I come from BASELINE.json itself.

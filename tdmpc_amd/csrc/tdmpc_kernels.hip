@@ -83,6 +83,7 @@ struct Layout {
     int A, L, M, E, Ap, Lp, Kx, Ar, Lr;
     int modality, obs_dim, img_c, img_hw, nch, conv_hw[5], flat;
     size_t enc_w1t, enc_b1, enc_w2t, enc_b2;         // state encoder, weights transposed [in][out]
+    size_t enc_lng, enc_lnb; int enc_norm;           // its LayerNorm (enc_norm), [E] each
     size_t cw[4], cb[4], pl_wt, pl_b;                // pixel encoder (conv dense, linear transposed)
     size_t w1x, b1x;                                 // panel [2M][Kx]: dynamics.0 rows then reward.0 rows
     size_t w2d, b2d, w2r, b2r;                       // panel [M][M]
@@ -106,10 +107,13 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
     if (d->modality == 0) {
         if (d->obs_dim <= 0 || d->enc_dim <= 0) return false;
         w->enc_w1t = take((size_t)w->E * d->obs_dim); w->enc_b1 = take(w->E);
+        w->enc_norm = d->enc_norm != 0;
+        w->enc_lng = take(w->E); w->enc_lnb = take(w->E);
         w->enc_w2t = take((size_t)w->L * w->E); w->enc_b2 = take(w->L);
         w->flat = 0;
     } else {
-        if (d->img_c <= 0 || d->img_hw <= 0 || d->num_channels <= 0) return false;
+        if (d->img_c <= 0 || d->img_hw <= 0 || d->num_channels <= 0 || d->enc_norm) return false;
+        w->enc_norm = 0;
         static const int ks[4] = {7, 5, 3, 3};
         int s = d->img_hw, cin = d->img_c;
         w->conv_hw[0] = s;
@@ -163,8 +167,9 @@ size_t pixel_act_floats(const Layout& w) {
     return m;
 }
 
-void make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k) {
-    const size_t B = d->max_batch, N = d->num_samples, P = d->num_pi, T = N + P, H = d->max_horizon;
+// extra: rows per env beyond N + P (the iCEM planner keeps up to K reused elite trajectories per env)
+void make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k, int extra = 0) {
+    const size_t B = d->max_batch, N = d->num_samples, P = d->num_pi, T = N + P + extra, H = d->max_horizon;
     const size_t M = w.M;
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += rup(bytes, 256); return base ? base + r : nullptr; };
@@ -1394,11 +1399,75 @@ __global__ void __launch_bounds__(256) prep_kernel(const PrepArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------ iCEM fill
+// iCEM candidate rows besides the sampled ones (tdmpc_icem_similarity_mlp.py:213-229), written into X_t's
+// action columns of each env's block of Tw rows:
+//   reused elites at rows [n0, n0 + E): mode 1 (first iteration, time shift): t < eH - 1 -> the previous
+//   plan's elite[t + 1] (`_elite_actions[1:]`), later steps -> clamp(mean + std * coloured noise) of a fresh
+//   sequence (`sample_action_sequence(...)[-1:]` / `[-2:]` when the horizon grew); mode 2 (later iterations,
+//   keep_previous_elites): the previous iteration's elites;
+//   mean_row: the last iteration's sample 0 becomes the CEM mean (icem best-a).
+struct FillArgs {
+    float* X; size_t x_stride; int Kx, apq, Tw;
+    int B, H, A, Hmax, K;
+    int n0, E, mode, eH, mean_row;
+    const float* mean; const float* stdv;          // [B][Hmax][A]
+    const float* elites;                           // [B][Hmax][K][A]
+    const float* eps; long eps_env; long reuse_off; // coloured noise [H][E][A] per env
+};
+
+__global__ void __launch_bounds__(256) icem_fill_kernel(const FillArgs a) {
+    const int rows = a.E + (a.mean_row ? 1 : 0);
+    const long total = (long)a.B * a.H * a.apq * rows;
+    for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
+        long r2 = it;
+        const int j = (int)(r2 % rows); r2 /= rows;
+        const int q = (int)(r2 % a.apq); r2 /= a.apq;
+        const int t = (int)(r2 % a.H);
+        const int e = (int)(r2 / a.H);
+        const float* mt = a.mean + ((size_t)e * a.Hmax + t) * a.A;
+        const float* sd = a.stdv + ((size_t)e * a.Hmax + t) * a.A;
+        float v[4];
+        int row;
+        if (j == a.E) {   // icem best-a: sample 0 = mean
+            row = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = q * 4 + k < a.A ? mt[q * 4 + k] : 0.f;
+        } else {
+            row = a.n0 + j;
+            const float* el = a.elites + (size_t)e * a.Hmax * a.K * a.A;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int cc = q * 4 + k;
+                float x = 0.f;
+                if (cc < a.A) {
+                    if (a.mode == 2) {
+                        x = el[((size_t)t * a.K + j) * a.A + cc];
+                    } else if (t < a.eH - 1) {
+                        x = el[((size_t)(t + 1) * a.K + j) * a.A + cc];
+                    } else {
+                        const float ep = a.eps[(size_t)e * a.eps_env + a.reuse_off + ((size_t)t * a.E + j) * a.A + cc];
+                        x = tclamp(fadd(mt[cc], fmul(sd[cc], ep)), -1.f, 1.f);
+                    }
+                }
+                v[k] = x;
+            }
+        }
+        const int gr = e * a.Tw + row;
+        *(float4*)(a.X + (size_t)t * a.x_stride + (size_t)(gr >> 5) * a.Kx * 32 + (size_t)q * 128 + (gr & 31) * 4) =
+            make_float4(v[0], v[1], v[2], v[3]);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------ CEM
 // One workgroup (16 waves) per environment, after each iteration's values: top-k (tdmpc.py:138-139),
 // softmax refit (:142-149); on the last iteration the output action (:152-160).
 struct CemArgs {
     int final_iter, iter, H, N, P, T, A, K, Kx, Hmax, I;
+    // candidate c of this iteration lives in row row_of(c) of its env's block of Tw rows: c < NE -> c, else
+    // pi_base + (c - NE) (TDMPC.plan: NE = Tw = T, identity; iCEM: [sampled | reused elites] then pi rows)
+    int Tw, NE, pi_base;
+    float* elite_store;                 // optional [B][Hmax][K][A]: this iteration's elites (iCEM reuse)
     const float* X; size_t x_stride;    // X_t panels: action columns of the pi rows
     const float* value;                 // [B*T] (layered path: value_kernel's output)
     const float* G; const float* qv; int q_ld; float discH;   // chain path: value = qvalue(G, q1, q2)
@@ -1451,6 +1520,8 @@ DEVI float wave_sum(float v) {
     return v;
 }
 
+DEVI int cem_row(const CemArgs& a, int c) { return c < a.NE ? c : a.pi_base + (c - a.NE); }
+
 __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int e = blockIdx.x, tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6;
@@ -1468,7 +1539,7 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
     float* red = (float*)(eidx + 64);                      // [32]
     float* gmean = a.mean + (size_t)e * a.Hmax * A;
     float* gstd = a.stdv + (size_t)e * a.Hmax * A;
-    const float* val = a.value + (size_t)e * T;
+    const float* val = a.value + (size_t)e * a.Tw;
 
     for (int i = tid; i < HA; i += nt) omean[i] = gmean[i];
     // ---- top-K (K <= 64): each wave sorts 64-key lists, then a merge tree keeps the best 64
@@ -1476,12 +1547,13 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
         const int i = l * 64 + lane;
         float v = 0.f;
         if (i < T) {
+            const int row = cem_row(a, i);
             if (a.qv) {
-                const size_t x = (size_t)e * T + i;
+                const size_t x = (size_t)e * a.Tw + row;
                 v = qvalue(a.G[x], a.qv[x], a.qv[a.q_ld + x], a.discH);
-                if (a.value_out) a.value_out[((size_t)e * a.I + a.iter) * T + i] = v;
+                if (a.value_out) a.value_out[((size_t)e * a.I + a.iter) * a.Tw + i] = v;
             } else {
-                v = val[i];
+                v = val[row];
             }
         }
         const unsigned long long k = i < T ? topk_key(v, i) : ~0ull;
@@ -1508,7 +1580,7 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
             const int idx = base + tid + u * nt;
             if (idx < HKA) {
                 const int t = idx / (K * A), k = (idx / A) % K, c = idx % A;
-                v[u] = a.X[(size_t)t * a.x_stride + pidx((size_t)e * T + eidx[k], c, a.Kx)];
+                v[u] = a.X[(size_t)t * a.x_stride + pidx((size_t)e * a.Tw + cem_row(a, eidx[k]), c, a.Kx)];
             }
         }
 #pragma unroll
@@ -1548,6 +1620,8 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
         if (a.mean_out) a.mean_out[((size_t)e * a.I + a.iter) * HA + i] = nm;
         if (a.std_out) a.std_out[((size_t)e * a.I + a.iter) * HA + i] = sd;
     }
+    if (a.elite_store)
+        for (int i = tid; i < HKA; i += nt) a.elite_store[(size_t)e * a.Hmax * a.K * A + i] = EA[i];
     if (!a.final_iter) return;
     if (a.elite_out)
         for (int i = tid; i < HKA; i += nt) a.elite_out[(size_t)e * HKA + i] = EA[i];
@@ -1555,7 +1629,7 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
     // estimate_value's reward.mean() of the last iteration: block reduction over the T rows
     {
         float s = 0.f;
-        for (int i = tid; i < T; i += nt) s += a.rlast[(size_t)e * T + i];
+        for (int i = tid; i < T; i += nt) s += a.rlast[(size_t)e * a.Tw + cem_row(a, i)];
         s = wave_sum(s);
         if (lane == 0) red[1 + wave] = s;
     }
@@ -1586,6 +1660,9 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
         float v = EA[(size_t)j * A + c];
         if (!a.eval_mode) v = fadd(v, fmul(sstd[c], a.eps[(size_t)e * a.eps_env + a.eps_act_off + c]));
         a.action[(size_t)e * A + c] = v;
+        // the reference adds the action noise in place to a view of its stored elites (`a = actions[0]`,
+        // tdmpc_icem_similarity_mlp.py:255-259): the kept elite[0][j] carries it
+        if (a.elite_store) a.elite_store[(size_t)e * a.Hmax * a.K * A + (size_t)j * A + c] = v;
     }
     for (int i = tid; i < HA; i += nt) a.prev_mean[(size_t)e * H * A + i] = smean[i];
 }
@@ -1602,6 +1679,9 @@ struct EncArgs {
     const float* w2t; const float* b2;
     float* z0;
     float* mean; float* stdv; const float* prev_mean; int warm, H, A, Hmax;
+    const float* ln_g; const float* ln_b;       // LayerNorm after the first Linear (or null)
+    int warm_keep_last;                         // iCEM warm start: mean[-1] = prev_mean[-1] (else 0)
+    float init_std;                             // 2 (TDMPC.plan) / 0.5 (iCEM)
 };
 
 // out[j] = sum_k wt[k*nout + j] * in[k] for j < nout, partial sums in part[] (nthr floats)
@@ -1630,12 +1710,35 @@ __global__ void __launch_bounds__(1024) encode_kernel(const EncArgs a) {
     if (a.w1t) {
         enc_matvec(a.w1t, x, a.xdim, a.E, part, tid, nt);  // E <= 1024 (check_dims)
         __syncthreads();
+        float v = 0.f;
         if (tid < a.E) {
             const int np = nt / a.E > 0 ? nt / a.E : 1;
             float s = 0.f;
             for (int p = 0; p < np; ++p) s += part[p * a.E + tid];
-            hh[tid] = elu1(s + a.b1[tid]);
+            v = s + a.b1[tid];
         }
+        if (a.ln_g) {
+            // LayerNorm over the E hidden units (biased variance, eps 1e-5), ATen's (x*rstd + -rstd*mean)*g + b
+            __syncthreads();
+            part[tid] = tid < a.E ? v : 0.f;
+            __syncthreads();
+            for (int off = nt / 2; off > 0; off >>= 1) {
+                if (tid < off) part[tid] += part[tid + off];
+                __syncthreads();
+            }
+            const float mean = part[0] / (float)a.E;
+            __syncthreads();
+            const float dv = v - mean;
+            part[tid] = tid < a.E ? dv * dv : 0.f;
+            __syncthreads();
+            for (int off = nt / 2; off > 0; off >>= 1) {
+                if (tid < off) part[tid] += part[tid + off];
+                __syncthreads();
+            }
+            const float rs = 1.0f / sqrtf(part[0] / (float)a.E + 1e-5f);
+            if (tid < a.E) v = fadd(fmul(fadd(fmul(v, rs), -rs * mean), a.ln_g[tid]), a.ln_b[tid]);
+        }
+        if (tid < a.E) hh[tid] = elu1(v);
         __syncthreads();
         hin = hh;
         E = a.E;
@@ -1658,8 +1761,9 @@ __global__ void __launch_bounds__(1024) encode_kernel(const EncArgs a) {
             const int t = i / a.A;
             float mv = 0.f;
             if (a.warm && t < a.H - 1) mv = a.prev_mean[(size_t)e * HA + i + a.A];  // mean[:-1] = prev[1:]
+            if (a.warm && t == a.H - 1 && a.warm_keep_last) mv = a.prev_mean[(size_t)e * HA + i];  // mean[-1] = prev[-1]
             a.mean[(size_t)e * a.Hmax * a.A + i] = mv;
-            a.stdv[(size_t)e * a.Hmax * a.A + i] = 2.f;
+            a.stdv[(size_t)e * a.Hmax * a.A + i] = a.init_std;
         }
     }
 }
@@ -2245,7 +2349,8 @@ int terminal_q(const Ctx& c, float discH, float* value_out, int I, int iter) {
 }
 
 // TOLD.h for `batch` observations -> z0 [B][Lp]; optionally initialises the CEM mean/std.
-int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, const float* prev_mean, int warm) {
+int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, const float* prev_mean, int warm,
+           int warm_keep_last = 0, float init_std = 2.f) {
     const Layout& w = c.w;
     const float* pw = c.pw;
     EncArgs a;
@@ -2254,6 +2359,7 @@ int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, const float*
     if (w.modality == 0) {
         a.x = (const float*)obs; a.x_stride = w.obs_dim; a.xdim = w.obs_dim; a.E = w.E;
         a.w1t = pw + w.enc_w1t; a.b1 = pw + w.enc_b1; a.w2t = pw + w.enc_w2t; a.b2 = pw + w.enc_b2;
+        if (w.enc_norm) { a.ln_g = pw + w.enc_lng; a.ln_b = pw + w.enc_lnb; }
     } else {
         static const int ks[4] = {7, 5, 3, 3};
         const size_t act = pixel_act_floats(w);
@@ -2276,6 +2382,7 @@ int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, const float*
     }
     if (prev_mean) {
         a.mean = c.k.mean; a.stdv = c.k.stdv; a.prev_mean = prev_mean; a.warm = warm;
+        a.warm_keep_last = warm_keep_last; a.init_std = init_std;
         a.H = c.H; a.A = c.A; a.Hmax = c.d->max_horizon;
     }
     const size_t lds = (rup(a.xdim, 4) + rup(std::max(a.E, 1), 4) + 1024) * 4;
@@ -2285,14 +2392,14 @@ int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, const float*
 }
 
 int setup_ctx(Ctx& c, const tdmpc_dims* d, const void* packed, void* ws, size_t ws_bytes, int batch, int H,
-              int I, hipStream_t s) {
+              int I, hipStream_t s, int extra_rows = 0) {
     if (!check_dims(d)) { snprintf(g_err, sizeof g_err, "bad dims"); return TDMPC_E_DIMS; }
     c.d = d;
     make_layout(d, &c.w);
     Work probe;
-    make_work(d, c.w, nullptr, &probe);
+    make_work(d, c.w, nullptr, &probe, extra_rows);
     if (ws_bytes < probe.total) { snprintf(g_err, sizeof g_err, "workspace too small"); return TDMPC_E_SIZE; }
-    make_work(d, c.w, (char*)ws, &c.k);
+    make_work(d, c.w, (char*)ws, &c.k, extra_rows);
     c.pw = (const float*)packed; c.s = s;
     c.B = batch; c.N = d->num_samples; c.P = d->num_pi; c.T = c.N + c.P; c.H = H; c.path = TDMPC_PATH_AUTO;
     c.A = c.w.A; c.M = c.w.M; c.Kx = c.w.Kx;
@@ -2359,7 +2466,7 @@ size_t tdmpc_noise_floats(const tdmpc_dims* d, int32_t H, int32_t I) {
 
 int tdmpc_num_param_tensors(const tdmpc_dims* d) {
     if (!d) return TDMPC_E_NULL;
-    return (d->modality ? 10 : 4) + 6 + 6 + 6 + 10 + 10;
+    return (d->modality ? 10 : (d->enc_norm ? 6 : 4)) + 6 + 6 + 6 + 10 + 10;
 }
 
 int tdmpc_pack_weights(const tdmpc_dims* d, const float* const* t, int32_t n, void* packed, size_t bytes,
@@ -2385,6 +2492,10 @@ int tdmpc_pack_weights(const tdmpc_dims* d, const float* const* t, int32_t n, vo
     if (w.modality == 0) {
         if ((rc = launch_transpose(t[i++], w.E, w.obs_dim, pw + w.enc_w1t, s))) return rc;
         HIPCHK(cp(w.enc_b1, t[i++], w.E));
+        if (w.enc_norm) {
+            HIPCHK(cp(w.enc_lng, t[i++], w.E));
+            HIPCHK(cp(w.enc_lnb, t[i++], w.E));
+        }
         if ((rc = launch_transpose(t[i++], L, w.E, pw + w.enc_w2t, s))) return rc;
         HIPCHK(cp(w.enc_b2, t[i++], L));
     } else {
@@ -2491,6 +2602,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     memset(&ca, 0, sizeof ca);
     ca.H = H; ca.N = N; ca.P = P; ca.T = T; ca.A = c.A; ca.K = d->num_elites; ca.Kx = c.Kx;
     ca.Hmax = d->max_horizon; ca.I = I;
+    ca.Tw = T; ca.NE = T; ca.pi_base = 0;
     ca.X = c.k.X; ca.x_stride = c.k.x_stride; ca.value = c.k.value; ca.rlast = c.k.rlast;
     ca.mean = c.k.mean; ca.stdv = c.k.stdv;
     ca.eps = noise; ca.eps_env = c.eps_env; ca.eps_cem_off = c.eps_cem_off; ca.eps_iter = c.eps_iter;
@@ -2513,6 +2625,116 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
                          prm->min_std)))
             return rc;
         if ((rc = terminal_q(c, prm->discount_pow[H], value_out, I, i))) return rc;
+        ca.final_iter = i == I - 1;
+        ca.iter = i;
+        hipLaunchKernelGGL(cem_kernel, dim3(B), dim3(1024), cem_lds, c.s, ca);
+        HIPCHK(hipGetLastError());
+    }
+    return 0;
+}
+
+int tdmpc_icem_sizes_for(const tdmpc_dims* d, tdmpc_sizes* out) {
+    if (!d || !out) return TDMPC_E_NULL;
+    if (!check_dims(d)) return TDMPC_E_DIMS;
+    Layout w;
+    make_layout(d, &w);
+    Work k;
+    make_work(d, w, nullptr, &k, d->num_elites);
+    out->packed_weight_bytes = rup(w.total * 4, 256);
+    out->workspace_bytes = k.total;
+    out->noise_floats_per_env = 0;   // the iCEM noise layout is the caller's (tdmpc_icem_params offsets)
+    return 0;
+}
+
+int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const void* packed, const void* obs,
+                    int32_t obs_is_u8, const float* noise, const double* u, float* prev_mean, float* elites,
+                    float* action, float* metrics, float* value_out, float* mean_out, float* std_out,
+                    void* workspace, size_t ws_bytes, void* stream) {
+    if (!d || !prm || !packed || !obs || !noise || !u || !prev_mean || !elites || !action || !metrics || !workspace)
+        return TDMPC_E_NULL;
+    Ctx c;
+    int rc;
+    const int H = prm->horizon, I = prm->iterations, B = prm->batch, K = d->num_elites;
+    if (I <= 0 || I > 16) { snprintf(g_err, sizeof g_err, "iCEM: 1..16 iterations"); return TDMPC_E_DIMS; }
+    if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream, K))) return rc;
+    c.path = TDMPC_PATH_CHAIN;
+    if (!chain_shape_ok(c.w)) { snprintf(g_err, sizeof g_err, "iCEM runs on the chain kernels: unsupported shape"); return TDMPC_E_DIMS; }
+    const int N = d->num_samples, Pmax = d->num_pi, Tw = N + K + Pmax, pi_base = N + K, P0 = prm->n_pi0;
+    c.T = Tw;
+    if (P0 <= 0 || P0 > Pmax || prm->n_samples[0] != N) { snprintf(g_err, sizeof g_err, "iCEM: bad counts"); return TDMPC_E_DIMS; }
+    for (int i = 0; i < I; ++i) {
+        const int Ni = prm->n_samples[i], Pi = prm->n_pi[i], Ei = prm->n_elite[i];
+        if (Ni <= 0 || Ni > N || Pi <= 0 || Pi > P0 || Ei < 0 || Ei > K || Ni + Ei + Pi < K ||
+            (Ei > 0 && i == 0 && !prm->has_elites) || (i == 0 && Ei > 0 && prm->elite_horizon != H && prm->elite_horizon != H - 1)) {
+            snprintf(g_err, sizeof g_err, "iCEM: bad counts at iteration %d", i);
+            return TDMPC_E_DIMS;
+        }
+    }
+    const long A = c.A, env = prm->env_stride;
+    // z0 = h(obs); mean = 0 (warm: mean[:-1] = prev[1:], mean[-1] = prev[-1]), std = init_std (0.5)
+    if ((rc = encode(c, obs, obs_is_u8, B, prev_mean, prm->warm_start, 1, prm->init_std))) return rc;
+    // pi pre-rollout of the P0 policy rows (tdmpc_icem_similarity_mlp.py:193-199); their rollout, reward
+    // prefix and z_H are the same in every iteration (same z, same pi actions), so they are computed once
+    const RowMap pm0 = {P0, Tw, pi_base};
+    {
+        PrepArgs pa;
+        memset(&pa, 0, sizeof pa);
+        pa.X = c.k.X; pa.x_stride = c.k.x_stride; pa.Kx = c.Kx; pa.apq = c.w.Ap / 4; pa.lpq = c.w.Lp / 4;
+        pa.B = B; pa.N = N; pa.T = Tw; pa.H = H; pa.A = c.A; pa.z0 = c.k.z0; pa.n_zq = (long)B * pa.lpq * Tw;
+        hipLaunchKernelGGL(prep_kernel, dim3((int)std::min<long>((pa.n_zq + 255) / 256, 2048)), dim3(256), 0, c.s, pa);
+        HIPCHK(hipGetLastError());
+    }
+    for (int t = 0; t < H; ++t) {
+        if ((rc = policy(c, t, B * P0, pm0, noise, env, P0, prm->pi_off + (long)t * P0 * A, prm->min_std))) return rc;
+        if ((rc = step_next(c, t, B * P0, pm0, prm->discount_pow[t], t == 0, t == H - 1))) return rc;
+    }
+    CemArgs ca;
+    memset(&ca, 0, sizeof ca);
+    ca.H = H; ca.A = c.A; ca.K = K; ca.Kx = c.Kx; ca.Hmax = d->max_horizon; ca.I = I;
+    ca.X = c.k.X; ca.x_stride = c.k.x_stride; ca.value = c.k.value; ca.rlast = c.k.rlast;
+    ca.mean = c.k.mean; ca.stdv = c.k.stdv; ca.Tw = Tw; ca.pi_base = pi_base;
+    ca.eps = noise; ca.eps_env = env; ca.eps_act_off = prm->act_off; ca.u = u; ca.prev_mean = prev_mean;
+    ca.eval_mode = prm->eval_mode; ca.temperature = prm->temperature; ca.momentum = prm->momentum;
+    ca.omm = prm->one_minus_momentum; ca.std_floor = prm->std_floor; ca.action = action; ca.metrics = metrics;
+    ca.mean_out = mean_out; ca.std_out = std_out; ca.elite_store = elites;
+    ca.G = c.k.G; ca.qv = c.k.qv; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H]; ca.value_out = value_out;
+    const size_t cem_lds = cem_lds_bytes(Tw, H, K, c.A);
+    for (int i = 0; i < I; ++i) {
+        const int Ni = prm->n_samples[i], Pi = prm->n_pi[i], Ei = prm->n_elite[i], NE = Ni + Ei;
+        {   // sampled candidates clamp(mean + std * noise) for rows [0, Ni) (sample_mix_action_sequence)
+            PrepArgs pa;
+            memset(&pa, 0, sizeof pa);
+            pa.X = c.k.X; pa.x_stride = c.k.x_stride; pa.Kx = c.Kx; pa.apq = c.w.Ap / 4; pa.lpq = c.w.Lp / 4;
+            pa.B = B; pa.N = Ni; pa.T = Tw; pa.H = H; pa.A = c.A;
+            pa.mean = c.k.mean; pa.stdv = c.k.stdv; pa.mstride = d->max_horizon * c.A;
+            pa.eps = noise; pa.eps_env = env; pa.eps_off = prm->samp_off[i];
+            pa.n_sq = (long)B * H * pa.apq * Ni;
+            hipLaunchKernelGGL(prep_kernel, dim3((int)std::min<long>((pa.n_sq + 255) / 256, 2048)), dim3(256), 0, c.s, pa);
+            HIPCHK(hipGetLastError());
+        }
+        if (Ei > 0 || i == I - 1) {
+            FillArgs fa;
+            memset(&fa, 0, sizeof fa);
+            fa.X = c.k.X; fa.x_stride = c.k.x_stride; fa.Kx = c.Kx; fa.apq = c.w.Ap / 4; fa.Tw = Tw;
+            fa.B = B; fa.H = H; fa.A = c.A; fa.Hmax = d->max_horizon; fa.K = K;
+            fa.n0 = Ni; fa.E = Ei; fa.mode = i == 0 ? 1 : 2; fa.eH = prm->elite_horizon; fa.mean_row = i == I - 1;
+            fa.mean = c.k.mean; fa.stdv = c.k.stdv; fa.elites = elites;
+            fa.eps = noise; fa.eps_env = env; fa.reuse_off = prm->reuse_off;
+            const long tot = (long)B * H * fa.apq * (Ei + fa.mean_row);
+            hipLaunchKernelGGL(icem_fill_kernel, dim3((int)std::min<long>((tot + 255) / 256, 2048)), dim3(256), 0, c.s, fa);
+            HIPCHK(hipGetLastError());
+        }
+        // rollout of the sampled + reused rows (the pi rows' is cached from the pre-rollout)
+        const RowMap blk = {NE, Tw, 0};
+        for (int t = 0; t < H; ++t)
+            if ((rc = step_next(c, t, B * NE, blk, prm->discount_pow[t], t == 0, t == H - 1))) return rc;
+        // terminal value of all T_i = NE + Pi candidates: pi(z_H) with this iteration's noise, Q
+        const RowMap pmi = {Pi, Tw, pi_base};
+        if ((rc = policy(c, H, B * NE, blk, noise, env, NE, prm->term_off[i], prm->min_std))) return rc;
+        if ((rc = policy(c, H, B * Pi, pmi, noise, env, Pi, prm->term_off[i] + (long)NE * A, prm->min_std))) return rc;
+        if ((rc = q_chain(c, B * NE, blk))) return rc;
+        if ((rc = q_chain(c, B * Pi, pmi))) return rc;
+        ca.N = Ni; ca.P = Pi; ca.T = NE + Pi; ca.NE = NE;
         ca.final_iter = i == I - 1;
         ca.iter = i;
         hipLaunchKernelGGL(cem_kernel, dim3(B), dim3(1024), cem_lds, c.s, ca);

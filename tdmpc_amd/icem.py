@@ -1,0 +1,248 @@
+"""`TdICEM`: drop-in for the reference iCEM agent's planning API on MI355X.
+
+Reference: `TdICemSimMlp` in /root/reference/src/algorithm/tdmpc_icem_similarity_mlp.py:74-265 (driven by
+src/train_icem_mlp.py). Same `plan(obs, eval_mode=False, step=None, t0=True) -> (action [A], metrics)`, the same
+planner state (`plan_horizon`, `mixture_coef`, `std`, `_prev_mean`, `_elite_actions`) and the same model heads
+(TOLD with the DSSM's LayerNorm state encoder when cfg.normalize / norm_type 'ln'). The whole plan -- encoder, the
+policy pre-rollout, every iteration's rollout of [sampled | reused elites] candidates, terminal policy + Q,
+top-k / softmax refit, elite reuse bookkeeping, the final pick -- is one `tdmpc_plan_icem` call on the chain
+kernels (include/tdmpc_hip.h); Python draws the random numbers and lays out their per-env stream.
+
+Differences from TDMPC.plan that the kernels follow: N shrinks per iteration (N_i = max(2K, int(N_{i-1} /
+factor_decrease_num))), P_i = int(mixture_coef(step) * N_i) (regularization_schedule), std starts at 0.5, a warm
+start keeps mean[-1] = prev_mean[-1], int(fraction_elites_reused * K) elites are re-evaluated (time-shifted from
+the previous plan in the first iteration with a fresh coloured tail, the previous iteration's afterwards), the last
+iteration's sample 0 is the mean, and the sample noise is white / pink (beta 1) / brown (beta 2.5) thirds.
+
+Randomness (`rng="reference"`): torch's and numpy's global generators in the reference's order; the coloured
+thirds come from tdmpc_amd.colored_noise on numpy's global RandomState (the reference's `colorednoise` is
+absent and unpinned). `plan(..., noise=IcemNoise)` takes explicit draws (parity tests).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from copy import deepcopy
+
+import numpy as np
+import torch
+
+from . import _lib
+from .colored_noise import powerlaw_psd_gaussian
+from .config import linear_schedule
+from .tdmpc import _discount_pows, pack_told
+from .told import TOLD
+
+
+def _thirds(n):
+    q, r = divmod(n, 3)
+    return [q, q, q] if r == 0 else ([q, q + 1, q] if r == 1 else [q, q + 1, q + 1])
+
+
+class TdICEM:
+    def __init__(self, cfg, max_batch: int = 1, rng: str = "reference"):
+        if getattr(cfg, "modality", "state") != "state":
+            raise NotImplementedError("iCEM drop-in: state observations (the pixel DSSM encoder is rlpyt's)")
+        enc_norm = bool(getattr(cfg, "normalize", False))
+        if enc_norm and getattr(cfg, "norm_type", "ln") != "ln":
+            raise NotImplementedError("iCEM drop-in: the LayerNorm state encoder (norm_type 'ln')")
+        if rng != "reference":
+            raise ValueError("rng: 'reference'")
+        self.cfg = cfg
+        self.device = torch.device(cfg.device)
+        self.std = linear_schedule(cfg.std_schedule, 0)                       # :84
+        self.mixture_coef = linear_schedule(cfg.regularization_schedule, 0)   # :85
+        self.model = TOLD(cfg, enc_norm=enc_norm).to(self.device)
+        self.model_target = deepcopy(self.model)
+        self.model.eval()
+        self.model_target.eval()
+        self.plan_horizon = 1                                                  # :93
+        self.max_batch = max_batch
+        A, K, N, H = cfg.action_dim, cfg.num_elites, cfg.num_samples, cfg.horizon
+        rs = str(cfg.regularization_schedule)
+        mix_max = max(linear_schedule(rs, 0), linear_schedule(rs, 10**12))
+        self.P_max = max(1, int(mix_max * N))
+        d = _lib.dims_from_cfg(cfg, max_batch=max_batch, enc_norm=enc_norm)
+        d.num_pi = self.P_max
+        self.dims = d
+        self.L = _lib.lib()
+        sz = _lib.Sizes()
+        _lib.check(self.L.tdmpc_icem_sizes_for(C.byref(d), C.byref(sz)), "tdmpc_icem_sizes_for")
+        dev = self.device
+        self.packed = torch.empty(sz.packed_weight_bytes // 4, dtype=torch.float32, device=dev)
+        self.workspace = torch.empty(sz.workspace_bytes // 4, dtype=torch.float32, device=dev)
+        self.E_max = int(cfg.fraction_elites_reused * K)
+        T_max = N + self.E_max + self.P_max
+        # per-env stream upper bound: pre-rollout + per iteration (samples + terminal) + reuse tail + action
+        self.stream_max = H * self.P_max * A + cfg.iterations * (H * N * A + T_max * A) + H * self.E_max * A + A
+        self.noise = torch.zeros(max_batch * self.stream_max, dtype=torch.float32, device=dev)
+        self.u = torch.zeros(max_batch, dtype=torch.float64, device=dev)
+        self.prev_mean_flat = torch.zeros(max_batch * H * A, dtype=torch.float32, device=dev)
+        self.elites = torch.zeros(max_batch, H, K, A, dtype=torch.float32, device=dev)
+        self.action = torch.zeros(max_batch, A, dtype=torch.float32, device=dev)
+        self.metrics = torch.zeros(max_batch, 2, dtype=torch.float32, device=dev)
+        self.obs_buf = torch.zeros(max_batch, cfg.obs_shape[0], dtype=torch.float32, device=dev)
+        self._packed_key = self._packed_model = None
+        self._packed_params = []
+        self._has_prev = False
+        self._has_elites = False
+        self._elite_H = 0
+
+    # ------------------------------------------------------------------ reference state
+    @property
+    def _prev_mean(self):
+        if not self._has_prev:
+            raise AttributeError("_prev_mean")
+        return self.prev_mean_flat[:self.plan_horizon * self.cfg.action_dim].view(self.plan_horizon, -1)
+
+    @property
+    def _elite_actions(self):
+        if not self._has_elites:
+            raise AttributeError("_elite_actions")
+        return self.elites[0, :self._elite_H]
+
+    # ------------------------------------------------------------------ plan
+    def counts(self, mixture, has_elites):
+        """(N_i, P_i, E_i) per iteration (tdmpc_icem_similarity_mlp.py:201-210)."""
+        cfg, out, n = self.cfg, [], self.cfg.num_samples
+        for i in range(cfg.iterations):
+            if i > 0:
+                n = max(2 * cfg.num_elites, int(n / cfg.factor_decrease_num))
+            p = int(mixture * n)
+            e = self.E_max if (cfg.fraction_elites_reused > 0 and (has_elites or i > 0)) else 0
+            out.append((n, p, e))
+        return out
+
+    def _layout(self, H, cts, reuse):
+        """Per-env noise stream offsets (floats)."""
+        A = self.cfg.action_dim
+        off = {"pi": 0}
+        o = H * cts[0][1] * A
+        off["samp"], off["term"] = [], []
+        off["reuse"] = 0
+        for i, (n, p, e) in enumerate(cts):
+            off["samp"].append(o)
+            o += H * n * A
+            if i == 0 and reuse:
+                off["reuse"] = o
+                o += H * e * A
+            off["term"].append(o)
+            o += (n + e + p) * A
+        off["act"] = o
+        off["total"] = o + A
+        return off
+
+    def _draw(self, e, H, cts, off, reuse, eval_mode):
+        """Env e's stream in the reference's draw order (torch / numpy global generators)."""
+        cfg, A = self.cfg, self.cfg.action_dim
+        S = off["total"]
+        buf = self.noise[e * S:(e + 1) * S]
+        dev = self.device
+        P0 = cts[0][1]
+        for t in range(H):
+            buf[t * P0 * A:(t + 1) * P0 * A].view(P0, A).normal_()
+
+        def col(beta, n, length):
+            return torch.from_numpy(powerlaw_psd_gaussian(beta, (n, A, length))).float().permute(2, 0, 1)
+
+        for i, (n, p, ne) in enumerate(cts):
+            n0, n1, n2 = _thirds(n)
+            samp = buf[off["samp"][i]:off["samp"][i] + H * n * A].view(H, n, A)
+            samp[:, :n0].copy_(torch.randn(H, n0, A, device=dev))
+            samp[:, n0:n0 + n1].copy_(col(1.0, n1, cfg.horizon)[:H].to(dev))
+            samp[:, n0 + n1:].copy_(col(2.5, n2, cfg.horizon)[:H].to(dev))
+            if i == 0 and reuse:
+                r = buf[off["reuse"]:off["reuse"] + H * ne * A].view(H, ne, A)
+                r.copy_(col(cfg.noise_beta, ne, H).to(dev) if cfg.noise_beta > 0 else torch.randn(H, ne, A, device=dev))
+            buf[off["term"][i]:off["term"][i] + (n + ne + p) * A].view(n + ne + p, A).normal_()
+        u = float(np.random.random_sample())
+        if not eval_mode:
+            buf[off["act"]:off["act"] + A].normal_()
+        return u
+
+    def _load(self, e, H, cts, off, reuse, nz):
+        """Write explicit draws (oracle IcemNoise) into env e's stream."""
+        A = self.cfg.action_dim
+        S = off["total"]
+        buf = self.noise[e * S:(e + 1) * S]
+        dev = self.device
+        P0 = cts[0][1]
+        buf[:H * P0 * A].copy_(nz.eps_pi.reshape(-1).to(dev))
+        for i, (n, p, ne) in enumerate(cts):
+            buf[off["samp"][i]:off["samp"][i] + H * n * A].copy_(nz.samp[i].reshape(-1).to(dev))
+            if i == 0 and reuse:
+                buf[off["reuse"]:off["reuse"] + H * ne * A].copy_(nz.reuse.reshape(-1).to(dev))
+            buf[off["term"][i]:off["term"][i] + (n + ne + p) * A].copy_(nz.term[i].reshape(-1).to(dev))
+        if nz.eps_act is not None:
+            buf[off["act"]:off["act"] + A].copy_(nz.eps_act.to(dev))
+        return float(nz.u)
+
+    @torch.no_grad()
+    def plan(self, obs, eval_mode=False, step=None, t0=True, noise=None, trace=None):
+        """tdmpc_icem_similarity_mlp.py:160-265 -> (action tensor [A], metrics dict)."""
+        cfg = self.cfg
+        metrics = {"external_reward_mean": 0.0, "current_std": 0.0}
+        if step < cfg.seed_steps and not eval_mode:
+            return torch.empty(cfg.action_dim, dtype=torch.float32, device=self.device).uniform_(-1, 1), metrics
+        horizon = int(min(cfg.horizon, linear_schedule(cfg.horizon_schedule, step)))
+        extend = False
+        if horizon != self.plan_horizon and t0:
+            self.plan_horizon, extend = horizon, True
+        H = self.plan_horizon
+        self.mixture_coef = linear_schedule(cfg.regularization_schedule, step)
+        cts = self.counts(self.mixture_coef, self._has_elites)
+        if cts[0][1] <= 0 or any(p <= 0 for _, p, _ in cts):
+            raise AssertionError("num_pi_trajs > 0")   # the reference asserts this (:187, :205)
+        if cts[0][1] > self.P_max:
+            raise ValueError("mixture_coef above the schedule's maximum")
+        if cfg.iterations > 1 and cts[1][2] > 0 and not cfg.keep_previous_elites:
+            # the reference would then re-use the first iteration's `reused_actions` (a stale loop variable)
+            raise NotImplementedError("fraction_elites_reused > 0 needs keep_previous_elites")
+        reuse = self._has_elites and cfg.shift_elites_over_time and cts[0][2] > 0
+        if reuse and self._elite_H not in (H, H - 1):
+            raise RuntimeError("elite horizon mismatch")   # the reference's torch.cat would fail here
+        off = self._layout(H, cts, reuse)
+        pack_told(self, self.model)
+        self.obs_buf[:1].copy_(torch.as_tensor(np.asarray(obs), dtype=torch.float32).view(1, -1))
+        u = self._draw(0, H, cts, off, reuse, eval_mode) if noise is None else self._load(0, H, cts, off, reuse, noise)
+        self.u[:1].fill_(u)
+        p = _lib.IcemParams()
+        p.horizon, p.iterations, p.batch = H, cfg.iterations, 1
+        p.warm_start = int((not t0) and self._has_prev)
+        p.eval_mode = int(eval_mode)
+        p.has_elites = int(reuse)
+        p.elite_horizon = self._elite_H if reuse else H
+        p.n_pi0 = cts[0][1]
+        for i, (n, pp, e) in enumerate(cts):
+            p.n_samples[i], p.n_pi[i], p.n_elite[i] = n, pp, e
+            p.samp_off[i], p.term_off[i] = off["samp"][i], off["term"][i]
+        p.reuse_off, p.pi_off, p.act_off, p.env_stride = off["reuse"], 0, off["act"], off["total"]
+        p.min_std, p.temperature, p.momentum = cfg.min_std, cfg.temperature, cfg.momentum
+        p.one_minus_momentum = float(1 - cfg.momentum)
+        p.std_floor, p.init_std = float(self.std), 0.5
+        for t, v in enumerate(_discount_pows(cfg.discount, H)):
+            p.discount_pow[t] = v
+        dev = self.device
+        value_out = mean_out = std_out = None
+        if trace is not None:
+            Tw = cfg.num_samples + cfg.num_elites + self.P_max
+            value_out = torch.zeros(1, cfg.iterations, Tw, device=dev)
+            mean_out = torch.zeros(1, cfg.iterations, H, cfg.action_dim, device=dev)
+            std_out = torch.zeros_like(mean_out)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = self.L.tdmpc_plan_icem(
+            C.byref(self.dims), C.byref(p), C.c_void_p(self.packed.data_ptr()), C.c_void_p(self.obs_buf.data_ptr()),
+            0, C.c_void_p(self.noise.data_ptr()), C.c_void_p(self.u.data_ptr()),
+            C.c_void_p(self.prev_mean_flat.data_ptr()), C.c_void_p(self.elites.data_ptr()),
+            C.c_void_p(self.action.data_ptr()), C.c_void_p(self.metrics.data_ptr()),
+            C.c_void_p(_lib.ptr(value_out)), C.c_void_p(_lib.ptr(mean_out)), C.c_void_p(_lib.ptr(std_out)),
+            C.c_void_p(self.workspace.data_ptr()), self.workspace.numel() * 4, C.c_void_p(stream))
+        _lib.check(rc, "tdmpc_plan_icem")
+        if trace is not None:
+            trace.update(value=[value_out[0, i, :n + e + pp] for i, (n, pp, e) in enumerate(cts)],
+                         mean=mean_out[0], std=std_out[0])
+        self._has_prev = True
+        self._has_elites = True
+        self._elite_H = H
+        m = self.metrics[0].double().cpu().numpy()
+        metrics.update({"external_reward_mean": float(m[0]), "current_std": float(m[1])})
+        return self.action[0].clone(), metrics

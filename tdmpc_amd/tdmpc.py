@@ -49,6 +49,28 @@ def load_checkpoint(fp, model, model_target, device="cpu"):
     model_target.load_state_dict(d["model_target"])
 
 
+def pack_told(pl, model):
+    """Pack `model`'s parameters (reference state_dict order) into pl.packed through tdmpc_pack_weights when any
+    of them changed since the last call (pl: an object with L, dims, device, packed and the _packed_* cache)."""
+    if pl._packed_key is not None and pl._packed_model is model:
+        key = tuple((p.data_ptr(), p._version) for p in pl._packed_params)
+        if key == pl._packed_key:
+            return
+    params = list(model.state_dict().values())
+    pl._packed_model, pl._packed_params = model, params
+    key = tuple((p.data_ptr(), p._version) for p in params)
+    params = [p.detach().to(pl.device, torch.float32).contiguous() for p in params]
+    n = pl.L.tdmpc_num_param_tensors(C.byref(pl.dims))
+    if n != len(params):
+        raise ValueError(f"TOLD has {len(params)} tensors, the packer expects {n}")
+    arr = (C.c_void_p * n)(*[p.data_ptr() for p in params])
+    stream = torch.cuda.current_stream(pl.device).cuda_stream
+    _lib.check(pl.L.tdmpc_pack_weights(C.byref(pl.dims), arr, n, C.c_void_p(pl.packed.data_ptr()),
+                                        pl.packed.numel() * 4, C.c_void_p(stream)), "tdmpc_pack_weights")
+    pl._keep = params  # keep source tensors alive until the stream has consumed them
+    pl._packed_key = key
+
+
 class HipPlanner:
     """Owns the device buffers of one planner instance and calls the C ABI."""
 
@@ -89,23 +111,7 @@ class HipPlanner:
     # ------------------------------------------------------------------ weights
     def pack(self, model: TOLD):
         """Pack TOLD parameters when any of them changed (in-place updates bump tensor versions)."""
-        if self._packed_key is not None and self._packed_model is model:
-            key = tuple((p.data_ptr(), p._version) for p in self._packed_params)
-            if key == self._packed_key:
-                return
-        params = list(model.state_dict().values())
-        self._packed_model, self._packed_params = model, params
-        key = tuple((p.data_ptr(), p._version) for p in params)
-        params = [p.detach().to(self.device, torch.float32).contiguous() for p in params]
-        n = self.L.tdmpc_num_param_tensors(C.byref(self.dims))
-        if n != len(params):
-            raise ValueError(f"TOLD has {len(params)} tensors, the packer expects {n}")
-        arr = (C.c_void_p * n)(*[p.data_ptr() for p in params])
-        stream = torch.cuda.current_stream(self.device).cuda_stream
-        _lib.check(self.L.tdmpc_pack_weights(C.byref(self.dims), arr, n, C.c_void_p(self.packed.data_ptr()),
-                                              self.packed.numel() * 4, C.c_void_p(stream)), "tdmpc_pack_weights")
-        self._keep = params  # keep source tensors alive until the stream has consumed them
-        self._packed_key = key
+        pack_told(self, model)
 
     # ------------------------------------------------------------------ noise
     def noise_view(self, H: int, I: int, B: int):

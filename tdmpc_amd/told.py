@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 
-def _enc(cfg) -> nn.Sequential:
+def _enc(cfg, enc_norm=False) -> nn.Sequential:
     if cfg.modality == "pixels":
         c = int(3 * cfg.frame_stack)
         nc = cfg.num_channels
@@ -34,6 +34,11 @@ def _enc(cfg) -> nn.Sequential:
         torch.randn(c, cfg.img_size, cfg.img_size)
         layers += [nn.Flatten(), nn.Linear(nc * s * s, cfg.latent_dim)]
         return nn.Sequential(*layers)
+    if enc_norm:
+        # helper.dmlab_enc_norm for state observations with norm_type 'ln' (helper.py:156-166, the iCEM agent's
+        # encoder): Linear, LayerNorm, ELU, Linear -- keys _encoder.{0,1,3}
+        return nn.Sequential(nn.Linear(cfg.obs_shape[0], cfg.enc_dim), nn.LayerNorm(cfg.enc_dim), nn.ELU(),
+                             nn.Linear(cfg.enc_dim, cfg.latent_dim))
     return nn.Sequential(nn.Linear(cfg.obs_shape[0], cfg.enc_dim), nn.ELU(),
                          nn.Linear(cfg.enc_dim, cfg.latent_dim))
 
@@ -61,10 +66,10 @@ def pixel_enc_out_hw(cfg) -> int:
 class TOLD(nn.Module):
     """Task-Oriented Latent Dynamics: encoder h, dynamics d, reward R, policy pi, twin Q."""
 
-    def __init__(self, cfg, init: str = "reference"):
+    def __init__(self, cfg, init: str = "reference", enc_norm: bool = False):
         super().__init__()
         self.cfg = cfg
-        self._encoder = _enc(cfg)
+        self._encoder = _enc(cfg, enc_norm)
         self._dynamics = _mlp(cfg.latent_dim + cfg.action_dim, cfg.mlp_dim, cfg.latent_dim)
         self._reward = _mlp(cfg.latent_dim + cfg.action_dim, cfg.mlp_dim, 1)
         self._pi = _mlp(cfg.latent_dim, cfg.mlp_dim, cfg.action_dim)
@@ -133,18 +138,19 @@ def _orthogonal_init(m):
             nn.init.zeros_(m.bias)
 
 
-def synthetic_state_dict(cfg, seed: int = 0) -> dict:
+def synthetic_state_dict(cfg, seed: int = 0, enc_norm: bool = False) -> dict:
     """Deterministic non-degenerate TOLD weights (BASELINE.md "Inputs"): every tensor of the reference
     state_dict drawn from `np.random.RandomState(seed + i)` in key order. Linear/conv weights are
     N(0, 1/fan_in) -- including the last layers of R/Q1/Q2, which the reference zero-inits and which would
     make every candidate's value identical (SURVEY.md §5 "Zero-init makes values degenerate"). Biases are
     N(0, 0.05^2); LayerNorm gains 1 + N(0, 0.1^2), shifts N(0, 0.1^2)."""
-    model = TOLD(cfg, init="none")
+    model = TOLD(cfg, init="none", enc_norm=enc_norm)
     sd = {}
     for i, (k, v) in enumerate(model.state_dict().items()):
         rs = np.random.RandomState(seed * 1000 + i)
         shape = tuple(v.shape)
-        is_ln = any(k.startswith(f"_Q{j}.{li}.") for j in (1, 2) for li in (1, 4))
+        is_ln = any(k.startswith(f"_Q{j}.{li}.") for j in (1, 2) for li in (1, 4)) or (
+            enc_norm and k.startswith("_encoder.1."))
         if is_ln and k.endswith("weight"):
             arr = 1.0 + 0.1 * rs.standard_normal(shape)
         elif is_ln:

@@ -13,9 +13,9 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def case_names():
-    """The plan() golden cases (make_golden.py); replay_* / learner_* belong to test_replay / test_learner."""
+    """The plan() golden cases (make_golden.py); replay_* / learner_* / icem_* belong to their own tests."""
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
-                  if not os.path.basename(p).startswith(("replay_", "learner_")))
+                  if not os.path.basename(p).startswith(("replay_", "learner_", "icem_")))
 
 
 def load_case(name):

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert "tdmpc_plan" in names and "tdmpc_replay_sample" in names and len(names) >= 12
     for n in names:
         assert hasattr(L, n), n
-    assert L.tdmpc_abi_version() == _lib.ABI_VERSION == 3
+    assert L.tdmpc_abi_version() == _lib.ABI_VERSION == 4
 
 
 @pytest.mark.parametrize("name", ["cartpole-swingup", "cheetah-run", "humanoid-run", "humanoid-run-l512",
