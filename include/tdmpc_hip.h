@@ -135,7 +135,7 @@ int tdmpc_plan(const tdmpc_dims* dims, const tdmpc_plan_params* params, const vo
                void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- iCEM planner: TdICemSimMlp.plan, /root/reference/src/algorithm/
- * tdmpc_icem_similarity_mlp.py:160-265, on the chain kernels. Per-iteration candidate counts shrink
+ * tdmpc_icem_similarity_mlp.py:160-265, on the planner's kernels (chain or layered, `path`). Per-iteration candidate counts shrink
  * (N_i = max(2K, int(N_{i-1} / factor))), a fraction of the elites is reused (shifted in time from the previous
  * plan in the first iteration, carried over from the previous iteration afterwards), the last iteration's
  * sample 0 is the CEM mean, and the sample noise is the caller's (white / pink / brown thirds, coloured noise
@@ -146,6 +146,7 @@ typedef struct tdmpc_icem_params {
     int32_t has_elites;       /* the elite buffer holds the previous plan's elites (hasattr(self, '_elite_actions')) */
     int32_t elite_horizon;    /* their horizon: H, or H - 1 right after the horizon schedule grew */
     int32_t n_pi0;            /* P0 = int(mixture_coef * num_samples): policy rollouts of the pre-rollout */
+    int32_t path;             /* TDMPC_PATH_*: kernel family (auto: chain kernels only for wide launches) */
     int32_t n_samples[16];    /* N_i (n_samples[0] == dims.num_samples) */
     int32_t n_pi[16];         /* P_i = int(mixture_coef * N_i) */
     int32_t n_elite[16];      /* E_i reused elite trajectories (0 when none) */

@@ -39,7 +39,7 @@ class PlanParams(C.Structure):
 
 class IcemParams(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("horizon", "iterations", "batch", "warm_start", "eval_mode", "has_elites",
-                                         "elite_horizon", "n_pi0")] + \
+                                         "elite_horizon", "n_pi0", "path")] + \
                [("n_samples", C.c_int32 * 16), ("n_pi", C.c_int32 * 16), ("n_elite", C.c_int32 * 16),
                 ("samp_off", C.c_int64 * 16), ("term_off", C.c_int64 * 16)] + \
                [(n, C.c_int64) for n in ("reuse_off", "pi_off", "act_off", "env_stride")] + \

@@ -996,10 +996,9 @@ DEVI void chain_store_lds(float* sH, const float (&v)[TN * 16], int cw0, int r, 
         }
 }
 
-template <int MODE, int TN>
+template <int MODE, int TN, int D = 4, int D3 = 8>
 __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int D = 4, D3 = 8;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     const int pb = blockIdx.y;
     const ChainProb& P = a.p[pb];
@@ -1296,7 +1295,8 @@ __global__ void __launch_bounds__(512) ln_tanh_kernel(const LnArgs a) {
 struct ValueArgs {
     const float* Y; long yts; const float2* st; int st_ld; int M_;
     const float* g2; const float* be2; const float* w3; const float* b3;
-    const float* G; float disc; float* value; float* value_out; int rows, T, I, iter;
+    const float* G; float disc; float* value; int rows;
+    RowMap map;                          // logical row -> row of G / value (the Q input rows were gathered)
 };
 
 __global__ void __launch_bounds__(512) value_kernel(const ValueArgs a) {
@@ -1343,9 +1343,8 @@ __global__ void __launch_bounds__(512) value_kernel(const ValueArgs a) {
             q[p] = s + a.b3[p];
         }
         const float qm = (q[0] != q[0] || q[1] != q[1]) ? NAN : fminf(q[0], q[1]);  // torch.min keeps NaN
-        const float v = nan_to_num(fadd(a.G[row], fmul(a.disc, qm)));
-        a.value[row] = v;
-        if (a.value_out) a.value_out[((size_t)(row / a.T) * a.I + a.iter) * a.T + row % a.T] = v;
+        const int x = map_row(a.map, row);
+        a.value[x] = nan_to_num(fadd(a.G[x], fmul(a.disc, qm)));
     }
 }
 
@@ -1554,6 +1553,7 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
                 if (a.value_out) a.value_out[((size_t)e * a.I + a.iter) * a.Tw + i] = v;
             } else {
                 v = val[row];
+                if (a.value_out) a.value_out[((size_t)e * a.I + a.iter) * a.Tw + i] = v;
             }
         }
         const unsigned long long k = i < T ? topk_key(v, i) : ~0ull;
@@ -2304,14 +2304,17 @@ int q_chain(const Ctx& c, int rows, RowMap map) {
     return launch_chain(CH_Q, a, 2, c.s);
 }
 
-int terminal_q(const Ctx& c, float discH, float* value_out, int I, int iter) {
+// Terminal value of `rows` rows of X_H mapped by `map`: the chain path leaves q1, q2 per row in k.qv (consumed
+// by cem_kernel / qvalue_kernel); the layered path gathers the rows into H1, runs the Q heads and writes
+// value = nan_to_num(G + gamma^H min(Q1, Q2)) back to the mapped rows (value_kernel).
+int terminal_q_rows(const Ctx& c, int rows, RowMap map, float discH, bool chain) {
     const Layout& w = c.w;
-    const int rows = c.B * c.T, M = c.M;
+    const int M = c.M;
     int rc;
-    if (use_chain(c, rows, 2)) return q_chain(c, rows, RowMap{1 << 30, 0, 0});
+    if (chain) return q_chain(c, rows, map);
     {   // y1 = Wq1[Q1;Q2] [a|z] + b -> H1, with LayerNorm partial moments per 64 columns
         LinArgs a = args0();
-        a.M = rows; a.K = c.Kx;
+        a.M = rows; a.K = c.Kx; a.a_mapped = 1; a.amap = map;
         LinProb& p = a.p[0];
         p.A = xop(c, c.H, 0); p.W = wop(c, w.wq1x, c.Kx); p.bias = c.pw + w.bq1x;
         p.C = hout(c.k.H1, c, 0); p.N = p.nvalid = p.nstore = 2 * M; p.epi = EPI_LNSTATS;
@@ -2340,12 +2343,16 @@ int terminal_q(const Ctx& c, float discH, float* value_out, int I, int iter) {
         ValueArgs v;
         v.Y = c.k.H1; v.yts = (long)2 * M * 32; v.st = c.k.st2; v.st_ld = 2 * M / 64; v.M_ = M;
         v.g2 = c.pw + w.g2; v.be2 = c.pw + w.be2; v.w3 = c.pw + w.wq3; v.b3 = c.pw + w.bq3;
-        v.G = c.k.G; v.disc = discH; v.value = c.k.value; v.value_out = value_out; v.rows = rows;
-        v.T = c.T; v.I = I; v.iter = iter;
+        v.G = c.k.G; v.disc = discH; v.value = c.k.value; v.rows = rows; v.map = map;
         hipLaunchKernelGGL(value_kernel, dim3((rows + 31) / 32), dim3(512), 0, c.s, v);
         HIPCHK(hipGetLastError());
     }
     return 0;
+}
+
+int terminal_q(const Ctx& c, float discH) {
+    const int rows = c.B * c.T;
+    return terminal_q_rows(c, rows, RowMap{1 << 30, 0, 0}, discH, use_chain(c, rows, 2));
 }
 
 // TOLD.h for `batch` observations -> z0 [B][Lp]; optionally initialises the CEM mean/std.
@@ -2610,8 +2617,9 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     ca.eval_mode = prm->eval_mode; ca.temperature = prm->temperature; ca.momentum = prm->momentum;
     ca.omm = prm->one_minus_momentum; ca.std_floor = prm->std_floor; ca.action = action; ca.metrics = metrics;
     ca.elite_out = elite_out; ca.score_out = score_out; ca.mean_out = mean_out; ca.std_out = std_out;
+    ca.value_out = value_out;
     if (use_chain(c, B * T, 2)) {   // terminal_q leaves q1, q2 per row; cem_kernel forms the values
-        ca.G = c.k.G; ca.qv = c.k.qv; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H]; ca.value_out = value_out;
+        ca.G = c.k.G; ca.qv = c.k.qv; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H];
     }
     const size_t cem_lds = cem_lds_bytes(T, H, ca.K, c.A);
 
@@ -2624,7 +2632,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
         if ((rc = policy(c, H, B * T, all, noise, c.eps_env, T, c.eps_cem_off + (long)i * c.eps_iter + c.eps_term_off,
                          prm->min_std)))
             return rc;
-        if ((rc = terminal_q(c, prm->discount_pow[H], value_out, I, i))) return rc;
+        if ((rc = terminal_q(c, prm->discount_pow[H]))) return rc;
         ca.final_iter = i == I - 1;
         ca.iter = i;
         hipLaunchKernelGGL(cem_kernel, dim3(B), dim3(1024), cem_lds, c.s, ca);
@@ -2657,8 +2665,8 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
     const int H = prm->horizon, I = prm->iterations, B = prm->batch, K = d->num_elites;
     if (I <= 0 || I > 16) { snprintf(g_err, sizeof g_err, "iCEM: 1..16 iterations"); return TDMPC_E_DIMS; }
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream, K))) return rc;
-    c.path = TDMPC_PATH_CHAIN;
-    if (!chain_shape_ok(c.w)) { snprintf(g_err, sizeof g_err, "iCEM runs on the chain kernels: unsupported shape"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 2) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    c.path = prm->path;
     const int N = d->num_samples, Pmax = d->num_pi, Tw = N + K + Pmax, pi_base = N + K, P0 = prm->n_pi0;
     c.T = Tw;
     if (P0 <= 0 || P0 > Pmax || prm->n_samples[0] != N) { snprintf(g_err, sizeof g_err, "iCEM: bad counts"); return TDMPC_E_DIMS; }
@@ -2697,7 +2705,7 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
     ca.eval_mode = prm->eval_mode; ca.temperature = prm->temperature; ca.momentum = prm->momentum;
     ca.omm = prm->one_minus_momentum; ca.std_floor = prm->std_floor; ca.action = action; ca.metrics = metrics;
     ca.mean_out = mean_out; ca.std_out = std_out; ca.elite_store = elites;
-    ca.G = c.k.G; ca.qv = c.k.qv; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H]; ca.value_out = value_out;
+    ca.G = c.k.G; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H]; ca.value_out = value_out;
     const size_t cem_lds = cem_lds_bytes(Tw, H, K, c.A);
     for (int i = 0; i < I; ++i) {
         const int Ni = prm->n_samples[i], Pi = prm->n_pi[i], Ei = prm->n_elite[i], NE = Ni + Ei;
@@ -2732,8 +2740,11 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
         const RowMap pmi = {Pi, Tw, pi_base};
         if ((rc = policy(c, H, B * NE, blk, noise, env, NE, prm->term_off[i], prm->min_std))) return rc;
         if ((rc = policy(c, H, B * Pi, pmi, noise, env, Pi, prm->term_off[i] + (long)NE * A, prm->min_std))) return rc;
-        if ((rc = q_chain(c, B * NE, blk))) return rc;
-        if ((rc = q_chain(c, B * Pi, pmi))) return rc;
+        // both row groups on the same Q path, so cem_kernel reads one kind of value (qv or value)
+        const bool qchain = use_chain(c, B * NE, 2) && use_chain(c, B * Pi, 2);
+        if ((rc = terminal_q_rows(c, B * NE, blk, prm->discount_pow[H], qchain))) return rc;
+        if ((rc = terminal_q_rows(c, B * Pi, pmi, prm->discount_pow[H], qchain))) return rc;
+        ca.qv = qchain ? c.k.qv : nullptr;
         ca.N = Ni; ca.P = Pi; ca.T = NE + Pi; ca.NE = NE;
         ca.final_iter = i == I - 1;
         ca.iter = i;
@@ -2771,7 +2782,7 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
         HIPCHK(hipGetLastError());
     }
     if ((rc = policy(c, H, B * T, all, eps_term, (long)T * c.A, T, 0, prm->min_std))) return rc;
-    if ((rc = terminal_q(c, prm->discount_pow[H], nullptr, 1, 0))) return rc;
+    if ((rc = terminal_q(c, prm->discount_pow[H]))) return rc;
     if (use_chain(c, B * T, 2)) {
         hipLaunchKernelGGL(qvalue_kernel, dim3((B * T + 255) / 256), dim3(256), 0, c.s, c.k.G, c.k.qv, c.k.xrows,
                            prm->discount_pow[H], c.k.value, B * T);

@@ -16,7 +16,9 @@ iteration's sample 0 is the mean, and the sample noise is white / pink (beta 1) 
 
 Randomness (`rng="reference"`): torch's and numpy's global generators in the reference's order; the coloured
 thirds come from tdmpc_amd.colored_noise on numpy's global RandomState (the reference's `colorednoise` is
-absent and unpinned). `plan(..., noise=IcemNoise)` takes explicit draws (parity tests).
+absent and unpinned; 2.x seeds each call from OS entropy, so its stream is not reproducible anyway).
+`rng="device"` draws the coloured noise (rocFFT) and the pick's uniform on the device too: same distributions,
+no host work. `plan(..., noise=IcemNoise)` takes explicit draws (parity tests).
 """
 from __future__ import annotations
 
@@ -27,7 +29,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .colored_noise import powerlaw_psd_gaussian
+from .colored_noise import _scales as _spectrum, powerlaw_psd_gaussian_torch
 from .config import linear_schedule
 from .tdmpc import _discount_pows, pack_told
 from .told import TOLD
@@ -39,14 +41,18 @@ def _thirds(n):
 
 
 class TdICEM:
-    def __init__(self, cfg, max_batch: int = 1, rng: str = "reference"):
+    def __init__(self, cfg, max_batch: int = 1, rng: str = "reference", path: str = "auto"):
         if getattr(cfg, "modality", "state") != "state":
             raise NotImplementedError("iCEM drop-in: state observations (the pixel DSSM encoder is rlpyt's)")
         enc_norm = bool(getattr(cfg, "normalize", False))
         if enc_norm and getattr(cfg, "norm_type", "ln") != "ln":
             raise NotImplementedError("iCEM drop-in: the LayerNorm state encoder (norm_type 'ln')")
-        if rng != "reference":
-            raise ValueError("rng: 'reference'")
+        if rng not in ("reference", "device"):
+            raise ValueError("rng: 'reference' or 'device'")
+        self.rng = rng
+        if path not in _lib.PATHS:
+            raise ValueError(f"path must be one of {sorted(_lib.PATHS)}")
+        self.path = path
         self.cfg = cfg
         self.device = torch.device(cfg.device)
         self.std = linear_schedule(cfg.std_schedule, 0)                       # :84
@@ -81,6 +87,10 @@ class TdICEM:
         self.action = torch.zeros(max_batch, A, dtype=torch.float32, device=dev)
         self.metrics = torch.zeros(max_batch, 2, dtype=torch.float32, device=dev)
         self.obs_buf = torch.zeros(max_batch, cfg.obs_shape[0], dtype=torch.float32, device=dev)
+        col_max = cfg.iterations * H * N * A + H * self.E_max * A   # coloured floats of one env and call
+        self._stage = torch.empty(col_max, dtype=torch.float32, device=dev)
+        self._pinned = torch.empty(col_max, dtype=torch.float32, pin_memory=dev.type == "cuda")
+        self._h2d_done = None
         self._packed_key = self._packed_model = None
         self._packed_params = []
         self._has_prev = False
@@ -131,30 +141,96 @@ class TdICEM:
         off["total"] = o + A
         return off
 
+    def _colored_specs(self, H, cts, reuse):
+        """The coloured-noise draws of one plan call in the reference's order: (beta, n, length, kind, i)."""
+        cfg, out = self.cfg, []
+        for i, (n, p, ne) in enumerate(cts):
+            n0, n1, n2 = _thirds(n)
+            out += [(1.0, n1, cfg.horizon, "samp", i), (2.5, n2, cfg.horizon, "samp", i)]
+            if i == 0 and reuse and cfg.noise_beta > 0:
+                out.append((cfg.noise_beta, ne, H, "reuse", i))
+        return out
+
+    def _colored_host(self, specs, H):
+        """All of a call's coloured noise on the host -> float32 [sum_k H * n_k * A] ([H][n][A] per draw).
+        Numbers identical to consecutive powerlaw_psd_gaussian calls on numpy's global RandomState: one
+        standard_normal draw of the whole call (the legacy generator's stream does not depend on how it is
+        chunked; normal(scale=s) is s * standard_normal), one irfft per spectrum length (row-independent)."""
+        A = self.cfg.action_dim
+        sizes = [n * A * ((L // 2) + 1) for _, n, L, _, _ in specs]
+        z = np.random.standard_normal(2 * sum(sizes))
+        parts, o = [], 0
+        for (beta, n, L, _, _), sz in zip(specs, sizes):
+            sc, sigma = _spectrum(beta, L)
+            sr = z[o:o + sz].reshape(n, A, -1) * sc
+            si = z[o + sz:o + 2 * sz].reshape(n, A, -1) * sc
+            o += 2 * sz
+            if not L % 2:
+                si[..., -1] = 0
+                sr[..., -1] *= np.sqrt(2)
+            si[..., 0] = 0
+            sr[..., 0] *= np.sqrt(2)
+            parts.append((sr + 1j * si, sigma))
+        out = []
+        for L in sorted({s[2] for s in specs}):
+            idx = [k for k, s in enumerate(specs) if s[2] == L]
+            y = np.fft.irfft(np.concatenate([parts[k][0] for k in idx]), n=L, axis=-1)
+            r = 0
+            for k in idx:
+                n = specs[k][1]
+                out.append((k, (y[r:r + n] / parts[k][1]).astype(np.float32)[:, :, :H].transpose(2, 0, 1)))
+                r += n
+        out.sort(key=lambda t: t[0])
+        return np.concatenate([a.reshape(-1) for _, a in out]) if out else np.zeros(0, np.float32)
+
     def _draw(self, e, H, cts, off, reuse, eval_mode):
-        """Env e's stream in the reference's draw order (torch / numpy global generators)."""
+        """Env e's stream in the reference's draw order on torch's (device) and numpy's global generators.
+        The two generators are independent, so the numpy draws (coloured thirds, reused-elite tail, the pick's
+        uniform) run first on the host and travel in ONE pinned async copy; the torch draws follow in order."""
         cfg, A = self.cfg, self.cfg.action_dim
         S = off["total"]
         buf = self.noise[e * S:(e + 1) * S]
         dev = self.device
+        specs = self._colored_specs(H, cts, reuse)
+        if self.rng == "device":
+            col = [powerlaw_psd_gaussian_torch(b, (n, A, L), dev)[:, :, :H].permute(2, 0, 1) for b, n, L, _, _ in specs]
+            u = None
+        else:
+            host = self._colored_host(specs, H)
+            u = float(np.random.random_sample())
+            if self._h2d_done is not None:
+                self._h2d_done.synchronize()   # the previous call's copy has left the pinned buffer
+            stage = self._pinned[:host.size]
+            stage.numpy()[:] = host
+            dst = self._stage[:host.size]
+            dst.copy_(stage, non_blocking=True)
+            self._h2d_done = torch.cuda.Event()
+            self._h2d_done.record()
+            col, o = [], 0
+            for b, n, L, _, _ in specs:
+                col.append(dst[o:o + H * n * A].view(H, n, A))
+                o += H * n * A
         P0 = cts[0][1]
         for t in range(H):
             buf[t * P0 * A:(t + 1) * P0 * A].view(P0, A).normal_()
-
-        def col(beta, n, length):
-            return torch.from_numpy(powerlaw_psd_gaussian(beta, (n, A, length))).float().permute(2, 0, 1)
-
+        k = 0
         for i, (n, p, ne) in enumerate(cts):
             n0, n1, n2 = _thirds(n)
             samp = buf[off["samp"][i]:off["samp"][i] + H * n * A].view(H, n, A)
             samp[:, :n0].copy_(torch.randn(H, n0, A, device=dev))
-            samp[:, n0:n0 + n1].copy_(col(1.0, n1, cfg.horizon)[:H].to(dev))
-            samp[:, n0 + n1:].copy_(col(2.5, n2, cfg.horizon)[:H].to(dev))
+            samp[:, n0:n0 + n1].copy_(col[k])
+            samp[:, n0 + n1:].copy_(col[k + 1])
+            k += 2
             if i == 0 and reuse:
                 r = buf[off["reuse"]:off["reuse"] + H * ne * A].view(H, ne, A)
-                r.copy_(col(cfg.noise_beta, ne, H).to(dev) if cfg.noise_beta > 0 else torch.randn(H, ne, A, device=dev))
+                if cfg.noise_beta > 0:
+                    r.copy_(col[k])
+                    k += 1
+                else:
+                    r.copy_(torch.randn(H, ne, A, device=dev))
             buf[off["term"][i]:off["term"][i] + (n + ne + p) * A].view(n + ne + p, A).normal_()
-        u = float(np.random.random_sample())
+        if u is None:
+            self.u[e:e + 1].uniform_()
         if not eval_mode:
             buf[off["act"]:off["act"] + A].normal_()
         return u
@@ -204,7 +280,8 @@ class TdICEM:
         pack_told(self, self.model)
         self.obs_buf[:1].copy_(torch.as_tensor(np.asarray(obs), dtype=torch.float32).view(1, -1))
         u = self._draw(0, H, cts, off, reuse, eval_mode) if noise is None else self._load(0, H, cts, off, reuse, noise)
-        self.u[:1].fill_(u)
+        if u is not None:
+            self.u[:1].fill_(u)
         p = _lib.IcemParams()
         p.horizon, p.iterations, p.batch = H, cfg.iterations, 1
         p.warm_start = int((not t0) and self._has_prev)
@@ -212,6 +289,7 @@ class TdICEM:
         p.has_elites = int(reuse)
         p.elite_horizon = self._elite_H if reuse else H
         p.n_pi0 = cts[0][1]
+        p.path = _lib.PATHS[self.path]
         for i, (n, pp, e) in enumerate(cts):
             p.n_samples[i], p.n_pi[i], p.n_elite[i] = n, pp, e
             p.samp_off[i], p.term_off[i] = off["samp"][i], off["term"][i]

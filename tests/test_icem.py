@@ -2,7 +2,7 @@
 
 * The oracle (oracle/icem_ref.py) reproduces the reference planner bit for bit on the CPU over six calls
   (t0 / warm start / horizon growth with the time-shifted elite reuse / eval), tests/golden/icem_humanoid.npz.
-* The GPU planner (tdmpc_amd.icem, chain kernels) against the oracle on identical noise; tolerance as in
+* The GPU planner (tdmpc_amd.icem, chain and layered kernels) against the oracle on identical noise; tolerance as in
   tests/test_gpu_plan.py (values 1e-5 + 1e-4 |ref|; action / mean atol 2e-5 while the elite sets agree).
 * Coloured-noise generator: restated, unpinned (colorednoise is absent and unpinned); its spectrum is checked.
 """
@@ -56,13 +56,14 @@ def _close(a, b, atol=1e-5, rtol=1e-4):
 
 
 @pytest.mark.gpu
-def test_gpu_icem_matches_oracle():
+@pytest.mark.parametrize("path", ["chain", "layered"])
+def test_gpu_icem_matches_oracle(path):
     """The golden call sequence on the GPU planner with the oracle's draws: per-iteration values within the fp32
     tolerance; actions, metrics, prev_mean and the kept elites while every iteration's elite set agrees."""
     from tdmpc_amd.icem import TdICEM
     cfg = icem_cfg()
     sd = synthetic_state_dict(cfg, 31, enc_norm=True)
-    agent = TdICEM(cfg)
+    agent = TdICEM(cfg, path=path)
     agent.model.load_state_dict(sd)
     agent.std = 0.05
     told = RefTOLD(sd, cfg)
@@ -92,3 +93,63 @@ def test_gpu_icem_matches_oracle():
         np.testing.assert_allclose(agent._elite_actions.cpu().numpy(), st.elite_actions.numpy(), atol=2e-5, rtol=0)
         np.testing.assert_allclose([gm["external_reward_mean"], gm["current_std"]],
                                    [rm["external_reward_mean"], rm["current_std"]], atol=2e-5, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("reuse,extend", [(False, False), (True, False), (True, True)])
+def test_gpu_icem_draw_order(reuse, extend):
+    """TdICEM's own draws (rng 'reference': batched host coloured noise, one pinned copy, torch draws on the
+    device) equal the oracle's reference-order draws from the same torch / numpy seeds, element for element."""
+    from tdmpc_amd.config import linear_schedule
+    from tdmpc_amd.icem import TdICEM
+    cfg = icem_cfg()
+    agent = TdICEM(cfg)
+    st = icem_ref.IcemState(0.05)
+    step = 17000 if extend else 10**6
+    st.plan_horizon = 3 if extend else cfg.horizon
+    if reuse:
+        st.elite_actions = torch.zeros(st.plan_horizon, cfg.num_elites, cfg.action_dim)
+    H, ext = icem_ref.next_horizon(cfg, st, step, True)
+    assert ext == extend
+    cts = agent.counts(linear_schedule(cfg.regularization_schedule, step), reuse)
+    off = agent._layout(H, cts, reuse)
+    S = off["total"]
+    for ev in (False, True):
+        torch.manual_seed(7)
+        np.random.seed(8)
+        nz = icem_ref.draw_icem_noise(cfg, st, step, True, ev, device="cuda")
+        after_ref = (torch.randn(4, device="cuda"), np.random.random_sample())
+        agent.noise.zero_()
+        agent._load(0, H, cts, off, reuse, nz)
+        want = agent.noise[:S].clone()
+        torch.manual_seed(7)
+        np.random.seed(8)
+        agent.noise.zero_()
+        u = agent._draw(0, H, cts, off, reuse, ev)
+        assert u == nz.u
+        assert torch.equal(agent.noise[:S], want)
+        # both generators are left where the reference's draws leave them
+        assert torch.equal(torch.randn(4, device="cuda"), after_ref[0])
+        assert np.random.random_sample() == after_ref[1]
+
+
+@pytest.mark.gpu
+def test_gpu_icem_device_rng():
+    """rng 'device' (coloured noise and the pick's uniform drawn on the device): seeded runs repeat exactly and
+    the plan is well formed (the distribution is the reference's; the numbers are not numpy's)."""
+    from tdmpc_amd.icem import TdICEM
+    cfg = icem_cfg()
+    sd = synthetic_state_dict(cfg, 31, enc_norm=True)
+    outs = []
+    for _ in range(2):
+        agent = TdICEM(cfg, rng="device")
+        agent.model.load_state_dict(sd)
+        agent.std = 0.05
+        torch.manual_seed(3)
+        acts = [agent.plan(G[f"c{ci}_obs"], eval_mode=ev, step=step, t0=t0)[0].cpu()
+                for ci, (step, t0, ev) in enumerate(CALLS)]
+        outs.append(torch.stack(acts))
+    assert torch.equal(outs[0], outs[1])
+    assert torch.isfinite(outs[0]).all()
+    ev_calls = [ci for ci, (_, _, ev) in enumerate(CALLS) if ev]
+    assert ev_calls and outs[0][ev_calls].abs().max() <= 1   # no exploration noise: an elite's action
