@@ -70,12 +70,15 @@ typedef struct tdmpc_plan_params {
     float std_floor;       /* self.std: lower clamp of the CEM std (tdmpc.py:148) */
     float discount_pow[17];/* float32(discount**t) for t = 0..H, the running Python-float product */
     int32_t path;          /* kernel path: 0 = auto by row count, 1 = layered GEMMs only, 2 = row-block chain
-                              kernels wherever the shape allows (results agree within the fp32 tolerance) */
+                              kernels wherever the shape allows (row block by launch size), 3 / 4 = chain
+                              kernels on 32- / 16-row blocks only (results agree within the fp32 tolerance) */
 } tdmpc_plan_params;
 
 #define TDMPC_PATH_AUTO 0
 #define TDMPC_PATH_LAYERED 1
 #define TDMPC_PATH_CHAIN 2
+#define TDMPC_PATH_CHAIN32 3
+#define TDMPC_PATH_CHAIN16 4
 
 /* Byte sizes the caller must allocate (all 256-byte aligned). */
 typedef struct tdmpc_sizes {

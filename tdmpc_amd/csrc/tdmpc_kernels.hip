@@ -844,7 +844,9 @@ struct ChainProb {
 struct ChainArgs {
     ChainProb p[2];
     int rows, M, K1, q1;                 // logical rows; hidden width; first-layer K and its X quad offset
-    int hfl;                             // floats of the LDS activation block (max(K1, M) * 32)
+    int rb;                              // row block: 32 (chain_kernel) or 16 (chain16_kernel)
+    int nw;                              // waves per workgroup of chain_kernel: 8 or 16
+    int hfl;                             // floats of the LDS activation block (max(K1, M) * rb, K1 to 16)
     RowMap amap;                         // logical row -> X row (input and output)
     const float* X; long x_ts;           // X_t panel (input)
     // last layer of dynamics / pi: panel [n3][M] + bias -> Xo quads [out_q0, out_q0 + nstore/4)
@@ -917,8 +919,8 @@ DEVI void ring_run(floatx16 (&acc)[TN], float4 (&wr)[D][TN], const float* sA, co
 }
 
 // Row mean and 1/sqrt(var + 1e-5) over the M columns of the block's rows (biased variance, two passes),
-// from each lane's TN*16 values of row r: per-wave partials through red0 / red1 ([8][32] each).
-template <int TN>
+// from each lane's TN*16 values of row r: per-wave partials through red0 / red1 ([NW][32] each).
+template <int TN, int NW>
 DEVI void chain_row_moments(const float (&v)[TN * 16], float* red0, float* red1, int wave, int r, int h, int M,
                             float& mean, float& rstd) {
     float s = 0.f;
@@ -929,7 +931,7 @@ DEVI void chain_row_moments(const float (&v)[TN * 16], float* red0, float* red1,
     __syncthreads();
     float tot = 0.f;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) tot += red0[w * 32 + r];
+    for (int w = 0; w < NW; ++w) tot += red0[w * 32 + r];
     mean = tot / (float)M;
     float m2 = 0.f;
 #pragma unroll
@@ -942,7 +944,7 @@ DEVI void chain_row_moments(const float (&v)[TN * 16], float* red0, float* red1,
     __syncthreads();
     float tot2 = 0.f;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) tot2 += red1[w * 32 + r];
+    for (int w = 0; w < NW; ++w) tot2 += red1[w * 32 + r];
     rstd = 1.0f / sqrtf(fmaxf(tot2 / (float)M, 0.f) + 1e-5f);
 }
 
@@ -996,8 +998,10 @@ DEVI void chain_store_lds(float* sH, const float (&v)[TN * 16], int cw0, int r, 
         }
 }
 
-template <int MODE, int TN, int D = 4, int D3 = 8>
-__global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
+// NW = 8 or 16 waves per workgroup (16: 4 waves per SIMD on one 32-row block, TN = M / 512).
+template <int MODE, int TN, int NW = 8, int D = 4, int D3 = 8>
+__global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
+    constexpr int NTH = 64 * NW;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     const int pb = blockIdx.y;
@@ -1005,9 +1009,9 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
     const int M = a.M;
     const int m0 = blockIdx.x * 32;
     float* sH = smem;                       // activation block [max(K1, M)/4][32][4]
-    float* red0 = smem + a.hfl;             // [8][32]
-    float* red1 = red0 + 256;               // [8][32]
-    float* sp = red1 + 256;                 // parameter vectors (chain_param_floats)
+    float* red0 = smem + a.hfl;             // [NW][32]
+    float* red1 = red0 + 32 * NW;           // [NW][32]
+    float* sp = red1 + 32 * NW;                // parameter vectors (chain_param_floats)
     float* sb1 = sp;
     float* sb2 = sp + M;
     float* sw3 = sp + 2 * M;                // reward / Q head weights
@@ -1029,13 +1033,13 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
     // consecutive lanes = 32 rows of one quad) and the parameter vectors
     float4 wr[D][TN];
     ring_fill<TN, D>(wr, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3);
-    for (int i = tid; i < (a.K1 >> 2) * 32; i += 512) {
+    for (int i = tid; i < (a.K1 >> 2) * 32; i += NTH) {
         const int row = i & 31, q = i >> 5;
         const int lm = m0 + row;
         const int xr = map_row(a.amap, lm < a.rows ? lm : 0);
         ((float4*)sH)[i] = *(const float4*)(a.X + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.q1 + q) * 128 + (xr & 31) * 4);
     }
-    for (int i = tid; i < M / 4; i += 512) {
+    for (int i = tid; i < M / 4; i += NTH) {
         ((float4*)sb1)[i] = ((const float4*)P.b1)[i];
         ((float4*)sb2)[i] = ((const float4*)P.b2)[i];
         if (head_dot) ((float4*)sw3)[i] = ((const float4*)P.w3v)[i];
@@ -1047,7 +1051,7 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
         }
     }
     if (!head_dot)
-        for (int i = tid; i < a.n3 / 4; i += 512) ((float4*)sb3)[i] = ((const float4*)a.b3)[i];
+        for (int i = tid; i < a.n3 / 4; i += NTH) ((float4*)sb3)[i] = ((const float4*)a.b3)[i];
     // early operands of the last stage: the running return (reward WG) / the policy noise (pi)
     float g_old = 0.f;
     if (MODE == CH_STEP && pb == 1 && tid < 32 && !a.first && m0 + tid < a.rows)
@@ -1080,7 +1084,7 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
         chain_bias<TN>(v, acc, sb1, cw0, h);
         if (MODE == CH_Q) {
             float mean, rs;
-            chain_row_moments<TN>(v, red0, red1, wave, r, h, M, mean, rs);
+            chain_row_moments<TN, NW>(v, red0, red1, wave, r, h, M, mean, rs);
             chain_ln<TN>(v, rs, -rs * mean, sg1, sbe1, cw0, h);
 #pragma unroll
             for (int i = 0; i < TN * 16; ++i) v[i] = tanh_f(v[i]);
@@ -1104,9 +1108,9 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
 #ifdef TDMPC_STAMPS
     STAMP(3);
 #endif
-    // layer-3 work items (32-column block, K part): narrow heads split K over all 8 waves (2 per SIMD)
+    // layer-3 work items (32-column block, K part): narrow heads split K over all NW waves
     const int nb3 = a.n3 >> 5;
-    const int ks = nb3 >= 8 ? 1 : 8 / nb3;
+    const int ks = nb3 >= NW ? 1 : NW / nb3;
     const int items = nb3 * ks;
     const int gper = (M >> 3) / ks;
     float4 w3r[D3][1];
@@ -1119,7 +1123,7 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
         // reward / Q last layer Linear(M -> 1) on the row: per-wave partial dots, then one lane per row
         if (MODE == CH_Q) {
             float mean, rs;
-            chain_row_moments<TN>(v, red0, red1, wave, r, h, M, mean, rs);
+            chain_row_moments<TN, NW>(v, red0, red1, wave, r, h, M, mean, rs);
             chain_ln<TN>(v, rs, -rs * mean, sg2, sbe2, cw0, h);
         }
         float s = 0.f;
@@ -1140,7 +1144,7 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
                 const int xr = map_row(a.amap, lm);
                 float tot = 0.f;
 #pragma unroll
-                for (int w = 0; w < 8; ++w) tot += red0[w * 32 + tid];
+                for (int w = 0; w < NW; ++w) tot += red0[w * 32 + tid];
                 const float o = tot + P.b3v[0];
                 if (MODE == CH_Q) {
                     a.q[(size_t)pb * a.q_ld + xr] = o;
@@ -1174,8 +1178,8 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
         const int blk = wave / ks, kp = wave % ks;
         ring_run<1, D3>(a3a, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
     }
-    if (wave + 8 < items) {
-        const int blk = (wave + 8) / ks, kp = (wave + 8) % ks;
+    if (wave + NW < items) {
+        const int blk = (wave + NW) / ks, kp = (wave + NW) % ks;
         ring_fill<1, D3>(w3r, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper);
         ring_run<1, D3>(a3b, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
     }
@@ -1185,12 +1189,12 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
         if (wave < items)
             *(float4*)(sH + (size_t)wave * 1024 + ((2 * q + h) * 32 + r) * 4) =
                 make_float4(a3a[0][4 * q], a3a[0][4 * q + 1], a3a[0][4 * q + 2], a3a[0][4 * q + 3]);
-        if (wave + 8 < items)
-            *(float4*)(sH + (size_t)(wave + 8) * 1024 + ((2 * q + h) * 32 + r) * 4) =
+        if (wave + NW < items)
+            *(float4*)(sH + (size_t)(wave + NW) * 1024 + ((2 * q + h) * 32 + r) * 4) =
                 make_float4(a3b[0][4 * q], a3b[0][4 * q + 1], a3b[0][4 * q + 2], a3b[0][4 * q + 3]);
     }
     __syncthreads();
-    for (int i = tid; i < (a.nstore >> 2) * 32; i += 512) {
+    for (int i = tid; i < (a.nstore >> 2) * 32; i += NTH) {
         const int row = i & 31, cq = i >> 5;
         const int lm = m0 + row;
         if (lm >= a.rows) continue;
@@ -1233,6 +1237,344 @@ __global__ void __launch_bounds__(512) chain_kernel(const ChainArgs a) {
     STAMP(4);
     STAMP_RECORD();
 #endif
+}
+
+// ------------------------------------------------------------------------------------------------ chain16
+// Row-block chain kernel on 16-row blocks (v_mfma_f32_16x16x4_f32), the same three modes as chain_kernel.
+// Why a second block size: a 32-row chain launch of the B = 8 bench shape is exactly one workgroup per CU
+// (2 waves per SIMD), which leaves every L2 fetch and layer epilogue exposed, and its 384-workgroup launches
+// (6144 rows) take two rounds on half the chip. Halving the row block doubles the workgroups: two co-resident
+// per CU (4 waves per SIMD, <= 128 VGPRs each), a dynamics and a reward workgroup side by side, so one's
+// epilogue hides under the other's MFMAs. The cost is twice the L2 -> CU weight traffic per FLOP (each 1 KiB
+// weight fragment now serves 16 rows): 32 B/clk/CU at the full MFMA rate, within the L1/L2 budget.
+//
+// Operand maps (swapped like chain_kernel: weights are the A operand, activations B, so the accumulator of
+// lane l holds batch row m = l & 15 and output features 4 (l >> 4) + 0..3 of its 16-column tile):
+//   k group g = 16 k values; lane l (m = l & 15, h4 = l >> 4) holds quad 4g + h4 of its row, element kk
+//   feeding MFMA kk of the group (k = 16g + 4 h4 + kk, the same permutation for both operands).
+//   weights: the 32-row panel [n/32][K/4][32][4] as is; tile of columns [n0, n0 + 16) at
+//            (n0 >> 5) * K * 32 + (n0 & 31) * 4 + (l & 15) * 4 + (4g + h4) * 128
+//   activations in LDS: [K/4][16][4]; lane l of group g at g * 256 + l * 4 (one conflict-free 1 KiB read).
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// Tile j of a wave's NT tiles: columns n0 + 16 j with n0 a multiple of 32, i.e. (j >> 1) blocks of the
+// 32-row panel (bs floats each) plus 64 floats for an odd tile. Wp is already offset by the lane.
+// A K that is not a multiple of 16 ends in a half group: its lanes h4 = 2, 3 clamp their quad to the last
+// real one (qmax) and meet zero-filled activation quads, so they add exactly 0.
+DEVI size_t wq16(int g, int gl, int h4, int qmax) { return (size_t)min(4 * min(g, gl) + h4, qmax) * 128; }
+
+template <int NT, int D>
+DEVI void ring16_fill(float4 (&wr)[D][NT], const float* Wp, long bs, int g0, int g1, int h4, int qmax) {
+    const int gl = g1 - 1;
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+            wr[d][j] = *(const float4*)(Wp + (j >> 1) * bs + (j & 1) * 64 + wq16(g0 + d, gl, h4, qmax));
+}
+
+template <int NT, int D>
+DEVI void ring16_run(floatx4 (&acc)[NT], float4 (&wr)[D][NT], const float* sA, const float* Wp, long bs, int g0,
+                     int g1, int lane, int qmax) {
+    const int gl = g1 - 1, h4 = lane >> 4;
+    const float* ap = sA + lane * 4;
+    float4 an = *(const float4*)(ap + (size_t)g0 * 256);
+    int gb = g0;
+    for (; gb + D <= g1; gb += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int g = gb + d;
+            const float4 av = an;
+            an = *(const float4*)(ap + (size_t)min(g + 1, gl) * 256);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(wr[d][j], kk), f4c(av, kk), acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+                wr[d][j] = *(const float4*)(Wp + (j >> 1) * bs + (j & 1) * 64 + wq16(g + D, gl, h4, qmax));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) {
+        if (gb + d < g1) {
+            const float4 av = an;
+            an = *(const float4*)(ap + (size_t)min(gb + d + 1, gl) * 256);
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(wr[d][j], kk), f4c(av, kk), acc[j], 0, 0, 0);
+        }
+    }
+}
+
+// sum over the 4 lanes of row m (h4 = 0..3), then over the 8 waves through red ([8][16])
+DEVI float row16_sum(float s, float* red, int wave, int lane) {
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    if (lane < 16) red[wave * 16 + lane] = s;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) tot += red[w * 16 + (lane & 15)];
+    return tot;
+}
+
+template <int NT>
+DEVI void chain16_row_moments(const float (&v)[NT * 4], float* red0, float* red1, int wave, int lane, int M,
+                              float& mean, float& rstd) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT * 4; ++i) s += v[i];
+    mean = row16_sum(s, red0, wave, lane) / (float)M;
+    float m2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT * 4; ++i) {
+        const float d = v[i] - mean;
+        m2 += d * d;
+    }
+    rstd = 1.0f / sqrtf(fmaxf(row16_sum(m2, red1, wave, lane) / (float)M, 0.f) + 1e-5f);
+}
+
+// features of tile j held by this lane: f0 + 16 j + 0..3 with f0 = 16 NT wave + 4 h4
+template <int NT>
+DEVI void chain16_bias(float (&v)[NT * 4], const floatx4 (&acc)[NT], const float* sb, int f0) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const float4 bb = *(const float4*)(sb + f0 + 16 * j);
+        v[4 * j + 0] = acc[j][0] + bb.x;
+        v[4 * j + 1] = acc[j][1] + bb.y;
+        v[4 * j + 2] = acc[j][2] + bb.z;
+        v[4 * j + 3] = acc[j][3] + bb.w;
+    }
+}
+
+template <int NT>
+DEVI void chain16_ln(float (&v)[NT * 4], float rs, float sh, const float* sg, const float* sbe, int f0) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const float4 gg = *(const float4*)(sg + f0 + 16 * j), bb = *(const float4*)(sbe + f0 + 16 * j);
+        float* x = v + 4 * j;
+        x[0] = fadd(fmul(fadd(fmul(x[0], rs), sh), gg.x), bb.x);
+        x[1] = fadd(fmul(fadd(fmul(x[1], rs), sh), gg.y), bb.y);
+        x[2] = fadd(fmul(fadd(fmul(x[2], rs), sh), gg.z), bb.z);
+        x[3] = fadd(fmul(fadd(fmul(x[3], rs), sh), gg.w), bb.w);
+    }
+}
+
+// the lane's quads into the [M/4][16][4] activation block: quad f0/4 + 4 j, row m (64 lanes = 1 KiB)
+template <int NT>
+DEVI void chain16_store_lds(float* sH, const float (&v)[NT * 4], int f0, int m) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+        *(float4*)(sH + ((f0 / 4 + 4 * j) * 16 + m) * 4) = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+}
+
+template <int MODE, int NT, int D = 4, int D3 = 4>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) chain16_kernel(const ChainArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, h4 = lane >> 4;
+    const int pb = blockIdx.y;
+    const ChainProb& P = a.p[pb];
+    const int M = a.M;
+    const int m0 = blockIdx.x * 16;
+    float* sH = smem;                       // activation block [max(K1, M)/4][16][4]
+    float* red0 = smem + a.hfl;             // [8][16]
+    float* red1 = red0 + 128;               // [8][16]
+    float* sp = red1 + 128;                 // parameter vectors (chain_param_floats)
+    float* sb1 = sp;
+    float* sb2 = sp + M;
+    float* sw3 = sp + 2 * M;
+    float* sb3 = sp + 3 * M;
+    float* sg1 = sp + 3 * M;
+    float* sbe1 = sp + 4 * M;
+    float* sg2 = sp + 5 * M;
+    float* sbe2 = sp + 6 * M;
+    const int lo = m * 4;                   // lane offset inside a weight-panel quad (quad: wq16)
+    const int q1max = (a.K1 >> 2) - 1, qMmax = (M >> 2) - 1;
+    const int g1n = (a.K1 + 15) >> 4;       // 16-k groups of layer 1 (the last may be half)
+    const int f0 = 16 * NT * wave + 4 * h4; // first output feature of this lane in the M-wide layers
+    const long wblk = (long)(NT / 2) * wave;  // first 32-row panel block of this wave
+    const bool head_dot = MODE == CH_Q || (MODE == CH_STEP && pb == 1);
+
+    float4 wr[D][NT];
+    ring16_fill<NT, D>(wr, P.W1 + wblk * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1n, h4, q1max);
+    for (int i = tid; i < g1n * 4 * 16; i += 512) {
+        const int row = i & 15, q = i >> 4;
+        const int lm = m0 + row;
+        const int xr = map_row(a.amap, lm < a.rows ? lm : 0);
+        ((float4*)sH)[i] = q <= q1max ? *(const float4*)(a.X + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.q1 + q) * 128 + (xr & 31) * 4)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    for (int i = tid; i < M / 4; i += 512) {
+        ((float4*)sb1)[i] = ((const float4*)P.b1)[i];
+        ((float4*)sb2)[i] = ((const float4*)P.b2)[i];
+        if (head_dot) ((float4*)sw3)[i] = ((const float4*)P.w3v)[i];
+        if (MODE == CH_Q) {
+            ((float4*)sg1)[i] = ((const float4*)P.g1)[i];
+            ((float4*)sbe1)[i] = ((const float4*)P.be1)[i];
+            ((float4*)sg2)[i] = ((const float4*)P.g2)[i];
+            ((float4*)sbe2)[i] = ((const float4*)P.be2)[i];
+        }
+    }
+    if (!head_dot)
+        for (int i = tid; i < a.n3 / 4; i += 512) ((float4*)sb3)[i] = ((const float4*)a.b3)[i];
+    float g_old = 0.f;
+    if (MODE == CH_STEP && pb == 1 && tid < 16 && !a.first && m0 + tid < a.rows)
+        g_old = a.G[map_row(a.amap, m0 + tid)];
+    float eps4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (MODE == CH_PI && tid < (a.nstore >> 2) * 16 && m0 + (tid & 15) < a.rows) {
+        const int lm = m0 + (tid & 15), c = 4 * (tid >> 4);
+        const int e = lm / a.eps_G, rr = lm % a.eps_G;
+        const float* ep = a.eps + (size_t)e * a.eps_env + a.eps_off + (size_t)rr * a.A;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) eps4[k] = c + k < a.nvalid ? ep[c + k] : 0.f;
+    }
+    __syncthreads();
+
+    // ---- layer 1
+    floatx4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    ring16_run<NT, D>(acc, wr, sH, P.W1 + wblk * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1n, lane, q1max);
+    ring16_fill<NT, D>(wr, P.W2 + wblk * M * 32 + lo, (long)M * 32, 0, M >> 4, h4, qMmax);
+    __syncthreads();
+    {
+        float v[NT * 4];
+        chain16_bias<NT>(v, acc, sb1, f0);
+        if (MODE == CH_Q) {
+            float mean, rs;
+            chain16_row_moments<NT>(v, red0, red1, wave, lane, M, mean, rs);
+            chain16_ln<NT>(v, rs, -rs * mean, sg1, sbe1, f0);
+#pragma unroll
+            for (int i = 0; i < NT * 4; ++i) v[i] = tanh_f(v[i]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NT * 4; ++i) v[i] = elu_f(v[i]);
+        }
+        chain16_store_lds<NT>(sH, v, f0, m);
+    }
+    __syncthreads();
+
+    // ---- layer 2
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    ring16_run<NT, D>(acc, wr, sH, P.W2 + wblk * M * 32 + lo, (long)M * 32, 0, M >> 4, lane, qMmax);
+
+    // layer-3 items (16-column tile, K part): up to 4 per wave (items <= 32)
+    const int nb3 = a.n3 >> 4;
+    const int ks = nb3 >= 8 ? 1 : 8 / nb3;
+    const int items = nb3 * ks;
+    const int gper = (M >> 4) / ks;
+    float4 w3r[D3][1];
+    auto w3p = [&](int it) { const int t = it / ks; return a.W3 + (size_t)(t >> 1) * M * 32 + (t & 1) * 64 + lo; };
+    if (!head_dot && wave < items)
+        ring16_fill<1, D3>(w3r, w3p(wave), (long)M * 32, (wave % ks) * gper, (wave % ks + 1) * gper, h4, qMmax);
+    float v[NT * 4];
+    chain16_bias<NT>(v, acc, sb2, f0);
+    if (head_dot) {
+        if (MODE == CH_Q) {
+            float mean, rs;
+            chain16_row_moments<NT>(v, red0, red1, wave, lane, M, mean, rs);
+            chain16_ln<NT>(v, rs, -rs * mean, sg2, sbe2, f0);
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const float4 w4 = *(const float4*)(sw3 + f0 + 16 * j);
+            const float* x = v + 4 * j;
+            s += (elu_f(x[0]) * w4.x + elu_f(x[1]) * w4.y) + (elu_f(x[2]) * w4.z + elu_f(x[3]) * w4.w);
+        }
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        if (lane < 16) red0[wave * 16 + lane] = s;
+        __syncthreads();
+        if (tid < 16) {
+            const int lm = m0 + tid;
+            if (lm < a.rows) {
+                const int xr = map_row(a.amap, lm);
+                float tot = 0.f;
+#pragma unroll
+                for (int w = 0; w < 8; ++w) tot += red0[w * 16 + tid];
+                const float o = tot + P.b3v[0];
+                if (MODE == CH_Q) {
+                    a.q[(size_t)pb * a.q_ld + xr] = o;
+                } else {
+                    const float dr = fmul(a.disc, o);
+                    a.G[xr] = a.first ? dr : fadd(g_old, dr);
+                    if (a.last) a.rlast[xr] = o;
+                }
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < NT * 4; ++i) v[i] = elu_f(v[i]);
+    __syncthreads();
+    chain16_store_lds<NT>(sH, v, f0, m);
+    __syncthreads();
+
+    // ---- layer 3: [16 x M] . W3^T -> [16 x n3]; partial tiles meet in the activation block after the reads
+    floatx4 a3[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a3[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int it = wave + 8 * u;
+        if (it < items) {
+            floatx4 t1[1] = {a3[u]};
+            if (u > 0) ring16_fill<1, D3>(w3r, w3p(it), (long)M * 32, (it % ks) * gper, (it % ks + 1) * gper, h4, qMmax);
+            ring16_run<1, D3>(t1, w3r, sH, w3p(it), (long)M * 32, (it % ks) * gper, (it % ks + 1) * gper, lane, qMmax);
+            a3[u] = t1[0];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int it = wave + 8 * u;
+        if (it < items) *(float4*)(sH + (size_t)it * 256 + lane * 4) = make_float4(a3[u][0], a3[u][1], a3[u][2], a3[u][3]);
+    }
+    __syncthreads();
+    for (int i = tid; i < (a.nstore >> 2) * 16; i += 512) {
+        const int row = i & 15, cq = i >> 4;
+        const int lm = m0 + row;
+        if (lm >= a.rows) continue;
+        const int t = cq >> 2, qi = cq & 3;
+        float4 s = *(const float4*)(sH + (size_t)(t * ks) * 256 + (qi * 16 + row) * 4);
+        for (int kp = 1; kp < ks; ++kp) {
+            const float4 u = *(const float4*)(sH + (size_t)(t * ks + kp) * 256 + (qi * 16 + row) * 4);
+            s.x += u.x; s.y += u.y; s.z += u.z; s.w += u.w;
+        }
+        const int c = 4 * cq;
+        const float4 bb = *(const float4*)(sb3 + c);
+        float o[4] = {s.x + bb.x, s.y + bb.y, s.z + bb.z, s.w + bb.w};
+        const int xr = map_row(a.amap, lm);
+        if (MODE == CH_PI) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float x = 0.f;
+                if (c + k < a.nvalid) {
+                    const float muv = tanhf(o[k]);
+                    x = muv;
+                    if (a.min_std > 0.f) {
+                        const float ee = tclamp(fmul(eps4[k], a.min_std), -0.3f, 0.3f);
+                        x = tclamp(fadd(muv, ee), a.lo, a.hi);
+                    }
+                }
+                o[k] = x;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (c + k >= a.nvalid) o[k] = 0.f;
+        }
+        *(float4*)(a.Xo + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.out_q0 + cq) * 128 + (xr & 31) * 4) =
+            make_float4(o[0], o[1], o[2], o[3]);
+    }
 }
 
 // estimate_value's terminal combination (tdmpc.py:91-92): G + gamma^H min(Q1, Q2), nan_to_num.
@@ -1879,6 +2221,14 @@ int init_attrs() {
     CHAIN_ATTR(CH_PI, 1) CHAIN_ATTR(CH_PI, 2) CHAIN_ATTR(CH_PI, 4)
     CHAIN_ATTR(CH_Q, 1) CHAIN_ATTR(CH_Q, 2) CHAIN_ATTR(CH_Q, 4)
 #undef CHAIN_ATTR
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+#define CHAIN16_ATTR(MODE, NT) \
+    HIPCHK(hipFuncSetAttribute((const void*)chain16_kernel<MODE, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CHAIN16_ATTR(CH_STEP, 2) CHAIN16_ATTR(CH_STEP, 4) CHAIN16_ATTR(CH_PI, 2) CHAIN16_ATTR(CH_PI, 4)
+    CHAIN16_ATTR(CH_Q, 2) CHAIN16_ATTR(CH_Q, 4)
+#undef CHAIN16_ATTR
     if (rc) return TDMPC_E_HIP;
     done = 1;
     return 0;
@@ -2066,16 +2416,17 @@ int launch_lin(const LinArgs& a, int nprob, int nmax, int wide64, int pro, hipSt
     return TDMPC_E_DIMS;
 }
 
-// ---- chain path (chain_kernel): on the auto path used for launches of at least chain_wgs() workgroups
-// (32-row blocks x problems; TDMPC_CHAIN_WGS, default 128, 0 disables): one chain workgroup takes ~50 us
-// whatever the row count, so with fewer workgroups than about half the CUs the layered GEMMs, whose K-split
-// tiles spread the same rows over more CUs, finish first (tools/mb/mb_linear.hip "chain" on MI355X:
-// 2048 pi rows 45 us chain vs 37 us layered; 4096 x 2 step rows 55 vs 69; 512 x 2 step rows 54 vs 23).
+// ---- chain path (chain_kernel / chain16_kernel): on the auto path used for launches of at least chain_wgs()
+// 32-row-block equivalents x problems (TDMPC_CHAIN_WGS, default 64, 0 disables). Narrow launches run on 16-row
+// blocks (chain_rb), so from 64 32-row blocks on they still spread over 128+ CUs; below that the layered
+// GEMMs, whose K-split tiles spread the same rows over more CUs, finish first. Measured on MI355X (humanoid
+// plan, tools/gpu38.sh): threshold 64 vs 128: B = 2 envs 1.65 vs 1.87 ms, B = 4 1.88 vs 1.98 ms; 32 loses
+// at one env (1.56 vs 1.38 ms).
 int chain_wgs() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("TDMPC_CHAIN_WGS");
-        v = e ? atoi(e) : 128;
+        v = e ? atoi(e) : 64;
     }
     return v;
 }
@@ -2096,6 +2447,20 @@ bool chain_shape_ok(const Layout& w) {
     return (hfl + 512 + pmax) * 4 <= 160 * 1024;
 }
 
+// Shapes chain16_kernel supports: M = 128 * NT (NT = 2, 4); last-layer items (16-column tile, K part) <= 32.
+bool chain16_shape_ok(const Layout& w) {
+    const int M = w.M;
+    if (M != 256 && M != 512) return false;
+    const size_t hfl = (size_t)std::max((int)rup(w.Kx, 16), M) * 16;
+    for (int n3 : {w.Lr, w.Ar}) {
+        const int nb3 = n3 / 16, ks = nb3 >= 8 ? 1 : 8 / nb3, items = nb3 * ks;
+        if (items > 32 || (size_t)items * 256 > hfl || (M / 16) % ks) return false;
+    }
+    if (w.Ap / 4 * 16 > 512) return false;
+    const int pmax = std::max(chain_param_floats(CH_Q, M, 0), chain_param_floats(CH_STEP, M, std::max(w.Lr, w.Ar)));
+    return (hfl + 256 + pmax) * 4 <= 64 * 1024;
+}
+
 // Algorithmic MACs per row of a chain launch (with the real widths, not the padded ones):
 // CH_STEP d + R = 2 (K1 M + M^2) + M L + M, CH_PI K1 M + M^2 + M A, CH_Q 2 (K1 M + M^2 + M).
 double chain_macs_per_row(int mode, const ChainArgs& a, int nprob) {
@@ -2107,16 +2472,37 @@ double chain_macs_per_row(int mode, const ChainArgs& a, int nprob) {
 
 int launch_chain(int mode, const ChainArgs& a, int nprob, hipStream_t s) {
     if (a.rows <= 0) return 0;
-    const size_t lds = ((size_t)a.hfl + 512 + chain_param_floats(mode, a.M, a.n3)) * 4;
-    const dim3 grid((a.rows + 31) / 32, nprob), block(512);
-    const int tn = a.M / 256;
+    const int nw = a.rb == 16 ? 8 : a.nw;
+    const size_t lds = ((size_t)a.hfl + (a.rb == 16 ? 256 : 64 * nw) + chain_param_floats(mode, a.M, a.n3)) * 4;
+    const dim3 grid((a.rows + a.rb - 1) / a.rb, nprob), block(64 * nw);
+    const int tn = a.M / (32 * nw);
     // diagnostic timer (tdmpc_profile_begin cfg 4 + mode): HIP events around matching chain launches
     Profiler& pf = g_prof;
     const bool prof = pf.armed && pf.cfg == 4 + mode && pf.n + 2 <= pf.cap && (pf.rows == 0 || a.rows == pf.rows);
     if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], s));
+    if (a.rb == 16) {
+        const int nt = a.M / 128;
+#define CHAIN16_LAUNCH(MODE, NT) \
+        if (mode == MODE && nt == NT) { \
+            hipLaunchKernelGGL((chain16_kernel<MODE, NT>), grid, block, lds, s, a); \
+            HIPCHK(hipGetLastError()); \
+            if (prof) { \
+                HIPCHK(hipEventRecord(pf.ev[pf.n + 1], s)); \
+                pf.n += 2; \
+                pf.flops += 2.0 * a.rows * chain_macs_per_row(mode, a, nprob); \
+            } \
+            return 0; \
+        }
+        CHAIN16_LAUNCH(CH_STEP, 2) CHAIN16_LAUNCH(CH_STEP, 4) CHAIN16_LAUNCH(CH_PI, 2) CHAIN16_LAUNCH(CH_PI, 4)
+        CHAIN16_LAUNCH(CH_Q, 2) CHAIN16_LAUNCH(CH_Q, 4)
+#undef CHAIN16_LAUNCH
+        snprintf(g_err, sizeof g_err, "chain16: unsupported mode %d / M %d", mode, a.M);
+        return TDMPC_E_DIMS;
+    }
 #define CHAIN_LAUNCH(MODE, TN) \
     if (mode == MODE && tn == TN) { \
-        hipLaunchKernelGGL((chain_kernel<MODE, TN>), grid, block, lds, s, a); \
+        if (nw == 16 && TN == 1) hipLaunchKernelGGL((chain_kernel<MODE, 1, 16>), grid, block, lds, s, a); \
+        else hipLaunchKernelGGL((chain_kernel<MODE, TN>), grid, block, lds, s, a); \
         HIPCHK(hipGetLastError()); \
         if (prof) { \
             HIPCHK(hipEventRecord(pf.ev[pf.n + 1], s)); \
@@ -2152,14 +2538,55 @@ struct Ctx {
 float* Xt(const Ctx& c, int t) { return c.k.X + (size_t)t * c.k.x_stride; }
 bool use_chain(const Ctx& c, int rows, int nprob) {
     if (c.path == TDMPC_PATH_LAYERED || !chain_shape_ok(c.w)) return false;
-    return c.path == TDMPC_PATH_CHAIN || (chain_wgs() > 0 && (rows + 31) / 32 * nprob >= chain_wgs());
+    return c.path != TDMPC_PATH_AUTO || (chain_wgs() > 0 && (rows + 31) / 32 * nprob >= chain_wgs());
 }
 
-ChainArgs chain0(const Ctx& c, int rows, RowMap map, int t, int K1, int q1) {
+// 16-wave 32-row chain workgroups: M = 512 (TN = 1), last-layer items <= 32 within the activation block.
+bool chain_nw16_ok(const Layout& w) {
+    if (w.M != 512) return false;
+    const size_t hfl = (size_t)std::max((int)rup(w.Kx, 16), w.M) * 32;
+    for (int n3 : {w.Lr, w.Ar}) {
+        const int nb3 = n3 / 32, ks = nb3 >= 16 ? 1 : 16 / nb3, items = nb3 * ks;
+        if (items > 32 || (size_t)items * 1024 > hfl || (w.M / 8) % ks) return false;
+    }
+    const int pmax = std::max(chain_param_floats(CH_Q, w.M, 0), chain_param_floats(CH_STEP, w.M, std::max(w.Lr, w.Ar)));
+    return (hfl + 1024 + pmax) * 4 <= 160 * 1024;
+}
+
+// Waves per 32-row chain workgroup (TDMPC_CHAIN_NW: 8 or 16; 16 needs M = 512).
+int chain_nw() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("TDMPC_CHAIN_NW");
+        v = e ? atoi(e) : 8;
+    }
+    return v;
+}
+
+// Row block of a chain launch. Auto: 32-row blocks once they occupy more than half the CUs (their weight
+// fragments serve twice the rows; measured on MI355X, humanoid: 57.5 vs 61 us for the 256-workgroup B = 8
+// step, 99 vs 114 us at B = 16, and 16-row blocks lose on the 192-workgroup pi launch too), else 16-row
+// blocks, which double the workgroups of a narrow launch (B = 4 step: 36.7 us vs 56 us on 128 32-row
+// workgroups). TDMPC_CHAIN_RB forces 16 or 32 for experiments.
+int chain_rb(const Ctx& c, int rows, int nprob) {
+    if (!chain16_shape_ok(c.w) || c.path == TDMPC_PATH_CHAIN32) return 32;
+    if (c.path == TDMPC_PATH_CHAIN16) return 16;
+    static int forced = -1;
+    if (forced < 0) {
+        const char* e = getenv("TDMPC_CHAIN_RB");
+        forced = e ? atoi(e) : 0;
+    }
+    if (forced == 16 || forced == 32) return forced;
+    return (rows + 31) / 32 * nprob > num_cus() / 2 ? 32 : 16;
+}
+
+ChainArgs chain0(const Ctx& c, int rows, RowMap map, int t, int K1, int q1, int nprob) {
     ChainArgs a;
     memset(&a, 0, sizeof a);
     a.rows = rows; a.M = c.M; a.K1 = K1; a.q1 = q1; a.amap = map;
-    a.hfl = std::max(c.Kx, c.M) * 32;
+    a.rb = chain_rb(c, rows, nprob);
+    a.nw = a.rb == 32 && chain_nw() == 16 && chain_nw16_ok(c.w) ? 16 : 8;
+    a.hfl = std::max((int)rup(c.Kx, 16), c.M) * a.rb;
     a.X = Xt(c, t); a.x_ts = (long)c.Kx * 32;
     return a;
 }
@@ -2176,7 +2603,7 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
     const int M = c.M;
     int rc;
     if (use_chain(c, rows, 2)) {
-        ChainArgs a = chain0(c, rows, map, t, c.Kx, 0);
+        ChainArgs a = chain0(c, rows, map, t, c.Kx, 0, 2);
         ChainProb& d = a.p[0];
         d.W1 = c.pw + w.w1x; d.b1 = c.pw + w.b1x; d.W2 = c.pw + w.w2d; d.b2 = c.pw + w.b2d;
         ChainProb& r = a.p[1];
@@ -2227,7 +2654,7 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
     const int M = c.M;
     int rc;
     if (use_chain(c, rows, 1)) {
-        ChainArgs a = chain0(c, rows, map, t, w.Lp, w.Ap / 4);
+        ChainArgs a = chain0(c, rows, map, t, w.Lp, w.Ap / 4, 1);
         ChainProb& p = a.p[0];
         p.W1 = c.pw + w.wp1; p.b1 = c.pw + w.bp1; p.W2 = c.pw + w.wp2; p.b2 = c.pw + w.bp2;
         a.W3 = c.pw + w.wp3; a.b3 = c.pw + w.bp3; a.n3 = w.Ar; a.nvalid = w.A; a.nstore = w.Ap;
@@ -2291,7 +2718,7 @@ int prep(const Ctx& c, const float* noise, int iter, const float* z0) {
 int q_chain(const Ctx& c, int rows, RowMap map) {
     const Layout& w = c.w;
     const int M = c.M;
-    ChainArgs a = chain0(c, rows, map, c.H, c.Kx, 0);
+    ChainArgs a = chain0(c, rows, map, c.H, c.Kx, 0, 2);
     for (int q = 0; q < 2; ++q) {
         ChainProb& p = a.p[q];
         p.W1 = c.pw + w.wq1x + (size_t)q * M * c.Kx; p.b1 = c.pw + w.bq1x + q * M;
@@ -2583,7 +3010,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     int rc;
     const int H = prm->horizon, I = prm->iterations, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 2) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 4) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T;
     // z0 = h(obs) and mean = 0 (warm: prev_mean shifted), std = 2
@@ -2665,7 +3092,7 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
     const int H = prm->horizon, I = prm->iterations, B = prm->batch, K = d->num_elites;
     if (I <= 0 || I > 16) { snprintf(g_err, sizeof g_err, "iCEM: 1..16 iterations"); return TDMPC_E_DIMS; }
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream, K))) return rc;
-    if (prm->path < 0 || prm->path > 2) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 4) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = d->num_samples, Pmax = d->num_pi, Tw = N + K + Pmax, pi_base = N + K, P0 = prm->n_pi0;
     c.T = Tw;
@@ -2763,7 +3190,7 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 2) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 4) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     if (rows != c.T) { snprintf(g_err, sizeof g_err, "rows must equal N+P"); return TDMPC_E_DIMS; }
     const int T = c.T, L = c.w.L;
