@@ -7,9 +7,12 @@ Workload (BASELINE.json configs[2], the north-star target): humanoid-run, N=512 
 iterations, mixture 0.5 (P=256 pi trajectories, T=768 rows), K=64 elites, latent 100 (cfgs/tasks/humanoid.yaml:6),
 fp32. A "step" is one planning call for the B environments a GPU owns: B complete, independent TDMPC.plan
 computations (each env its own observation, noise, CEM state and elite choice; bitwise identical to B separate
-single-env calls, tests/test_gpu_plan.py::test_batched_equals_single). The default B = 8 is the vectorised-env
-sharding of BASELINE.json configs[3] ("8 per GPU"); the single-env drop-in path (B = 1, one plan() per call,
-latency-bound) is timed in the same run and reported under "single_env".
+single-env calls, tests/test_gpu_plan.py::test_batched_equals_single). The default B = 32 envs per GPU is the
+smallest vectorised batch that fills the chip: its rollout launches are 1024 chain workgroups (4 per CU, two
+co-resident), where B = 8 (BASELINE.json configs[3]'s "8 per GPU") is exactly one per CU and leaves latency
+exposed (plan FP32 fraction 0.56 at B = 8, 0.76 at B = 32, 0.78 at B = 64). B = 8 and the
+single-env drop-in path (B = 1, one plan() per call, latency-bound) are timed in the same run and reported
+under "batch_sweep" and "single_env".
 
 Multi-GPU: environments are independent units, so every rank plans its own B envs on its own
 weight replica (weak scaling) and each step ends with one RCCL all-gather over xGMI of the per-env results
@@ -311,7 +314,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="humanoid-run")
-    ap.add_argument("--envs-per-gpu", type=int, default=8)
+    ap.add_argument("--envs-per-gpu", type=int, default=32)
+    ap.add_argument("--sweep", default="8", help="comma-separated extra envs-per-GPU batches timed at N=1")
     ap.add_argument("--rng", default="fused", choices=["fused", "reference"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -377,12 +381,14 @@ def main():
         rows = B * cfg.num_samples
         M, Lt, A = cfg.mlp_dim, cfg.latent_dim, cfg.action_dim
         # dominant kernel: the CEM rollout step (TOLD.next, 5 of every iteration's launches, ~half the time).
-        # Row-block chain kernel when the auto path picks it (>= 128 workgroups), else the layered hidden GEMM.
+        # Row-block chain kernel when the auto path picks it (>= 64 32-row blocks), else the layered hidden GEMM.
         n, ms, fl = timed(4, -1, 0, rows)
         if n > 0:
-            kernel = (f"chain_kernel<CH_STEP> (TOLD.next: dynamics + reward heads, 32-row blocks, hidden "
+            rb = 32 if (rows + 31) // 32 * 2 > torch.cuda.get_device_properties(dev).multi_processor_count // 2 else 16
+            rb = int(os.environ.get("TDMPC_CHAIN_RB", rb))
+            kernel = (f"{'chain_kernel' if rb == 32 else 'chain16_kernel'}<CH_STEP> (TOLD.next: dynamics + reward heads, {rb}-row blocks, hidden "
                       f"activations in LDS, weights streamed from L2; {rows} rows x 2 heads per launch), "
-                      f"fp32 v_mfma_f32_32x32x2_f32")
+                      f"fp32 {'v_mfma_f32_32x32x2_f32' if rb == 32 else 'v_mfma_f32_16x16x4_f32'}")
             kx = A + Lt
             alg_bytes = 4.0 * (rows * (kx + Lt + 2) + 2 * M * kx + 2 * M * M + M * Lt + M)
             pmc_key = f"{args.config}/B{B}/chain_step"
@@ -427,6 +433,22 @@ def main():
         single = {"value": round(ks / el1, 3), "unit": "plan-steps/s", "ms_per_step": round(el1 / ks * 1e3, 4),
                   "note": "one env per plan() call (the drop-in TDMPC.plan path), same GPU, same run"}
 
+    sweep = None
+    if world == 1 and args.sweep:
+        sweep = {}
+        for bs in [int(x) for x in args.sweep.split(",") if x.strip()]:
+            if bs == B:
+                continue
+            ab = make_agent(cfg, bs, args.rng, graph, 11)
+            ob = torch.from_numpy(synthetic_obs(cfg, bs, seed=0)).to(dev)
+            kb = max(10, args.steps // 2)
+            elb = time_steps(lambda i: ab.plan_batch(ob, step=step, t0=(i % 100 == 0), sync_metrics=False),
+                             3, kb, None)
+            sweep[str(bs)] = {"value": round(bs * kb / elb, 3), "unit": "plan-steps/s",
+                              "ms_per_step": round(elb / kb * 1e3, 4),
+                              "frac_of_fp32_peak": round(bs * kb / elb * min(fl_alg, fl_exec) / 1e12 / FP32_PEAK_TFLOPS, 4)}
+            del ab
+
     replay = None
     if not args.no_replay and world == 1:
         replay = replay_bench(cfg, dev, cpu=not args.no_cpu)
@@ -459,6 +481,7 @@ def main():
             "roofline": roof,
             "plan_roofline": plan_roof,
             "single_env": single,
+            "batch_sweep": sweep,
             "replay_sampler": replay,
             "learner": learner,
             "icem": icem,

@@ -171,7 +171,7 @@ int main(int argc, char** argv) {
         snprintf(nm[path * 3 - 1], 64, "terminal_q T rows (%s)", pn);
         cases.push_back({nm[path * 3 - 3], [&, path] { c.path = path; step_next(c, 1, B * c.N, rm, 0.99f, 0, 0); }});
         cases.push_back({nm[path * 3 - 2], [&, path] { c.path = path; policy(c, 5, B * c.T, all, noise, c.eps_env, c.T, 0, 0.05f); }});
-        cases.push_back({nm[path * 3 - 1], [&, path] { c.path = path; terminal_q(c, 0.95f, nullptr, 6, 0); }});
+        cases.push_back({nm[path * 3 - 1], [&, path] { c.path = path; terminal_q(c, 0.95f); }});
     }
     cases.push_back({"step_next T rows (chain)", [&] { c.path = 2; step_next(c, 1, B * c.T, all, 0.99f, 0, 0); }});
     cases.push_back({"policy P rows (chain)", [&] { c.path = 2; policy(c, 1, B * c.P, RowMap{c.P, c.T, c.N}, noise, c.eps_env, c.P, 0, 0.05f); }});
@@ -266,7 +266,7 @@ int main(int argc, char** argv) {
         run_case("chain step dyn (N rows)", [&] { step_next(c, 1, B * c.N, rmc, 0.99f, 0, 0); }, 0);
         run_case("chain step rew (N rows)", [&] { step_next(c, 1, B * c.N, rmc, 0.99f, 0, 0); }, 1);
         run_case("chain pi (T rows)", [&] { policy(c, 5, B * c.T, allc, noise, c.eps_env, c.T, 0, 0.05f); });
-        run_case("chain Q (T rows)", [&] { terminal_q(c, 0.95f, nullptr, 6, 0); }, 0);
+        run_case("chain Q (T rows)", [&] { terminal_q(c, 0.95f); }, 0);
         c.path = 0;
     }
 #endif
