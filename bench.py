@@ -407,6 +407,15 @@ def main():
                 "launches": n, "avg_launch_us": round(avg_s * 1e6, 3), "flops_per_launch": per_launch,
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "hbm_gbs_algorithmic": round(alg_bytes / avg_s / 1e9, 1)}
+        mf = os.path.join(REPO, "profiles", "pmc_mfma.json")
+        if os.path.exists(mf):
+            try:
+                t = json.load(open(mf)).get(pmc_key)
+                if t:   # rocprofv3 PMC pass of the same kernel and shape (tools/gpu41.sh, tools/pmc_mfma.py)
+                    roof["mfma_util_pmc"] = t.get("mfma_util")
+                    roof["clock_ghz_pmc"] = t.get("clock_ghz")
+            except (OSError, ValueError):
+                pass
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
