@@ -8,7 +8,13 @@ broadcasts total_loss [B, 1] against weights [B] to [B, B]; the TD target uses t
 with the target Q; the policy update re-samples TruncatedNormal noise.
 
 What is MI355X-specific is how it runs. A reference update is ~1,500 small kernel launches issued one by one
-from Python with seven host syncs (`.item()` metrics, the host-side replay choice). Here, after `warmup`
+from Python with seven host syncs (`.item()` metrics, the host-side replay choice). Here only the latent
+dynamics chain z_{t+1} = d(z_t, a_t) stays a loop over the horizon; everything off that chain is batched into
+one pass over H*B rows (the TD targets with their encoders, policy and target Q; the Q heads and the reward
+head on (z_t, a_t); the losses as rho-weighted sums over the horizon axis) and the policy update is one pass
+over (H+1)*B rows -- per row the same math, far fewer and wider launches (the horizon steps' TruncatedNormal
+draws come from one [H*B, A] call instead of H calls of [B, A]; with explicit noise they are the same
+numbers). Then, after `warmup`
 eager updates (which also create Adam's state), one whole update -- the device replay sample
 (tdmpc_amd.replay), encoder / dynamics / reward / Q forward over the horizon, the TD targets, backward,
 grad-norm clipping, Adam (capturable, foreach), the priority write-back, the policy update -- is captured
@@ -79,6 +85,10 @@ class Learner:
         agent.pi_optim = torch.optim.Adam(self.pi_params, lr=self.cfg.lr, capturable=graph, foreach=True)
         self.calls = 0
         self._graphs = {}
+        H = self.cfg.horizon
+        # rho^t, t = 0..H, as float32 like the reference's Python-float scalar multiplies (tdmpc.py:212, 179)
+        self._rho = torch.tensor([self.cfg.rho ** t for t in range(H + 1)], dtype=torch.float32,
+                                 device=agent.device).view(H + 1, 1, 1)
 
     # ------------------------------------------------------------------ reference math
     @torch.no_grad()
@@ -89,15 +99,15 @@ class Learner:
         return reward + cfg.discount * torch.min(*a.model_target.Q(next_z, a.model.pi(next_z, cfg.min_std, eps=eps)))
 
     def update_pi(self, zs, eps=None):
-        """tdmpc.py:165-182 -> pi_loss (tensor)."""
+        """tdmpc.py:165-182 -> pi_loss (tensor): the H+1 latents in one pass, sum_t -mean(min Q_t) rho^t."""
         a, cfg = self.agent, self.cfg
         a.pi_optim.zero_grad(set_to_none=True)
         a.model.track_q_grad(False)
-        pi_loss = 0
-        for t, z in enumerate(zs):
-            act = a.model.pi(z, cfg.min_std, eps=None if eps is None else eps[t])
-            q = torch.min(*a.model.Q(z, act))
-            pi_loss += -q.mean() * (cfg.rho ** t)
+        n = len(zs)
+        Z = torch.cat(zs)
+        act = a.model.pi(Z, cfg.min_std, eps=None if eps is None else torch.cat(list(eps[:n])))
+        q = torch.min(*a.model.Q(Z, act)).view(n, -1)
+        pi_loss = (-q.mean(dim=1) * self._rho[:n].view(n)).sum()
         pi_loss.backward()
         torch.nn.utils.clip_grad_norm_(self.pi_params, cfg.grad_clip_norm, error_if_nonfinite=False, foreach=True)
         a.pi_optim.step()
@@ -108,25 +118,32 @@ class Learner:
         """One TDMPC.update without the EMA (tdmpc.py:192-241) -> metrics tensor [7] (METRICS order).
         noise: optional list of 2H+1 [B, A] TruncatedNormal draws (H for the TD targets, H+1 for update_pi)."""
         a, cfg = self.agent, self.cfg
+        m = a.model
         H = cfg.horizon
         obs, next_obses, action, reward, idxs, weights = buffer.sample()
+        B = obs.shape[0]
         a.optim.zero_grad(set_to_none=True)
-        z = a.model.h(a.aug(obs))
-        zs = [z.detach()]
-        consistency_loss, reward_loss, value_loss, priority_loss = 0, 0, 0, 0
+        act, rew = action[:H], reward[:H]                                   # [H, B, A], [H, B, 1]
+        with torch.no_grad():   # targets of every horizon step at once (tdmpc.py:206-208, 184-190)
+            next_obs = a.aug(next_obses[:H].reshape(H * B, *next_obses.shape[2:]))
+            next_z = a.model_target.h(next_obs).view(H, B, -1)
+            td_target = self.td_target(next_obs, rew.reshape(H * B, 1),
+                                       eps=None if noise is None else torch.cat(list(noise[:H]))).view(H, B, 1)
+        # the latent dynamics chain (tdmpc.py:203-205): the only sequential part
+        z = m.h(a.aug(obs))
+        zs = [z]
         for t in range(H):
-            Q1, Q2 = a.model.Q(z, action[t])
-            z, reward_pred = a.model.next(z, action[t])
-            with torch.no_grad():
-                next_obs = a.aug(next_obses[t])
-                next_z = a.model_target.h(next_obs)
-                td_target = self.td_target(next_obs, reward[t], eps=None if noise is None else noise[t])
-            zs.append(z.detach())
-            rho = cfg.rho ** t
-            consistency_loss += rho * torch.mean(_mse(z, next_z), dim=1, keepdim=True)
-            reward_loss += rho * _mse(reward_pred, reward[t])
-            value_loss += rho * (_mse(Q1, td_target) + _mse(Q2, td_target))
-            priority_loss += rho * (_l1(Q1, td_target) + _l1(Q2, td_target))
+            z = m._dynamics(torch.cat([z, act[t]], dim=-1))
+            zs.append(z)
+        x = torch.cat([torch.stack(zs[:H]), act], dim=-1).view(H * B, -1)  # (z_t, a_t), t < H
+        Q1, Q2 = m._Q1(x).view(H, B, 1), m._Q2(x).view(H, B, 1)
+        reward_pred = m._reward(x).view(H, B, 1)
+        rho = self._rho[:H]
+        consistency_loss = (rho * torch.mean(_mse(torch.stack(zs[1:]), next_z), dim=2, keepdim=True)).sum(0)
+        reward_loss = (rho * _mse(reward_pred, rew)).sum(0)
+        value_loss = (rho * (_mse(Q1, td_target) + _mse(Q2, td_target))).sum(0)
+        priority_loss = (rho * (_l1(Q1, td_target) + _l1(Q2, td_target))).sum(0)
+        zs = [zz.detach() for zz in zs]
         total_loss = cfg.consistency_coef * consistency_loss.clamp(max=1e4) + \
             cfg.reward_coef * reward_loss.clamp(max=1e4) + \
             cfg.value_coef * value_loss.clamp(max=1e4)

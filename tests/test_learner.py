@@ -120,3 +120,42 @@ def test_graph_replay_equals_eager():
     for x, y in zip(list(a1.model.parameters()) + list(a1.model_target.parameters()),
                     list(a2.model.parameters()) + list(a2.model_target.parameters())):
         assert torch.equal(x, y)
+
+
+class _CpuAgent:
+    """The attributes Learner reads from a TDMPC agent, on the CPU (no planner, no HIP library)."""
+
+    def __init__(self, cfg, sd, sdt):
+        from tdmpc_amd.learner import RandomShiftsAug
+        from tdmpc_amd.told import TOLD
+        self.cfg, self.device = cfg, torch.device("cpu")
+        self.model, self.model_target = TOLD(cfg), TOLD(cfg)
+        self.model.load_state_dict(sd)
+        self.model_target.load_state_dict(sdt)
+        self.aug = RandomShiftsAug(cfg)
+        self.planner = type("P", (), {"_packed_key": None})()
+
+
+def test_cpu_batched_learner_matches_oracle():
+    """The learner's horizon-batched formulation (TD targets, Q / reward heads and the policy update as one
+    pass over H*B rows; only the dynamics chain loops) against the oracle's per-step reference order, run on
+    the CPU with the same draws: same tolerance as the GPU test."""
+    from tdmpc_amd.learner import Learner
+    cfg = learner_cfg()
+    agent = _CpuAgent(cfg, synthetic_state_dict(cfg, 21), synthetic_state_dict(cfg, 22))
+    ln = Learner(agent, graph=False)
+    ref = RefLearner(cfg, synthetic_state_dict(cfg, 21), synthetic_state_dict(cfg, 22))
+    b = batch(cfg)
+    buf = _DeviceBatchBuffer(b, device="cpu")
+    H, B, A = cfg.horizon, cfg.batch_size, cfg.action_dim
+    torch.manual_seed(0)
+    noise = [[torch.empty(B, A).normal_() for _ in range(2 * H + 1)] for _ in range(2)]
+    torch.manual_seed(0)
+    for k, step in enumerate((1, 2)):
+        m = ln.update(buf, step, noise=noise[k])
+        rm, rprio = ref.update(b, step)
+        np.testing.assert_allclose(m.numpy(), [rm[n] for n in METRICS], rtol=2e-5, atol=1e-7)
+        np.testing.assert_allclose(buf.prio.numpy(), rprio.numpy(), rtol=2e-5, atol=1e-6)
+        sd, sdt = ref.state_dicts()
+        _params_close(agent.model.state_dict(), sd, cfg.lr)
+        _params_close(agent.model_target.state_dict(), sdt, cfg.lr)
