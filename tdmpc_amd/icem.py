@@ -17,8 +17,9 @@ iteration's sample 0 is the mean, and the sample noise is white / pink (beta 1) 
 Randomness (`rng="reference"`): torch's and numpy's global generators in the reference's order; the coloured
 thirds come from tdmpc_amd.colored_noise on numpy's global RandomState (the reference's `colorednoise` is
 absent and unpinned; 2.x seeds each call from OS entropy, so its stream is not reproducible anyway).
-`rng="device"` draws the coloured noise (rocFFT) and the pick's uniform on the device too: same distributions,
-no host work. `plan(..., noise=IcemNoise)` takes explicit draws (parity tests).
+`rng="device"` draws everything on the device in ~8 launches (the stream white in one draw, every coloured third
+and reuse tail from one batched spectrum draw per sample length with the irfft as a matmul, the pick's uniform):
+same distributions, no host work. `plan(..., noise=IcemNoise)` takes explicit draws (parity tests).
 """
 from __future__ import annotations
 
@@ -29,7 +30,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .colored_noise import _scales as _spectrum, powerlaw_psd_gaussian_torch
+from .colored_noise import BatchedColoredNoise, _scales as _spectrum
 from .config import linear_schedule
 from .tdmpc import _discount_pows, pack_told
 from .told import TOLD
@@ -91,6 +92,7 @@ class TdICEM:
         self._stage = torch.empty(col_max, dtype=torch.float32, device=dev)
         self._pinned = torch.empty(col_max, dtype=torch.float32, pin_memory=dev.type == "cuda")
         self._h2d_done = None
+        self._dev_plans = {}
         self._packed_key = self._packed_model = None
         self._packed_params = []
         self._has_prev = False
@@ -183,6 +185,38 @@ class TdICEM:
         out.sort(key=lambda t: t[0])
         return np.concatenate([a.reshape(-1) for _, a in out]) if out else np.zeros(0, np.float32)
 
+    def _device_plan(self, H, cts, off, reuse):
+        """rng 'device': per sample length, a BatchedColoredNoise over that length's coloured specs and the
+        stream positions [R, H] its rows land on (samp thirds [H][n][A] at their column offset, reuse tail)."""
+        key = (H, tuple(cts), reuse)
+        plan = self._dev_plans.get(key)
+        if plan is not None:
+            return plan
+        A = self.cfg.action_dim
+        groups = {}
+        for beta, n, L, kind, i in self._colored_specs(H, cts, reuse):
+            nt = cts[i][0]
+            n0, n1, _ = _thirds(nt)
+            if kind == "samp":
+                base, rows, c0 = off["samp"][i], nt, (n0 if beta == 1.0 else n0 + n1)
+            else:
+                base, rows, c0 = off["reuse"], n, 0
+            t = np.arange(H)[None, None, :]
+            r = np.arange(n)[:, None, None]
+            a = np.arange(A)[None, :, None]
+            pos = base + t * rows * A + (c0 + r) * A + a                   # [n, A, H]
+            g = groups.setdefault(L, ([], []))
+            g[0].append((beta, n))
+            g[1].append(pos.reshape(n * A, H))
+        plan = []
+        for L, (sp, pos) in sorted(groups.items()):
+            plan.append((BatchedColoredNoise(sp, A, L, H, self.device),
+                         torch.as_tensor(np.concatenate(pos), dtype=torch.int64, device=self.device)))
+        if len(self._dev_plans) > 16:
+            self._dev_plans.clear()
+        self._dev_plans[key] = plan
+        return plan
+
     def _draw(self, e, H, cts, off, reuse, eval_mode):
         """Env e's stream in the reference's draw order on torch's (device) and numpy's global generators.
         The two generators are independent, so the numpy draws (coloured thirds, reused-elite tail, the pick's
@@ -193,23 +227,27 @@ class TdICEM:
         dev = self.device
         specs = self._colored_specs(H, cts, reuse)
         if self.rng == "device":
-            col = [powerlaw_psd_gaussian_torch(b, (n, A, L), dev)[:, :, :H].permute(2, 0, 1) for b, n, L, _, _ in specs]
-            u = None
-        else:
-            host = self._colored_host(specs, H)
-            u = float(np.random.random_sample())
-            if self._h2d_done is not None:
-                self._h2d_done.synchronize()   # the previous call's copy has left the pinned buffer
-            stage = self._pinned[:host.size]
-            stage.numpy()[:] = host
-            dst = self._stage[:host.size]
-            dst.copy_(stage, non_blocking=True)
-            self._h2d_done = torch.cuda.Event()
-            self._h2d_done.record()
-            col, o = [], 0
-            for b, n, L, _, _ in specs:
-                col.append(dst[o:o + H * n * A].view(H, n, A))
-                o += H * n * A
+            # the whole stream white in one draw, then every coloured third / reuse tail overwritten from one
+            # batched spectrum draw per sample length, then the pick's uniform: ~8 launches per call
+            buf.normal_()
+            for gen, pos in self._device_plan(H, cts, off, reuse):
+                buf[pos] = gen.draw()
+            self.u[e:e + 1].uniform_()
+            return None
+        host = self._colored_host(specs, H)
+        u = float(np.random.random_sample())
+        if self._h2d_done is not None:
+            self._h2d_done.synchronize()   # the previous call's copy has left the pinned buffer
+        stage = self._pinned[:host.size]
+        stage.numpy()[:] = host
+        dst = self._stage[:host.size]
+        dst.copy_(stage, non_blocking=True)
+        self._h2d_done = torch.cuda.Event()
+        self._h2d_done.record()
+        col, o = [], 0
+        for b, n, L, _, _ in specs:
+            col.append(dst[o:o + H * n * A].view(H, n, A))
+            o += H * n * A
         P0 = cts[0][1]
         for t in range(H):
             buf[t * P0 * A:(t + 1) * P0 * A].view(P0, A).normal_()
@@ -229,8 +267,6 @@ class TdICEM:
                 else:
                     r.copy_(torch.randn(H, ne, A, device=dev))
             buf[off["term"][i]:off["term"][i] + (n + ne + p) * A].view(n + ne + p, A).normal_()
-        if u is None:
-            self.u[e:e + 1].uniform_()
         if not eval_mode:
             buf[off["act"]:off["act"] + A].normal_()
         return u

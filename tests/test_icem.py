@@ -153,3 +153,44 @@ def test_gpu_icem_device_rng():
     assert torch.isfinite(outs[0]).all()
     ev_calls = [ci for ci, (_, _, ev) in enumerate(CALLS) if ev]
     assert ev_calls and outs[0][ev_calls].abs().max() <= 1   # no exploration noise: an elite's action
+
+
+def test_batched_colored_noise_spectrum():
+    """BatchedColoredNoise (the fused-RNG form: matmul irfft, per-row spectrum factors) has the generator's
+    statistics: unit variance, log-log PSD slope ~ -beta, per spec of a mixed batch."""
+    from tdmpc_amd.colored_noise import BatchedColoredNoise
+    torch.manual_seed(0)
+    L, A = 256, 4
+    gen = BatchedColoredNoise([(1.0, 500), (2.5, 500)], A, L, L, "cpu")
+    y = gen.draw().double().numpy()
+    for k, beta in enumerate((1.0, 2.5)):
+        yk = y[k * 500 * A:(k + 1) * 500 * A]
+        assert abs(yk.std() - 1.0) < (0.1 if beta < 2 else 0.2)
+        psd = (np.abs(np.fft.rfft(yk, axis=-1)) ** 2).mean(0)[1:64]
+        f = np.fft.rfftfreq(L)[1:64]
+        slope = np.polyfit(np.log(f), np.log(psd), 1)[0]
+        assert abs(slope + beta) < 0.15, (beta, slope)
+
+
+def test_device_rng_positions_cover_colored_slots():
+    """The fused-RNG stream plan writes every coloured third and reuse-tail slot exactly once and nothing else
+    (checked against the layout the kernels read, on the CPU)."""
+    from tdmpc_amd.icem import TdICEM, _thirds
+    cfg = icem_cfg()
+    cfg.device = "cpu"
+    agent = TdICEM(cfg, rng="device")
+    A, H = cfg.action_dim, cfg.horizon
+    cts = agent.counts(0.5, True)
+    off = agent._layout(H, cts, True)
+    want = set()
+    for i, (n, p, e) in enumerate(cts):
+        n0, n1, n2 = _thirds(n)
+        for t in range(H):
+            for r in range(n0, n):
+                want.update(off["samp"][i] + t * n * A + r * A + a for a in range(A))
+    if cfg.noise_beta > 0:
+        ne = cts[0][2]
+        want.update(off["reuse"] + j for j in range(H * ne * A))
+    got = np.concatenate([pos.numpy().reshape(-1) for _, pos in agent._device_plan(H, cts, off, True)])
+    assert len(got) == len(set(got.tolist())) == len(want)
+    assert set(got.tolist()) == want
