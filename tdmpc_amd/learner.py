@@ -1,10 +1,11 @@
 """The TD-MPC learner on the GPU: `TDMPC.update / update_pi / _td_target`.
 
 Reference: /root/reference/src/algorithm/tdmpc.py:165-245 (+ helper.py:19-26 mse / l1, 48-52 ema, 71-96
-TruncatedNormal, 250-283 RandomShiftsAug). The math is the reference's, op for op (the oracle restatement
+TruncatedNormal, 250-283 RandomShiftsAug). The math is the reference's (the oracle restatement
 oracle/learner_ref.py is pinned bit-exact to the reference on the CPU; tests/test_learner.py holds this
 against it within the fp32 tolerance stated there), including the reference's quirks: the IS-weighted mean
-broadcasts total_loss [B, 1] against weights [B] to [B, B]; the TD target uses the ONLINE encoder and policy
+is the mean over the [B, B] broadcast of total_loss [B, 1] against weights [B] (computed as the equal
+mean(total_loss) * mean(weights)); the TD target uses the ONLINE encoder and policy
 with the target Q; the policy update re-samples TruncatedNormal noise.
 
 What is MI355X-specific is how it runs. A reference update is ~1,500 small kernel launches issued one by one
@@ -81,8 +82,8 @@ class Learner:
         self.pi_params = list(model._pi.parameters())
         self.target_params = list(agent.model_target.parameters())
         # tdmpc.py:62-63 (Adam over all TOLD parameters; the policy's own Adam, both at cfg.lr)
-        agent.optim = torch.optim.Adam(self.params, lr=self.cfg.lr, capturable=graph, foreach=True)
-        agent.pi_optim = torch.optim.Adam(self.pi_params, lr=self.cfg.lr, capturable=graph, foreach=True)
+        agent.optim = torch.optim.Adam(self.params, lr=self.cfg.lr, capturable=graph, fused=True)
+        agent.pi_optim = torch.optim.Adam(self.pi_params, lr=self.cfg.lr, capturable=graph, fused=True)
         self.calls = 0
         self._graphs = {}
         H = self.cfg.horizon
@@ -147,7 +148,9 @@ class Learner:
         total_loss = cfg.consistency_coef * consistency_loss.clamp(max=1e4) + \
             cfg.reward_coef * reward_loss.clamp(max=1e4) + \
             cfg.value_coef * value_loss.clamp(max=1e4)
-        weighted_loss = (total_loss * weights).mean()
+        # the reference's (total_loss [B, 1] * weights [B]).mean() is a mean over the [B, B] broadcast, i.e.
+        # mean(total_loss) * mean(weights): computed in that factored form (no B x B tensor, same gradient)
+        weighted_loss = total_loss.mean() * weights.mean()
         weighted_loss.register_hook(lambda grad: grad * (1 / H))
         weighted_loss.backward()
         grad_norm = torch.nn.utils.clip_grad_norm_(self.params, cfg.grad_clip_norm, error_if_nonfinite=False,
