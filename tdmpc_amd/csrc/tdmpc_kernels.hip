@@ -918,6 +918,13 @@ DEVI void ring_run(floatx16 (&acc)[TN], float4 (&wr)[D][TN], const float* sA, co
     }
 }
 
+// Workgroup barrier for the chain kernels' LDS hand-offs: waits for this wave's LDS traffic only. HIP's
+// __syncthreads() carries a fence that drains vmcnt, i.e. it also waits for every global load in flight (the next
+// layer's weight ring prefetched before the epilogue, the ring's tail refills). No chain-kernel barrier orders
+// global memory between waves. Measured neutral on MI355X (stamps, tools/gpu48.sh: the layer-boundary cost is
+// the MFMA pipe draining before each epilogue, not the load wait), kept as the precise primitive.
+DEVI void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Row mean and 1/sqrt(var + 1e-5) over the M columns of the block's rows (biased variance, two passes),
 // from each lane's TN*16 values of row r: per-wave partials through red0 / red1 ([NW][32] each).
 template <int TN, int NW>
@@ -928,7 +935,7 @@ DEVI void chain_row_moments(const float (&v)[TN * 16], float* red0, float* red1,
     for (int i = 0; i < TN * 16; ++i) s += v[i];
     s += __shfl_xor(s, 32);
     if (h == 0) red0[wave * 32 + r] = s;
-    __syncthreads();
+    lds_barrier();
     float tot = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) tot += red0[w * 32 + r];
@@ -941,7 +948,7 @@ DEVI void chain_row_moments(const float (&v)[TN * 16], float* red0, float* red1,
     }
     m2 += __shfl_xor(m2, 32);
     if (h == 0) red1[wave * 32 + r] = m2;
-    __syncthreads();
+    lds_barrier();
     float tot2 = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) tot2 += red1[w * 32 + r];
@@ -1064,7 +1071,7 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) eps4[k] = c + k < a.nvalid ? ep[c + k] : 0.f;
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---- layer 1: [32 x K1] . W1^T -> [32 x M]
     floatx16 acc[TN];
@@ -1075,7 +1082,7 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
     ring_run<TN, D>(acc, wr, sH, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3, r, h);
     // layer-2 weights in flight during the epilogue
     ring_fill<TN, D>(wr, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3);
-    __syncthreads();   // every wave is done with the input tile: sH becomes h1
+    lds_barrier();   // every wave is done with the input tile: sH becomes h1
 #ifdef TDMPC_STAMPS
     STAMP(1);
 #endif
@@ -1094,7 +1101,7 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
         }
         chain_store_lds<TN>(sH, v, cw0, r, h);
     }
-    __syncthreads();
+    lds_barrier();
 #ifdef TDMPC_STAMPS
     STAMP(2);
 #endif
@@ -1137,7 +1144,7 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
             }
         s += __shfl_xor(s, 32);
         if (h == 0) red0[wave * 32 + r] = s;
-        __syncthreads();
+        lds_barrier();
         if (tid < 32) {
             const int lm = m0 + tid;
             if (lm < a.rows) {
@@ -1157,7 +1164,7 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
             }
         }
 #ifdef TDMPC_STAMPS
-        __syncthreads();
+        lds_barrier();
         STAMP(4);
         STAMP_RECORD();
 #endif
@@ -1166,9 +1173,9 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
     // dynamics / pi: h2 = ELU(y2) back into the activation block once every wave is done reading h1
 #pragma unroll
     for (int i = 0; i < TN * 16; ++i) v[i] = elu_f(v[i]);
-    __syncthreads();
+    lds_barrier();
     chain_store_lds<TN>(sH, v, cw0, r, h);
-    __syncthreads();
+    lds_barrier();
 
     // ---- layer 3: [32 x M] . W3^T -> [32 x n3]; partial tiles meet in the activation block after the reads
     floatx16 a3a[1], a3b[1];
@@ -1183,7 +1190,7 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
         ring_fill<1, D3>(w3r, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper);
         ring_run<1, D3>(a3b, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         if (wave < items)
@@ -1193,7 +1200,7 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
             *(float4*)(sH + (size_t)(wave + NW) * 1024 + ((2 * q + h) * 32 + r) * 4) =
                 make_float4(a3b[0][4 * q], a3b[0][4 * q + 1], a3b[0][4 * q + 2], a3b[0][4 * q + 3]);
     }
-    __syncthreads();
+    lds_barrier();
     for (int i = tid; i < (a.nstore >> 2) * 32; i += NTH) {
         const int row = i & 31, cq = i >> 5;
         const int lm = m0 + row;
@@ -1233,7 +1240,7 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
             make_float4(o[0], o[1], o[2], o[3]);
     }
 #ifdef TDMPC_STAMPS
-    __syncthreads();
+    lds_barrier();
     STAMP(4);
     STAMP_RECORD();
 #endif
@@ -1317,7 +1324,7 @@ DEVI float row16_sum(float s, float* red, int wave, int lane) {
     s += __shfl_xor(s, 16);
     s += __shfl_xor(s, 32);
     if (lane < 16) red[wave * 16 + lane] = s;
-    __syncthreads();
+    lds_barrier();
     float tot = 0.f;
 #pragma unroll
     for (int w = 0; w < 8; ++w) tot += red[w * 16 + (lane & 15)];
@@ -1434,7 +1441,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
 #pragma unroll
         for (int k = 0; k < 4; ++k) eps4[k] = c + k < a.nvalid ? ep[c + k] : 0.f;
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---- layer 1
     floatx4 acc[NT];
@@ -1442,7 +1449,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
     ring16_run<NT, D>(acc, wr, sH, P.W1 + wblk * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1n, lane, q1max);
     ring16_fill<NT, D>(wr, P.W2 + wblk * M * 32 + lo, (long)M * 32, 0, M >> 4, h4, qMmax);
-    __syncthreads();
+    lds_barrier();
     {
         float v[NT * 4];
         chain16_bias<NT>(v, acc, sb1, f0);
@@ -1458,7 +1465,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
         }
         chain16_store_lds<NT>(sH, v, f0, m);
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---- layer 2
 #pragma unroll
@@ -1492,7 +1499,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
         s += __shfl_xor(s, 16);
         s += __shfl_xor(s, 32);
         if (lane < 16) red0[wave * 16 + lane] = s;
-        __syncthreads();
+        lds_barrier();
         if (tid < 16) {
             const int lm = m0 + tid;
             if (lm < a.rows) {
@@ -1514,9 +1521,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     }
 #pragma unroll
     for (int i = 0; i < NT * 4; ++i) v[i] = elu_f(v[i]);
-    __syncthreads();
+    lds_barrier();
     chain16_store_lds<NT>(sH, v, f0, m);
-    __syncthreads();
+    lds_barrier();
 
     // ---- layer 3: [16 x M] . W3^T -> [16 x n3]; partial tiles meet in the activation block after the reads
     floatx4 a3[4];
@@ -1532,13 +1539,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
             a3[u] = t1[0];
         }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int it = wave + 8 * u;
         if (it < items) *(float4*)(sH + (size_t)it * 256 + lane * 4) = make_float4(a3[u][0], a3[u][1], a3[u][2], a3[u][3]);
     }
-    __syncthreads();
+    lds_barrier();
     for (int i = tid; i < (a.nstore >> 2) * 16; i += 512) {
         const int row = i & 15, cq = i >> 4;
         const int lm = m0 + row;

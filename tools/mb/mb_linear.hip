@@ -231,7 +231,12 @@ int main(int argc, char** argv) {
                 xcc_hist[o[7] & 7]++;
             }
             double span_rt = 0, span_cy = 0;
-            for (unsigned i = 0; i < n; ++i) { span_rt += double(h[8 * i + 7] >> 8); span_cy += double(h[8 * i + 5] - h[8 * i + 1]); }
+            unsigned long long rtend = 0;
+            for (unsigned i = 0; i < n; ++i) {
+                span_rt += double(h[8 * i + 7] >> 8); span_cy += double(h[8 * i + 5] - h[8 * i + 1]);
+                rtend = std::max(rtend, h[8 * i] + (h[8 * i + 7] >> 8));
+            }
+            printf("%s: kernel wall (first start -> last end) %.2f us\n", name, (rtend - rtmin) / 100.0);
             printf("%s: %u WGs, start skew %.2f us, WG span %.2f us @ %.2f GHz, avg cycles: ph0 %.0f ph1 %.0f ph2 %.0f ph3 %.0f | max %.0f %.0f %.0f %.0f | xcc",
                    name, n, (rtmax - rtmin) / 100.0, span_rt / n / 100.0, span_cy / (span_rt * 10.0) , ph[0] / n, ph[1] / n, ph[2] / n, ph[3] / n, phmax[0], phmax[1], phmax[2], phmax[3]);
             for (int k = 0; k < 8; ++k) printf(" %d", xcc_hist[k]);
