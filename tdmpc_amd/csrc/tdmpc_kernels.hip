@@ -85,6 +85,7 @@ struct Layout {
     size_t enc_w1t, enc_b1, enc_w2t, enc_b2;         // state encoder, weights transposed [in][out]
     size_t enc_lng, enc_lnb; int enc_norm;           // its LayerNorm (enc_norm), [E] each
     size_t cw[4], cb[4], pl_wt, pl_b;                // pixel encoder (conv dense, linear transposed)
+    size_t cwt[4];                                   // conv weights again as [ci][ky][kx][co] (conv_tile_kernel)
     size_t w1x, b1x;                                 // panel [2M][Kx]: dynamics.0 rows then reward.0 rows
     size_t w2d, b2d, w2r, b2r;                       // panel [M][M]
     size_t w3d, b3d, w3r, b3r;                       // panel [Lr][M]; reward.4 dense [M]
@@ -119,6 +120,7 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
         w->conv_hw[0] = s;
         for (int i = 0; i < 4; ++i) {
             w->cw[i] = take((size_t)w->nch * cin * ks[i] * ks[i]);
+            w->cwt[i] = take((size_t)w->nch * cin * ks[i] * ks[i]);
             w->cb[i] = take(w->nch);
             s = (s - ks[i]) / 2 + 1; cin = w->nch;
             w->conv_hw[i + 1] = s;
@@ -2143,6 +2145,66 @@ __global__ void __launch_bounds__(256) conv_relu_kernel(const void* in, int in_u
     out[(size_t)e * out_bstride + idx] = fmaxf(s + b[co], 0.f);
 }
 
+// LDS-tiled form of the same convolution (+ ReLU, uint8 / 255 on the first layer): a workgroup computes all cout
+// channels of `toy` output rows of one env. It stages in LDS the input rows those outputs read (every input
+// element converted once) and the layer's weights (packed a second time as [ci][ky][kx][cout], so staging is a
+// straight copy and the 8 output channels of a thread's item come from two broadcast float4 LDS reads); each
+// thread then owns items of PX consecutive output pixels x 8 channels: PX input reads + 2 weight reads feed
+// 8 PX FMAs. Per output the sum runs in the same (ci, ky, kx) order as conv_relu_kernel. Item pixels past the
+// row end read in-bounds LDS (the next row / the weight block) and are not stored.
+template <int PX>
+__global__ void __launch_bounds__(256) conv_tile_kernel(const void* in, int in_u8, long in_bstride, int cin, int hin,
+                                                        float* out, long out_bstride, int cout, int hout, int ks,
+                                                        int toy, const float* w, const float* b) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int e = blockIdx.y;
+    const int oy0 = blockIdx.x * toy;
+    const int ny = min(toy, hout - oy0);
+    const int rows = 2 * (ny - 1) + ks;                  // input rows read by this tile
+    const int iy0 = 2 * oy0;
+    float* sIn = smem;                                   // [cin][rows][hin]
+    float* sW = smem + ((size_t)cin * (2 * (toy - 1) + ks) * hin + 3) / 4 * 4;   // [cin][ks][ks][cout]
+    const int kk = ks * ks;
+    for (int i = threadIdx.x; i < cin * rows * hin; i += 256) {
+        const int ci = i / (rows * hin), r = (i / hin) % rows, x = i % hin;
+        const long g = (long)e * in_bstride + ((long)ci * hin + iy0 + r) * hin + x;
+        sIn[i] = in_u8 ? __fdiv_rn((float)((const uint8_t*)in)[g], 255.f) : ((const float*)in)[g];
+    }
+    for (int i = threadIdx.x; i < cout * cin * kk / 4; i += 256) ((float4*)sW)[i] = ((const float4*)w)[i];
+    __syncthreads();
+    const int ng = cout / 8, nxq = (hout + PX - 1) / PX, nitem = ny * nxq;
+    for (int it = threadIdx.x; it < nitem * ng; it += 256) {
+        const int g = it / nitem, p = it % nitem;        // consecutive threads: consecutive pixels, same group
+        const int ty = p / nxq, ox0 = (p % nxq) * PX;
+        float acc[PX][8];
+#pragma unroll
+        for (int q = 0; q < PX; ++q)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) acc[q][c] = 0.f;
+        for (int ci = 0; ci < cin; ++ci)
+            for (int ky = 0; ky < ks; ++ky) {
+                const float* ip = sIn + ((size_t)ci * rows + 2 * ty + ky) * hin + 2 * ox0;
+                const float* wp = sW + ((size_t)(ci * ks + ky) * ks) * cout + 8 * g;
+                for (int kx = 0; kx < ks; ++kx) {
+                    const float4 w0 = *(const float4*)(wp + kx * cout), w1 = *(const float4*)(wp + kx * cout + 4);
+#pragma unroll
+                    for (int q = 0; q < PX; ++q) {
+                        const float v = ip[2 * q + kx];
+                        acc[q][0] += w0.x * v; acc[q][1] += w0.y * v; acc[q][2] += w0.z * v; acc[q][3] += w0.w * v;
+                        acc[q][4] += w1.x * v; acc[q][5] += w1.y * v; acc[q][6] += w1.z * v; acc[q][7] += w1.w * v;
+                    }
+                }
+            }
+#pragma unroll
+        for (int q = 0; q < PX; ++q) {
+            if (ox0 + q >= hout) break;
+            float* op = out + (size_t)e * out_bstride + (size_t)(8 * g) * hout * hout + (size_t)(oy0 + ty) * hout + ox0 + q;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) op[(size_t)c * hout * hout] = fmaxf(acc[q][c] + b[8 * g + c], 0.f);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------ packing
 // dst panel (total `dcols` columns): element (r, dc0 + c) = src[r * sld + sc0 + c], r < rows, c < cols
 __global__ void pack_panel_kernel(const float* src, int sld, int sc0, int rows, int cols, float* dst, int dcols,
@@ -2216,6 +2278,9 @@ int init_attrs() {
     FOR_EACH_LINEAR(SET_ATTR)
 #undef SET_ATTR
     HIPCHK(hipFuncSetAttribute((const void*)cem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 #define LDS_ATTR1(...) \
     HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<__VA_ARGS__>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 #define LDS_ATTR(...) LDS_ATTR1(__VA_ARGS__, true) LDS_ATTR1(__VA_ARGS__, false)
@@ -2810,11 +2875,44 @@ int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, const float*
         long in_bs = (long)w.img_c * w.img_hw * w.img_hw;
         int cin = w.img_c;
         for (int i = 0; i < 4; ++i) {
-            const int ho = w.conv_hw[i + 1];
+            const int ho = w.conv_hw[i + 1], hi = w.conv_hw[i];
             const int total = w.nch * ho * ho;
             float* out = bufs[i & 1];
-            hipLaunchKernelGGL(conv_relu_kernel, dim3((total + 255) / 256, batch), dim3(256), 0, c.s, in, in_u8,
-                               in_bs, cin, w.conv_hw[i], out, (long)act, w.nch, ho, ks[i], pw + w.cw[i], pw + w.cb[i]);
+            // tiled form when the channels split into groups of 8: (pixels per item, output rows per tile) by a
+            // cost model -- rounds of workgroups over the CUs x rounds of items over 256 threads x an item's
+            // instructions, plus the staging -- among the shapes whose tile fits LDS
+            int toy = 0, px = 1;
+            if (w.nch % 8 == 0) {
+                double best = 1e300;
+                const int kk = ks[i] * ks[i];
+                for (int pxc : {1, 2, 4})
+                    for (int t = 1; t <= ho; ++t) {
+                        const size_t fl = rup((size_t)cin * (2 * (t - 1) + ks[i]) * hi, 4) + (size_t)w.nch * cin * kk;
+                        if (fl * 4 > 160 * 1024) break;
+                        const long tiles = (long)((ho + t - 1) / t) * batch;
+                        const long items = (long)t * ((ho + pxc - 1) / pxc) * (w.nch / 8);
+                        const double cost = (double)((tiles + num_cus() - 1) / num_cus()) *
+                                            ((double)((items + 255) / 256) * cin * kk * (8.0 * pxc + pxc + 2) +
+                                             (double)fl / 256 * 4);
+                        if (cost < best) { best = cost; toy = t; px = pxc; }
+                    }
+            }
+            if (toy > 0) {
+                const size_t lds = (rup((size_t)cin * (2 * (toy - 1) + ks[i]) * hi, 4) + (size_t)w.nch * cin * ks[i] * ks[i]) * 4;
+                const dim3 grid((ho + toy - 1) / toy, batch);
+                if (px == 4)
+                    hipLaunchKernelGGL(conv_tile_kernel<4>, grid, dim3(256), lds, c.s, in, in_u8, in_bs, cin, hi, out,
+                                       (long)act, w.nch, ho, ks[i], toy, pw + w.cwt[i], pw + w.cb[i]);
+                else if (px == 2)
+                    hipLaunchKernelGGL(conv_tile_kernel<2>, grid, dim3(256), lds, c.s, in, in_u8, in_bs, cin, hi, out,
+                                       (long)act, w.nch, ho, ks[i], toy, pw + w.cwt[i], pw + w.cb[i]);
+                else
+                    hipLaunchKernelGGL(conv_tile_kernel<1>, grid, dim3(256), lds, c.s, in, in_u8, in_bs, cin, hi, out,
+                                       (long)act, w.nch, ho, ks[i], toy, pw + w.cwt[i], pw + w.cb[i]);
+            } else {
+                hipLaunchKernelGGL(conv_relu_kernel, dim3((total + 255) / 256, batch), dim3(256), 0, c.s, in, in_u8,
+                                   in_bs, cin, hi, out, (long)act, w.nch, ho, ks[i], pw + w.cw[i], pw + w.cb[i]);
+            }
             HIPCHK(hipGetLastError());
             in = out; in_u8 = 0; in_bs = (long)act; cin = w.nch;
         }
@@ -2944,6 +3042,7 @@ int tdmpc_pack_weights(const tdmpc_dims* d, const float* const* t, int32_t n, vo
         int cin = w.img_c;
         for (int c = 0; c < 4; ++c) {
             HIPCHK(cp(w.cw[c], t[i++], (size_t)w.nch * cin * ks[c] * ks[c]));
+            if ((rc = launch_transpose(t[i - 1], w.nch, cin * ks[c] * ks[c], pw + w.cwt[c], s))) return rc;
             HIPCHK(cp(w.cb[c], t[i++], w.nch));
             cin = w.nch;
         }
