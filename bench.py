@@ -49,6 +49,7 @@ from tdmpc_amd.tdmpc import TDMPC  # noqa: E402
 from tdmpc_amd.told import synthetic_state_dict  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector peak (spec)
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
 
 
 def plan_flops(cfg, executed: bool) -> float:
@@ -433,6 +434,12 @@ def main():
                     roof["traffic_source"] = t.get("source")
             except (OSError, ValueError):
                 pass
+        # the HBM roofline the north star asks for, next to the binding MFMA one: algorithmic and PMC bytes per
+        # launch over the measured launch time, as fractions of the 8 TB/s peak
+        roof["hbm_frac_algorithmic"] = round(roof["hbm_gbs_algorithmic"] / HBM_PEAK_GBS, 4)
+        if roof["traffic"]:
+            roof["hbm_gbs_pmc"] = round(roof["traffic"] / avg_s / 1e9, 1)
+            roof["hbm_frac_pmc"] = round(roof["hbm_gbs_pmc"] / HBM_PEAK_GBS, 4)
 
     fl_alg = plan_flops(cfg, executed=False)
     fl_exec = plan_flops(cfg, executed=True)

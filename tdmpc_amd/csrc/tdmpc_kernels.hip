@@ -2608,9 +2608,26 @@ struct Ctx {
 };
 
 float* Xt(const Ctx& c, int t) { return c.k.X + (size_t)t * c.k.x_stride; }
-bool use_chain(const Ctx& c, int rows, int nprob) {
+// Per-head thresholds (TDMPC_CHAIN_WGS_STEP / _PI / _Q override). The Q heads' layered form is four launches
+// (two GEMMs with LayerNorm partial moments, the LN+tanh pass, the value kernel), so the chain form wins from half
+// the step threshold: one env's 768 terminal rows 1.42 -> 1.32 ms per plan (tools/gpu52.sh); the step and pi
+// heads keep chain_wgs() (lower thresholds measured slower for them).
+enum { CK_STEP = 0, CK_PI = 1, CK_Q = 2 };
+int chain_wgs_kind(int kind) {
+    static int v[3] = {-2, -2, -2};
+    if (v[kind] == -2) {
+        static const char* names[3] = {"TDMPC_CHAIN_WGS_STEP", "TDMPC_CHAIN_WGS_PI", "TDMPC_CHAIN_WGS_Q"};
+        const char* e = getenv(names[kind]);
+        v[kind] = e ? atoi(e) : -1;
+    }
+    if (v[kind] >= 0) return v[kind];
+    return kind == CK_Q ? chain_wgs() / 2 : chain_wgs();
+}
+
+bool use_chain(const Ctx& c, int rows, int nprob, int kind) {
     if (c.path == TDMPC_PATH_LAYERED || !chain_shape_ok(c.w)) return false;
-    return c.path != TDMPC_PATH_AUTO || (chain_wgs() > 0 && (rows + 31) / 32 * nprob >= chain_wgs());
+    const int th = chain_wgs_kind(kind);
+    return c.path != TDMPC_PATH_AUTO || (th > 0 && (rows + 31) / 32 * nprob >= th);
 }
 
 // 16-wave 32-row chain workgroups: M = 512 (TN = 1), last-layer items <= 32 within the activation block.
@@ -2674,7 +2691,7 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
-    if (use_chain(c, rows, 2)) {
+    if (use_chain(c, rows, 2, CK_STEP)) {
         ChainArgs a = chain0(c, rows, map, t, c.Kx, 0, 2);
         ChainProb& d = a.p[0];
         d.W1 = c.pw + w.w1x; d.b1 = c.pw + w.b1x; d.W2 = c.pw + w.w2d; d.b2 = c.pw + w.b2d;
@@ -2725,7 +2742,7 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
-    if (use_chain(c, rows, 1)) {
+    if (use_chain(c, rows, 1, CK_PI)) {
         ChainArgs a = chain0(c, rows, map, t, w.Lp, w.Ap / 4, 1);
         ChainProb& p = a.p[0];
         p.W1 = c.pw + w.wp1; p.b1 = c.pw + w.bp1; p.W2 = c.pw + w.wp2; p.b2 = c.pw + w.bp2;
@@ -2851,7 +2868,7 @@ int terminal_q_rows(const Ctx& c, int rows, RowMap map, float discH, bool chain)
 
 int terminal_q(const Ctx& c, float discH) {
     const int rows = c.B * c.T;
-    return terminal_q_rows(c, rows, RowMap{1 << 30, 0, 0}, discH, use_chain(c, rows, 2));
+    return terminal_q_rows(c, rows, RowMap{1 << 30, 0, 0}, discH, use_chain(c, rows, 2, CK_Q));
 }
 
 // TOLD.h for `batch` observations -> z0 [B][Lp]; optionally initialises the CEM mean/std.
@@ -3151,7 +3168,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     ca.omm = prm->one_minus_momentum; ca.std_floor = prm->std_floor; ca.action = action; ca.metrics = metrics;
     ca.elite_out = elite_out; ca.score_out = score_out; ca.mean_out = mean_out; ca.std_out = std_out;
     ca.value_out = value_out;
-    if (use_chain(c, B * T, 2)) {   // terminal_q leaves q1, q2 per row; cem_kernel forms the values
+    if (use_chain(c, B * T, 2, CK_Q)) {   // terminal_q leaves q1, q2 per row; cem_kernel forms the values
         ca.G = c.k.G; ca.qv = c.k.qv; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H];
     }
     const size_t cem_lds = cem_lds_bytes(T, H, ca.K, c.A);
@@ -3274,7 +3291,7 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
         if ((rc = policy(c, H, B * NE, blk, noise, env, NE, prm->term_off[i], prm->min_std))) return rc;
         if ((rc = policy(c, H, B * Pi, pmi, noise, env, Pi, prm->term_off[i] + (long)NE * A, prm->min_std))) return rc;
         // both row groups on the same Q path, so cem_kernel reads one kind of value (qv or value)
-        const bool qchain = use_chain(c, B * NE, 2) && use_chain(c, B * Pi, 2);
+        const bool qchain = use_chain(c, B * NE, 2, CK_Q) && use_chain(c, B * Pi, 2, CK_Q);
         if ((rc = terminal_q_rows(c, B * NE, blk, prm->discount_pow[H], qchain))) return rc;
         if ((rc = terminal_q_rows(c, B * Pi, pmi, prm->discount_pow[H], qchain))) return rc;
         ca.qv = qchain ? c.k.qv : nullptr;
@@ -3316,7 +3333,7 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     }
     if ((rc = policy(c, H, B * T, all, eps_term, (long)T * c.A, T, 0, prm->min_std))) return rc;
     if ((rc = terminal_q(c, prm->discount_pow[H]))) return rc;
-    if (use_chain(c, B * T, 2)) {
+    if (use_chain(c, B * T, 2, CK_Q)) {
         hipLaunchKernelGGL(qvalue_kernel, dim3((B * T + 255) / 256), dim3(256), 0, c.s, c.k.G, c.k.qv, c.k.xrows,
                            prm->discount_pow[H], c.k.value, B * T);
         HIPCHK(hipGetLastError());
