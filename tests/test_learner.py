@@ -159,3 +159,16 @@ def test_cpu_batched_learner_matches_oracle():
         sd, sdt = ref.state_dicts()
         _params_close(agent.model.state_dict(), sd, cfg.lr)
         _params_close(agent.model_target.state_dict(), sdt, cfg.lr)
+
+
+def test_random_shifts_aug_matches_reference():
+    """tdmpc_amd.learner.RandomShiftsAug (helper.py:250-283) against the reference module's outputs on the same
+    frames and torch seed (tests/golden/aug_pixels.npz, make_aug_golden.py): 4-D and 5-D (horizon) batches."""
+    from types import SimpleNamespace
+    from tdmpc_amd.learner import RandomShiftsAug
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "aug_pixels.npz"))
+    aug = RandomShiftsAug(SimpleNamespace(img_size=84, modality="pixels"))
+    for k in ("4", "5"):
+        torch.manual_seed(11)
+        y = aug(torch.from_numpy(g["x" + k].astype(np.float32))).numpy()
+        assert np.array_equal(y, g["y" + k]), k
