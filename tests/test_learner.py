@@ -172,3 +172,43 @@ def test_random_shifts_aug_matches_reference():
         torch.manual_seed(11)
         y = aug(torch.from_numpy(g["x" + k].astype(np.float32))).numpy()
         assert np.array_equal(y, g["y" + k]), k
+
+
+@pytest.mark.gpu
+def test_gpu_pixel_update_graph_equals_eager():
+    """Pixel TOLD (quadruped frames, conv encoder, RandomShiftsAug on the device): 4 updates from a fixed batch,
+    3 eager warm-ups + 1 graph replay vs 4 eager updates; metrics finite. Not bitwise: MIOpen's convolution
+    backward (the encoder's weight gradient) may sum in a different order between calls, so the comparison is
+    at the learner tolerance (rtol 2e-5 on the metrics, parameters within 1e-6 + 1e-4 |x|)."""
+    from tdmpc_amd.config import make_cfg
+    from tdmpc_amd.tdmpc import TDMPC
+    cfg = make_cfg("quadruped", modality="pixels", num_samples=32, num_elites=8, iterations=2, horizon=3,
+                   batch_size=16)
+    rs = np.random.RandomState(1)
+    B, H, A = cfg.batch_size, cfg.horizon, cfg.action_dim
+    obs_shape = tuple(cfg.obs_shape)
+    b = (torch.from_numpy(rs.randint(0, 256, (B,) + obs_shape).astype(np.float32)),
+         torch.from_numpy(rs.randint(0, 256, (H + 1, B) + obs_shape).astype(np.float32)),
+         torch.from_numpy(rs.uniform(-1, 1, (H + 1, B, A)).astype(np.float32)),
+         torch.from_numpy(rs.standard_normal((H + 1, B, 1)).astype(np.float32)),
+         torch.arange(B), torch.ones(B))
+
+    class Buf(_DeviceBatchBuffer):
+        graph_safe, idx, _full = True, 0, False
+
+    outs = []
+    for warm in (3, 100):
+        agent = TDMPC(cfg)
+        agent.model.load_state_dict(synthetic_state_dict(cfg, 4))
+        agent.model_target.load_state_dict(synthetic_state_dict(cfg, 5))
+        agent.learner(graph=True, warmup=warm)
+        buf = Buf(b)
+        torch.manual_seed(9)
+        ms = [agent.update(buf, s + 1, sync_metrics=False).clone() for s in range(4)]
+        outs.append((agent, torch.stack(ms)))
+    (a1, m1), (a2, m2) = outs
+    assert a1.learner()._graphs and not a2.learner()._graphs
+    assert torch.isfinite(m1).all()
+    torch.testing.assert_close(m1, m2, rtol=2e-5, atol=1e-6)
+    for x, y in zip(a1.model.parameters(), a2.model.parameters()):
+        torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-6)
