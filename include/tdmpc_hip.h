@@ -71,7 +71,8 @@ typedef struct tdmpc_plan_params {
     float discount_pow[17];/* float32(discount**t) for t = 0..H, the running Python-float product */
     int32_t path;          /* kernel path: 0 = auto by row count, 1 = layered GEMMs only, 2 = row-block chain
                               kernels wherever the shape allows (row block by launch size), 3 / 4 = chain
-                              kernels on 32- / 16-row blocks only (results agree within the fp32 tolerance) */
+                              kernels on 32- / 16-row blocks only, 5 = TOLD.next on the column-split step kernel
+                              (others layered); results agree within the fp32 tolerance */
 } tdmpc_plan_params;
 
 #define TDMPC_PATH_AUTO 0
@@ -79,6 +80,7 @@ typedef struct tdmpc_plan_params {
 #define TDMPC_PATH_CHAIN 2
 #define TDMPC_PATH_CHAIN32 3
 #define TDMPC_PATH_CHAIN16 4
+#define TDMPC_PATH_SPLIT 5
 
 /* Byte sizes the caller must allocate (all 256-byte aligned). */
 typedef struct tdmpc_sizes {

@@ -143,6 +143,11 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
 }
 
 // ------------------------------------------------------------------------------------------------ workspace
+// split_step_kernel: the M-wide second layer is split over SPLIT_S column slices (one workgroup each) for launches
+// of at most SPLIT_MAX_ROWS rows.
+constexpr int SPLIT_S = 4;
+constexpr int SPLIT_MAX_ROWS = 4096;
+
 struct Work {
     float* X;        // (Hmax+1) panels [Xrows][Kx]: step inputs [a|z]; X_H is the terminal input
     float* H1;       // panel [Xrows][2M]
@@ -154,6 +159,9 @@ struct Work {
     float* rlast;    // [B*T] reward at t = H-1
     float* value;    // [B*T]
     float* qv;       // [2][xrows] Q-head outputs of the chain path
+    float* zpart;    // [2][SPLIT_S][split_rows][Lr] split-step partial z' (split_step_kernel), two step parities
+    float* rpart_s;  // [2][SPLIT_S][split_rows] split-step partial reward dots
+    int split_rows;  // rows the split partial buffers hold (min(xrows, SPLIT_MAX_ROWS))
     float* z0;       // [B][Lp] dense
     float* mean;     // [B][Hmax][A]
     float* stdv;     // [B][Hmax][A]
@@ -187,6 +195,9 @@ void make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k, int ex
     k->rlast = (float*)take(B * T * 4);
     k->value = (float*)take(B * T * 4);
     k->qv = (float*)take(2 * (size_t)k->xrows * 4);
+    k->split_rows = std::min(k->xrows, SPLIT_MAX_ROWS);
+    k->zpart = (float*)take((size_t)2 * SPLIT_S * k->split_rows * w.Lr * 4);
+    k->rpart_s = (float*)take((size_t)2 * SPLIT_S * k->split_rows * 4);
     k->z0 = (float*)take(B * w.Lp * 4);
     k->mean = (float*)take(B * H * w.A * 4);
     k->stdv = (float*)take(B * H * w.A * 4);
@@ -1586,6 +1597,200 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     }
 }
 
+// ------------------------------------------------------------------------------------------------ split step
+// TOLD.next for narrow launches (one env: 512 / 768 rows), where even 16-row chain workgroups leave most CUs
+// idle and the layered path pays three dependent launches per step. Grid (16-row blocks, SPLIT_S slices, 2 heads):
+// every workgroup computes the full first layer of its head for its 16 rows (K = L + A: cheap), then only its
+// slice of the M x M second layer (M / SPLIT_S columns, one 16-column tile per wave), then the slice's share of
+// the last layer: dynamics z' partial = W3[:, slice] . h2[slice] (K = M / SPLIT_S) into zpart[s], reward partial
+// dot w3[slice] . ELU(h2[slice]) into rpart_s[s]. split_finish_kernel sums the SPLIT_S partials in slice order
+// (+ bias) into X_{t+1}'s latent columns and the return update. Repeating the first layer SPLIT_S times costs
+// ~13 % extra MFMA work at humanoid sizes on a chip that one env leaves mostly idle.
+struct SplitArgs {
+    ChainProb p[2];
+    int rows, M, K1, q1;
+    RowMap amap;
+    const float* X; long x_ts;
+    const float* W3; int n3;                 // dynamics last layer: panel [n3][M]
+    float* zpart; float* rpart; int prow;    // partial buffers (logical rows, row stride prow)
+    // deferred finish of the previous step (zin != null): its partials are summed while staging X_t's latent
+    // quads [zq0, zq0 + Lp/4) (written back to X_t by slice 0's dynamics workgroup), and slice 0's reward
+    // workgroup applies its return update
+    const float* zin; const float* rin; const float* b3d; const float* b3r; int L, Lp, zq0;
+    float* Xw; float* G; float disc_in; int first_in;
+};
+
+__host__ __device__ inline int split_hfl(int K1, int M) { return ((int)rup(K1, 16) > M ? (int)rup(K1, 16) : M) * 16; }
+__host__ __device__ inline int split_lds_floats(int K1, int M) {
+    return split_hfl(K1, M) + (M / SPLIT_S) * 16 + 128 + M + 2 * (M / SPLIT_S);
+}
+
+template <int NT, int D = 4>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) split_step_kernel(const SplitArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, h4 = lane >> 4;
+    const int sl = blockIdx.y, pb = blockIdx.z;
+    const ChainProb& P = a.p[pb];
+    const int M = a.M, SW = M / SPLIT_S;     // slice width = 8 waves x 16 columns
+    const int m0 = blockIdx.x * 16;
+    float* sH = smem;                        // input block, then h1 [M/4][16][4]
+    float* sS = smem + split_hfl(a.K1, M);   // h2 slice [SW/4][16][4]
+    float* red = sS + SW * 16;               // [8][16]
+    float* sb1 = red + 128;                  // [M]
+    float* sb2 = sb1 + M;                    // [SW] second-layer bias of the slice
+    float* sw3 = sb2 + SW;                   // [SW] reward head weights of the slice
+    const int lo = m * 4;
+    const int q1max = (a.K1 >> 2) - 1, qMmax = (M >> 2) - 1;
+    const int g1n = (a.K1 + 15) >> 4;
+    const int f0 = 16 * NT * wave + 4 * h4;
+    const long wblk = (long)(NT / 2) * wave;
+
+    float4 wr[D][NT];
+    ring16_fill<NT, D>(wr, P.W1 + wblk * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1n, h4, q1max);
+    for (int i = tid; i < g1n * 4 * 16; i += 512) {
+        const int row = i & 15, q = i >> 4;
+        const int lm = m0 + row;
+        const int lr = lm < a.rows ? lm : 0;
+        const int xr = map_row(a.amap, lr);
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        const size_t xo = (size_t)(xr >> 5) * a.x_ts + (size_t)(a.q1 + q) * 128 + (xr & 31) * 4;
+        if (a.zin && q >= a.zq0 && q < a.zq0 + (a.Lp >> 2)) {
+            float o[4];
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                const int col = 4 * (q - a.zq0) + cc;
+                if (col < a.L) {
+                    float sz = a.zin[(size_t)lr * a.n3 + col];
+#pragma unroll
+                    for (int sl2 = 1; sl2 < SPLIT_S; ++sl2) sz += a.zin[((size_t)sl2 * a.prow + lr) * a.n3 + col];
+                    o[cc] = sz + a.b3d[col];
+                } else {
+                    o[cc] = 0.f;
+                }
+            }
+            x = make_float4(o[0], o[1], o[2], o[3]);
+            if (sl == 0 && pb == 0 && lm < a.rows) *(float4*)(a.Xw + xo) = x;
+        } else if (q <= q1max) {
+            x = *(const float4*)(a.X + xo);
+        }
+        ((float4*)sH)[i] = x;
+    }
+    if (a.rin && sl == 0 && pb == 1 && tid < 16 && m0 + tid < a.rows) {
+        const int lm = m0 + tid, xr = map_row(a.amap, lm);
+        float r = a.rin[lm];
+#pragma unroll
+        for (int sl2 = 1; sl2 < SPLIT_S; ++sl2) r += a.rin[(size_t)sl2 * a.prow + lm];
+        const float dr = fmul(a.disc_in, r + a.b3r[0]);
+        a.G[xr] = a.first_in ? dr : fadd(a.G[xr], dr);
+    }
+    for (int i = tid; i < M / 4; i += 512) ((float4*)sb1)[i] = ((const float4*)P.b1)[i];
+    for (int i = tid; i < SW / 4; i += 512) {
+        ((float4*)sb2)[i] = ((const float4*)(P.b2 + sl * SW))[i];
+        if (pb == 1) ((float4*)sw3)[i] = ((const float4*)(P.w3v + sl * SW))[i];
+    }
+    lds_barrier();
+
+    // ---- layer 1, all M columns
+    floatx4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    ring16_run<NT, D>(acc, wr, sH, P.W1 + wblk * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1n, lane, q1max);
+    // this wave's 16 columns of the slice in the second layer; its weights in flight during the epilogue
+    const int n2 = sl * SW + 16 * wave;
+    const float* W2p = P.W2 + (size_t)(n2 >> 5) * M * 32 + (n2 & 31) * 4 + lo;
+    float4 w2[D][1];
+    ring16_fill<1, D>(w2, W2p, (long)M * 32, 0, M >> 4, h4, qMmax);
+    lds_barrier();   // every wave is done with the input block
+    {
+        float v[NT * 4];
+        chain16_bias<NT>(v, acc, sb1, f0);
+#pragma unroll
+        for (int i = 0; i < NT * 4; ++i) v[i] = elu_f(v[i]);
+        chain16_store_lds<NT>(sH, v, f0, m);
+    }
+    lds_barrier();
+
+    // ---- layer 2, the slice
+    floatx4 a2[1] = {floatx4{0.f, 0.f, 0.f, 0.f}};
+    ring16_run<1, D>(a2, w2, sH, W2p, (long)M * 32, 0, M >> 4, lane, qMmax);
+    const int c2 = 16 * wave + 4 * h4;       // slice-local feature of a2[0][0]
+    float v2[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v2[k] = elu_f(a2[0][k] + sb2[c2 + k]);
+    if (pb == 1) {
+        // reward: partial dot of the slice, reduced over the row's 4 lanes and the 8 waves
+        float sd = (v2[0] * sw3[c2] + v2[1] * sw3[c2 + 1]) + (v2[2] * sw3[c2 + 2] + v2[3] * sw3[c2 + 3]);
+        sd += __shfl_xor(sd, 16);
+        sd += __shfl_xor(sd, 32);
+        if (lane < 16) red[wave * 16 + lane] = sd;
+        lds_barrier();
+        if (tid < 16 && m0 + tid < a.rows) {
+            float tot = 0.f;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) tot += red[w * 16 + tid];
+            a.rpart[(size_t)sl * a.prow + m0 + tid] = tot;
+        }
+        return;
+    }
+    *(float4*)(sS + ((c2 >> 2) * 16 + m) * 4) = make_float4(v2[0], v2[1], v2[2], v2[3]);
+    lds_barrier();
+    // ---- the slice's share of the last layer: K = the slice's SW columns = 16-k groups [gs0, gs1) of W3
+    const int gs0 = sl * (SW >> 4), gs1 = gs0 + (SW >> 4);
+    for (int t = wave; t < (a.n3 >> 4); t += 8) {
+        const float* W3p = a.W3 + (size_t)(t >> 1) * M * 32 + (t & 1) * 64 + lo;
+        float4 w3[D][1];
+        ring16_fill<1, D>(w3, W3p, (long)M * 32, gs0, gs1, h4, qMmax);
+        floatx4 a3[1] = {floatx4{0.f, 0.f, 0.f, 0.f}};
+        ring16_run<1, D>(a3, w3, sS - (size_t)gs0 * 256, W3p, (long)M * 32, gs0, gs1, lane, qMmax);
+        if (m0 + m < a.rows)
+            *(float4*)(a.zpart + ((size_t)sl * a.prow + m0 + m) * a.n3 + t * 16 + 4 * h4) =
+                make_float4(a3[0][0], a3[0][1], a3[0][2], a3[0][3]);
+    }
+}
+
+struct SplitFinishArgs {
+    int rows; RowMap amap;
+    const float* zpart; const float* rpart; int prow, n3, L, Lp;
+    const float* b3d; const float* b3r;
+    float* Xo; long x_ts; int out_q0;
+    float* G; float* rlast; float disc; int first, last;
+};
+
+// z' = sum_s zpart[s] + b into X_{t+1}'s latent quads (zero past L); reward = sum_s rpart[s] + b, G += disc * r
+// (tdmpc.py:88-90), r_{H-1} kept on the last step. One thread per (row, latent quad | reward).
+__global__ void __launch_bounds__(256) split_finish_kernel(const SplitFinishArgs a) {
+    const int nq = a.Lp / 4;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int row = (int)(i / (nq + 1)), q = (int)(i % (nq + 1));
+    if (row >= a.rows) return;
+    const int xr = map_row(a.amap, row);
+    if (q < nq) {
+        float o[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int col = 4 * q + c;
+            if (col < a.L) {
+                float s = a.zpart[(size_t)row * a.n3 + col];
+#pragma unroll
+                for (int sl = 1; sl < SPLIT_S; ++sl) s += a.zpart[((size_t)sl * a.prow + row) * a.n3 + col];
+                o[c] = s + a.b3d[col];
+            } else {
+                o[c] = 0.f;
+            }
+        }
+        *(float4*)(a.Xo + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.out_q0 + q) * 128 + (xr & 31) * 4) =
+            make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+        float r = a.rpart[row];
+#pragma unroll
+        for (int sl = 1; sl < SPLIT_S; ++sl) r += a.rpart[(size_t)sl * a.prow + row];
+        const float o = r + a.b3r[0];
+        const float dr = fmul(a.disc, o);
+        a.G[xr] = a.first ? dr : fadd(a.G[xr], dr);
+        if (a.last) a.rlast[xr] = o;
+    }
+}
+
 // estimate_value's terminal combination (tdmpc.py:91-92): G + gamma^H min(Q1, Q2), nan_to_num.
 DEVI float qvalue(float G, float q1, float q2, float discH) {
     const float qm = (q1 != q1 || q2 != q2) ? NAN : fminf(q1, q2);   // torch.min keeps NaN
@@ -2605,6 +2810,11 @@ struct Ctx {
     int B, N, P, T, H, A, M, Kx;
     int path;        // TDMPC_PATH_*
     long eps_env, eps_cem_off, eps_iter, eps_term_off, eps_act_off;
+    // split-step finish deferred into the next step's launch (step_next(..., defer = 1))
+    mutable int split_pend = 0, split_par = 0, split_first = 0;
+    mutable float split_disc = 0.f;
+    mutable RowMap split_map = {1 << 30, 0, 0};
+    mutable int split_rows = 0, split_t = 0;
 };
 
 float* Xt(const Ctx& c, int t) { return c.k.X + (size_t)t * c.k.x_stride; }
@@ -2625,7 +2835,7 @@ int chain_wgs_kind(int kind) {
 }
 
 bool use_chain(const Ctx& c, int rows, int nprob, int kind) {
-    if (c.path == TDMPC_PATH_LAYERED || !chain_shape_ok(c.w)) return false;
+    if (c.path == TDMPC_PATH_LAYERED || c.path == TDMPC_PATH_SPLIT || !chain_shape_ok(c.w)) return false;
     const int th = chain_wgs_kind(kind);
     return c.path != TDMPC_PATH_AUTO || (th > 0 && (rows + 31) / 32 * nprob >= th);
 }
@@ -2685,12 +2895,58 @@ Opnd hop(const float* H, const Ctx& c, int q0) { return Opnd{H, (long)2 * c.M * 
 Outp hout(float* H, const Ctx& c, int q0) { return Outp{H, (long)2 * c.M * 32, q0}; }
 Opnd wop(const Ctx& c, size_t off, int K) { return Opnd{c.pw + off, (long)K * 32, 0}; }
 
+// split_step_kernel for a step launch: auto where the chain kernels are not used (narrow launches, TDMPC_SPLIT=0
+// disables), forced by TDMPC_PATH_SPLIT; M = 512 (NT = 4), the rows fit the partial buffers, LDS fits.
+bool use_split(const Ctx& c, int rows) {
+    const Layout& w = c.w;
+    if (w.M != 512 || rows > c.k.split_rows || (size_t)split_lds_floats(w.Kx, w.M) * 4 > 64 * 1024) return false;
+    if (c.path == TDMPC_PATH_SPLIT) return true;
+    if (c.path != TDMPC_PATH_AUTO) return false;
+    static int en = -1;
+    if (en < 0) {
+        const char* e = getenv("TDMPC_SPLIT");
+        en = e ? atoi(e) : 1;
+    }
+    return en && !use_chain(c, rows, 2, CK_STEP);
+}
+
 // One TOLD.next step (tdmpc.py:34-37) for `rows` logical rows mapped onto X rows, plus the return update
 // of estimate_value (:88-90). X_t holds the rows' [a|z] (prep_kernel wrote the sampled actions and z0).
-int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last) {
+// The split step's separate finish launch: partial sums of step t into X_{t+1}'s latent columns and the return.
+int split_finish(const Ctx& c, int t, int rows, RowMap map, const float* zp, const float* rp, float disc, int first,
+                 int last) {
+    const Layout& w = c.w;
+    SplitFinishArgs f;
+    memset(&f, 0, sizeof f);
+    f.rows = rows; f.amap = map; f.zpart = zp; f.rpart = rp; f.prow = c.k.split_rows;
+    f.n3 = w.Lr; f.L = w.L; f.Lp = w.Lp; f.b3d = c.pw + w.b3d; f.b3r = c.pw + w.b3r;
+    f.Xo = Xt(c, t + 1); f.x_ts = (long)c.Kx * 32; f.out_q0 = w.Ap / 4;
+    f.G = c.k.G; f.rlast = c.k.rlast; f.disc = disc; f.first = first; f.last = last;
+    const long nth = (long)rows * (w.Lp / 4 + 1);
+    hipLaunchKernelGGL(split_finish_kernel, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, c.s, f);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// A deferred split finish that no later step launch picked up (a non-split launch comes next): run it now.
+int flush_split(const Ctx& c) {
+    if (!c.split_pend) return 0;
+    c.split_pend = 0;
+    const int par = 1 - c.split_par;
+    const size_t zs = (size_t)SPLIT_S * c.k.split_rows * c.w.Lr, rs = (size_t)SPLIT_S * c.k.split_rows;
+    return split_finish(c, c.split_t, c.split_rows, c.split_map, c.k.zpart + par * zs, c.k.rpart_s + par * rs,
+                        c.split_disc, c.split_first, 0);
+}
+
+// defer = 1 (a loop of consecutive steps over the same rows, nothing reading X_{t+1}'s latents in between): on the
+// split path the finish of this step is folded into the next step's launch.
+int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, int defer = 0) {
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
+    if (c.split_pend && (!use_split(c, rows) || rows != c.split_rows || t != c.split_t + 1 ||
+                         memcmp(&map, &c.split_map, sizeof map)))
+        if ((rc = flush_split(c))) return rc;
     if (use_chain(c, rows, 2, CK_STEP)) {
         ChainArgs a = chain0(c, rows, map, t, c.Kx, 0, 2);
         ChainProb& d = a.p[0];
@@ -2702,6 +2958,37 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         a.Xo = Xt(c, t + 1); a.out_q0 = w.Ap / 4;
         a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
         return launch_chain(CH_STEP, a, 2, c.s);
+    }
+    if (use_split(c, rows)) {
+        const int par = c.split_par;
+        const size_t zs = (size_t)SPLIT_S * c.k.split_rows * w.Lr, rs = (size_t)SPLIT_S * c.k.split_rows;
+        SplitArgs a;
+        memset(&a, 0, sizeof a);
+        a.rows = rows; a.M = M; a.K1 = c.Kx; a.q1 = 0; a.amap = map;
+        a.X = Xt(c, t); a.x_ts = (long)c.Kx * 32;
+        ChainProb& d = a.p[0];
+        d.W1 = c.pw + w.w1x; d.b1 = c.pw + w.b1x; d.W2 = c.pw + w.w2d; d.b2 = c.pw + w.b2d;
+        ChainProb& r = a.p[1];
+        r.W1 = c.pw + w.w1x + (size_t)M * c.Kx; r.b1 = c.pw + w.b1x + M; r.W2 = c.pw + w.w2r; r.b2 = c.pw + w.b2r;
+        r.w3v = c.pw + w.w3r;
+        a.W3 = c.pw + w.w3d; a.n3 = w.Lr;
+        a.zpart = c.k.zpart + par * zs; a.rpart = c.k.rpart_s + par * rs; a.prow = c.k.split_rows;
+        a.b3d = c.pw + w.b3d; a.b3r = c.pw + w.b3r; a.L = w.L; a.Lp = w.Lp; a.zq0 = w.Ap / 4;
+        if (c.split_pend) {   // the previous step's finish, folded into this launch's staging
+            a.zin = c.k.zpart + (1 - par) * zs; a.rin = c.k.rpart_s + (1 - par) * rs;
+            a.Xw = Xt(c, t); a.G = c.k.G; a.disc_in = c.split_disc; a.first_in = c.split_first;
+        }
+        const size_t lds = (size_t)split_lds_floats(c.Kx, M) * 4;
+        hipLaunchKernelGGL((split_step_kernel<4>), dim3((rows + 15) / 16, SPLIT_S, 2), dim3(512), lds, c.s, a);
+        HIPCHK(hipGetLastError());
+        c.split_pend = 0;
+        c.split_par = 1 - par;
+        if (defer && !last) {
+            c.split_pend = 1; c.split_disc = disc; c.split_first = first;
+            c.split_map = map; c.split_rows = rows; c.split_t = t;
+            return 0;
+        }
+        return split_finish(c, t, rows, map, a.zpart, a.rpart, disc, first, last);
     }
     {   // h1 = ELU(W1[d;r] [a|z] + b)   (dynamics.0 and reward.0 fused: N = 2M)
         LinArgs a = args0();
@@ -3133,7 +3420,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     int rc;
     const int H = prm->horizon, I = prm->iterations, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 4) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 5) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T;
     // z0 = h(obs) and mean = 0 (warm: prev_mean shifted), std = 2
@@ -3177,7 +3464,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
         if (i > 0 && (rc = prep(c, noise, i, nullptr))) return rc;
         if (i > 0 || P == 0)
             for (int t = 0; t < H; ++t)
-                if ((rc = step_next(c, t, B * N, rm, prm->discount_pow[t], t == 0, t == H - 1)))
+                if ((rc = step_next(c, t, B * N, rm, prm->discount_pow[t], t == 0, t == H - 1, 1)))
                     return rc;
         if ((rc = policy(c, H, B * T, all, noise, c.eps_env, T, c.eps_cem_off + (long)i * c.eps_iter + c.eps_term_off,
                          prm->min_std)))
@@ -3215,7 +3502,7 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
     const int H = prm->horizon, I = prm->iterations, B = prm->batch, K = d->num_elites;
     if (I <= 0 || I > 16) { snprintf(g_err, sizeof g_err, "iCEM: 1..16 iterations"); return TDMPC_E_DIMS; }
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream, K))) return rc;
-    if (prm->path < 0 || prm->path > 4) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 5) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = d->num_samples, Pmax = d->num_pi, Tw = N + K + Pmax, pi_base = N + K, P0 = prm->n_pi0;
     c.T = Tw;
@@ -3285,7 +3572,7 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
         // rollout of the sampled + reused rows (the pi rows' is cached from the pre-rollout)
         const RowMap blk = {NE, Tw, 0};
         for (int t = 0; t < H; ++t)
-            if ((rc = step_next(c, t, B * NE, blk, prm->discount_pow[t], t == 0, t == H - 1))) return rc;
+            if ((rc = step_next(c, t, B * NE, blk, prm->discount_pow[t], t == 0, t == H - 1, 1))) return rc;
         // terminal value of all T_i = NE + Pi candidates: pi(z_H) with this iteration's noise, Q
         const RowMap pmi = {Pi, Tw, pi_base};
         if ((rc = policy(c, H, B * NE, blk, noise, env, NE, prm->term_off[i], prm->min_std))) return rc;
@@ -3313,7 +3600,7 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 4) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 5) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     if (rows != c.T) { snprintf(g_err, sizeof g_err, "rows must equal N+P"); return TDMPC_E_DIMS; }
     const int T = c.T, L = c.w.L;

@@ -1,4 +1,4 @@
-"""Generate tests/golden/aug_pixels.npz by running the REFERENCE `helper.RandomShiftsAug` in this container.
+"""Generate tests/golden/learner_aug_pixels.npz by running the REFERENCE `helper.RandomShiftsAug` in this container.
 
 Run once in the build container (where /root/reference exists):   python tests/golden/make_aug_golden.py
 Imports the reference like make_golden.py (rlpyt stub; CPU). Inputs: seeded uint8-valued float frames, a 4-D
@@ -33,9 +33,9 @@ def main():
     y4 = aug(torch.from_numpy(x4)).numpy()
     torch.manual_seed(11)
     y5 = aug(torch.from_numpy(x5)).numpy()
-    np.savez_compressed(os.path.join(HERE, "aug_pixels.npz"), x4=x4.astype(np.uint8), y4=y4,
+    np.savez_compressed(os.path.join(HERE, "learner_aug_pixels.npz"), x4=x4.astype(np.uint8), y4=y4,
                         x5=x5.astype(np.uint8), y5=y5)
-    print("wrote aug_pixels.npz", y4.shape, y5.shape)
+    print("wrote learner_aug_pixels.npz", y4.shape, y5.shape)
 
 
 if __name__ == "__main__":

@@ -163,10 +163,10 @@ def test_cpu_batched_learner_matches_oracle():
 
 def test_random_shifts_aug_matches_reference():
     """tdmpc_amd.learner.RandomShiftsAug (helper.py:250-283) against the reference module's outputs on the same
-    frames and torch seed (tests/golden/aug_pixels.npz, make_aug_golden.py): 4-D and 5-D (horizon) batches."""
+    frames and torch seed (tests/golden/learner_aug_pixels.npz, make_aug_golden.py): 4-D and 5-D (horizon) batches."""
     from types import SimpleNamespace
     from tdmpc_amd.learner import RandomShiftsAug
-    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "aug_pixels.npz"))
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "learner_aug_pixels.npz"))
     aug = RandomShiftsAug(SimpleNamespace(img_size=84, modality="pixels"))
     for k in ("4", "5"):
         torch.manual_seed(11)
