@@ -159,7 +159,7 @@ struct Work {
     float* rlast;    // [B*T] reward at t = H-1
     float* value;    // [B*T]
     float* qv;       // [2][xrows] Q-head outputs of the chain path
-    float* zpart;    // [2][SPLIT_S][split_rows][Lr] split-step partial z' (split_step_kernel), two step parities
+    float* zpart;    // [2][SPLIT_S][split_rows][max(Lr, Ar)] split-step partial z' / pi outputs, two parities
     float* rpart_s;  // [2][SPLIT_S][split_rows] split-step partial reward dots
     int split_rows;  // rows the split partial buffers hold (min(xrows, SPLIT_MAX_ROWS))
     float* z0;       // [B][Lp] dense
@@ -196,7 +196,7 @@ void make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k, int ex
     k->value = (float*)take(B * T * 4);
     k->qv = (float*)take(2 * (size_t)k->xrows * 4);
     k->split_rows = std::min(k->xrows, SPLIT_MAX_ROWS);
-    k->zpart = (float*)take((size_t)2 * SPLIT_S * k->split_rows * w.Lr * 4);
+    k->zpart = (float*)take((size_t)2 * SPLIT_S * k->split_rows * std::max(w.Lr, w.Ar) * 4);
     k->rpart_s = (float*)take((size_t)2 * SPLIT_S * k->split_rows * 4);
     k->z0 = (float*)take(B * w.Lp * 4);
     k->mean = (float*)take(B * H * w.A * 4);
@@ -1791,6 +1791,46 @@ __global__ void __launch_bounds__(256) split_finish_kernel(const SplitFinishArgs
     }
 }
 
+struct SplitPiArgs {
+    int rows; RowMap amap;
+    const float* part; int prow, n3, A, Ap;
+    const float* b3;
+    float* Xo; long x_ts;
+    const float* eps; int eps_G; long eps_env; long eps_off; float min_std, lo, hi;
+};
+
+// The split pi head's finish: mu = tanh(sum_s part[s] + b) and the TruncatedNormal sample (tdmpc.py:39-45,
+// helper.py:86-96; the chain CH_PI epilogue's exact arithmetic) into X_t's action quads. One thread per
+// (row, action quad).
+__global__ void __launch_bounds__(256) split_pi_finish_kernel(const SplitPiArgs a) {
+    const int nq = a.Ap / 4;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int row = (int)(i / nq), q = (int)(i % nq);
+    if (row >= a.rows) return;
+    const int xr = map_row(a.amap, row);
+    const int e = row / a.eps_G, rr = row % a.eps_G;
+    const float* ep = a.eps + (size_t)e * a.eps_env + a.eps_off + (size_t)rr * a.A;
+    float o[4];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+        const int col = 4 * q + cc;
+        float x = 0.f;
+        if (col < a.A) {
+            float sv = a.part[(size_t)row * a.n3 + col];
+#pragma unroll
+            for (int sl = 1; sl < SPLIT_S; ++sl) sv += a.part[((size_t)sl * a.prow + row) * a.n3 + col];
+            const float muv = tanhf(sv + a.b3[col]);
+            x = muv;
+            if (a.min_std > 0.f) {
+                const float ee = tclamp(fmul(ep[col], a.min_std), -0.3f, 0.3f);
+                x = tclamp(fadd(muv, ee), a.lo, a.hi);
+            }
+        }
+        o[cc] = x;
+    }
+    *(float4*)(a.Xo + (size_t)(xr >> 5) * a.x_ts + (size_t)q * 128 + (xr & 31) * 4) = make_float4(o[0], o[1], o[2], o[3]);
+}
+
 // estimate_value's terminal combination (tdmpc.py:91-92): G + gamma^H min(Q1, Q2), nan_to_num.
 DEVI float qvalue(float G, float q1, float q2, float discH) {
     const float qm = (q1 != q1 || q2 != q2) ? NAN : fminf(q1, q2);   // torch.min keeps NaN
@@ -2910,6 +2950,20 @@ bool use_split(const Ctx& c, int rows) {
     return en && !use_chain(c, rows, 2, CK_STEP);
 }
 
+// split_step_kernel for the pi head (grid z = 1: no reward head; its finish is split_pi_finish_kernel).
+bool use_split_pi(const Ctx& c, int rows) {
+    const Layout& w = c.w;
+    if (w.M != 512 || rows > c.k.split_rows || (size_t)split_lds_floats(w.Lp, w.M) * 4 > 64 * 1024) return false;
+    if (c.path == TDMPC_PATH_SPLIT) return true;
+    if (c.path != TDMPC_PATH_AUTO) return false;
+    static int en = -1;
+    if (en < 0) {
+        const char* e = getenv("TDMPC_SPLIT_PI");
+        en = e ? atoi(e) : 1;
+    }
+    return en && !use_chain(c, rows, 1, CK_PI);
+}
+
 // One TOLD.next step (tdmpc.py:34-37) for `rows` logical rows mapped onto X rows, plus the return update
 // of estimate_value (:88-90). X_t holds the rows' [a|z] (prep_kernel wrote the sampled actions and z0).
 // The split step's separate finish launch: partial sums of step t into X_{t+1}'s latent columns and the return.
@@ -2933,7 +2987,7 @@ int flush_split(const Ctx& c) {
     if (!c.split_pend) return 0;
     c.split_pend = 0;
     const int par = 1 - c.split_par;
-    const size_t zs = (size_t)SPLIT_S * c.k.split_rows * c.w.Lr, rs = (size_t)SPLIT_S * c.k.split_rows;
+    const size_t zs = (size_t)SPLIT_S * c.k.split_rows * std::max(c.w.Lr, c.w.Ar), rs = (size_t)SPLIT_S * c.k.split_rows;
     return split_finish(c, c.split_t, c.split_rows, c.split_map, c.k.zpart + par * zs, c.k.rpart_s + par * rs,
                         c.split_disc, c.split_first, 0);
 }
@@ -2961,7 +3015,7 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
     }
     if (use_split(c, rows)) {
         const int par = c.split_par;
-        const size_t zs = (size_t)SPLIT_S * c.k.split_rows * w.Lr, rs = (size_t)SPLIT_S * c.k.split_rows;
+        const size_t zs = (size_t)SPLIT_S * c.k.split_rows * std::max(w.Lr, w.Ar), rs = (size_t)SPLIT_S * c.k.split_rows;
         SplitArgs a;
         memset(&a, 0, sizeof a);
         a.rows = rows; a.M = M; a.K1 = c.Kx; a.q1 = 0; a.amap = map;
@@ -3038,6 +3092,30 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
         a.eps = eps; a.eps_G = eps_G; a.eps_env = eps_env; a.eps_off = eps_off; a.A = w.A;
         a.min_std = min_std; a.lo = (float)(-1.0 + 1e-6); a.hi = (float)(1.0 - 1e-6);
         return launch_chain(CH_PI, a, 1, c.s);
+    }
+    if (use_split_pi(c, rows)) {
+        if ((rc = flush_split(c))) return rc;
+        SplitArgs a;
+        memset(&a, 0, sizeof a);
+        a.rows = rows; a.M = M; a.K1 = w.Lp; a.q1 = w.Ap / 4; a.amap = map;
+        a.X = Xt(c, t); a.x_ts = (long)c.Kx * 32;
+        ChainProb& p = a.p[0];
+        p.W1 = c.pw + w.wp1; p.b1 = c.pw + w.bp1; p.W2 = c.pw + w.wp2; p.b2 = c.pw + w.bp2;
+        a.W3 = c.pw + w.wp3; a.n3 = w.Ar;
+        a.zpart = c.k.zpart; a.rpart = c.k.rpart_s; a.prow = c.k.split_rows;
+        const size_t lds = (size_t)split_lds_floats(w.Lp, M) * 4;
+        hipLaunchKernelGGL((split_step_kernel<4>), dim3((rows + 15) / 16, SPLIT_S, 1), dim3(512), lds, c.s, a);
+        HIPCHK(hipGetLastError());
+        SplitPiArgs f;
+        memset(&f, 0, sizeof f);
+        f.rows = rows; f.amap = map; f.part = c.k.zpart; f.prow = c.k.split_rows; f.n3 = w.Ar; f.A = w.A;
+        f.Ap = w.Ap; f.b3 = c.pw + w.bp3; f.Xo = Xt(c, t); f.x_ts = (long)c.Kx * 32;
+        f.eps = eps; f.eps_G = eps_G; f.eps_env = eps_env; f.eps_off = eps_off; f.min_std = min_std;
+        f.lo = (float)(-1.0 + 1e-6); f.hi = (float)(1.0 - 1e-6);
+        const long nth = (long)rows * (w.Ap / 4);
+        hipLaunchKernelGGL(split_pi_finish_kernel, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, c.s, f);
+        HIPCHK(hipGetLastError());
+        return 0;
     }
     {
         LinArgs a = args0();
