@@ -259,13 +259,29 @@ def icem_bench(cfg, dev, cpu=True, steps=20):
 
     dt, agent = timed("device")
     dt_ref, _ = timed("reference")
+    # vectorised: 32 envs per call (TdICEM.plan_batch), the chain kernels' regime
+    Bv = 32
+    ab = TdICEM(icfg, max_batch=Bv, rng="device")
+    ab.model.load_state_dict(synthetic_state_dict(icfg, 0, enc_norm=True))
+    ab.std = 0.05
+    ob = torch.from_numpy(synthetic_obs(icfg, Bv, seed=0))
+    for i in range(3):
+        ab.plan_batch(ob, step=step, t0=(i == 0), sync_metrics=False)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for i in range(steps):
+        ab.plan_batch(ob, step=step, t0=False, sync_metrics=False)
+    torch.cuda.synchronize()
+    dtb = (time.perf_counter() - t) / steps
     out = {"config": f"{icfg.task}: N={icfg.num_samples} (x1/{icfg.factor_decrease_num} per iteration) H={icfg.horizon} "
                      f"iters={icfg.iterations} K={icfg.num_elites} reuse={agent.E_max} elites, 1 env per call, "
                      "all noise drawn on the device (rng='device', inside the timed call)",
            "value": round(1.0 / dt, 2), "unit": "plan-steps/s", "ms_per_step": round(dt * 1e3, 3),
            "reference_rng": {"value": round(1.0 / dt_ref, 2), "ms_per_step": round(dt_ref * 1e3, 3),
                              "note": "noise drawn in the reference's order on torch's / numpy's global "
-                                     "generators (host numpy coloured noise included)"}}
+                                     "generators (host numpy coloured noise included)"},
+           "batch32": {"value": round(Bv / dtb, 2), "unit": "plan-steps/s", "ms_per_step": round(dtb * 1e3, 3),
+                       "note": "TdICEM.plan_batch, 32 envs per call, device RNG"}}
     if cpu:
         from oracle import icem_ref
         from oracle.tdmpc_ref import RefTOLD

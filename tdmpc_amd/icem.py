@@ -185,10 +185,11 @@ class TdICEM:
         out.sort(key=lambda t: t[0])
         return np.concatenate([a.reshape(-1) for _, a in out]) if out else np.zeros(0, np.float32)
 
-    def _device_plan(self, H, cts, off, reuse):
-        """rng 'device': per sample length, a BatchedColoredNoise over that length's coloured specs and the
-        stream positions [R, H] its rows land on (samp thirds [H][n][A] at their column offset, reuse tail)."""
-        key = (H, tuple(cts), reuse)
+    def _device_plan(self, H, cts, off, reuse, B=1):
+        """rng 'device': per sample length, a BatchedColoredNoise over that length's coloured specs of B envs and
+        the stream positions [R, H] its rows land on (samp thirds [H][n][A] at their column offset, reuse tail;
+        env e's stream at e * off['total'])."""
+        key = (H, tuple(cts), reuse, B)
         plan = self._dev_plans.get(key)
         if plan is not None:
             return plan
@@ -206,8 +207,9 @@ class TdICEM:
             a = np.arange(A)[None, :, None]
             pos = base + t * rows * A + (c0 + r) * A + a                   # [n, A, H]
             g = groups.setdefault(L, ([], []))
-            g[0].append((beta, n))
-            g[1].append(pos.reshape(n * A, H))
+            for e in range(B):
+                g[0].append((beta, n))
+                g[1].append(pos.reshape(n * A, H) + e * off["total"])
         plan = []
         for L, (sp, pos) in sorted(groups.items()):
             plan.append((BatchedColoredNoise(sp, A, L, H, self.device),
@@ -216,6 +218,14 @@ class TdICEM:
             self._dev_plans.clear()
         self._dev_plans[key] = plan
         return plan
+
+    def _draw_device(self, B, H, cts, off, reuse):
+        """rng 'device' for B envs: the B streams white in one draw, every coloured third / reuse tail overwritten
+        from one batched spectrum draw per sample length, the picks' uniforms: ~8 launches per call."""
+        self.noise[:B * off["total"]].normal_()
+        for gen, pos in self._device_plan(H, cts, off, reuse, B):
+            self.noise[pos] = gen.draw()
+        self.u[:B].uniform_()
 
     def _draw(self, e, H, cts, off, reuse, eval_mode):
         """Env e's stream in the reference's draw order on torch's (device) and numpy's global generators.
@@ -226,14 +236,6 @@ class TdICEM:
         buf = self.noise[e * S:(e + 1) * S]
         dev = self.device
         specs = self._colored_specs(H, cts, reuse)
-        if self.rng == "device":
-            # the whole stream white in one draw, then every coloured third / reuse tail overwritten from one
-            # batched spectrum draw per sample length, then the pick's uniform: ~8 launches per call
-            buf.normal_()
-            for gen, pos in self._device_plan(H, cts, off, reuse):
-                buf[pos] = gen.draw()
-            self.u[e:e + 1].uniform_()
-            return None
         host = self._colored_host(specs, H)
         u = float(np.random.random_sample())
         if self._h2d_done is not None:
@@ -295,6 +297,30 @@ class TdICEM:
         metrics = {"external_reward_mean": 0.0, "current_std": 0.0}
         if step < cfg.seed_steps and not eval_mode:
             return torch.empty(cfg.action_dim, dtype=torch.float32, device=self.device).uniform_(-1, 1), metrics
+        obs = torch.as_tensor(np.asarray(obs), dtype=torch.float32).view(1, -1)
+        a, m = self._plan_envs(obs, eval_mode, step, t0, [noise] if noise is not None else None, trace)
+        m = m[0].double().cpu().numpy()
+        metrics.update({"external_reward_mean": float(m[0]), "current_std": float(m[1])})
+        return a[0].clone(), metrics
+
+    @torch.no_grad()
+    def plan_batch(self, obs, eval_mode=False, step=None, t0=True, sync_metrics=True):
+        """B independent iCEM plans in one call (vectorised envs, all at the same step / t0): obs [B, obs_dim] ->
+        (actions [B, A], metrics). Env e's result equals a single-env plan() on its own noise stream
+        (tests/test_icem.py::test_gpu_icem_batched_equals_single). Seed steps are not batched."""
+        if step < self.cfg.seed_steps and not eval_mode:
+            raise ValueError("plan_batch: seed steps draw uniform actions; call plan() per env")
+        obs = torch.as_tensor(obs, dtype=torch.float32)
+        a, m = self._plan_envs(obs.view(obs.shape[0], -1), eval_mode, step, t0, None, None)
+        if not sync_metrics:
+            return a, m
+        return a, [{"external_reward_mean": float(r), "current_std": float(sd)} for r, sd in m.double().cpu().numpy()]
+
+    def _plan_envs(self, obs, eval_mode, step, t0, noise, trace):
+        cfg = self.cfg
+        B = obs.shape[0]
+        if B > self.max_batch:
+            raise ValueError(f"batch {B} > max_batch {self.max_batch}")
         horizon = int(min(cfg.horizon, linear_schedule(cfg.horizon_schedule, step)))
         extend = False
         if horizon != self.plan_horizon and t0:
@@ -314,12 +340,17 @@ class TdICEM:
             raise RuntimeError("elite horizon mismatch")   # the reference's torch.cat would fail here
         off = self._layout(H, cts, reuse)
         pack_told(self, self.model)
-        self.obs_buf[:1].copy_(torch.as_tensor(np.asarray(obs), dtype=torch.float32).view(1, -1))
-        u = self._draw(0, H, cts, off, reuse, eval_mode) if noise is None else self._load(0, H, cts, off, reuse, noise)
-        if u is not None:
-            self.u[:1].fill_(u)
+        self.obs_buf[:B].copy_(obs.to(self.device))
+        if noise is not None:
+            for e, nz in enumerate(noise):
+                self.u[e:e + 1].fill_(self._load(e, H, cts, off, reuse, nz))
+        elif self.rng == "device":
+            self._draw_device(B, H, cts, off, reuse)
+        else:
+            us = [self._draw(e, H, cts, off, reuse, eval_mode) for e in range(B)]
+            self.u[:B].copy_(torch.tensor(us, dtype=torch.float64))
         p = _lib.IcemParams()
-        p.horizon, p.iterations, p.batch = H, cfg.iterations, 1
+        p.horizon, p.iterations, p.batch = H, cfg.iterations, B
         p.warm_start = int((not t0) and self._has_prev)
         p.eval_mode = int(eval_mode)
         p.has_elites = int(reuse)
@@ -339,8 +370,8 @@ class TdICEM:
         value_out = mean_out = std_out = None
         if trace is not None:
             Tw = cfg.num_samples + cfg.num_elites + self.P_max
-            value_out = torch.zeros(1, cfg.iterations, Tw, device=dev)
-            mean_out = torch.zeros(1, cfg.iterations, H, cfg.action_dim, device=dev)
+            value_out = torch.zeros(B, cfg.iterations, Tw, device=dev)
+            mean_out = torch.zeros(B, cfg.iterations, H, cfg.action_dim, device=dev)
             std_out = torch.zeros_like(mean_out)
         stream = torch.cuda.current_stream(dev).cuda_stream
         rc = self.L.tdmpc_plan_icem(
@@ -357,6 +388,4 @@ class TdICEM:
         self._has_prev = True
         self._has_elites = True
         self._elite_H = H
-        m = self.metrics[0].double().cpu().numpy()
-        metrics.update({"external_reward_mean": float(m[0]), "current_std": float(m[1])})
-        return self.action[0].clone(), metrics
+        return self.action[:B], self.metrics[:B]

@@ -194,3 +194,40 @@ def test_device_rng_positions_cover_colored_slots():
     got = np.concatenate([pos.numpy().reshape(-1) for _, pos in agent._device_plan(H, cts, off, True)])
     assert len(got) == len(set(got.tolist())) == len(want)
     assert set(got.tolist()) == want
+    # B envs: env e's slots shifted by e streams, each exactly once
+    got3 = np.concatenate([pos.numpy().reshape(-1) for _, pos in agent._device_plan(H, cts, off, True, B=3)])
+    want3 = {w + e * off["total"] for e in range(3) for w in want}
+    assert len(got3) == len(set(got3.tolist())) == len(want3) and set(got3.tolist()) == want3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["chain16", "layered", "split"])
+def test_gpu_icem_batched_equals_single(path):
+    """TdICEM.plan_batch over 3 envs (each its own observation and noise stream) equals 3 single-env plans on the
+    same draws, bitwise, over a cold call and a warm call with elite reuse (forced kernel path: the same kernels
+    at both widths)."""
+    from tdmpc_amd.icem import TdICEM
+    cfg = icem_cfg()
+    sd = synthetic_state_dict(cfg, 41, enc_norm=True)
+    B, step = 3, 10**6
+    rs = np.random.RandomState(5)
+    obs = rs.standard_normal((B, cfg.obs_shape[0])).astype(np.float32)
+    st = icem_ref.IcemState(0.05)
+    st.plan_horizon = icem_ref.next_horizon(cfg, st, step, True)[0]
+    torch.manual_seed(12)
+    np.random.seed(13)
+    calls = []
+    for t0 in (True, False):
+        calls.append((t0, [icem_ref.draw_icem_noise(cfg, st, step, t0, False, device="cuda") for _ in range(B)]))
+        st.elite_actions = torch.zeros(st.plan_horizon, cfg.num_elites, cfg.action_dim)
+    batched = TdICEM(cfg, max_batch=B, path=path)
+    singles = [TdICEM(cfg, path=path) for _ in range(B)]
+    for ag in [batched] + singles:
+        ag.model.load_state_dict(sd)
+        ag.std = 0.05
+    for t0, nzs in calls:
+        a, _ = batched._plan_envs(torch.from_numpy(obs), False, step, t0, nzs, None)
+        for e in range(B):
+            a1, _ = singles[e].plan(obs[e], step=step, t0=t0, noise=nzs[e])
+            assert torch.equal(a[e], a1), (t0, e)
+        assert torch.equal(batched.elites[:B, :batched._elite_H], torch.stack([s.elites[0, :s._elite_H] for s in singles]))

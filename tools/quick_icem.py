@@ -29,6 +29,9 @@ for path in ("auto", "chain", "layered"):
     torch.cuda.synchronize()
     t = time.perf_counter()
     for i in range(K):
-        agent._draw(0, H, cts, off, True, False)
+        if rng == "device":
+            agent._draw_device(1, H, cts, off, True)
+        else:
+            agent._draw(0, H, cts, off, True, False)
     torch.cuda.synchronize()
     print(f"noise draws: {(time.perf_counter() - t) / K * 1e3:.3f} ms/call")
