@@ -217,6 +217,29 @@ def test_plan_fullsize_vs_oracle(path):
         np.testing.assert_allclose(tr["std"][0, -1].cpu().numpy(), rtr["std"][-1].numpy(), atol=2e-5, rtol=0)
 
 
+@pytest.mark.parametrize("path", PATHS)
+def test_plan_ragged_vs_oracle(path):
+    """Ragged shapes: N = 77 candidates (P = 38, T = 115 rows: partial 16- and 32-row blocks), K = 13, 3 envs in
+    one call (rows of env e at e*T: blocks straddle envs), dog dims (A = 38: 10 action quads), vs the oracle."""
+    cfg = make_cfg("dog", num_samples=77, num_elites=13, iterations=3, horizon=4)
+    B = 3
+    agent = _agent(cfg, 17, B=B, path=path)
+    told = tdmpc_ref.RefTOLD(synthetic_state_dict(cfg, 17), cfg)
+    rs = np.random.RandomState(8)
+    obs = rs.standard_normal((B, cfg.obs_shape[0])).astype(np.float32)
+    torch.manual_seed(3)
+    np.random.seed(3)
+    noises = [tdmpc_ref.draw_noise(cfg, 10**6, False) for _ in range(B)]
+    tr = {}
+    a, m = agent._plan_envs(obs, False, 10**6, [True] * B, trace=tr, noise=noises)
+    for e in range(B):
+        st, rtr = tdmpc_ref.PlanState(0.05), {}
+        ra, rm = tdmpc_ref.plan(told, cfg, st, obs[e], noises[e], eval_mode=False, step=10**6, t0=True, trace=rtr)
+        ref_vals = torch.stack(rtr["value"]).squeeze(-1).numpy()
+        if _compare_iterations(tr["value"][e].cpu().numpy(), ref_vals, cfg.num_elites):
+            np.testing.assert_allclose(a[e].cpu().numpy(), ra.numpy(), atol=2e-5, rtol=0)
+
+
 def test_bench_batch_vs_oracle():
     """The bench workload's shape: 8 humanoid envs in one plan_batch call (auto path: the row-block chain
     kernels at 4096 / 6144 rows), every env against the oracle on its own noise."""
