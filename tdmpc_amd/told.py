@@ -6,8 +6,7 @@ Reference: `TOLD` in `src/algorithm/tdmpc.py:9-50`, built from `helper.enc` (`he
 The module exists so that a reference checkpoint (`{'model': sd, 'model_target': sd}`, `tdmpc.py:68-81`)
 loads with `load_state_dict` unchanged and so that `TDMPC.model` exposes the same attributes. Planning does
 NOT run these modules: `TDMPC.plan` packs the parameters into one device buffer and runs the HIP kernels.
-The eager `forward`-style helpers (`h`, `next`, `pi`, `Q`) are kept for inspection and for the learner,
-which is outside this round's scope.
+The `forward`-style helpers (`h`, `next`, `pi`, `Q`) are what the learner (tdmpc_amd.learner) differentiates.
 """
 from __future__ import annotations
 
