@@ -1,0 +1,42 @@
+/*
+ * tdmpc_learner.h -- C ABI of the learner's fused loss in libtdmpc_hip.so.
+ *
+ * Replaces the loss composition of TDMPC.update (/root/reference/src/algorithm/tdmpc.py:209-224: the rho-weighted
+ * consistency / reward / value / priority losses over the horizon, the 1e4 clamps, the coefficient sum, the
+ * IS-weighted mean) and its backward: ~60 one-op ATen launches per update become three HIP launches. Inputs are
+ * the horizon-batched tensors of tdmpc_amd.learner (row-major, contiguous, float32, device pointers):
+ *   zp [H][B][L] predicted latents z_{t+1}, nz [H][B][L] target-encoder latents, q1 q2 rp [H][B] Q heads and
+ *   reward head, rw [H][B] rewards, td [H][B] TD targets, w [B] importance weights, rho [H] = float32(rho**t).
+ * Stream-ordered, no allocation, graph-capturable; 0 or a negative TDMPC_E* code.
+ */
+#ifndef TDMPC_LEARNER_H
+#define TDMPC_LEARNER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tdmpc_loss_args {
+    const float* zp; const float* nz; const float* q1; const float* q2; const float* rp; const float* rw;
+    const float* td; const float* w; const float* rho;
+    int32_t H, B, L;
+    float consistency_coef, reward_coef, value_coef;
+} tdmpc_loss_args;
+
+/* Forward. rows [5][B]: consistency, reward, value losses, priority loss clamped at 1e4, total loss per row;
+ * scal [6]: mean consistency, mean reward, mean value, mean total, weighted = mean(total) * mean(w) (the
+ * reference's mean over its [B, B] broadcast of total [B, 1] * w [B]), mean(w). */
+int tdmpc_loss_forward(const tdmpc_loss_args* a, float* rows, float* scal, void* stream);
+
+/* Backward of `weighted`: gw (device scalar) = dL/dweighted (the 1/H hook already applied). Writes dzp [H][B][L],
+ * dq1, dq2, drp [H][B] (any may be null: not computed). rows / scal: the forward's outputs. */
+int tdmpc_loss_backward(const tdmpc_loss_args* a, const float* rows, const float* scal, const float* gw,
+                        float* dzp, float* dq1, float* dq2, float* drp, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -19,7 +19,9 @@ EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc
             "tdmpc_profile_begin", "tdmpc_profile_end", "tdmpc_icem_sizes_for", "tdmpc_plan_icem",
             # include/tdmpc_replay.h
             "tdmpc_replay_workspace_bytes", "tdmpc_replay_add_priorities", "tdmpc_replay_update_priorities",
-            "tdmpc_replay_sample")
+            "tdmpc_replay_sample",
+            # include/tdmpc_learner.h
+            "tdmpc_loss_forward", "tdmpc_loss_backward")
 
 
 class Dims(C.Structure):
@@ -55,6 +57,12 @@ class ReplayDims(C.Structure):
 class ReplayStore(C.Structure):
     _fields_ = [("obs", C.c_void_p), ("last_obs", C.c_void_p), ("action", C.c_void_p), ("reward", C.c_void_p),
                 ("priorities", C.c_void_p)]
+
+
+class LossArgs(C.Structure):   # tdmpc_loss_args (include/tdmpc_learner.h)
+    _fields_ = [(n, C.c_void_p) for n in ("zp", "nz", "q1", "q2", "rp", "rw", "td", "w", "rho")] + \
+               [("H", C.c_int32), ("B", C.c_int32), ("L", C.c_int32), ("consistency_coef", C.c_float),
+                ("reward_coef", C.c_float), ("value_coef", C.c_float)]
 
 
 class Sizes(C.Structure):
@@ -99,6 +107,8 @@ def lib():
     L.tdmpc_replay_update_priorities.argtypes = [C.POINTER(ReplayDims), vp, vp, vp, i32, C.c_float, vp]
     L.tdmpc_replay_sample.argtypes = [C.POINTER(ReplayDims), C.POINTER(ReplayStore), i32, i32, C.c_float,
                                       C.c_float, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
+    L.tdmpc_loss_forward.argtypes = [C.POINTER(LossArgs), vp, vp, vp]
+    L.tdmpc_loss_backward.argtypes = [C.POINTER(LossArgs), vp, vp, vp, vp, vp, vp, vp, vp]
     for name in EXPORTED:
         if not hasattr(L, name):
             raise RuntimeError(f"{LIB_PATH} does not export {name}")

@@ -11,7 +11,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-SRCS = [os.path.join(HERE, "csrc", "tdmpc_kernels.hip"), os.path.join(HERE, "csrc", "replay_kernels.hip")]
+SRCS = [os.path.join(HERE, "csrc", "tdmpc_kernels.hip"), os.path.join(HERE, "csrc", "replay_kernels.hip"),
+        os.path.join(HERE, "csrc", "learner_kernels.hip")]
 OUT = os.path.join(HERE, "libtdmpc_hip.so")
 ARCH = os.environ.get("TDMPC_OFFLOAD_ARCH", "gfx950")
 
@@ -24,7 +25,7 @@ def hipcc() -> str:
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
-    deps = SRCS + [os.path.join(REPO, "include", "tdmpc_hip.h"), os.path.join(REPO, "include", "tdmpc_replay.h")]
+    deps = SRCS + [os.path.join(REPO, "include", h) for h in ("tdmpc_hip.h", "tdmpc_replay.h", "tdmpc_learner.h")]
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
     tmp = OUT + ".tmp"

@@ -24,6 +24,8 @@ into ONE HIP graph per (buffer fill, EMA) shape and replayed: no Python in the l
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 import torch.nn.functional as F
 
@@ -59,6 +61,49 @@ class RandomShiftsAug(torch.nn.Module):
         if shape_len == 5:
             shifted = shifted.reshape(t, n, c, hh, ww)
         return shifted
+
+
+class _FusedLoss(torch.autograd.Function):
+    """TDMPC.update's loss composition (tdmpc.py:209-224) and its backward as HIP kernels (include/tdmpc_learner.h):
+    forward(zp, nz, q1, q2, rp, rw, td, w, rho) -> (scal [6], rows [5, B]); scal = (mean consistency, mean reward,
+    mean value, mean total, weighted, mean w), rows = (consistency, reward, value, clamped priority, total) per
+    batch row. Only scal[4] (the weighted loss) carries a gradient."""
+
+    @staticmethod
+    def forward(ctx, zp, nz, q1, q2, rp, rw, td, w, rho, coefs):
+        from . import _lib
+        H, B, L = zp.shape
+        ins = [t.detach().contiguous() for t in (zp, nz, q1, q2, rp, rw, td, w, rho)]
+        args = _lib.LossArgs(*[t.data_ptr() for t in ins], H, B, L, *coefs)
+        rows = torch.empty(5, B, dtype=torch.float32, device=zp.device)
+        scal = torch.empty(6, dtype=torch.float32, device=zp.device)
+        stream = torch.cuda.current_stream(zp.device).cuda_stream
+        _lib.check(_lib.lib().tdmpc_loss_forward(C.byref(args), C.c_void_p(rows.data_ptr()),
+                                                  C.c_void_p(scal.data_ptr()), C.c_void_p(stream)),
+                   "tdmpc_loss_forward")
+        ctx.save_for_backward(*ins, rows, scal)
+        ctx.coefs = coefs
+        ctx.mark_non_differentiable(rows)
+        return scal, rows
+
+    @staticmethod
+    def backward(ctx, g_scal, g_rows):
+        from . import _lib
+        zp, nz, q1, q2, rp, rw, td, w, rho, rows, scal = ctx.saved_tensors
+        H, B, L = zp.shape
+        args = _lib.LossArgs(*[t.data_ptr() for t in (zp, nz, q1, q2, rp, rw, td, w, rho)], H, B, L, *ctx.coefs)
+        g = g_scal.contiguous()
+        need = ctx.needs_input_grad
+        dzp = torch.empty_like(zp) if need[0] else None
+        dq1 = torch.empty_like(q1) if need[2] else None
+        dq2 = torch.empty_like(q2) if need[3] else None
+        drp = torch.empty_like(rp) if need[4] else None
+        stream = torch.cuda.current_stream(zp.device).cuda_stream
+        _lib.check(_lib.lib().tdmpc_loss_backward(
+            C.byref(args), C.c_void_p(rows.data_ptr()), C.c_void_p(scal.data_ptr()), C.c_void_p(g.data_ptr() + 16),
+            C.c_void_p(_lib.ptr(dzp)), C.c_void_p(_lib.ptr(dq1)), C.c_void_p(_lib.ptr(dq2)),
+            C.c_void_p(_lib.ptr(drp)), C.c_void_p(stream)), "tdmpc_loss_backward")
+        return dzp, None, dq1, dq2, drp, None, None, None, None, None
 
 
 def _mse(pred, target):
@@ -140,26 +185,38 @@ class Learner:
         Q1, Q2 = m._Q1(x).view(H, B, 1), m._Q2(x).view(H, B, 1)
         reward_pred = m._reward(x).view(H, B, 1)
         rho = self._rho[:H]
-        consistency_loss = (rho * torch.mean(_mse(torch.stack(zs[1:]), next_z), dim=2, keepdim=True)).sum(0)
-        reward_loss = (rho * _mse(reward_pred, rew)).sum(0)
-        value_loss = (rho * (_mse(Q1, td_target) + _mse(Q2, td_target))).sum(0)
-        priority_loss = (rho * (_l1(Q1, td_target) + _l1(Q2, td_target))).sum(0)
+        if obs.is_cuda:
+            # the loss composition and its backward as three HIP launches (_FusedLoss) instead of ~60 ATen ones
+            scal, rows = _FusedLoss.apply(torch.stack(zs[1:]), next_z, Q1.view(H, B), Q2.view(H, B),
+                                          reward_pred.view(H, B), rew.reshape(H, B), td_target.view(H, B),
+                                          weights, rho.view(H),
+                                          (float(cfg.consistency_coef), float(cfg.reward_coef),
+                                           float(cfg.value_coef)))
+            means = (scal[0], scal[1], scal[2], scal[3])
+            weighted_loss = scal[4]
+            prio = rows[3].view(B, 1)   # [B, 1] like the reference's priority_loss
+        else:
+            consistency_loss = (rho * torch.mean(_mse(torch.stack(zs[1:]), next_z), dim=2, keepdim=True)).sum(0)
+            reward_loss = (rho * _mse(reward_pred, rew)).sum(0)
+            value_loss = (rho * (_mse(Q1, td_target) + _mse(Q2, td_target))).sum(0)
+            priority_loss = (rho * (_l1(Q1, td_target) + _l1(Q2, td_target))).sum(0)
+            total_loss = cfg.consistency_coef * consistency_loss.clamp(max=1e4) + \
+                cfg.reward_coef * reward_loss.clamp(max=1e4) + \
+                cfg.value_coef * value_loss.clamp(max=1e4)
+            # the reference's (total_loss [B, 1] * weights [B]).mean() is a mean over the [B, B] broadcast, i.e.
+            # mean(total_loss) * mean(weights): computed in that factored form (no B x B tensor, same gradient)
+            weighted_loss = total_loss.mean() * weights.mean()
+            means = (consistency_loss.mean(), reward_loss.mean(), value_loss.mean(), total_loss.mean())
+            prio = priority_loss.clamp(max=1e4).detach()
         zs = [zz.detach() for zz in zs]
-        total_loss = cfg.consistency_coef * consistency_loss.clamp(max=1e4) + \
-            cfg.reward_coef * reward_loss.clamp(max=1e4) + \
-            cfg.value_coef * value_loss.clamp(max=1e4)
-        # the reference's (total_loss [B, 1] * weights [B]).mean() is a mean over the [B, B] broadcast, i.e.
-        # mean(total_loss) * mean(weights): computed in that factored form (no B x B tensor, same gradient)
-        weighted_loss = total_loss.mean() * weights.mean()
         weighted_loss.register_hook(lambda grad: grad * (1 / H))
         weighted_loss.backward()
         grad_norm = torch.nn.utils.clip_grad_norm_(self.params, cfg.grad_clip_norm, error_if_nonfinite=False,
                                                    foreach=True)
         a.optim.step()
-        buffer.update_priorities(idxs, priority_loss.clamp(max=1e4).detach())
+        buffer.update_priorities(idxs, prio)
         pi_loss = self.update_pi(zs, eps=None if noise is None else noise[H:])
-        return torch.stack([consistency_loss.mean(), reward_loss.mean(), value_loss.mean(), pi_loss,
-                            total_loss.mean(), weighted_loss.mean(), grad_norm]).detach()
+        return torch.stack([means[0], means[1], means[2], pi_loss, means[3], weighted_loss, grad_norm]).detach()
 
     @torch.no_grad()
     def ema(self):

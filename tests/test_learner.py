@@ -212,3 +212,40 @@ def test_gpu_pixel_update_graph_equals_eager():
     torch.testing.assert_close(m1, m2, rtol=2e-5, atol=1e-6)
     for x, y in zip(a1.model.parameters(), a2.model.parameters()):
         torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_gpu_fused_loss_matches_aten():
+    """The fused HIP loss (include/tdmpc_learner.h) against the reference's ATen composition on the same tensors:
+    per-row losses, means, weighted loss and every input gradient (rtol 1e-5), with some rows past the 1e4 clamp."""
+    from tdmpc_amd.learner import _FusedLoss, _l1, _mse
+    g = torch.Generator().manual_seed(3)
+    H, B, L = 5, 96, 50
+    mk = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).cuda()  # noqa: E731
+    zp, nz = mk(H, B, L).requires_grad_(), mk(H, B, L)
+    q1, q2, rp = mk(H, B, sc=30).requires_grad_(), mk(H, B, sc=30).requires_grad_(), mk(H, B).requires_grad_()
+    rw, td = mk(H, B), mk(H, B, sc=30)
+    q1.data[:, :5] += 300.0                      # value loss of rows 0-4 above 1e4: clamped, no gradient
+    w = torch.rand(B, generator=g).cuda() + 0.5
+    rho = torch.tensor([0.5 ** t for t in range(H)], device="cuda")
+    coefs = (2.0, 0.5, 0.1)
+    scal, rows = _FusedLoss.apply(zp, nz, q1, q2, rp, rw, td, w, rho, coefs)
+    (scal[4] * 0.2).backward()
+    got = [zp.grad.clone(), q1.grad.clone(), q2.grad.clone(), rp.grad.clone()]
+    for t in (zp, q1, q2, rp):
+        t.grad = None
+    r = rho.view(H, 1)
+    cons = (r * _mse(zp, nz).mean(dim=2)).sum(0)
+    rew = (r * _mse(rp, rw)).sum(0)
+    val = (r * (_mse(q1, td) + _mse(q2, td))).sum(0)
+    pri = (r * (_l1(q1, td) + _l1(q2, td))).sum(0).clamp(max=1e4)
+    tot = coefs[0] * cons.clamp(max=1e4) + coefs[1] * rew.clamp(max=1e4) + coefs[2] * val.clamp(max=1e4)
+    wl = (tot.view(B, 1) * w).mean()
+    (wl * 0.2).backward()
+    assert (val[:5] > 1e4).all()
+    for x, y in zip(rows, (cons, rew, val, pri, tot)):
+        torch.testing.assert_close(x, y.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(scal[:5], torch.stack([cons.mean(), rew.mean(), val.mean(), tot.mean(), wl]).detach(),
+                               rtol=1e-5, atol=1e-6)
+    for x, y in zip(got, (zp.grad, q1.grad, q2.grad, rp.grad)):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-9)
