@@ -13,11 +13,12 @@ HEADER = "include/tdmpc_hip.h"
 
 
 def _declared():
+    import glob
     import os
-    root = os.path.dirname(os.path.dirname(__file__))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     names = set()
-    for hdr in (HEADER, "include/tdmpc_replay.h"):
-        src = open(os.path.join(root, hdr)).read()
+    for hdr in sorted(glob.glob(os.path.join(root, "include", "*.h"))):
+        src = open(hdr).read()
         names |= set(re.findall(r"^(?:int|size_t|const char\*)\s+(tdmpc_\w+)\(", src, re.M))
     return sorted(names)
 
@@ -25,7 +26,8 @@ def _declared():
 def test_library_exports_every_declared_symbol():
     L = _lib.lib()
     names = _declared()
-    assert "tdmpc_plan" in names and "tdmpc_replay_sample" in names and len(names) >= 12
+    assert "tdmpc_plan" in names and "tdmpc_replay_sample" in names and "tdmpc_loss_forward" in names
+    assert len(names) >= 14
     for n in names:
         assert hasattr(L, n), n
     assert L.tdmpc_abi_version() == _lib.ABI_VERSION == 4
