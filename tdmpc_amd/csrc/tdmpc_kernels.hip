@@ -2941,7 +2941,9 @@ bool use_split(const Ctx& c, int rows) {
     const Layout& w = c.w;
     if (w.M != 512 || rows > c.k.split_rows || (size_t)split_lds_floats(w.Kx, w.M) * 4 > 64 * 1024) return false;
     if (c.path == TDMPC_PATH_SPLIT) return true;
-    if (c.path != TDMPC_PATH_AUTO) return false;
+    // auto: only while the first layer, repeated per slice, stays cheap next to the slice of the M x M layer
+    // (humanoid-run L512: K1 = 536 made the one-env plan 1.3x slower than the layered path)
+    if (c.path != TDMPC_PATH_AUTO || (int)rup(w.Kx, 16) > w.M / 2) return false;
     static int en = -1;
     if (en < 0) {
         const char* e = getenv("TDMPC_SPLIT");
@@ -2955,7 +2957,7 @@ bool use_split_pi(const Ctx& c, int rows) {
     const Layout& w = c.w;
     if (w.M != 512 || rows > c.k.split_rows || (size_t)split_lds_floats(w.Lp, w.M) * 4 > 64 * 1024) return false;
     if (c.path == TDMPC_PATH_SPLIT) return true;
-    if (c.path != TDMPC_PATH_AUTO) return false;
+    if (c.path != TDMPC_PATH_AUTO || (int)rup(w.Lp, 16) > w.M / 2) return false;
     static int en = -1;
     if (en < 0) {
         const char* e = getenv("TDMPC_SPLIT_PI");
