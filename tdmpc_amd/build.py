@@ -38,5 +38,25 @@ def build(force: bool = False, verbose: bool = True) -> str:
     return OUT
 
 
+EXAMPLE_SRC = os.path.join(REPO, "examples", "plan_c.cpp")
+EXAMPLE_OUT = os.path.join(REPO, "examples", "plan_c")
+
+
+def build_example(force: bool = False, verbose: bool = True) -> str:
+    """examples/plan_c: a plain C++ host of the C ABI, linked against the in-tree library (rpath $ORIGIN)."""
+    deps = [EXAMPLE_SRC, OUT, os.path.join(REPO, "include", "tdmpc_hip.h")]
+    if not force and os.path.exists(EXAMPLE_OUT) and all(os.path.getmtime(EXAMPLE_OUT) >= os.path.getmtime(d)
+                                                          for d in deps):
+        return EXAMPLE_OUT
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-o", EXAMPLE_OUT + ".tmp", EXAMPLE_SRC,
+           "-L", HERE, "-ltdmpc_hip", "-Wl,-rpath,$ORIGIN/../tdmpc_amd"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(EXAMPLE_OUT + ".tmp", EXAMPLE_OUT)
+    return EXAMPLE_OUT
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_example(force="--force" in sys.argv)

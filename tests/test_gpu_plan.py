@@ -285,3 +285,15 @@ def test_graph_replay_equals_eager_batched():
         outs.append(res)
     for (a1, m1), (a2, m2) in zip(*outs):
         assert torch.equal(a1, a2) and torch.equal(m1, m2)
+
+
+def test_c_host_example():
+    """examples/plan_c (built by __graft_entry__.build()): the C ABI from a plain C++ host -- sizes, packing,
+    cold and warm tdmpc_plan on 32 humanoid envs -- runs and returns finite actions, inside [-1, 1] in eval mode."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "plan_c")
+    assert os.path.exists(exe), "examples/plan_c missing: run __graft_entry__.build()"
+    r = subprocess.run([exe, "32", "5"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "plan-steps/s" in r.stdout and "bad 0" in r.stdout, r.stdout
