@@ -190,6 +190,33 @@ int tdmpc_estimate_value(const tdmpc_dims* dims, const tdmpc_plan_params* params
                          float* value, float* reward_last, float* z_last,
                          void* workspace, size_t workspace_bytes, void* stream);
 
+/* The policy pre-rollout of TDMPC.plan (tdmpc.py:113-118) for `batch` envs: z = z0 repeated P times, then for
+ * t < H: pi_actions[t] = TOLD.pi(z, min_std) with the caller's TruncatedNormal eps, z = TOLD.next(z, .)[0]
+ * (the last step's next is not computed: its latent is unused).
+ *   z0         [batch, L]
+ *   eps_pi     [batch, H, P, A]   _standard_normal draws of the H pi calls (P = dims.num_pi)
+ *   pi_actions [batch, H, P, A] out */
+int tdmpc_pi_rollout(const tdmpc_dims* dims, const tdmpc_plan_params* params, const void* packed,
+                     const float* z0, const float* eps_pi, float* pi_actions,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* One CEM iteration of TDMPC.plan (tdmpc.py:127-149) for `batch` envs: candidates
+ * clamp(mean + std * eps_cem, -1, 1) followed by the P pi_actions, estimate_value (nan_to_num), top-K, softmax
+ * refit; mean = momentum * mean + (1 - momentum) * _mean, std = _std.clamp(std_floor, 2).
+ *   z0            [batch, L]
+ *   pi_actions    [batch, H, P, A]   (tdmpc_pi_rollout's output; NULL when P == 0)
+ *   eps_cem       [batch, H, N, A]   the torch.randn draw of the candidates
+ *   eps_term      [batch, T, A]      the horizon pi call's eps (T = N + P)
+ *   mean, std     [batch, H, A] in/out
+ *   elite_actions [batch, H, K, A] out   (elite order = torch.topk order)
+ *   score         [batch, K] out
+ *   value         [batch, T] out     optional: estimate_value's output for the T candidates
+ *   reward_mean   [batch] out        estimate_value's mean reward at t = H-1 (external_reward_mean) */
+int tdmpc_cem_iter(const tdmpc_dims* dims, const tdmpc_plan_params* params, const void* packed,
+                   const float* z0, const float* pi_actions, const float* eps_cem, const float* eps_term,
+                   float* mean, float* std, float* elite_actions, float* score, float* value, float* reward_mean,
+                   void* workspace, size_t workspace_bytes, void* stream);
+
 /* Diagnostic kernel timer for the roofline report (bench.py). Arms a per-thread recorder: every later
  * launch issued from this thread that matches is bracketed by HIP events on its stream (at most
  * max_launches).

@@ -15,7 +15,8 @@ ABI_VERSION = 4
 PATHS = {"auto": 0, "layered": 1, "chain": 2, "chain32": 3, "chain16": 4, "split": 5}
 
 EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc_num_param_tensors",
-            "tdmpc_pack_weights", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_last_error",
+            "tdmpc_pack_weights", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_pi_rollout",
+            "tdmpc_cem_iter", "tdmpc_last_error",
             "tdmpc_profile_begin", "tdmpc_profile_end", "tdmpc_icem_sizes_for", "tdmpc_plan_icem",
             # include/tdmpc_replay.h
             "tdmpc_replay_workspace_bytes", "tdmpc_replay_add_priorities", "tdmpc_replay_update_priorities",
@@ -95,6 +96,9 @@ def lib():
                              vp, vp, vp, vp, vp, vp, sz, vp]
     L.tdmpc_estimate_value.argtypes = [C.POINTER(Dims), C.POINTER(PlanParams), vp, vp, vp, vp, i32, vp, vp,
                                        vp, vp, sz, vp]
+    L.tdmpc_pi_rollout.argtypes = [C.POINTER(Dims), C.POINTER(PlanParams), vp, vp, vp, vp, vp, sz, vp]
+    L.tdmpc_cem_iter.argtypes = [C.POINTER(Dims), C.POINTER(PlanParams), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                 vp, vp, sz, vp]
     L.tdmpc_last_error.restype = C.c_char_p
     L.tdmpc_profile_begin.argtypes = [i32, i32, i32, i32, i32]
     L.tdmpc_profile_end.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_double), C.POINTER(C.c_double)]

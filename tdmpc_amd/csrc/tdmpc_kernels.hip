@@ -2075,6 +2075,7 @@ struct CemArgs {
     float temperature, momentum, omm, std_floor;
     float* action; float* metrics;
     float* elite_out; float* score_out; float* mean_out; float* std_out;
+    int no_pick; float* reward_out;     // tdmpc_cem_iter: stop after the refit; reward mean -> reward_out [B]
 };
 
 DEVI uint32_t f2ord(float v) {
@@ -2230,6 +2231,14 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
         if (lane == 0) red[1 + wave] = s;
     }
     __syncthreads();
+    if (a.no_pick) {
+        if (tid == 0) {
+            float rs = 0.f;
+            for (int w = 0; w < nwv; ++w) rs += red[1 + w];
+            a.reward_out[e] = rs / (float)T;
+        }
+        return;
+    }
     // np.random.choice(K, p=score): float64 cdf of the float32 scores, cdf /= cdf[-1], searchsorted right
     int* jsel = (int*)(red + 20);
     if (tid == 0) {
@@ -2471,16 +2480,30 @@ __global__ void pack_transpose_kernel(const float* src, int rows, int cols, floa
 }
 
 // Candidate actions [B][H][T][A] -> X_t panels' action columns (zero pad to Ap) (estimate_value entry).
-__global__ void scatter_actions_kernel(const float* act, float* X, size_t x_stride, int H, int T, int A, int Ap,
-                                       int Kx, int B) {
-    const size_t total = (size_t)B * H * T * Ap;
+// candidate actions act [B][H][Ts][A] -> the action columns of rows e * Td + r0 + r of X_t (t < H)
+__global__ void scatter_actions_kernel(const float* act, float* X, size_t x_stride, int H, int Ts, int A, int Ap,
+                                       int Kx, int B, int Td, int r0) {
+    const size_t total = (size_t)B * H * Ts * Ap;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
         const int c = i % Ap;
-        const size_t r = (i / Ap) % T;
-        const int t = (i / ((size_t)Ap * T)) % H;
-        const size_t e = i / ((size_t)Ap * T * H);
-        const float v = c < A ? act[((e * H + t) * T + r) * A + c] : 0.f;
-        X[(size_t)t * x_stride + pidx(e * T + r, c, Kx)] = v;
+        const size_t r = (i / Ap) % Ts;
+        const int t = (i / ((size_t)Ap * Ts)) % H;
+        const size_t e = i / ((size_t)Ap * Ts * H);
+        const float v = c < A ? act[((e * H + t) * Ts + r) * A + c] : 0.f;
+        X[(size_t)t * x_stride + pidx(e * Td + r0 + r, c, Kx)] = v;
+    }
+}
+
+// the inverse: action columns of rows e * Td + r0 + r of X_t -> out [B][H][Ts][A]
+__global__ void gather_actions_kernel(const float* X, size_t x_stride, int H, int Ts, int A, int Kx, int B, int Td,
+                                      int r0, float* out) {
+    const size_t total = (size_t)B * H * Ts * A;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int c = i % A;
+        const size_t r = (i / A) % Ts;
+        const int t = (i / ((size_t)A * Ts)) % H;
+        const size_t e = i / ((size_t)A * Ts * H);
+        out[i] = X[(size_t)t * x_stride + pidx(e * Td + r0 + r, c, Kx)];
     }
 }
 
@@ -3687,7 +3710,7 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     HIPCHK(hipMemsetAsync(c.k.z0, 0, (size_t)B * c.w.Lp * 4, c.s));
     HIPCHK(hipMemcpy2DAsync(c.k.z0, c.w.Lp * 4, z0, L * 4, L * 4, B, hipMemcpyDeviceToDevice, c.s));
     hipLaunchKernelGGL(scatter_actions_kernel, dim3(512), dim3(256), 0, c.s, actions, c.k.X, c.k.x_stride, H, T, c.A,
-                       c.w.Ap, c.Kx, B);
+                       c.w.Ap, c.Kx, B, T, 0);
     HIPCHK(hipGetLastError());
     if ((rc = prep(c, nullptr, 0, c.k.z0))) return rc;
     const RowMap all = {T, T, 0};
@@ -3707,6 +3730,90 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     }
     HIPCHK(hipMemcpyAsync(value, c.k.value, (size_t)B * T * 4, hipMemcpyDeviceToDevice, c.s));
     HIPCHK(hipMemcpyAsync(reward_last, c.k.rlast, (size_t)B * T * 4, hipMemcpyDeviceToDevice, c.s));
+    return 0;
+}
+
+// z0 [B][L] -> the workspace's padded z0 [B][Lp] and the latent columns of X_0 for all T rows of every env
+static int load_z0(const Ctx& c, const float* z0) {
+    const int L = c.w.L;
+    HIPCHK(hipMemsetAsync(c.k.z0, 0, (size_t)c.B * c.w.Lp * 4, c.s));
+    HIPCHK(hipMemcpy2DAsync(c.k.z0, c.w.Lp * 4, z0, L * 4, L * 4, c.B, hipMemcpyDeviceToDevice, c.s));
+    return prep(c, nullptr, 0, c.k.z0);
+}
+
+int tdmpc_pi_rollout(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* packed, const float* z0,
+                     const float* eps_pi, float* pi_actions, void* workspace, size_t ws_bytes, void* stream) {
+    if (!d || !prm || !packed || !z0 || !eps_pi || !pi_actions || !workspace) return TDMPC_E_NULL;
+    Ctx c;
+    int rc;
+    const int H = prm->horizon, B = prm->batch;
+    if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
+    if (prm->path < 0 || prm->path > 5) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    c.path = prm->path;
+    const int N = c.N, P = c.P, T = c.T;
+    const long A = c.A;
+    if (P <= 0) { snprintf(g_err, sizeof g_err, "num_pi is 0"); return TDMPC_E_DIMS; }
+    if ((rc = load_z0(c, z0))) return rc;
+    // the policy rows sit where tdmpc_plan keeps them: rows N..T-1 of each env's block of T
+    const RowMap pm = {P, T, N};
+    for (int t = 0; t < H; ++t) {
+        if ((rc = policy(c, t, B * P, pm, eps_pi, (long)H * P * A, P, (long)t * P * A, prm->min_std))) return rc;
+        if (t < H - 1 && (rc = step_next(c, t, B * P, pm, prm->discount_pow[t], t == 0, 0))) return rc;
+    }
+    hipLaunchKernelGGL(gather_actions_kernel, dim3(512), dim3(256), 0, c.s, c.k.X, c.k.x_stride, H, P, c.A, c.Kx, B,
+                       T, N, pi_actions);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int tdmpc_cem_iter(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* packed, const float* z0,
+                   const float* pi_actions, const float* eps_cem, const float* eps_term, float* mean, float* stdv,
+                   float* elite_actions, float* score, float* value, float* reward_mean, void* workspace,
+                   size_t ws_bytes, void* stream) {
+    if (!d || !prm || !packed || !z0 || !eps_cem || !eps_term || !mean || !stdv || !elite_actions || !score ||
+        !reward_mean || !workspace)
+        return TDMPC_E_NULL;
+    Ctx c;
+    int rc;
+    const int H = prm->horizon, B = prm->batch;
+    if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
+    if (prm->path < 0 || prm->path > 5) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    c.path = prm->path;
+    const int N = c.N, P = c.P, T = c.T, A = c.A, HA = H * A;
+    if (P > 0 && !pi_actions) return TDMPC_E_NULL;
+    // the caller's mean/std [B][H][A] -> the workspace's [B][Hmax][A]
+    const size_t mp = (size_t)d->max_horizon * A * 4;
+    HIPCHK(hipMemcpy2DAsync(c.k.mean, mp, mean, HA * 4, HA * 4, B, hipMemcpyDeviceToDevice, c.s));
+    HIPCHK(hipMemcpy2DAsync(c.k.stdv, mp, stdv, HA * 4, HA * 4, B, hipMemcpyDeviceToDevice, c.s));
+    if ((rc = load_z0(c, z0))) return rc;
+    // candidates clamp(mean + std * eps_cem) in rows 0..N-1 (the eps stream of one env is [H][N][A])
+    c.eps_env = (long)H * N * A; c.eps_cem_off = 0; c.eps_iter = 0;
+    if ((rc = prep(c, eps_cem, 0, nullptr))) return rc;
+    if (P > 0) {
+        hipLaunchKernelGGL(scatter_actions_kernel, dim3(512), dim3(256), 0, c.s, pi_actions, c.k.X, c.k.x_stride, H, P,
+                           A, c.w.Ap, c.Kx, B, T, N);
+        HIPCHK(hipGetLastError());
+    }
+    const RowMap all = {T, T, 0};
+    for (int t = 0; t < H; ++t)
+        if ((rc = step_next(c, t, B * T, all, prm->discount_pow[t], t == 0, t == H - 1, 1))) return rc;
+    if ((rc = policy(c, H, B * T, all, eps_term, (long)T * A, T, 0, prm->min_std))) return rc;
+    if ((rc = terminal_q(c, prm->discount_pow[H]))) return rc;
+    CemArgs ca;
+    memset(&ca, 0, sizeof ca);
+    ca.H = H; ca.N = N; ca.P = P; ca.T = T; ca.A = A; ca.K = d->num_elites; ca.Kx = c.Kx;
+    ca.Hmax = d->max_horizon; ca.I = 1; ca.iter = 0; ca.final_iter = 1; ca.no_pick = 1;
+    ca.Tw = T; ca.NE = T; ca.pi_base = 0;
+    ca.X = c.k.X; ca.x_stride = c.k.x_stride; ca.value = c.k.value; ca.rlast = c.k.rlast;
+    ca.mean = c.k.mean; ca.stdv = c.k.stdv;
+    ca.temperature = prm->temperature; ca.momentum = prm->momentum; ca.omm = prm->one_minus_momentum;
+    ca.std_floor = prm->std_floor;
+    ca.elite_out = elite_actions; ca.score_out = score; ca.value_out = value; ca.reward_out = reward_mean;
+    if (use_chain(c, B * T, 2, CK_Q)) { ca.G = c.k.G; ca.qv = c.k.qv; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H]; }
+    hipLaunchKernelGGL(cem_kernel, dim3(B), dim3(1024), cem_lds_bytes(T, H, ca.K, A), c.s, ca);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy2DAsync(mean, HA * 4, c.k.mean, mp, HA * 4, B, hipMemcpyDeviceToDevice, c.s));
+    HIPCHK(hipMemcpy2DAsync(stdv, HA * 4, c.k.stdv, mp, HA * 4, B, hipMemcpyDeviceToDevice, c.s));
     return 0;
 }
 

@@ -227,6 +227,53 @@ class HipPlanner:
         _lib.check(rc, "tdmpc_estimate_value")
         return value, rlast, zl
 
+    def pi_rollout(self, z0, eps_pi, H: int):
+        """The policy pre-rollout of TDMPC.plan (tdmpc.py:113-118) through the C ABI for B envs: z0 [B, L],
+        eps_pi [B, H, P, A] (TruncatedNormal eps of the H pi calls) -> pi_actions [B, H, P, A]."""
+        B = z0.shape[0]
+        prm = self.params(H, 1, B, False, True, 0.05)
+        dev = self.device
+        z0 = z0.to(dev, torch.float32).contiguous()
+        eps_pi = eps_pi.to(dev, torch.float32).contiguous()
+        out = torch.empty(B, H, self.P, self.A, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = self.L.tdmpc_pi_rollout(C.byref(self.dims), C.byref(prm), C.c_void_p(self.packed.data_ptr()),
+                                     C.c_void_p(z0.data_ptr()), C.c_void_p(eps_pi.data_ptr()),
+                                     C.c_void_p(out.data_ptr()), C.c_void_p(self.workspace.data_ptr()),
+                                     self.workspace.numel() * 4, C.c_void_p(stream))
+        _lib.check(rc, "tdmpc_pi_rollout")
+        return out
+
+    def cem_iter(self, z0, pi_actions, eps_cem, eps_term, mean, std, H: int, std_floor: float = 0.05):
+        """One CEM iteration of TDMPC.plan (tdmpc.py:127-149) through the C ABI for B envs: z0 [B, L],
+        pi_actions [B, H, P, A] (or None when P == 0), eps_cem [B, H, N, A], eps_term [B, T, A]; mean/std
+        [B, H, A] are updated in place. Returns (elite_actions [B, H, K, A], score [B, K], value [B, T],
+        reward_mean [B])."""
+        B = z0.shape[0]
+        K = self.dims.num_elites
+        prm = self.params(H, 1, B, False, True, std_floor)
+        dev = self.device
+        z0 = z0.to(dev, torch.float32).contiguous()
+        pa = None if pi_actions is None else pi_actions.to(dev, torch.float32).contiguous()
+        eps_cem = eps_cem.to(dev, torch.float32).contiguous()
+        eps_term = eps_term.to(dev, torch.float32).contiguous()
+        for t in (mean, std):
+            if not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous() or t.shape != (B, H, self.A):
+                raise ValueError("mean/std must be contiguous fp32 [B, H, A] device tensors")
+        elite = torch.empty(B, H, K, self.A, device=dev)
+        score = torch.empty(B, K, device=dev)
+        value = torch.empty(B, self.T, device=dev)
+        rmean = torch.empty(B, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        vp = C.c_void_p
+        rc = self.L.tdmpc_cem_iter(C.byref(self.dims), C.byref(prm), vp(self.packed.data_ptr()), vp(z0.data_ptr()),
+                                   vp(_lib.ptr(pa)), vp(eps_cem.data_ptr()), vp(eps_term.data_ptr()),
+                                   vp(mean.data_ptr()), vp(std.data_ptr()), vp(elite.data_ptr()),
+                                   vp(score.data_ptr()), vp(value.data_ptr()), vp(rmean.data_ptr()),
+                                   vp(self.workspace.data_ptr()), self.workspace.numel() * 4, vp(stream))
+        _lib.check(rc, "tdmpc_cem_iter")
+        return elite, score, value, rmean
+
     def encode(self, obs):
         """TOLD.h for a batch of observations through the C ABI -> z0 [B, L]."""
         B = obs.shape[0]

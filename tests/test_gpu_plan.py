@@ -297,3 +297,76 @@ def test_c_host_example():
     r = subprocess.run([exe, "32", "5"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "plan-steps/s" in r.stdout and "bad 0" in r.stdout, r.stdout
+
+
+@pytest.mark.parametrize("path", ["layered", "chain32", "split"])
+@pytest.mark.parametrize("task,ov", [("humanoid", dict(num_samples=128, num_elites=16, iterations=3)),
+                                     ("cheetah", dict(num_samples=64, num_elites=8, iterations=2, mixture_coef=0.0))])
+def test_building_blocks_compose_plan(task, ov, path):
+    """The SURVEY §8b building blocks -- tdmpc_encode, tdmpc_pi_rollout, I x tdmpc_cem_iter, then the
+    np.random.choice pick on the host -- reproduce the oracle's TDMPC.plan trace (tdmpc.py:113-163) for 2 envs:
+    pi actions, per-iteration values, elite sets, scores, mean/std, reward mean and the action."""
+    cfg = make_cfg(task, **ov)
+    B, H = 2, 5
+    agent = _agent(cfg, 9, B=B, path=path)
+    pl = agent.planner
+    pl.pack(agent.model)
+    N, P, A, K, I = pl.N, pl.P, pl.A, cfg.num_elites, cfg.iterations
+    T = N + P
+    g = torch.Generator().manual_seed(4)
+    obs = torch.randn(B, cfg.obs_shape[0], generator=g)
+    eps_pi = torch.randn(B, H, P, A, generator=g)
+    eps_cem = torch.randn(B, I, H, N, A, generator=g)
+    eps_term = torch.randn(B, I, T, A, generator=g)
+    eps_act = torch.randn(B, A, generator=g)
+    us = [0.3, 0.85]
+    told = tdmpc_ref.RefTOLD(synthetic_state_dict(cfg, 9), cfg)
+    traces, refs = [], []
+    for e in range(B):
+        nb = tdmpc_ref.NoiseBundle(eps_pi=eps_pi[e] if P > 0 else None, eps_cem=list(eps_cem[e]),
+                                   eps_term=list(eps_term[e]), u=us[e], eps_act=eps_act[e])
+        tr = {}
+        a, m = tdmpc_ref.plan(told, cfg, tdmpc_ref.PlanState(0.05), obs[e].numpy(), nb, step=10**6, t0=True, trace=tr)
+        traces.append(tr)
+        refs.append((a, m))
+
+    z0 = pl.encode(obs)
+    for e in range(B):
+        assert _close(z0[e].cpu().numpy(), traces[e]["z0"].numpy()).all()
+    pi = None
+    if P > 0:
+        pi = pl.pi_rollout(z0, eps_pi, H)
+        for e in range(B):
+            assert _close(pi[e].cpu().numpy(), traces[e]["pi_actions"].numpy()).all(), \
+                np.abs(pi[e].cpu().numpy() - traces[e]["pi_actions"].numpy()).max()
+    mean = torch.zeros(B, H, A, device=pl.device)
+    std = torch.full((B, H, A), 2.0, device=pl.device)
+    diverged = [False] * B
+    for i in range(I):
+        elite, score, value, rmean = pl.cem_iter(z0, pi, eps_cem[:, i], eps_term[:, i], mean, std, H)
+        for e in range(B):
+            if diverged[e]:
+                continue
+            tr = traces[e]
+            rv = tr["value"][i][:, 0].numpy()
+            gv = value[e].cpu().numpy()
+            assert _close(gv, rv).all(), f"env {e} iteration {i}: max |dG| {np.abs(gv - rv).max():.3e}"
+            ref_idx = tr["elite_idxs"][i].numpy()
+            eg, er = _elites(gv, K), set(ref_idx.tolist())
+            if eg != er:
+                assert _near_tie(rv, eg, er, K)
+                diverged[e] = True
+                continue
+            ref_elite = tr["actions"][i][:, ref_idx].numpy()
+            np.testing.assert_allclose(elite[e].cpu().numpy(), ref_elite, atol=2e-5, rtol=0)
+            np.testing.assert_allclose(score[e].cpu().numpy(), tr["score"][i][:, 0].numpy(), atol=2e-5, rtol=1e-4)
+            np.testing.assert_allclose(mean[e].cpu().numpy(), tr["mean"][i].numpy(), atol=2e-5, rtol=0)
+            np.testing.assert_allclose(std[e].cpu().numpy(), tr["std"][i].numpy(), atol=2e-5, rtol=0)
+            np.testing.assert_allclose(float(rmean[e]), tr["reward_mean"][i], atol=2e-5, rtol=1e-4)
+    for e in range(B):
+        if diverged[e]:
+            continue
+        # the output pick of tdmpc.py:152-158 on the host from the last iteration's score / elites / std
+        j = tdmpc_ref.choice_index(score[e].cpu().numpy(), us[e])
+        a = elite[e, 0, j].cpu() + std[e, 0].cpu() * eps_act[e]
+        np.testing.assert_allclose(a.numpy(), refs[e][0].numpy(), atol=2e-5, rtol=0)
