@@ -860,6 +860,7 @@ struct ChainArgs {
     int rb;                              // row block: 32 (chain_kernel) or 16 (chain16_kernel)
     int nw;                              // waves per workgroup of chain_kernel: 8 or 16
     int hfl;                             // floats of the LDS activation block (max(K1, M) * rb, K1 to 16)
+    int il;                              // > 0: the problems interleaved along blockIdx.x (pb = x % il)
     RowMap amap;                         // logical row -> X row (input and output)
     const float* X; long x_ts;           // X_t panel (input)
     // last layer of dynamics / pi: panel [n3][M] + bias -> Xo quads [out_q0, out_q0 + nstore/4)
@@ -1024,10 +1025,10 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
     constexpr int NTH = 64 * NW;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-    const int pb = blockIdx.y;
+    const int pb = a.il ? blockIdx.x % a.il : blockIdx.y;
     const ChainProb& P = a.p[pb];
     const int M = a.M;
-    const int m0 = blockIdx.x * 32;
+    const int m0 = (a.il ? blockIdx.x / a.il : blockIdx.x) * 32;
     float* sH = smem;                       // activation block [max(K1, M)/4][32][4]
     float* red0 = smem + a.hfl;             // [NW][32]
     float* red1 = red0 + 32 * NW;           // [NW][32]
@@ -1398,10 +1399,10 @@ template <int MODE, int NT, int D = 4, int D3 = 4>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) chain16_kernel(const ChainArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, h4 = lane >> 4;
-    const int pb = blockIdx.y;
+    const int pb = a.il ? blockIdx.x % a.il : blockIdx.y;
     const ChainProb& P = a.p[pb];
     const int M = a.M;
-    const int m0 = blockIdx.x * 16;
+    const int m0 = (a.il ? blockIdx.x / a.il : blockIdx.x) * 16;
     float* sH = smem;                       // activation block [max(K1, M)/4][16][4]
     float* red0 = smem + a.hfl;             // [8][16]
     float* red1 = red0 + 128;               // [8][16]
@@ -2810,11 +2811,28 @@ double chain_macs_per_row(int mode, const ChainArgs& a, int nprob) {
     return nprob * (K1 * M + M * M + M);
 }
 
-int launch_chain(int mode, const ChainArgs& a, int nprob, hipStream_t s) {
-    if (a.rows <= 0) return 0;
+// TDMPC_CHAIN_IL=1: the two problems of a launch (dynamics / reward, Q1 / Q2) alternate along blockIdx.x, so a
+// CU's co-resident workgroups are one of each (different layer-3 phases) instead of two of the same head. Off by
+// default: measured on MI355X (humanoid-run, tools/gpu68.sh) 9.50 vs 8.99 ms per B = 32 plan, 3.08 vs 3.04 at
+// B = 8 -- two workgroups of the same head on a CU stream the same weight panels at about the same time and
+// share them through the CU's L1, which the mixed pair loses.
+int chain_il() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("TDMPC_CHAIN_IL");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+
+int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
+    if (a0.rows <= 0) return 0;
+    ChainArgs a = a0;
     const int nw = a.rb == 16 ? 8 : a.nw;
     const size_t lds = ((size_t)a.hfl + (a.rb == 16 ? 256 : 64 * nw) + chain_param_floats(mode, a.M, a.n3)) * 4;
-    const dim3 grid((a.rows + a.rb - 1) / a.rb, nprob), block(64 * nw);
+    const int nblk = (a.rows + a.rb - 1) / a.rb;
+    a.il = nprob > 1 && chain_il() ? nprob : 0;
+    const dim3 grid(a.il ? nblk * nprob : nblk, a.il ? 1 : nprob), block(64 * nw);
     const int tn = a.M / (32 * nw);
     // diagnostic timer (tdmpc_profile_begin cfg 4 + mode): HIP events around matching chain launches
     Profiler& pf = g_prof;
