@@ -49,6 +49,9 @@ from tdmpc_amd.tdmpc import TDMPC  # noqa: E402
 from tdmpc_amd.told import synthetic_state_dict  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector peak (spec)
+# x6 chain kernels: each fp32 product is 6 bf16 MFMA products (three-way split of both operands), so their roof is
+# the dense BF16 MFMA peak / 6 in fp32-product FLOP/s (BF16 = 16 x the f32 MFMA rate, MI355X_MICROARCH.md)
+X6_PEAK_TFLOPS = round(FP32_PEAK_TFLOPS * 16 / 6, 1)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
 
 
@@ -308,9 +311,9 @@ def args_config_for_learner(cfg):
             "cartpole": "cartpole-swingup"}.get(cfg.task, "humanoid-run")
 
 
-def make_agent(cfg, B, rng, graph, seed):
+def make_agent(cfg, B, rng, graph, seed, path="auto"):
     torch.manual_seed(seed)
-    agent = TDMPC(cfg, max_batch=B, rng=rng, graph=graph)
+    agent = TDMPC(cfg, max_batch=B, rng=rng, graph=graph, path=path)
     agent.model.load_state_dict(synthetic_state_dict(cfg, 0))
     agent.std = 0.05   # trained-regime value of std_schedule
     return agent
@@ -350,6 +353,7 @@ def main():
     ap.add_argument("--no-replay", action="store_true")
     ap.add_argument("--no-learner", action="store_true")
     ap.add_argument("--no-icem", action="store_true")
+    ap.add_argument("--no-exact", action="store_true", help="skip the exact-f32-MFMA comparison run")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -408,15 +412,24 @@ def main():
         # dominant kernel: the CEM rollout step (TOLD.next, 5 of every iteration's launches, ~half the time).
         # Row-block chain kernel when the auto path picks it (>= 64 32-row blocks), else the layered hidden GEMM.
         n, ms, fl = timed(4, -1, 0, rows)
+        peak = FP32_PEAK_TFLOPS
         if n > 0:
             rb = 32 if (rows + 31) // 32 * 2 > torch.cuda.get_device_properties(dev).multi_processor_count // 2 else 16
             rb = int(os.environ.get("TDMPC_CHAIN_RB", rb))
-            kernel = (f"{'chain_kernel' if rb == 32 else 'chain16_kernel'}<CH_STEP> (TOLD.next: dynamics + reward heads, {rb}-row blocks, hidden "
-                      f"activations in LDS, weights streamed from L2; {rows} rows x 2 heads per launch), "
-                      f"fp32 {'v_mfma_f32_32x32x2_f32' if rb == 32 else 'v_mfma_f32_16x16x4_f32'}")
+            x6 = rb == 32 and M == 512 and os.environ.get("TDMPC_X6", "1") != "0"
+            if x6:
+                peak = X6_PEAK_TFLOPS
+                kernel = (f"chain_kernel<CH_STEP, X6> (TOLD.next: dynamics + reward heads, 32-row blocks, hidden "
+                          f"activations in LDS, weights streamed from L2; {rows} rows x 2 heads per launch), fp32 "
+                          f"products from a three-way bf16 split of both operands: 6 v_mfma_f32_32x32x16_bf16 per "
+                          f"product, fp32 accumulation (peak = dense BF16 / 6)")
+            else:
+                kernel = (f"{'chain_kernel' if rb == 32 else 'chain16_kernel'}<CH_STEP> (TOLD.next: dynamics + reward heads, {rb}-row blocks, hidden "
+                          f"activations in LDS, weights streamed from L2; {rows} rows x 2 heads per launch), "
+                          f"fp32 {'v_mfma_f32_32x32x2_f32' if rb == 32 else 'v_mfma_f32_16x16x4_f32'}")
             kx = A + Lt
             alg_bytes = 4.0 * (rows * (kx + Lt + 2) + 2 * M * kx + 2 * M * M + M * Lt + M)
-            pmc_key = f"{args.config}/B{B}/chain_step"
+            pmc_key = f"{args.config}/B{B}/chain_step" + ("_x6" if x6 else "")
         else:
             n, ms, fl = timed(0, 0, M, rows)
             kernel = (f"linear_lds_kernel (128x128 LDS-staged tile): CEM rollout layer 2 (dynamics + reward "
@@ -427,8 +440,9 @@ def main():
         avg_s = ms / max(n, 1) * 1e-3
         per_launch = fl / max(n, 1)
         achieved = per_launch / avg_s / 1e12
-        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None, "kernel": kernel,
+        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "frac_of_fp32_mfma_peak": round(achieved / FP32_PEAK_TFLOPS, 4),
+                "traffic": None, "kernel": kernel,
                 "launches": n, "avg_launch_us": round(avg_s * 1e6, 3), "flops_per_launch": per_launch,
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "hbm_gbs_algorithmic": round(alg_bytes / avg_s / 1e9, 1)}
@@ -461,7 +475,20 @@ def main():
     fl_exec = plan_flops(cfg, executed=True)
     plan_roof = {"flop_per_plan_step_algorithmic": fl_alg, "flop_per_plan_step_executed": fl_exec,
                  "tflops_per_gpu_algorithmic": round(value / world * fl_alg / 1e12, 3),
-                 "frac_of_fp32_peak": round(value / world * min(fl_alg, fl_exec) / 1e12 / FP32_PEAK_TFLOPS, 4)}
+                 "frac_of_fp32_peak": round(value / world * min(fl_alg, fl_exec) / 1e12 / FP32_PEAK_TFLOPS, 4),
+                 "frac_of_x6_peak": round(value / world * min(fl_alg, fl_exec) / 1e12 / X6_PEAK_TFLOPS, 4)}
+
+    # the same workload on the exact f32 MFMA chain kernels (path chain32: v_mfma_f32_32x32x2_f32), same run
+    exact = None
+    if not args.no_exact and world == 1 and cfg.mlp_dim == 512:
+        ae = make_agent(cfg, B, args.rng, graph, 1 + rank, path="chain32")
+        ke = max(10, args.steps // 2)
+        ele = time_steps(lambda i: ae.plan_batch(obs, step=step, t0=(i % 100 == 0), sync_metrics=False), 3, ke, None)
+        exact = {"value": round(B * ke / ele, 3), "unit": "plan-steps/s", "ms_per_step": round(ele / ke * 1e3, 4),
+                 "frac_of_fp32_peak": round(B * ke / ele * min(plan_flops(cfg, False), plan_flops(cfg, True)) / 1e12
+                                            / FP32_PEAK_TFLOPS, 4),
+                 "note": "exact f32 MFMA (v_mfma_f32_32x32x2_f32) chain kernels, path chain32, same envs"}
+        del ae
 
     single = None
     if not args.no_single and world == 1:
@@ -511,6 +538,9 @@ def main():
             "value": round(value, 3), "unit": "plan-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "fp32_products": ("three-way bf16 split of both operands, 6 bf16 MFMA products per fp32 product, fp32 "
+                              "accumulation (x6 chain kernels; parity tests at the fp32 tolerance)"
+                              if cfg.mlp_dim == 512 and os.environ.get("TDMPC_X6", "1") != "0" else "f32 MFMA"),
             "data": "synthetic: seeded N(0,1/fan_in) TOLD weights, N(0,1) observations, noise drawn on device",
             "config": {"workload": f"{args.config}: TDMPC.plan N={cfg.num_samples} H={cfg.horizon} "
                                    f"iters={cfg.iterations} mixture={cfg.mixture_coef} K={cfg.num_elites} "
@@ -520,6 +550,7 @@ def main():
                        "rng": args.rng, "hip_graph": graph},
             "roofline": roof,
             "plan_roofline": plan_roof,
+            "exact_f32_mfma": exact,
             "single_env": single,
             "batch_sweep": sweep,
             "replay_sampler": replay,

@@ -72,7 +72,8 @@ typedef struct tdmpc_plan_params {
     int32_t path;          /* kernel path: 0 = auto by row count, 1 = layered GEMMs only, 2 = row-block chain
                               kernels wherever the shape allows (row block by launch size), 3 / 4 = chain
                               kernels on 32- / 16-row blocks only, 5 = TOLD.next on the column-split step kernel
-                              (others layered); results agree within the fp32 tolerance */
+                              (others layered), 6 = chain kernels with fp32 products from a three-way bf16
+                              split (TDMPC_PATH_CHAIN_X6); results agree within the fp32 tolerance */
 } tdmpc_plan_params;
 
 #define TDMPC_PATH_AUTO 0
@@ -81,6 +82,7 @@ typedef struct tdmpc_plan_params {
 #define TDMPC_PATH_CHAIN32 3
 #define TDMPC_PATH_CHAIN16 4
 #define TDMPC_PATH_SPLIT 5
+#define TDMPC_PATH_CHAIN_X6 6   /* chain kernels, fp32 products from a three-way bf16 split (M = 512) */
 
 /* Byte sizes the caller must allocate (all 256-byte aligned). */
 typedef struct tdmpc_sizes {

@@ -93,8 +93,33 @@ struct Layout {
     size_t wq1x, bq1x, g1, be1;                      // panel [2M][Kx]; LN1 gamma/beta [2M]
     size_t wq2, bq2, g2, be2;                        // 2 panels [M][M]; LN2 [2M]
     size_t wq3, bq3;                                 // [2][M], [2]
+    // the chain kernels' weight panels again as three bf16 planes (x6 layout, X6_* below, pack_x6_kernel)
+    size_t x6[9];
     size_t total;
 };
+
+// Matrices kept in the x6 layout: fp32 = hi + mid + lo, three bf16 planes. Block (nb, g) of 32 rows x 16 k is
+// [3 planes][64 lanes][8 bf16]: lane l (r = l & 31, h = l >> 5) element j holds row 32 nb + r,
+// k = 16 g + 8 (j >> 2) + 4 h + (j & 3) -- the v_mfma_f32_32x32x16_bf16 A fragment, with the k order the chain
+// kernel's fp32 activation panel gives its B fragment (two ds_read_b128 of quads 4g + h and 4g + 2 + h).
+enum { X6_W1X, X6_W2D, X6_W2R, X6_W3D, X6_WP1, X6_WP2, X6_WP3, X6_WQ1X, X6_WQ2, X6_N };
+// rows / k of x6 matrix i (the source panel's rows and columns)
+__host__ __device__ inline void x6_shape(const Layout& w, int i, int* rows, int* k) {
+    const int M = w.M;
+    switch (i) {
+        case X6_W1X: *rows = 2 * M; *k = w.Kx; break;
+        case X6_W2D: case X6_W2R: case X6_WP2: *rows = M; *k = M; break;
+        case X6_W3D: *rows = w.Lr; *k = M; break;
+        case X6_WP1: *rows = M; *k = w.Lp; break;
+        case X6_WP3: *rows = w.Ar; *k = M; break;
+        case X6_WQ1X: *rows = 2 * M; *k = w.Kx; break;
+        default: *rows = 2 * M; *k = M; break;   // X6_WQ2: the two Q heads' panels stacked
+    }
+}
+inline size_t x6_src(const Layout& w, int i) {
+    const size_t src[X6_N] = {w.w1x, w.w2d, w.w2r, w.w3d, w.wp1, w.wp2, w.wp3, w.wq1x, w.wq2};
+    return src[i];
+}
 
 bool make_layout(const tdmpc_dims* d, Layout* w) {
     if (!d || d->action_dim <= 0 || d->latent_dim <= 0 || d->mlp_dim <= 0 || d->mlp_dim % 64) return false;
@@ -138,6 +163,11 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
     w->wq1x = take(2 * M * w->Kx); w->bq1x = take(2 * M); w->g1 = take(2 * M); w->be1 = take(2 * M);
     w->wq2 = take(2 * M * M); w->bq2 = take(2 * M); w->g2 = take(2 * M); w->be2 = take(2 * M);
     w->wq3 = take(2 * M); w->bq3 = take(2);
+    for (int i = 0; i < X6_N; ++i) {
+        int r, k;
+        x6_shape(*w, i, &r, &k);
+        w->x6[i] = take(rup(r, 32) * rup(k, 16) * 3 / 2);   // bf16 elements / 2 = floats
+    }
     w->total = o;
     return true;
 }
@@ -852,6 +882,7 @@ struct ChainProb {
     const float* W2; const float* b2;    // panel [M][M], bias [M]
     const float* g1; const float* be1; const float* g2; const float* be2;  // CH_Q LayerNorm affines [M]
     const float* w3v; const float* b3v;  // reward / Q last layer: dense [M] + bias [1]
+    const unsigned short* X1; const unsigned short* X2;   // W1 / W2 in the x6 layout (chain_kernel<..., X6>)
 };
 
 struct ChainArgs {
@@ -861,10 +892,12 @@ struct ChainArgs {
     int nw;                              // waves per workgroup of chain_kernel: 8 or 16
     int hfl;                             // floats of the LDS activation block (max(K1, M) * rb, K1 to 16)
     int il;                              // > 0: the problems interleaved along blockIdx.x (pb = x % il)
+    int x6;                              // chain_kernel<..., X6 = true>: fp32 products from split bf16
     RowMap amap;                         // logical row -> X row (input and output)
     const float* X; long x_ts;           // X_t panel (input)
     // last layer of dynamics / pi: panel [n3][M] + bias -> Xo quads [out_q0, out_q0 + nstore/4)
     const float* W3; const float* b3; int n3, nvalid, nstore;
+    const unsigned short* X3;            // W3 in the x6 layout
     float* Xo; int out_q0;
     // CH_STEP reward: G update (EPI_LIN_Z of the layered path)
     float* G; float* rlast; float disc; int first, last;
@@ -928,6 +961,104 @@ DEVI void ring_run(floatx16 (&acc)[TN], float4 (&wr)[D][TN], const float* sA, co
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
                     acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4c(wr[d][j], kk), f4c(av, kk), acc[j], 0, 0, 0);
+        }
+    }
+}
+
+// ---- x6: fp32 products from a three-way bf16 split on v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA rate). Each
+// operand x = hi + mid + lo (bf16 each, the residuals exact in fp32); a product keeps the six terms down to
+// 2^-16 relative (hi.hi, hi.mid, mid.hi, hi.lo, lo.hi, mid.mid), dropping mid.lo, lo.mid, lo.lo (<= 2^-24
+// relative, the size of one fp32 rounding), and accumulates in fp32: the accuracy of an fp32 GEMM, at 6/16 of
+// the f32 MFMA cycles. Weights come pre-split (Layout::x6, pack_x6_kernel); the activations stay fp32 in LDS
+// and are split as they are read.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+DEVI bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+DEVI void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
+    hi = (__bf16)x;
+    const float r1 = __fsub_rn(x, (float)hi);
+    mid = (__bf16)r1;
+    lo = (__bf16)__fsub_rn(r1, (float)mid);
+}
+
+DEVI void split8(const float4& a0, const float4& a1, bf16x8_t& bh, bf16x8_t& bm, bf16x8_t& bl) {
+    const float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        __bf16 h, m, l;
+        split3(x[e], h, m, l);
+        bh[e] = h; bm[e] = m; bl[e] = l;
+    }
+}
+
+// Weight ring of the x6 form: D k groups (16 k each) x TN blocks x 3 planes of 1 KiB wave loads. Wp is the wave's
+// first block already offset by the lane (lane * 8 bf16); blocks wbs bf16 apart.
+template <int TN, int D>
+DEVI void ring6_fill(uint4 (&wr)[D][TN][3], const unsigned short* Wp, long wbs, int g0, int g1) {
+    const int gl = g1 - 1;
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                wr[d][j][p] = *(const uint4*)(Wp + j * wbs + ((size_t)min(g0 + d, gl) * 3 + p) * 512);
+}
+
+template <int TN>
+DEVI void x6_group(floatx16 (&acc)[TN], const uint4 (&w)[TN][3], const float4& a0, const float4& a1) {
+    bf16x8_t bh, bm, bl;
+    split8(a0, a1, bh, bm, bl);
+    // small terms first, the hi.hi term last
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][1]), bm, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][2]), bh, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), bl, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][1]), bh, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), bm, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), bh, acc[j], 0, 0, 0);
+}
+
+// acc[j] += W(block j) . A over k groups [g0, g1); A from the fp32 LDS block [K/4][32][4] (quads 4g + h and
+// 4g + 2 + h of row r: the x6 k order), one group ahead; W refilled D groups ahead, as ring_run.
+template <int TN, int D>
+DEVI void ring6_run(floatx16 (&acc)[TN], uint4 (&wr)[D][TN][3], const float* sA, const unsigned short* Wp, long wbs,
+                    int g0, int g1, int r, int h) {
+    const int gl = g1 - 1;
+    const float* ap = sA + (h * 32 + r) * 4;
+    float4 n0 = *(const float4*)(ap + (size_t)g0 * 512), n1 = *(const float4*)(ap + (size_t)g0 * 512 + 256);
+    int gb = g0;
+    for (; gb + D <= g1; gb += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int g = gb + d;
+            const float4 a0 = n0, a1 = n1;
+            const size_t gn = (size_t)min(g + 1, gl) * 512;
+            n0 = *(const float4*)(ap + gn);
+            n1 = *(const float4*)(ap + gn + 256);
+            __builtin_amdgcn_sched_barrier(0);
+            x6_group<TN>(acc, wr[d], a0, a1);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    wr[d][j][p] = *(const uint4*)(Wp + j * wbs + ((size_t)min(g + D, gl) * 3 + p) * 512);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) {
+        if (gb + d < g1) {
+            const float4 a0 = n0, a1 = n1;
+            const size_t gn = (size_t)min(gb + d + 1, gl) * 512;
+            n0 = *(const float4*)(ap + gn);
+            n1 = *(const float4*)(ap + gn + 256);
+            x6_group<TN>(acc, wr[d], a0, a1);
         }
     }
 }
@@ -1020,8 +1151,8 @@ DEVI void chain_store_lds(float* sH, const float (&v)[TN * 16], int cw0, int r, 
 }
 
 // NW = 8 or 16 waves per workgroup (16: 4 waves per SIMD on one 32-row block, TN = M / 512).
-template <int MODE, int TN, int NW = 8, int D = 4, int D3 = 8>
-__global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
+template <int MODE, int TN, int NW = 8, int D = 4, int D3 = 8, bool X6 = false>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6 ? 4 : 1))) chain_kernel(const ChainArgs a) {
     constexpr int NTH = 64 * NW;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
@@ -1042,6 +1173,9 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
     float* sg2 = sp + 5 * M;
     float* sbe2 = sp + 6 * M;
     const int lo = h * 128 + r * 4;         // lane offset inside a weight-panel k group
+    // x6: k groups of 16, blocks of 32 rows x K16 x 3 planes (bf16 elements)
+    const int g1n = X6 ? (int)(rup(a.K1, 16) >> 4) : a.K1 >> 3, g2n = X6 ? M >> 4 : M >> 3;
+    const long wb1 = (long)g1n * 1536, wb2 = (long)g2n * 1536;
     const int cw0 = wave * TN;              // first 32-column block of this wave in the M-wide layers
     const bool head_dot = MODE == CH_Q || (MODE == CH_STEP && pb == 1);
 #ifdef TDMPC_STAMPS
@@ -1052,13 +1186,19 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
 
     // ---- layer-1 weights in flight first, then the block's input rows (X quads [q1, q1 + K1/4); 32
     // consecutive lanes = 32 rows of one quad) and the parameter vectors
-    float4 wr[D][TN];
-    ring_fill<TN, D>(wr, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3);
-    for (int i = tid; i < (a.K1 >> 2) * 32; i += NTH) {
+    float4 wr[X6 ? 1 : D][TN];
+    uint4 wx[X6 ? D : 1][TN][3];
+    if constexpr (X6) ring6_fill<TN, D>(wx, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n);
+    else ring_fill<TN, D>(wr, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3);
+    // (x6: K1 rounded to 16 with zero quads)
+    const int q1n = X6 ? g1n * 4 : a.K1 >> 2;
+    for (int i = tid; i < q1n * 32; i += NTH) {
         const int row = i & 31, q = i >> 5;
         const int lm = m0 + row;
         const int xr = map_row(a.amap, lm < a.rows ? lm : 0);
-        ((float4*)sH)[i] = *(const float4*)(a.X + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.q1 + q) * 128 + (xr & 31) * 4);
+        ((float4*)sH)[i] = q < (a.K1 >> 2)
+            ? *(const float4*)(a.X + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.q1 + q) * 128 + (xr & 31) * 4)
+            : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     for (int i = tid; i < M / 4; i += NTH) {
         ((float4*)sb1)[i] = ((const float4*)P.b1)[i];
@@ -1093,9 +1233,11 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
     for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    ring_run<TN, D>(acc, wr, sH, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3, r, h);
+    if constexpr (X6) ring6_run<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n, r, h);
+    else ring_run<TN, D>(acc, wr, sH, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3, r, h);
     // layer-2 weights in flight during the epilogue
-    ring_fill<TN, D>(wr, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3);
+    if constexpr (X6) ring6_fill<TN, D>(wx, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n);
+    else ring_fill<TN, D>(wr, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3);
     lds_barrier();   // every wave is done with the input tile: sH becomes h1
 #ifdef TDMPC_STAMPS
     STAMP(1);
@@ -1125,7 +1267,8 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
     for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    ring_run<TN, D>(acc, wr, sH, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3, r, h);
+    if constexpr (X6) ring6_run<TN, D>(acc, wx, sH, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n, r, h);
+    else ring_run<TN, D>(acc, wr, sH, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3, r, h);
 #ifdef TDMPC_STAMPS
     STAMP(3);
 #endif
@@ -1133,11 +1276,17 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
     const int nb3 = a.n3 >> 5;
     const int ks = nb3 >= NW ? 1 : NW / nb3;
     const int items = nb3 * ks;
-    const int gper = (M >> 3) / ks;
-    float4 w3r[D3][1];
-    if (!head_dot && wave < items)
-        ring_fill<1, D3>(w3r, a.W3 + (size_t)(wave / ks) * M * 32 + lo, (long)M * 32, (wave % ks) * gper,
-                         (wave % ks + 1) * gper);
+    const int gper = g2n / ks;
+    float4 w3r[X6 ? 1 : D3][1];
+    uint4 w3x[X6 ? D3 : 1][1][3];
+    if (!head_dot && wave < items) {
+        if constexpr (X6)
+            ring6_fill<1, D3>(w3x, a.X3 + (size_t)(wave / ks) * wb2 + lane * 8, wb2, (wave % ks) * gper,
+                              (wave % ks + 1) * gper);
+        else
+            ring_fill<1, D3>(w3r, a.W3 + (size_t)(wave / ks) * M * 32 + lo, (long)M * 32, (wave % ks) * gper,
+                             (wave % ks + 1) * gper);
+    }
     float v[TN * 16];
     chain_bias<TN>(v, acc, sb2, cw0, h);
     if (head_dot) {
@@ -1197,12 +1346,20 @@ __global__ void __launch_bounds__(64 * NW) chain_kernel(const ChainArgs a) {
     for (int e = 0; e < 16; ++e) { a3a[0][e] = 0.f; a3b[0][e] = 0.f; }
     if (wave < items) {
         const int blk = wave / ks, kp = wave % ks;
-        ring_run<1, D3>(a3a, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
+        if constexpr (X6)
+            ring6_run<1, D3>(a3a, w3x, sH, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, r, h);
+        else
+            ring_run<1, D3>(a3a, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
     }
     if (wave + NW < items) {
         const int blk = (wave + NW) / ks, kp = (wave + NW) % ks;
-        ring_fill<1, D3>(w3r, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper);
-        ring_run<1, D3>(a3b, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
+        if constexpr (X6) {
+            ring6_fill<1, D3>(w3x, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper);
+            ring6_run<1, D3>(a3b, w3x, sH, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, r, h);
+        } else {
+            ring_fill<1, D3>(w3r, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper);
+            ring_run<1, D3>(a3b, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
+        }
     }
     lds_barrier();
 #pragma unroll
@@ -2481,6 +2638,25 @@ __global__ void pack_transpose_kernel(const float* src, int rows, int cols, floa
 }
 
 // Candidate actions [B][H][T][A] -> X_t panels' action columns (zero pad to Ap) (estimate_value entry).
+// fp32 weight panel [rows/32][K/4][32][4] -> the x6 planes (Layout::x6): block (nb, g) [3][64][8] bf16
+__global__ void pack_x6_kernel(const float* src, int rows, int K, unsigned short* dst) {
+    const int G = (K + 15) / 16;
+    const size_t total = (size_t)((rows + 31) / 32) * G * 512;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int j = i & 7, lane = (i >> 3) & 63;
+        const size_t blk = i >> 9;
+        const int g = (int)(blk % G), nb = (int)(blk / G);
+        const int r = lane & 31, h = lane >> 5;
+        const int k = 16 * g + 8 * (j >> 2) + 4 * h + (j & 3);
+        const float x = k < K ? src[(size_t)nb * K * 32 + (size_t)(k >> 2) * 128 + r * 4 + (k & 3)] : 0.f;
+        __bf16 hi, mid, lo;
+        split3(x, hi, mid, lo);
+        dst[(blk * 3 + 0) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, hi);
+        dst[(blk * 3 + 1) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, mid);
+        dst[(blk * 3 + 2) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, lo);
+    }
+}
+
 // candidate actions act [B][H][Ts][A] -> the action columns of rows e * Td + r0 + r of X_t (t < H)
 __global__ void scatter_actions_kernel(const float* act, float* X, size_t x_stride, int H, int Ts, int A, int Ap,
                                        int Kx, int B, int Td, int r0) {
@@ -2562,6 +2738,9 @@ int init_attrs() {
     CHAIN_ATTR(CH_PI, 1) CHAIN_ATTR(CH_PI, 2) CHAIN_ATTR(CH_PI, 4)
     CHAIN_ATTR(CH_Q, 1) CHAIN_ATTR(CH_Q, 2) CHAIN_ATTR(CH_Q, 4)
 #undef CHAIN_ATTR
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 2, 8, 2, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 2, 8, 2, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 2, 8, 2, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -2859,7 +3038,8 @@ int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
     }
 #define CHAIN_LAUNCH(MODE, TN) \
     if (mode == MODE && tn == TN) { \
-        if (nw == 16 && TN == 1) hipLaunchKernelGGL((chain_kernel<MODE, 1, 16>), grid, block, lds, s, a); \
+        if (a.x6 && TN == 2) hipLaunchKernelGGL((chain_kernel<MODE, 2, 8, 2, 2, true>), grid, block, lds, s, a); \
+        else if (nw == 16 && TN == 1) hipLaunchKernelGGL((chain_kernel<MODE, 1, 16>), grid, block, lds, s, a); \
         else hipLaunchKernelGGL((chain_kernel<MODE, TN>), grid, block, lds, s, a); \
         HIPCHK(hipGetLastError()); \
         if (prof) { \
@@ -2899,6 +3079,7 @@ struct Ctx {
 };
 
 float* Xt(const Ctx& c, int t) { return c.k.X + (size_t)t * c.k.x_stride; }
+const unsigned short* x6p(const Ctx& c, int i) { return (const unsigned short*)(c.pw + c.w.x6[i]); }
 // Per-head thresholds (TDMPC_CHAIN_WGS_STEP / _PI / _Q override). The Q heads' layered form is four launches
 // (two GEMMs with LayerNorm partial moments, the LN+tanh pass, the value kernel), so the chain form wins from half
 // the step threshold: one env's 768 terminal rows 1.42 -> 1.32 ms per plan (tools/gpu52.sh); the step and pi
@@ -2943,13 +3124,28 @@ int chain_nw() {
     return v;
 }
 
+// x6 chain kernels (fp32 products from a three-way bf16 split, chain_kernel<..., X6>) for 32-row chain launches:
+// forced by TDMPC_PATH_CHAIN_X6, the default of the auto / chain paths (TDMPC_X6=0 turns it off there); the
+// chain32 / chain16 paths keep the exact f32 MFMA. M = 512 only (the one instantiated width). Measured on MI355X
+// (humanoid-run, tools/gpu72.sh): 8.89 -> 6.52 ms per B = 32 plan, 3.03 -> 2.19 ms at B = 8.
+bool use_x6(const Ctx& c) {
+    if (c.w.M != 512) return false;
+    if (c.path == TDMPC_PATH_CHAIN_X6) return true;
+    static int en = -1;
+    if (en < 0) {
+        const char* e = getenv("TDMPC_X6");
+        en = e ? atoi(e) : 1;
+    }
+    return en && (c.path == TDMPC_PATH_AUTO || c.path == TDMPC_PATH_CHAIN);
+}
+
 // Row block of a chain launch. Auto: 32-row blocks once they occupy more than half the CUs (their weight
 // fragments serve twice the rows; measured on MI355X, humanoid: 57.5 vs 61 us for the 256-workgroup B = 8
 // step, 99 vs 114 us at B = 16, and 16-row blocks lose on the 192-workgroup pi launch too), else 16-row
 // blocks, which double the workgroups of a narrow launch (B = 4 step: 36.7 us vs 56 us on 128 32-row
 // workgroups). TDMPC_CHAIN_RB forces 16 or 32 for experiments.
 int chain_rb(const Ctx& c, int rows, int nprob) {
-    if (!chain16_shape_ok(c.w) || c.path == TDMPC_PATH_CHAIN32) return 32;
+    if (!chain16_shape_ok(c.w) || c.path == TDMPC_PATH_CHAIN32 || c.path == TDMPC_PATH_CHAIN_X6) return 32;
     if (c.path == TDMPC_PATH_CHAIN16) return 16;
     static int forced = -1;
     if (forced < 0) {
@@ -2965,7 +3161,8 @@ ChainArgs chain0(const Ctx& c, int rows, RowMap map, int t, int K1, int q1, int 
     memset(&a, 0, sizeof a);
     a.rows = rows; a.M = c.M; a.K1 = K1; a.q1 = q1; a.amap = map;
     a.rb = chain_rb(c, rows, nprob);
-    a.nw = a.rb == 32 && chain_nw() == 16 && chain_nw16_ok(c.w) ? 16 : 8;
+    a.x6 = a.rb == 32 && use_x6(c);
+    a.nw = a.rb == 32 && !a.x6 && chain_nw() == 16 && chain_nw16_ok(c.w) ? 16 : 8;
     a.hfl = std::max((int)rup(c.Kx, 16), c.M) * a.rb;
     a.X = Xt(c, t); a.x_ts = (long)c.Kx * 32;
     return a;
@@ -3052,6 +3249,11 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         r.W1 = c.pw + w.w1x + (size_t)M * c.Kx; r.b1 = c.pw + w.b1x + M; r.W2 = c.pw + w.w2r; r.b2 = c.pw + w.b2r;
         r.w3v = c.pw + w.w3r; r.b3v = c.pw + w.b3r;
         a.W3 = c.pw + w.w3d; a.b3 = c.pw + w.b3d; a.n3 = w.Lr; a.nvalid = w.L; a.nstore = w.Lp;
+        if (a.x6) {
+            const size_t rb1 = (size_t)(M / 32) * (rup(c.Kx, 16) / 16) * 1536;   // bf16 per M rows of x6 W1
+            d.X1 = x6p(c, X6_W1X); r.X1 = x6p(c, X6_W1X) + rb1;
+            d.X2 = x6p(c, X6_W2D); r.X2 = x6p(c, X6_W2R); a.X3 = x6p(c, X6_W3D);
+        }
         a.Xo = Xt(c, t + 1); a.out_q0 = w.Ap / 4;
         a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
         return launch_chain(CH_STEP, a, 2, c.s);
@@ -3131,6 +3333,7 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
         ChainProb& p = a.p[0];
         p.W1 = c.pw + w.wp1; p.b1 = c.pw + w.bp1; p.W2 = c.pw + w.wp2; p.b2 = c.pw + w.bp2;
         a.W3 = c.pw + w.wp3; a.b3 = c.pw + w.bp3; a.n3 = w.Ar; a.nvalid = w.A; a.nstore = w.Ap;
+        if (a.x6) { p.X1 = x6p(c, X6_WP1); p.X2 = x6p(c, X6_WP2); a.X3 = x6p(c, X6_WP3); }
         a.Xo = Xt(c, t); a.out_q0 = 0;
         a.eps = eps; a.eps_G = eps_G; a.eps_env = eps_env; a.eps_off = eps_off; a.A = w.A;
         a.min_std = min_std; a.lo = (float)(-1.0 + 1e-6); a.hi = (float)(1.0 - 1e-6);
@@ -3223,6 +3426,10 @@ int q_chain(const Ctx& c, int rows, RowMap map) {
         p.W2 = c.pw + w.wq2 + (size_t)q * M * M; p.b2 = c.pw + w.bq2 + q * M;
         p.g2 = c.pw + w.g2 + q * M; p.be2 = c.pw + w.be2 + q * M;
         p.w3v = c.pw + w.wq3 + q * M; p.b3v = c.pw + w.bq3 + q;
+        if (a.x6) {
+            p.X1 = x6p(c, X6_WQ1X) + (size_t)q * (M / 32) * (rup(c.Kx, 16) / 16) * 1536;
+            p.X2 = x6p(c, X6_WQ2) + (size_t)q * (M / 32) * (M / 16) * 1536;
+        }
     }
     a.q = c.k.qv; a.q_ld = c.k.xrows;
     return launch_chain(CH_Q, a, 2, c.s);
@@ -3515,6 +3722,15 @@ int tdmpc_pack_weights(const tdmpc_dims* d, const float* const* t, int32_t n, vo
         HIPCHK(cp(w.g2 + q * M, t[i++], M)); HIPCHK(cp(w.be2 + q * M, t[i++], M));
         HIPCHK(cp(w.wq3 + q * M, t[i++], M)); HIPCHK(cp(w.bq3 + q, t[i++], 1));
     }
+    // the x6 copies of the chain kernels' panels (stream-ordered after the panels above)
+    for (int x = 0; x < X6_N; ++x) {
+        int rows, k;
+        x6_shape(w, x, &rows, &k);
+        const size_t n = (size_t)rup(rows, 32) * rup(k, 16) * 3;
+        hipLaunchKernelGGL(pack_x6_kernel, dim3((unsigned)std::min<size_t>(2048, (n / 3 + 255) / 256)), dim3(256), 0, s,
+                           pw + x6_src(w, x), rows, k, (unsigned short*)(pw + w.x6[x]));
+        HIPCHK(hipGetLastError());
+    }
     return 0;
 }
 
@@ -3541,7 +3757,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     int rc;
     const int H = prm->horizon, I = prm->iterations, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 5) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 6) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T;
     // z0 = h(obs) and mean = 0 (warm: prev_mean shifted), std = 2
@@ -3623,7 +3839,7 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
     const int H = prm->horizon, I = prm->iterations, B = prm->batch, K = d->num_elites;
     if (I <= 0 || I > 16) { snprintf(g_err, sizeof g_err, "iCEM: 1..16 iterations"); return TDMPC_E_DIMS; }
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream, K))) return rc;
-    if (prm->path < 0 || prm->path > 5) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 6) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = d->num_samples, Pmax = d->num_pi, Tw = N + K + Pmax, pi_base = N + K, P0 = prm->n_pi0;
     c.T = Tw;
@@ -3721,7 +3937,7 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 5) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 6) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     if (rows != c.T) { snprintf(g_err, sizeof g_err, "rows must equal N+P"); return TDMPC_E_DIMS; }
     const int T = c.T, L = c.w.L;
@@ -3766,7 +3982,7 @@ int tdmpc_pi_rollout(const tdmpc_dims* d, const tdmpc_plan_params* prm, const vo
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 5) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 6) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T;
     const long A = c.A;
@@ -3795,7 +4011,7 @@ int tdmpc_cem_iter(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 5) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 6) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T, A = c.A, HA = H * A;
     if (P > 0 && !pi_actions) return TDMPC_E_NULL;
