@@ -1063,6 +1063,88 @@ DEVI void ring6_run(floatx16 (&acc)[TN], uint4 (&wr)[D][TN][3], const float* sA,
     }
 }
 
+// Planes form of the x6 activations (X6 = 2): the LDS block holds the split activations, group g (16 k) as
+// [3 planes][64 lanes][8 bf16] in the weights' k order, written once by the producing epilogue (or the input
+// staging) instead of being split again by every wave at every read.
+DEVI uint4 as_u4(const bf16x8_t& v) { return __builtin_bit_cast(uint4, v); }
+
+template <int TN, int D>
+DEVI void ring6p_run(floatx16 (&acc)[TN], uint4 (&wr)[D][TN][3], const float* sA, const unsigned short* Wp, long wbs,
+                     int g0, int g1, int lane) {
+    const int gl = g1 - 1;
+    const uint4* ap = (const uint4*)sA + lane;   // group g plane p at ap[(3g + p) * 64]
+    uint4 n[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) n[p] = ap[(size_t)(3 * g0 + p) * 64];
+    int gb = g0;
+    for (; gb + D <= g1; gb += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int g = gb + d;
+            const bf16x8_t bh = as_bf16x8(n[0]), bm = as_bf16x8(n[1]), bl = as_bf16x8(n[2]);
+            const int gn = min(g + 1, gl);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) n[p] = ap[(size_t)(3 * gn + p) * 64];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), bm, acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][2]), bh, acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bl, acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), bh, acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bm, acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bh, acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    wr[d][j][p] = *(const uint4*)(Wp + j * wbs + ((size_t)min(g + D, gl) * 3 + p) * 512);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) {
+        if (gb + d < g1) {
+            const bf16x8_t bh = as_bf16x8(n[0]), bm = as_bf16x8(n[1]), bl = as_bf16x8(n[2]);
+            const int gn = min(gb + d + 1, gl);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) n[p] = ap[(size_t)(3 * gn + p) * 64];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), bm, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][2]), bh, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bl, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), bh, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bm, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bh, acc[j], 0, 0, 0);
+            }
+        }
+    }
+}
+
+// a layer's register tile into the planes block: tile j's registers 8s..8s+7 are exactly group 2(cw0 + j) + s of
+// the lane's row in the x6 k order (the accumulator-as-operand map), so each is one split and 3 b128 stores
+template <int TN>
+DEVI void chain_store_planes(float* sH, const float (&v)[TN * 16], int cw0, int lane) {
+    uint4* dst = (uint4*)sH + lane;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const float* x = v + j * 16 + 8 * s2;
+            bf16x8_t bh, bm, bl;
+            split8(make_float4(x[0], x[1], x[2], x[3]), make_float4(x[4], x[5], x[6], x[7]), bh, bm, bl);
+            const size_t g = 2 * (cw0 + j) + s2;
+            dst[(3 * g + 0) * 64] = as_u4(bh);
+            dst[(3 * g + 1) * 64] = as_u4(bm);
+            dst[(3 * g + 2) * 64] = as_u4(bl);
+        }
+}
+
 // Workgroup barrier for the chain kernels' LDS hand-offs: waits for this wave's LDS traffic only. HIP's
 // __syncthreads() carries a fence that drains vmcnt, i.e. it also waits for every global load in flight (the next
 // layer's weight ring prefetched before the epilogue, the ring's tail refills). No chain-kernel barrier orders
@@ -1151,8 +1233,10 @@ DEVI void chain_store_lds(float* sH, const float (&v)[TN * 16], int cw0, int r, 
 }
 
 // NW = 8 or 16 waves per workgroup (16: 4 waves per SIMD on one 32-row block, TN = M / 512).
-template <int MODE, int TN, int NW = 8, int D = 4, int D3 = 8, bool X6 = false>
-__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6 ? 4 : 1))) chain_kernel(const ChainArgs a) {
+// X6: 0 = f32 MFMA; 1 = x6 with the activations kept fp32 in LDS and split as read; 2 = x6 with the activations as
+// split planes in LDS (one workgroup per CU: 96 KB at M = 512).
+template <int MODE, int TN, int NW = 8, int D = 4, int D3 = 8, int X6 = 0>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6 == 1 ? 4 : 1))) chain_kernel(const ChainArgs a) {
     constexpr int NTH = 64 * NW;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
@@ -1196,9 +1280,29 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
         const int row = i & 31, q = i >> 5;
         const int lm = m0 + row;
         const int xr = map_row(a.amap, lm < a.rows ? lm : 0);
-        ((float4*)sH)[i] = q < (a.K1 >> 2)
+        const float4 x = q < (a.K1 >> 2)
             ? *(const float4*)(a.X + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.q1 + q) * 128 + (xr & 31) * 4)
             : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (X6 == 2) {
+            // quad q = 4g + qq: lane half qq & 1, elements 4 (qq >> 1) .. + 3 of the group's slot
+            const int g = q >> 2, qq = q & 3, ln = (qq & 1) * 32 + row, j0 = 4 * (qq >> 1);
+            const float xs[4] = {x.x, x.y, x.z, x.w};
+            unsigned short hb[4], mb[4], lb[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                __bf16 hh, mm, ll;
+                split3(xs[e], hh, mm, ll);
+                hb[e] = __builtin_bit_cast(unsigned short, hh);
+                mb[e] = __builtin_bit_cast(unsigned short, mm);
+                lb[e] = __builtin_bit_cast(unsigned short, ll);
+            }
+            unsigned short* d16 = (unsigned short*)sH;
+            *(uint2*)(d16 + ((size_t)(3 * g + 0) * 64 + ln) * 8 + j0) = make_uint2(hb[0] | (hb[1] << 16), hb[2] | (hb[3] << 16));
+            *(uint2*)(d16 + ((size_t)(3 * g + 1) * 64 + ln) * 8 + j0) = make_uint2(mb[0] | (mb[1] << 16), mb[2] | (mb[3] << 16));
+            *(uint2*)(d16 + ((size_t)(3 * g + 2) * 64 + ln) * 8 + j0) = make_uint2(lb[0] | (lb[1] << 16), lb[2] | (lb[3] << 16));
+        } else {
+            ((float4*)sH)[i] = x;
+        }
     }
     for (int i = tid; i < M / 4; i += NTH) {
         ((float4*)sb1)[i] = ((const float4*)P.b1)[i];
@@ -1233,7 +1337,8 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    if constexpr (X6) ring6_run<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n, r, h);
+    if constexpr (X6 == 2) ring6p_run<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n, lane);
+    else if constexpr (X6 == 1) ring6_run<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n, r, h);
     else ring_run<TN, D>(acc, wr, sH, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3, r, h);
     // layer-2 weights in flight during the epilogue
     if constexpr (X6) ring6_fill<TN, D>(wx, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n);
@@ -1255,7 +1360,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
 #pragma unroll
             for (int i = 0; i < TN * 16; ++i) v[i] = elu_f(v[i]);
         }
-        chain_store_lds<TN>(sH, v, cw0, r, h);
+        if constexpr (X6 == 2) chain_store_planes<TN>(sH, v, cw0, lane); else chain_store_lds<TN>(sH, v, cw0, r, h);
     }
     lds_barrier();
 #ifdef TDMPC_STAMPS
@@ -1267,7 +1372,8 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    if constexpr (X6) ring6_run<TN, D>(acc, wx, sH, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n, r, h);
+    if constexpr (X6 == 2) ring6p_run<TN, D>(acc, wx, sH, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n, lane);
+    else if constexpr (X6 == 1) ring6_run<TN, D>(acc, wx, sH, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n, r, h);
     else ring_run<TN, D>(acc, wr, sH, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3, r, h);
 #ifdef TDMPC_STAMPS
     STAMP(3);
@@ -1337,7 +1443,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
 #pragma unroll
     for (int i = 0; i < TN * 16; ++i) v[i] = elu_f(v[i]);
     lds_barrier();
-    chain_store_lds<TN>(sH, v, cw0, r, h);
+    if constexpr (X6 == 2) chain_store_planes<TN>(sH, v, cw0, lane); else chain_store_lds<TN>(sH, v, cw0, r, h);
     lds_barrier();
 
     // ---- layer 3: [32 x M] . W3^T -> [32 x n3]; partial tiles meet in the activation block after the reads
@@ -1346,7 +1452,9 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     for (int e = 0; e < 16; ++e) { a3a[0][e] = 0.f; a3b[0][e] = 0.f; }
     if (wave < items) {
         const int blk = wave / ks, kp = wave % ks;
-        if constexpr (X6)
+        if constexpr (X6 == 2)
+            ring6p_run<1, D3>(a3a, w3x, sH, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, lane);
+        else if constexpr (X6 == 1)
             ring6_run<1, D3>(a3a, w3x, sH, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, r, h);
         else
             ring_run<1, D3>(a3a, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
@@ -1355,7 +1463,10 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
         const int blk = (wave + NW) / ks, kp = (wave + NW) % ks;
         if constexpr (X6) {
             ring6_fill<1, D3>(w3x, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper);
-            ring6_run<1, D3>(a3b, w3x, sH, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, r, h);
+            if constexpr (X6 == 2)
+                ring6p_run<1, D3>(a3b, w3x, sH, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, lane);
+            else
+                ring6_run<1, D3>(a3b, w3x, sH, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, r, h);
         } else {
             ring_fill<1, D3>(w3r, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper);
             ring_run<1, D3>(a3b, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
@@ -2738,9 +2849,12 @@ int init_attrs() {
     CHAIN_ATTR(CH_PI, 1) CHAIN_ATTR(CH_PI, 2) CHAIN_ATTR(CH_PI, 4)
     CHAIN_ATTR(CH_Q, 1) CHAIN_ATTR(CH_Q, 2) CHAIN_ATTR(CH_Q, 4)
 #undef CHAIN_ATTR
-    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 2, 8, 2, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 2, 8, 2, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 2, 8, 2, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 2, 8, 2, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 2, 8, 4, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 2, 8, 2, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 2, 8, 4, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 2, 8, 2, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 2, 8, 4, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -3038,7 +3152,8 @@ int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
     }
 #define CHAIN_LAUNCH(MODE, TN) \
     if (mode == MODE && tn == TN) { \
-        if (a.x6 && TN == 2) hipLaunchKernelGGL((chain_kernel<MODE, 2, 8, 2, 2, true>), grid, block, lds, s, a); \
+        if (a.x6 == 2 && TN == 2) hipLaunchKernelGGL((chain_kernel<MODE, 2, 8, 4, 4, 2>), grid, block, lds, s, a); \
+        else if (a.x6 && TN == 2) hipLaunchKernelGGL((chain_kernel<MODE, 2, 8, 2, 2, 1>), grid, block, lds, s, a); \
         else if (nw == 16 && TN == 1) hipLaunchKernelGGL((chain_kernel<MODE, 1, 16>), grid, block, lds, s, a); \
         else hipLaunchKernelGGL((chain_kernel<MODE, TN>), grid, block, lds, s, a); \
         HIPCHK(hipGetLastError()); \
@@ -3128,15 +3243,17 @@ int chain_nw() {
 // forced by TDMPC_PATH_CHAIN_X6, the default of the auto / chain paths (TDMPC_X6=0 turns it off there); the
 // chain32 / chain16 paths keep the exact f32 MFMA. M = 512 only (the one instantiated width). Measured on MI355X
 // (humanoid-run, tools/gpu72.sh): 8.89 -> 6.52 ms per B = 32 plan, 3.03 -> 2.19 ms at B = 8.
-bool use_x6(const Ctx& c) {
-    if (c.w.M != 512) return false;
-    if (c.path == TDMPC_PATH_CHAIN_X6) return true;
+// Returns the X6 mode of chain_kernel (0 = f32 MFMA, 1 = split as read, 2 = split planes in LDS; TDMPC_X6 picks
+// 1 or 2, 0 turns x6 off on the auto / chain paths).
+int use_x6(const Ctx& c) {
+    if (c.w.M != 512) return 0;
     static int en = -1;
     if (en < 0) {
         const char* e = getenv("TDMPC_X6");
         en = e ? atoi(e) : 1;
     }
-    return en && (c.path == TDMPC_PATH_AUTO || c.path == TDMPC_PATH_CHAIN);
+    if (c.path == TDMPC_PATH_CHAIN_X6) return en == 2 ? 2 : 1;
+    return (c.path == TDMPC_PATH_AUTO || c.path == TDMPC_PATH_CHAIN) ? en : 0;
 }
 
 // Row block of a chain launch. Auto: 32-row blocks once they occupy more than half the CUs (their weight
@@ -3161,9 +3278,10 @@ ChainArgs chain0(const Ctx& c, int rows, RowMap map, int t, int K1, int q1, int 
     memset(&a, 0, sizeof a);
     a.rows = rows; a.M = c.M; a.K1 = K1; a.q1 = q1; a.amap = map;
     a.rb = chain_rb(c, rows, nprob);
-    a.x6 = a.rb == 32 && use_x6(c);
+    a.x6 = a.rb == 32 ? use_x6(c) : 0;
     a.nw = a.rb == 32 && !a.x6 && chain_nw() == 16 && chain_nw16_ok(c.w) ? 16 : 8;
-    a.hfl = std::max((int)rup(c.Kx, 16), c.M) * a.rb;
+    // activation block: fp32 [K/4][rb][4], or for x6 mode 2 the split planes (6 bytes per value)
+    a.hfl = std::max((int)rup(c.Kx, 16), c.M) * (a.x6 == 2 ? 48 : a.rb);
     a.X = Xt(c, t); a.x_ts = (long)c.Kx * 32;
     return a;
 }
