@@ -73,7 +73,8 @@ typedef struct tdmpc_plan_params {
                               kernels wherever the shape allows (row block by launch size), 3 / 4 = chain
                               kernels on 32- / 16-row blocks only, 5 = TOLD.next on the column-split step kernel
                               (others layered), 6 = chain kernels with fp32 products from a three-way bf16
-                              split (TDMPC_PATH_CHAIN_X6); results agree within the fp32 tolerance */
+                              split (TDMPC_PATH_CHAIN_X6), 7 = path 5 with those products; results agree within
+                              the fp32 tolerance */
 } tdmpc_plan_params;
 
 #define TDMPC_PATH_AUTO 0
@@ -83,6 +84,7 @@ typedef struct tdmpc_plan_params {
 #define TDMPC_PATH_CHAIN16 4
 #define TDMPC_PATH_SPLIT 5
 #define TDMPC_PATH_CHAIN_X6 6   /* chain kernels, fp32 products from a three-way bf16 split (M = 512) */
+#define TDMPC_PATH_SPLIT_X6 7   /* the split path (5) with the x6 products (M = 512) */
 
 /* Byte sizes the caller must allocate (all 256-byte aligned). */
 typedef struct tdmpc_sizes {

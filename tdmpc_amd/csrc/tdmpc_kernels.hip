@@ -1601,6 +1601,84 @@ DEVI void ring16_run(floatx4 (&acc)[NT], float4 (&wr)[D][NT], const float* sA, c
     }
 }
 
+// ---- x6 on 16-row blocks (v_mfma_f32_16x16x32_bf16), reusing the 32-row x6 weight layout: a 32-k group G of a
+// 16-row tile is the two 16-k groups 2G, 2G + 1 of its 32-row block; lane l (m = l & 15, h4 = l >> 4) takes group
+// 2G + (h4 >> 1) of slot (h4 & 1) * 32 + 16 * half + m, whose k order is quads 8G + 4 (h4 >> 1) + (h4 & 1) and that
+// + 2 -- the activation quads the lane reads from the fp32 [K/4][16][4] LDS block. Groups past the matrix clamp to
+// its last one and meet zero activation quads (the staging zero-fills to a multiple of 32 k).
+// Tile j of a wave covers features nf0 + 16 j; Wb = the matrix's x6 base, gmax its 16-k groups.
+template <int NT, int D>
+DEVI void ring16x6_fill(uint4 (&wr)[D][NT][3], const unsigned short* Wb, int nf0, int gmax, int g0, int g1, int lane) {
+    const int gl = g1 - 1, m = lane & 15, h4 = lane >> 4;
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int nf = nf0 + 16 * j, gi = min(2 * min(g0 + d, gl) + (h4 >> 1), gmax - 1);
+            const unsigned short* q = Wb + ((size_t)(nf >> 5) * gmax + gi) * 1536 + ((h4 & 1) * 32 + (nf & 16) + m) * 8;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) wr[d][j][p] = *(const uint4*)(q + p * 512);
+        }
+}
+
+template <int NT>
+DEVI void x6_group16(floatx4 (&acc)[NT], const uint4 (&w)[NT][3], const float4& a0, const float4& a1) {
+    bf16x8_t bh, bm, bl;
+    split8(a0, a1, bh, bm, bl);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][1]), bm, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][2]), bh, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][0]), bl, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][1]), bh, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][0]), bm, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][0]), bh, acc[j], 0, 0, 0);
+}
+
+// acc[j] += W(tile j) . A over 32-k groups [g0, g1); A = the fp32 16-row LDS block (group G at sA + G * 512)
+template <int NT, int D>
+DEVI void ring16x6_run(floatx4 (&acc)[NT], uint4 (&wr)[D][NT][3], const float* sA, const unsigned short* Wb, int nf0,
+                       int gmax, int g0, int g1, int lane) {
+    const int gl = g1 - 1, m = lane & 15, h4 = lane >> 4;
+    const float* ap = sA + ((4 * (h4 >> 1) + (h4 & 1)) * 16 + m) * 4;   // quad qa of group 0; qb = qa + 2
+    float4 n0 = *(const float4*)(ap + (size_t)g0 * 512), n1 = *(const float4*)(ap + (size_t)g0 * 512 + 128);
+    int gb = g0;
+    for (; gb + D <= g1; gb += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int g = gb + d;
+            const float4 a0 = n0, a1 = n1;
+            const size_t gn = (size_t)min(g + 1, gl) * 512;
+            n0 = *(const float4*)(ap + gn);
+            n1 = *(const float4*)(ap + gn + 128);
+            __builtin_amdgcn_sched_barrier(0);
+            x6_group16<NT>(acc, wr[d], a0, a1);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int nf = nf0 + 16 * j, gi = min(2 * min(g + D, gl) + (h4 >> 1), gmax - 1);
+                const unsigned short* q = Wb + ((size_t)(nf >> 5) * gmax + gi) * 1536 + ((h4 & 1) * 32 + (nf & 16) + m) * 8;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) wr[d][j][p] = *(const uint4*)(q + p * 512);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) {
+        if (gb + d < g1) {
+            const float4 a0 = n0, a1 = n1;
+            const size_t gn = (size_t)min(gb + d + 1, gl) * 512;
+            n0 = *(const float4*)(ap + gn);
+            n1 = *(const float4*)(ap + gn + 128);
+            x6_group16<NT>(acc, wr[d], a0, a1);
+        }
+    }
+}
+
 // sum over the 4 lanes of row m (h4 = 0..3), then over the 8 waves through red ([8][16])
 DEVI float row16_sum(float s, float* red, int wave, int lane) {
     s += __shfl_xor(s, 16);
@@ -1887,14 +1965,16 @@ struct SplitArgs {
     // workgroup applies its return update
     const float* zin; const float* rin; const float* b3d; const float* b3r; int L, Lp, zq0;
     float* Xw; float* G; float disc_in; int first_in;
+    const unsigned short* X3;                // x6 form (split_step_kernel<..., X6 = 1>): W3 in the x6 layout
 };
 
-__host__ __device__ inline int split_hfl(int K1, int M) { return ((int)rup(K1, 16) > M ? (int)rup(K1, 16) : M) * 16; }
+__host__ __device__ inline int split_hfl(int K1, int M) { return ((int)rup(K1, 32) > M ? (int)rup(K1, 32) : M) * 16; }
 __host__ __device__ inline int split_lds_floats(int K1, int M) {
     return split_hfl(K1, M) + (M / SPLIT_S) * 16 + 128 + M + 2 * (M / SPLIT_S);
 }
 
-template <int NT, int D = 4>
+// X6 = 1: the three layers on v_mfma_f32_16x16x32_bf16 with the x6 split (ring16x6_*), same data flow.
+template <int NT, int D = 4, int X6 = 0>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) split_step_kernel(const SplitArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, h4 = lane >> 4;
@@ -1913,10 +1993,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     const int g1n = (a.K1 + 15) >> 4;
     const int f0 = 16 * NT * wave + 4 * h4;
     const long wblk = (long)(NT / 2) * wave;
+    // x6: 32-k groups; the x6 matrices' 16-k group counts
+    const int g1x = (a.K1 + 31) >> 5, gm1 = (a.K1 + 15) >> 4, gmM = M >> 4;
 
-    float4 wr[D][NT];
-    ring16_fill<NT, D>(wr, P.W1 + wblk * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1n, h4, q1max);
-    for (int i = tid; i < g1n * 4 * 16; i += 512) {
+    float4 wr[X6 ? 1 : D][NT];
+    uint4 wx[X6 ? 2 : 1][X6 ? NT / 2 : 1][3];   // x6 layer 1: two passes of NT / 2 tiles, 2 groups deep
+    if constexpr (X6) ring16x6_fill<NT / 2, 2>(wx, P.X1, 16 * NT * wave, gm1, 0, g1x, lane);
+    else ring16_fill<NT, D>(wr, P.W1 + wblk * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1n, h4, q1max);
+    for (int i = tid; i < (X6 ? g1x * 8 : g1n * 4) * 16; i += 512) {
         const int row = i & 15, q = i >> 4;
         const int lm = m0 + row;
         const int lr = lm < a.rows ? lm : 0;
@@ -1963,12 +2047,27 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     floatx4 acc[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    ring16_run<NT, D>(acc, wr, sH, P.W1 + wblk * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1n, lane, q1max);
-    // this wave's 16 columns of the slice in the second layer; its weights in flight during the epilogue
     const int n2 = sl * SW + 16 * wave;
+    float4 w2[X6 ? 1 : D][1];
+    uint4 w2x[X6 ? D : 1][1][3];
+    if constexpr (X6) {
+        floatx4 ah[NT / 2];
+#pragma unroll
+        for (int j = 0; j < NT / 2; ++j) ah[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        ring16x6_run<NT / 2, 2>(ah, wx, sH, P.X1, 16 * NT * wave, gm1, 0, g1x, lane);
+#pragma unroll
+        for (int j = 0; j < NT / 2; ++j) { acc[j] = ah[j]; ah[j] = floatx4{0.f, 0.f, 0.f, 0.f}; }
+        ring16x6_fill<NT / 2, 2>(wx, P.X1, 16 * NT * wave + 16 * (NT / 2), gm1, 0, g1x, lane);
+        ring16x6_run<NT / 2, 2>(ah, wx, sH, P.X1, 16 * NT * wave + 16 * (NT / 2), gm1, 0, g1x, lane);
+#pragma unroll
+        for (int j = 0; j < NT / 2; ++j) acc[NT / 2 + j] = ah[j];
+        ring16x6_fill<1, D>(w2x, P.X2, n2, gmM, 0, M >> 5, lane);
+    } else {
+        ring16_run<NT, D>(acc, wr, sH, P.W1 + wblk * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1n, lane, q1max);
+    }
+    // this wave's 16 columns of the slice in the second layer; its weights in flight during the epilogue
     const float* W2p = P.W2 + (size_t)(n2 >> 5) * M * 32 + (n2 & 31) * 4 + lo;
-    float4 w2[D][1];
-    ring16_fill<1, D>(w2, W2p, (long)M * 32, 0, M >> 4, h4, qMmax);
+    if constexpr (!X6) ring16_fill<1, D>(w2, W2p, (long)M * 32, 0, M >> 4, h4, qMmax);
     lds_barrier();   // every wave is done with the input block
     {
         float v[NT * 4];
@@ -1981,7 +2080,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
 
     // ---- layer 2, the slice
     floatx4 a2[1] = {floatx4{0.f, 0.f, 0.f, 0.f}};
-    ring16_run<1, D>(a2, w2, sH, W2p, (long)M * 32, 0, M >> 4, lane, qMmax);
+    if constexpr (X6) ring16x6_run<1, D>(a2, w2x, sH, P.X2, n2, gmM, 0, M >> 5, lane);
+    else ring16_run<1, D>(a2, w2, sH, W2p, (long)M * 32, 0, M >> 4, lane, qMmax);
     const int c2 = 16 * wave + 4 * h4;       // slice-local feature of a2[0][0]
     float v2[4];
 #pragma unroll
@@ -2006,11 +2106,18 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     // ---- the slice's share of the last layer: K = the slice's SW columns = 16-k groups [gs0, gs1) of W3
     const int gs0 = sl * (SW >> 4), gs1 = gs0 + (SW >> 4);
     for (int t = wave; t < (a.n3 >> 4); t += 8) {
-        const float* W3p = a.W3 + (size_t)(t >> 1) * M * 32 + (t & 1) * 64 + lo;
-        float4 w3[D][1];
-        ring16_fill<1, D>(w3, W3p, (long)M * 32, gs0, gs1, h4, qMmax);
         floatx4 a3[1] = {floatx4{0.f, 0.f, 0.f, 0.f}};
-        ring16_run<1, D>(a3, w3, sS - (size_t)gs0 * 256, W3p, (long)M * 32, gs0, gs1, lane, qMmax);
+        if constexpr (X6) {
+            const int gx0 = sl * (SW >> 5), gx1 = gx0 + (SW >> 5);
+            uint4 w3x[D][1][3];
+            ring16x6_fill<1, D>(w3x, a.X3, 16 * t, gmM, gx0, gx1, lane);
+            ring16x6_run<1, D>(a3, w3x, sS - (size_t)gx0 * 512, a.X3, 16 * t, gmM, gx0, gx1, lane);
+        } else {
+            const float* W3p = a.W3 + (size_t)(t >> 1) * M * 32 + (t & 1) * 64 + lo;
+            float4 w3[D][1];
+            ring16_fill<1, D>(w3, W3p, (long)M * 32, gs0, gs1, h4, qMmax);
+            ring16_run<1, D>(a3, w3, sS - (size_t)gs0 * 256, W3p, (long)M * 32, gs0, gs1, lane, qMmax);
+        }
         if (m0 + m < a.rows)
             *(float4*)(a.zpart + ((size_t)sl * a.prow + m0 + m) * a.n3 + t * 16 + 4 * h4) =
                 make_float4(a3[0][0], a3[0][1], a3[0][2], a3[0][3]);
@@ -3212,7 +3319,8 @@ int chain_wgs_kind(int kind) {
 }
 
 bool use_chain(const Ctx& c, int rows, int nprob, int kind) {
-    if (c.path == TDMPC_PATH_LAYERED || c.path == TDMPC_PATH_SPLIT || !chain_shape_ok(c.w)) return false;
+    if (c.path == TDMPC_PATH_LAYERED || c.path == TDMPC_PATH_SPLIT || c.path == TDMPC_PATH_SPLIT_X6 || !chain_shape_ok(c.w))
+        return false;
     const int th = chain_wgs_kind(kind);
     return c.path != TDMPC_PATH_AUTO || (th > 0 && (rows + 31) / 32 * nprob >= th);
 }
@@ -3253,6 +3361,7 @@ int use_x6(const Ctx& c) {
         en = e ? atoi(e) : 1;
     }
     if (c.path == TDMPC_PATH_CHAIN_X6) return en == 2 ? 2 : 1;
+    if (c.path == TDMPC_PATH_SPLIT_X6) return 1;
     return (c.path == TDMPC_PATH_AUTO || c.path == TDMPC_PATH_CHAIN) ? en : 0;
 }
 
@@ -3296,7 +3405,7 @@ Opnd wop(const Ctx& c, size_t off, int K) { return Opnd{c.pw + off, (long)K * 32
 bool use_split(const Ctx& c, int rows) {
     const Layout& w = c.w;
     if (w.M != 512 || rows > c.k.split_rows || (size_t)split_lds_floats(w.Kx, w.M) * 4 > 64 * 1024) return false;
-    if (c.path == TDMPC_PATH_SPLIT) return true;
+    if (c.path == TDMPC_PATH_SPLIT || c.path == TDMPC_PATH_SPLIT_X6) return true;
     // auto: only while the first layer, repeated per slice, stays cheap next to the slice of the M x M layer
     // (humanoid-run L512: K1 = 536 made the one-env plan 1.3x slower than the layered path)
     if (c.path != TDMPC_PATH_AUTO || (int)rup(w.Kx, 16) > w.M / 2) return false;
@@ -3312,7 +3421,7 @@ bool use_split(const Ctx& c, int rows) {
 bool use_split_pi(const Ctx& c, int rows) {
     const Layout& w = c.w;
     if (w.M != 512 || rows > c.k.split_rows || (size_t)split_lds_floats(w.Lp, w.M) * 4 > 64 * 1024) return false;
-    if (c.path == TDMPC_PATH_SPLIT) return true;
+    if (c.path == TDMPC_PATH_SPLIT || c.path == TDMPC_PATH_SPLIT_X6) return true;
     if (c.path != TDMPC_PATH_AUTO || (int)rup(w.Lp, 16) > w.M / 2) return false;
     static int en = -1;
     if (en < 0) {
@@ -3391,12 +3500,18 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         a.W3 = c.pw + w.w3d; a.n3 = w.Lr;
         a.zpart = c.k.zpart + par * zs; a.rpart = c.k.rpart_s + par * rs; a.prow = c.k.split_rows;
         a.b3d = c.pw + w.b3d; a.b3r = c.pw + w.b3r; a.L = w.L; a.Lp = w.Lp; a.zq0 = w.Ap / 4;
+        const bool x6 = use_x6(c) != 0;
+        if (x6) {
+            d.X1 = x6p(c, X6_W1X); r.X1 = x6p(c, X6_W1X) + (size_t)(M / 32) * (rup(c.Kx, 16) / 16) * 1536;
+            d.X2 = x6p(c, X6_W2D); r.X2 = x6p(c, X6_W2R); a.X3 = x6p(c, X6_W3D);
+        }
         if (c.split_pend) {   // the previous step's finish, folded into this launch's staging
             a.zin = c.k.zpart + (1 - par) * zs; a.rin = c.k.rpart_s + (1 - par) * rs;
             a.Xw = Xt(c, t); a.G = c.k.G; a.disc_in = c.split_disc; a.first_in = c.split_first;
         }
         const size_t lds = (size_t)split_lds_floats(c.Kx, M) * 4;
-        hipLaunchKernelGGL((split_step_kernel<4>), dim3((rows + 15) / 16, SPLIT_S, 2), dim3(512), lds, c.s, a);
+        if (x6) hipLaunchKernelGGL((split_step_kernel<4, 4, 1>), dim3((rows + 15) / 16, SPLIT_S, 2), dim3(512), lds, c.s, a);
+        else hipLaunchKernelGGL((split_step_kernel<4>), dim3((rows + 15) / 16, SPLIT_S, 2), dim3(512), lds, c.s, a);
         HIPCHK(hipGetLastError());
         c.split_pend = 0;
         c.split_par = 1 - par;
@@ -3468,7 +3583,12 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
         a.W3 = c.pw + w.wp3; a.n3 = w.Ar;
         a.zpart = c.k.zpart; a.rpart = c.k.rpart_s; a.prow = c.k.split_rows;
         const size_t lds = (size_t)split_lds_floats(w.Lp, M) * 4;
-        hipLaunchKernelGGL((split_step_kernel<4>), dim3((rows + 15) / 16, SPLIT_S, 1), dim3(512), lds, c.s, a);
+        if (use_x6(c)) {
+            p.X1 = x6p(c, X6_WP1); p.X2 = x6p(c, X6_WP2); a.X3 = x6p(c, X6_WP3);
+            hipLaunchKernelGGL((split_step_kernel<4, 4, 1>), dim3((rows + 15) / 16, SPLIT_S, 1), dim3(512), lds, c.s, a);
+        } else {
+            hipLaunchKernelGGL((split_step_kernel<4>), dim3((rows + 15) / 16, SPLIT_S, 1), dim3(512), lds, c.s, a);
+        }
         HIPCHK(hipGetLastError());
         SplitPiArgs f;
         memset(&f, 0, sizeof f);
@@ -3875,7 +3995,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     int rc;
     const int H = prm->horizon, I = prm->iterations, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 6) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 7) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T;
     // z0 = h(obs) and mean = 0 (warm: prev_mean shifted), std = 2
@@ -3957,7 +4077,7 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
     const int H = prm->horizon, I = prm->iterations, B = prm->batch, K = d->num_elites;
     if (I <= 0 || I > 16) { snprintf(g_err, sizeof g_err, "iCEM: 1..16 iterations"); return TDMPC_E_DIMS; }
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream, K))) return rc;
-    if (prm->path < 0 || prm->path > 6) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 7) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = d->num_samples, Pmax = d->num_pi, Tw = N + K + Pmax, pi_base = N + K, P0 = prm->n_pi0;
     c.T = Tw;
@@ -4055,7 +4175,7 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 6) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 7) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     if (rows != c.T) { snprintf(g_err, sizeof g_err, "rows must equal N+P"); return TDMPC_E_DIMS; }
     const int T = c.T, L = c.w.L;
@@ -4100,7 +4220,7 @@ int tdmpc_pi_rollout(const tdmpc_dims* d, const tdmpc_plan_params* prm, const vo
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 6) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 7) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T;
     const long A = c.A;
@@ -4129,7 +4249,7 @@ int tdmpc_cem_iter(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 6) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 7) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T, A = c.A, HA = H * A;
     if (P > 0 && !pi_actions) return TDMPC_E_NULL;
