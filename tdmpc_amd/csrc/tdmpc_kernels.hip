@@ -1330,6 +1330,9 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
         for (int k = 0; k < 4; ++k) eps4[k] = c + k < a.nvalid ? ep[c + k] : 0.f;
     }
     lds_barrier();
+#if defined(TDMPC_STAMPS) && defined(TDMPC_STAMPS_STAGE)
+    STAMP(1);   // diagnostic variant: phase 0 = staging only, phase 1 = layer 1 + its epilogue
+#endif
 
     // ---- layer 1: [32 x K1] . W1^T -> [32 x M]
     floatx16 acc[TN];
@@ -1344,7 +1347,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     if constexpr (X6) ring6_fill<TN, D>(wx, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n);
     else ring_fill<TN, D>(wr, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3);
     lds_barrier();   // every wave is done with the input tile: sH becomes h1
-#ifdef TDMPC_STAMPS
+#if defined(TDMPC_STAMPS) && !defined(TDMPC_STAMPS_STAGE)
     STAMP(1);
 #endif
     {
