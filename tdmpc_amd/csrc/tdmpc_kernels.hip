@@ -1041,14 +1041,18 @@ DEVI void ring6_run(floatx16 (&acc)[TN], uint4 (&wr)[D][TN][3], const float* sA,
             const size_t gn = (size_t)min(g + 1, gl) * 512;
             n0 = *(const float4*)(ap + gn);
             n1 = *(const float4*)(ap + gn + 256);
+#ifndef TDMPC_X6_FREE_SCHED
             __builtin_amdgcn_sched_barrier(0);
+#endif
             x6_group<TN>(acc, wr[d], a0, a1);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int p = 0; p < 3; ++p)
                     wr[d][j][p] = *(const uint4*)(Wp + j * wbs + ((size_t)min(g + D, gl) * 3 + p) * 512);
+#ifndef TDMPC_X6_FREE_SCHED
             __builtin_amdgcn_sched_barrier(0);
+#endif
         }
     }
 #pragma unroll

@@ -370,3 +370,32 @@ def test_building_blocks_compose_plan(task, ov, path):
         j = tdmpc_ref.choice_index(score[e].cpu().numpy(), us[e])
         a = elite[e, 0, j].cpu() + std[e, 0].cpu() * eps_act[e]
         np.testing.assert_allclose(a.numpy(), refs[e][0].numpy(), atol=2e-5, rtol=0)
+
+
+def test_x6_accuracy_matches_f32_mfma():
+    """The x6 products (three-way bf16 split, fp32 accumulation) are as accurate as the exact f32 MFMA: at
+    BASELINE size (humanoid, T = 768, H = 5) both paths' estimate_value G is compared with a float64 evaluation
+    of the same TOLD, and the x6 error may not exceed twice the f32 MFMA error (+1e-6 absolute)."""
+    cfg = make_cfg("humanoid", num_samples=512, num_elites=64)
+    H = 5
+    g = torch.Generator().manual_seed(5)
+    outs = {}
+    for path in ("chain32", "chain_x6"):
+        agent = _agent(cfg, 13, path=path)
+        pl = agent.planner
+        pl.pack(agent.model)
+        T, A, L = pl.T, cfg.action_dim, cfg.latent_dim
+        g.manual_seed(5)
+        z0 = torch.randn(1, L, generator=g)
+        actions = torch.rand(1, H, T, A, generator=g) * 2 - 1
+        eps = torch.randn(1, T, A, generator=g)
+        v, _, _ = pl.estimate_value(z0, actions, eps, H)
+        outs[path] = v[0].double().cpu().numpy()
+    told = tdmpc_ref.RefTOLD(synthetic_state_dict(cfg, 13), cfg)
+    told.sd = {k: t.double() for k, t in told.sd.items()}
+    G64 = tdmpc_ref.estimate_value(told, cfg, z0.double().repeat(T, 1), actions[0].double(), H, eps[0].double())[0]
+    G64 = G64[:, 0].numpy()
+    e32 = np.abs(outs["chain32"] - G64).max()
+    ex6 = np.abs(outs["chain_x6"] - G64).max()
+    print(f"max |G - G_fp64|: f32 MFMA {e32:.3e}, x6 {ex6:.3e}")
+    assert ex6 <= 2 * e32 + 1e-6, (e32, ex6)
