@@ -972,6 +972,9 @@ DEVI void ring_run(floatx16 (&acc)[TN], float4 (&wr)[D][TN], const float* sA, co
 // the f32 MFMA cycles. Weights come pre-split (Layout::x6, pack_x6_kernel); the activations stay fp32 in LDS
 // and are split as they are read.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+#ifndef X6_D3
+#define X6_D3 2   // weight-ring depth of the x6 chain kernel's last layer (k groups of 16)
+#endif
 DEVI bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 
 DEVI void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
@@ -2963,11 +2966,11 @@ int init_attrs() {
     CHAIN_ATTR(CH_PI, 1) CHAIN_ATTR(CH_PI, 2) CHAIN_ATTR(CH_PI, 4)
     CHAIN_ATTR(CH_Q, 1) CHAIN_ATTR(CH_Q, 2) CHAIN_ATTR(CH_Q, 4)
 #undef CHAIN_ATTR
-    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 2, 8, 2, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 2, 8, 2, X6_D3, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 2, 8, 4, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 2, 8, 2, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 2, 8, 2, X6_D3, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 2, 8, 4, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 2, 8, 2, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 2, 8, 2, X6_D3, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 2, 8, 4, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -3267,7 +3270,7 @@ int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
 #define CHAIN_LAUNCH(MODE, TN) \
     if (mode == MODE && tn == TN) { \
         if (a.x6 == 2 && TN == 2) hipLaunchKernelGGL((chain_kernel<MODE, 2, 8, 4, 4, 2>), grid, block, lds, s, a); \
-        else if (a.x6 && TN == 2) hipLaunchKernelGGL((chain_kernel<MODE, 2, 8, 2, 2, 1>), grid, block, lds, s, a); \
+        else if (a.x6 && TN == 2) hipLaunchKernelGGL((chain_kernel<MODE, 2, 8, 2, X6_D3, 1>), grid, block, lds, s, a); \
         else if (nw == 16 && TN == 1) hipLaunchKernelGGL((chain_kernel<MODE, 1, 16>), grid, block, lds, s, a); \
         else hipLaunchKernelGGL((chain_kernel<MODE, TN>), grid, block, lds, s, a); \
         HIPCHK(hipGetLastError()); \

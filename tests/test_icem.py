@@ -56,7 +56,7 @@ def _close(a, b, atol=1e-5, rtol=1e-4):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["chain16", "chain32", "layered", "split"])
+@pytest.mark.parametrize("path", ["chain16", "chain32", "layered", "split", "chain_x6", "split_x6"])
 def test_gpu_icem_matches_oracle(path):
     """The golden call sequence on the GPU planner with the oracle's draws: per-iteration values within the fp32
     tolerance; actions, metrics, prev_mean and the kept elites while every iteration's elite set agrees."""
@@ -201,7 +201,7 @@ def test_device_rng_positions_cover_colored_slots():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["chain16", "layered", "split"])
+@pytest.mark.parametrize("path", ["chain16", "layered", "split", "chain_x6"])
 def test_gpu_icem_batched_equals_single(path):
     """TdICEM.plan_batch over 3 envs (each its own observation and noise stream) equals 3 single-env plans on the
     same draws, bitwise, over a cold call and a warm call with elite reuse (forced kernel path: the same kernels
