@@ -416,10 +416,11 @@ def main():
         if n > 0:
             rb = 32 if (rows + 31) // 32 * 2 > torch.cuda.get_device_properties(dev).multi_processor_count // 2 else 16
             rb = int(os.environ.get("TDMPC_CHAIN_RB", rb))
-            x6 = rb == 32 and M == 512 and os.environ.get("TDMPC_X6", "1") != "0"
+            x6 = rb == 32 and M == 512 and os.environ.get("TDMPC_X6", "3") != "0"
             if x6:
                 peak = X6_PEAK_TFLOPS
-                kernel = (f"chain_kernel<CH_STEP, X6> (TOLD.next: dynamics + reward heads, 32-row blocks, hidden "
+                kernel = (f"chain_kernel<CH_STEP, TN=4, NW=4, X6> (TOLD.next: dynamics + reward heads, 32-row blocks "
+                          f"of 4 waves x 128 columns, hidden "
                           f"activations in LDS, weights streamed from L2; {rows} rows x 2 heads per launch), fp32 "
                           f"products from a three-way bf16 split of both operands: 6 v_mfma_f32_32x32x16_bf16 per "
                           f"product, fp32 accumulation (peak = dense BF16 / 6)")
@@ -542,7 +543,7 @@ def main():
                               "accumulation (x6 chain kernels; parity tests at the fp32 tolerance; max |G - G_fp64| "
                               "2.8e-6 vs 4.0e-6 for the exact f32 MFMA, tests/test_gpu_plan.py::"
                               "test_x6_accuracy_matches_f32_mfma)"
-                              if cfg.mlp_dim == 512 and os.environ.get("TDMPC_X6", "1") != "0" else "f32 MFMA"),
+                              if cfg.mlp_dim == 512 and os.environ.get("TDMPC_X6", "3") != "0" else "f32 MFMA"),
             "data": "synthetic: seeded N(0,1/fan_in) TOLD weights, N(0,1) observations, noise drawn on device",
             "config": {"workload": f"{args.config}: TDMPC.plan N={cfg.num_samples} H={cfg.horizon} "
                                    f"iters={cfg.iterations} mixture={cfg.mixture_coef} K={cfg.num_elites} "

@@ -1243,7 +1243,7 @@ DEVI void chain_store_lds(float* sH, const float (&v)[TN * 16], int cw0, int r, 
 // X6: 0 = f32 MFMA; 1 = x6 with the activations kept fp32 in LDS and split as read; 2 = x6 with the activations as
 // split planes in LDS (one workgroup per CU: 96 KB at M = 512).
 template <int MODE, int TN, int NW = 8, int D = 4, int D3 = 8, int X6 = 0>
-__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6 == 1 ? 4 : 1))) chain_kernel(const ChainArgs a) {
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6 == 1 && NW == 8 ? 4 : X6 == 1 && NW == 4 ? 2 : 1))) chain_kernel(const ChainArgs a) {
     constexpr int NTH = 64 * NW;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
@@ -2968,10 +2968,13 @@ int init_attrs() {
 #undef CHAIN_ATTR
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 2, 8, 2, X6_D3, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 2, 8, 4, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 4, 4, 2, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 2, 8, 2, X6_D3, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 2, 8, 4, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 4, 4, 2, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 2, 8, 2, X6_D3, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 2, 8, 4, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 4, 4, 2, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -3269,7 +3272,8 @@ int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
     }
 #define CHAIN_LAUNCH(MODE, TN) \
     if (mode == MODE && tn == TN) { \
-        if (a.x6 == 2 && TN == 2) hipLaunchKernelGGL((chain_kernel<MODE, 2, 8, 4, 4, 2>), grid, block, lds, s, a); \
+        if (a.x6 == 3 && TN == 4 && nw == 4) hipLaunchKernelGGL((chain_kernel<MODE, 4, 4, 2, 2, 1>), grid, block, lds, s, a); \
+        else if (a.x6 == 2 && TN == 2) hipLaunchKernelGGL((chain_kernel<MODE, 2, 8, 4, 4, 2>), grid, block, lds, s, a); \
         else if (a.x6 && TN == 2) hipLaunchKernelGGL((chain_kernel<MODE, 2, 8, 2, X6_D3, 1>), grid, block, lds, s, a); \
         else if (nw == 16 && TN == 1) hipLaunchKernelGGL((chain_kernel<MODE, 1, 16>), grid, block, lds, s, a); \
         else hipLaunchKernelGGL((chain_kernel<MODE, TN>), grid, block, lds, s, a); \
@@ -3361,16 +3365,18 @@ int chain_nw() {
 // forced by TDMPC_PATH_CHAIN_X6, the default of the auto / chain paths (TDMPC_X6=0 turns it off there); the
 // chain32 / chain16 paths keep the exact f32 MFMA. M = 512 only (the one instantiated width). Measured on MI355X
 // (humanoid-run, tools/gpu72.sh): 8.89 -> 6.52 ms per B = 32 plan, 3.03 -> 2.19 ms at B = 8.
-// Returns the X6 mode of chain_kernel (0 = f32 MFMA, 1 = split as read, 2 = split planes in LDS; TDMPC_X6 picks
-// 1 or 2, 0 turns x6 off on the auto / chain paths).
+// Returns the x6 mode of a chain launch (0 = f32 MFMA; 1 = 8-wave workgroups, activations split as read; 2 = split
+// planes in LDS; 3 = mode 1 on 4-wave workgroups of 128 columns per wave, the default: the per-wave split serves
+// twice the MFMAs -- measured 6.37 vs 6.60 ms per B = 32 plan, 2.23 vs 2.28 at B = 8, tools/gpu83.sh). TDMPC_X6
+// picks the mode, 0 turns x6 off on the auto / chain paths.
 int use_x6(const Ctx& c) {
     if (c.w.M != 512) return 0;
     static int en = -1;
     if (en < 0) {
         const char* e = getenv("TDMPC_X6");
-        en = e ? atoi(e) : 1;
+        en = e ? atoi(e) : 3;
     }
-    if (c.path == TDMPC_PATH_CHAIN_X6) return en == 2 ? 2 : 1;
+    if (c.path == TDMPC_PATH_CHAIN_X6) return en >= 1 && en <= 3 ? en : 3;
     if (c.path == TDMPC_PATH_SPLIT_X6) return 1;
     return (c.path == TDMPC_PATH_AUTO || c.path == TDMPC_PATH_CHAIN) ? en : 0;
 }
@@ -3398,7 +3404,11 @@ ChainArgs chain0(const Ctx& c, int rows, RowMap map, int t, int K1, int q1, int 
     a.rows = rows; a.M = c.M; a.K1 = K1; a.q1 = q1; a.amap = map;
     a.rb = chain_rb(c, rows, nprob);
     a.x6 = a.rb == 32 ? use_x6(c) : 0;
-    a.nw = a.rb == 32 && !a.x6 && chain_nw() == 16 && chain_nw16_ok(c.w) ? 16 : 8;
+    // x6 mode 3: 4-wave workgroups, 128 columns per wave (the per-wave split amortised over twice the MFMAs); the pi
+    // head's noise prefetch (one quad per thread) then needs Ap / 4 * 32 <= 256, and the last layer's 32-column
+    // blocks (at most two per wave) Lr, Ar <= 256; otherwise mode 1
+    if (a.x6 == 3 && (c.w.Ap / 4 * 32 > 256 || std::max(c.w.Lr, c.w.Ar) > 2 * 4 * 32)) a.x6 = 1;
+    a.nw = a.x6 == 3 ? 4 : a.rb == 32 && !a.x6 && chain_nw() == 16 && chain_nw16_ok(c.w) ? 16 : 8;
     // activation block: fp32 [K/4][rb][4], or for x6 mode 2 the split planes (6 bytes per value)
     a.hfl = std::max((int)rup(c.Kx, 16), c.M) * (a.x6 == 2 ? 48 : a.rb);
     a.X = Xt(c, t); a.x_ts = (long)c.Kx * 32;
