@@ -1328,13 +1328,21 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     float g_old = 0.f;
     if (MODE == CH_STEP && pb == 1 && tid < 32 && !a.first && m0 + tid < a.rows)
         g_old = a.G[map_row(a.amap, m0 + tid)];
-    float eps4[4] = {0.f, 0.f, 0.f, 0.f};
-    if (MODE == CH_PI && tid < (a.nstore >> 2) * 32 && m0 + (tid & 31) < a.rows) {
-        const int lm = m0 + (tid & 31), c = 4 * (tid >> 5);
-        const int e = lm / a.eps_G, rr = lm % a.eps_G;
-        const float* ep = a.eps + (size_t)e * a.eps_env + a.eps_off + (size_t)rr * a.A;
+    // (one output quad per thread and pass: NIT passes cover nstore/4 * 32 <= 512 quads)
+    constexpr int NIT = NTH >= 512 ? 1 : 512 / NTH;
+    float eps4[NIT][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) eps4[k] = c + k < a.nvalid ? ep[c + k] : 0.f;
+    for (int it = 0; it < NIT; ++it) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) eps4[it][k] = 0.f;
+        const int iq = tid + it * NTH;
+        if (MODE == CH_PI && iq < (a.nstore >> 2) * 32 && m0 + (iq & 31) < a.rows) {
+            const int lm = m0 + (iq & 31), c = 4 * (iq >> 5);
+            const int e = lm / a.eps_G, rr = lm % a.eps_G;
+            const float* ep = a.eps + (size_t)e * a.eps_env + a.eps_off + (size_t)rr * a.A;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) eps4[it][k] = c + k < a.nvalid ? ep[c + k] : 0.f;
+        }
     }
     lds_barrier();
 #if defined(TDMPC_STAMPS) && defined(TDMPC_STAMPS_STAGE)
@@ -1509,7 +1517,8 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
         const int xr = map_row(a.amap, lm);
         if (MODE == CH_PI) {
             // TOLD.pi + TruncatedNormal.sample(clip=0.3) (tdmpc.py:39-45, helper.py:86-96); this thread's noise
-            // was loaded at kernel start (i == tid: nstore/4 * 32 <= 512 items)
+            // was loaded at kernel start (pass (i - tid) / NTH < NIT: nstore/4 * 32 <= 512 items)
+            const bool second = NIT > 1 && i >= tid + NTH;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 float x = 0.f;
@@ -1517,7 +1526,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
                     const float muv = tanhf(o[k]);
                     x = muv;
                     if (a.min_std > 0.f) {
-                        const float ee = tclamp(fmul(eps4[k], a.min_std), -0.3f, 0.3f);
+                        const float ee = tclamp(fmul(second ? eps4[NIT - 1][k] : eps4[0][k], a.min_std), -0.3f, 0.3f);
                         x = tclamp(fadd(muv, ee), a.lo, a.hi);
                     }
                 }
@@ -3405,9 +3414,9 @@ ChainArgs chain0(const Ctx& c, int rows, RowMap map, int t, int K1, int q1, int 
     a.rb = chain_rb(c, rows, nprob);
     a.x6 = a.rb == 32 ? use_x6(c) : 0;
     // x6 mode 3: 4-wave workgroups, 128 columns per wave (the per-wave split amortised over twice the MFMAs); the pi
-    // head's noise prefetch (one quad per thread) then needs Ap / 4 * 32 <= 256, and the last layer's 32-column
-    // blocks (at most two per wave) Lr, Ar <= 256; otherwise mode 1
-    if (a.x6 == 3 && (c.w.Ap / 4 * 32 > 256 || std::max(c.w.Lr, c.w.Ar) > 2 * 4 * 32)) a.x6 = 1;
+    // head's noise prefetch (two quads per thread) needs Ap / 4 * 32 <= 512, and the last layer's 32-column blocks
+    // (at most two per wave) Lr, Ar <= 256; otherwise mode 1
+    if (a.x6 == 3 && (c.w.Ap / 4 * 32 > 512 || std::max(c.w.Lr, c.w.Ar) > 2 * 4 * 32)) a.x6 = 1;
     a.nw = a.x6 == 3 ? 4 : a.rb == 32 && !a.x6 && chain_nw() == 16 && chain_nw16_ok(c.w) ? 16 : 8;
     // activation block: fp32 [K/4][rb][4], or for x6 mode 2 the split planes (6 bytes per value)
     a.hfl = std::max((int)rup(c.Kx, 16), c.M) * (a.x6 == 2 ? 48 : a.rb);
