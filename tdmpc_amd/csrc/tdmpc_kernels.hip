@@ -1490,6 +1490,20 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
             ring_run<1, D3>(a3b, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
         }
     }
+    // 4-wave x6 workgroups (mode 3) take up to four last-layer items per wave (L512: 16 blocks)
+    constexpr bool IT4 = NW == 4 && X6 == 1;
+    floatx16 a3c[1], a3d[1];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { a3c[0][e] = 0.f; a3d[0][e] = 0.f; }
+    if constexpr (IT4) {
+        auto item = [&](floatx16 (&acc)[1], int it) {
+            const int blk = it / ks, kp = it % ks;
+            ring6_fill<1, D3>(w3x, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper);
+            ring6_run<1, D3>(acc, w3x, sH, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, r, h);
+        };
+        if (wave + 2 * NW < items) item(a3c, wave + 2 * NW);
+        if (wave + 3 * NW < items) item(a3d, wave + 3 * NW);
+    }
     lds_barrier();
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1499,6 +1513,12 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
         if (wave + NW < items)
             *(float4*)(sH + (size_t)(wave + NW) * 1024 + ((2 * q + h) * 32 + r) * 4) =
                 make_float4(a3b[0][4 * q], a3b[0][4 * q + 1], a3b[0][4 * q + 2], a3b[0][4 * q + 3]);
+        if (IT4 && wave + 2 * NW < items)
+            *(float4*)(sH + (size_t)(wave + 2 * NW) * 1024 + ((2 * q + h) * 32 + r) * 4) =
+                make_float4(a3c[0][4 * q], a3c[0][4 * q + 1], a3c[0][4 * q + 2], a3c[0][4 * q + 3]);
+        if (IT4 && wave + 3 * NW < items)
+            *(float4*)(sH + (size_t)(wave + 3 * NW) * 1024 + ((2 * q + h) * 32 + r) * 4) =
+                make_float4(a3d[0][4 * q], a3d[0][4 * q + 1], a3d[0][4 * q + 2], a3d[0][4 * q + 3]);
     }
     lds_barrier();
     for (int i = tid; i < (a.nstore >> 2) * 32; i += NTH) {
@@ -3415,8 +3435,8 @@ ChainArgs chain0(const Ctx& c, int rows, RowMap map, int t, int K1, int q1, int 
     a.x6 = a.rb == 32 ? use_x6(c) : 0;
     // x6 mode 3: 4-wave workgroups, 128 columns per wave (the per-wave split amortised over twice the MFMAs); the pi
     // head's noise prefetch (two quads per thread) needs Ap / 4 * 32 <= 512, and the last layer's 32-column blocks
-    // (at most two per wave) Lr, Ar <= 256; otherwise mode 1
-    if (a.x6 == 3 && (c.w.Ap / 4 * 32 > 512 || std::max(c.w.Lr, c.w.Ar) > 2 * 4 * 32)) a.x6 = 1;
+    // (at most four per wave) Lr, Ar <= 512; otherwise mode 1
+    if (a.x6 == 3 && (c.w.Ap / 4 * 32 > 512 || std::max(c.w.Lr, c.w.Ar) > 4 * 4 * 32)) a.x6 = 1;
     a.nw = a.x6 == 3 ? 4 : a.rb == 32 && !a.x6 && chain_nw() == 16 && chain_nw16_ok(c.w) ? 16 : 8;
     // activation block: fp32 [K/4][rb][4], or for x6 mode 2 the split planes (6 bytes per value)
     a.hfl = std::max((int)rup(c.Kx, 16), c.M) * (a.x6 == 2 ? 48 : a.rb);
