@@ -1780,7 +1780,9 @@ DEVI void chain16_store_lds(float* sH, const float (&v)[NT * 4], int f0, int m) 
         *(float4*)(sH + ((f0 / 4 + 4 * j) * 16 + m) * 4) = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
 }
 
-template <int MODE, int NT, int D = 4, int D3 = 4>
+// X6 = 1: layers 1 and 2 on v_mfma_f32_16x16x32_bf16 with the x6 split (ring16x6_*, two passes of NT / 2 tiles);
+// the last layer stays f32 MFMA.
+template <int MODE, int NT, int D = 4, int D3 = 4, int X6 = 0>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) chain16_kernel(const ChainArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, h4 = lane >> 4;
@@ -1807,9 +1809,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     const long wblk = (long)(NT / 2) * wave;  // first 32-row panel block of this wave
     const bool head_dot = MODE == CH_Q || (MODE == CH_STEP && pb == 1);
 
-    float4 wr[D][NT];
-    ring16_fill<NT, D>(wr, P.W1 + wblk * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1n, h4, q1max);
-    for (int i = tid; i < g1n * 4 * 16; i += 512) {
+    const int g1x = (a.K1 + 31) >> 5, gm1 = (a.K1 + 15) >> 4, gmM = M >> 4;   // x6: 32-k groups
+    float4 wr[X6 ? 1 : D][NT];
+    uint4 wx[X6 ? 2 : 1][X6 ? NT / 2 : 1][3];
+    if constexpr (X6) ring16x6_fill<NT / 2, 2>(wx, P.X1, 16 * NT * wave, gm1, 0, g1x, lane);
+    else ring16_fill<NT, D>(wr, P.W1 + wblk * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1n, h4, q1max);
+    for (int i = tid; i < (X6 ? g1x * 8 : g1n * 4) * 16; i += 512) {
         const int row = i & 15, q = i >> 4;
         const int lm = m0 + row;
         const int xr = map_row(a.amap, lm < a.rows ? lm : 0);
@@ -1846,8 +1851,28 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     floatx4 acc[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    ring16_run<NT, D>(acc, wr, sH, P.W1 + wblk * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1n, lane, q1max);
-    ring16_fill<NT, D>(wr, P.W2 + wblk * M * 32 + lo, (long)M * 32, 0, M >> 4, h4, qMmax);
+    // x6: the NT tiles in two passes of NT / 2 (the ring of the second pass fills after the first runs)
+    auto x6_layer = [&](const unsigned short* W, int gmax, int gn, const float* sA) {
+      if constexpr (X6 != 0) {
+        floatx4 ah[NT / 2];
+#pragma unroll
+        for (int j = 0; j < NT / 2; ++j) ah[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        ring16x6_run<NT / 2, 2>(ah, wx, sA, W, 16 * NT * wave, gmax, 0, gn, lane);
+#pragma unroll
+        for (int j = 0; j < NT / 2; ++j) { acc[j] = ah[j]; ah[j] = floatx4{0.f, 0.f, 0.f, 0.f}; }
+        ring16x6_fill<NT / 2, 2>(wx, W, 16 * NT * wave + 16 * (NT / 2), gmax, 0, gn, lane);
+        ring16x6_run<NT / 2, 2>(ah, wx, sA, W, 16 * NT * wave + 16 * (NT / 2), gmax, 0, gn, lane);
+#pragma unroll
+        for (int j = 0; j < NT / 2; ++j) acc[NT / 2 + j] = ah[j];
+      }
+    };
+    if constexpr (X6) {
+        x6_layer(P.X1, gm1, g1x, sH);
+        if constexpr (X6 != 0) ring16x6_fill<NT / 2, 2>(wx, P.X2, 16 * NT * wave, gmM, 0, M >> 5, lane);
+    } else {
+        ring16_run<NT, D>(acc, wr, sH, P.W1 + wblk * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1n, lane, q1max);
+        ring16_fill<NT, D>(wr, P.W2 + wblk * M * 32 + lo, (long)M * 32, 0, M >> 4, h4, qMmax);
+    }
     lds_barrier();
     {
         float v[NT * 4];
@@ -1869,7 +1894,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     // ---- layer 2
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    ring16_run<NT, D>(acc, wr, sH, P.W2 + wblk * M * 32 + lo, (long)M * 32, 0, M >> 4, lane, qMmax);
+    if constexpr (X6) x6_layer(P.X2, gmM, M >> 5, sH);
+    else ring16_run<NT, D>(acc, wr, sH, P.W2 + wblk * M * 32 + lo, (long)M * 32, 0, M >> 4, lane, qMmax);
 
     // layer-3 items (16-column tile, K part): up to 4 per wave (items <= 32)
     const int nb3 = a.n3 >> 4;
@@ -3011,6 +3037,9 @@ int init_attrs() {
     HIPCHK(hipFuncSetAttribute((const void*)chain16_kernel<MODE, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     CHAIN16_ATTR(CH_STEP, 2) CHAIN16_ATTR(CH_STEP, 4) CHAIN16_ATTR(CH_PI, 2) CHAIN16_ATTR(CH_PI, 4)
     CHAIN16_ATTR(CH_Q, 2) CHAIN16_ATTR(CH_Q, 4)
+    HIPCHK(hipFuncSetAttribute((const void*)chain16_kernel<CH_STEP, 4, 4, 4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain16_kernel<CH_PI, 4, 4, 4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)chain16_kernel<CH_Q, 4, 4, 4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 #undef CHAIN16_ATTR
     if (rc) return TDMPC_E_HIP;
     done = 1;
@@ -3234,7 +3263,7 @@ bool chain_shape_ok(const Layout& w) {
 bool chain16_shape_ok(const Layout& w) {
     const int M = w.M;
     if (M != 256 && M != 512) return false;
-    const size_t hfl = (size_t)std::max((int)rup(w.Kx, 16), M) * 16;
+    const size_t hfl = (size_t)std::max((int)rup(w.Kx, 32), M) * 16;
     for (int n3 : {w.Lr, w.Ar}) {
         const int nb3 = n3 / 16, ks = nb3 >= 8 ? 1 : 8 / nb3, items = nb3 * ks;
         if (items > 32 || (size_t)items * 256 > hfl || (M / 16) % ks) return false;
@@ -3284,7 +3313,8 @@ int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
         const int nt = a.M / 128;
 #define CHAIN16_LAUNCH(MODE, NT) \
         if (mode == MODE && nt == NT) { \
-            hipLaunchKernelGGL((chain16_kernel<MODE, NT>), grid, block, lds, s, a); \
+            if (a.x6 && NT == 4) hipLaunchKernelGGL((chain16_kernel<MODE, 4, 4, 4, 1>), grid, block, lds, s, a); \
+            else hipLaunchKernelGGL((chain16_kernel<MODE, NT>), grid, block, lds, s, a); \
             HIPCHK(hipGetLastError()); \
             if (prof) { \
                 HIPCHK(hipEventRecord(pf.ev[pf.n + 1], s)); \
@@ -3432,14 +3462,14 @@ ChainArgs chain0(const Ctx& c, int rows, RowMap map, int t, int K1, int q1, int 
     memset(&a, 0, sizeof a);
     a.rows = rows; a.M = c.M; a.K1 = K1; a.q1 = q1; a.amap = map;
     a.rb = chain_rb(c, rows, nprob);
-    a.x6 = a.rb == 32 ? use_x6(c) : 0;
+    a.x6 = a.rb == 32 ? use_x6(c) : (use_x6(c) ? 1 : 0);   // 16-row blocks: chain16_kernel<..., X6 = 1>
     // x6 mode 3: 4-wave workgroups, 128 columns per wave (the per-wave split amortised over twice the MFMAs); the pi
     // head's noise prefetch (two quads per thread) needs Ap / 4 * 32 <= 512, and the last layer's 32-column blocks
     // (at most four per wave) Lr, Ar <= 512; otherwise mode 1
     if (a.x6 == 3 && (c.w.Ap / 4 * 32 > 512 || std::max(c.w.Lr, c.w.Ar) > 4 * 4 * 32)) a.x6 = 1;
     a.nw = a.x6 == 3 ? 4 : a.rb == 32 && !a.x6 && chain_nw() == 16 && chain_nw16_ok(c.w) ? 16 : 8;
     // activation block: fp32 [K/4][rb][4], or for x6 mode 2 the split planes (6 bytes per value)
-    a.hfl = std::max((int)rup(c.Kx, 16), c.M) * (a.x6 == 2 ? 48 : a.rb);
+    a.hfl = std::max((int)rup(c.Kx, 32), c.M) * (a.x6 == 2 ? 48 : a.rb);
     a.X = Xt(c, t); a.x_ts = (long)c.Kx * 32;
     return a;
 }

@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 RTOL, ATOL = 1e-4, 1e-5
 
 
-PATHS = ["layered", "chain16", "chain32", "split", "chain_x6", "split_x6"]
+PATHS = ["layered", "chain16", "chain32", "split", "chain_x6", "split_x6", "chain"]
 
 
 def _agent(cfg, wseed, B=1, path="auto"):

@@ -56,7 +56,7 @@ def _close(a, b, atol=1e-5, rtol=1e-4):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["chain16", "chain32", "layered", "split", "chain_x6", "split_x6"])
+@pytest.mark.parametrize("path", ["chain16", "chain32", "layered", "split", "chain_x6", "split_x6", "chain"])
 def test_gpu_icem_matches_oracle(path):
     """The golden call sequence on the GPU planner with the oracle's draws: per-iteration values within the fp32
     tolerance; actions, metrics, prev_mean and the kept elites while every iteration's elite set agrees."""
