@@ -975,6 +975,12 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 #ifndef X6_D3
 #define X6_D3 2   // weight-ring depth of the x6 chain kernel's last layer (k groups of 16)
 #endif
+#ifndef X6_PIPE
+// 1: 4-wave x6 chain workgroups split group g + 1 under group g's MFMAs (ring6_run_pipe). Off: measured 3 % slower
+// (6.56 vs 6.35 ms per B = 32 plan, 2.31 vs 2.22 at B = 8, tools/gpu92.sh) -- the other wave on the SIMD already
+// fills the split's VALU slots, and the extra live operands cost more than the overlap gains
+#define X6_PIPE 0
+#endif
 DEVI bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 
 DEVI void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
@@ -1066,6 +1072,69 @@ DEVI void ring6_run(floatx16 (&acc)[TN], uint4 (&wr)[D][TN][3], const float* sA,
             n0 = *(const float4*)(ap + gn);
             n1 = *(const float4*)(ap + gn + 256);
             x6_group<TN>(acc, wr[d], a0, a1);
+        }
+    }
+}
+
+// Software-pipelined form of ring6_run (4-wave workgroups, which have the VGPRs): group g + 1's operand split is
+// issued in the same scheduling region as group g's MFMAs, so the VALU work fills the MFMA gaps of its own wave.
+template <int TN>
+DEVI void x6_mfma6(floatx16 (&acc)[TN], const uint4 (&w)[TN][3], const bf16x8_t& bh, const bf16x8_t& bm,
+                   const bf16x8_t& bl) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][1]), bm, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][2]), bh, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), bl, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][1]), bh, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), bm, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), bh, acc[j], 0, 0, 0);
+}
+
+template <int TN, int D>
+DEVI void ring6_run_pipe(floatx16 (&acc)[TN], uint4 (&wr)[D][TN][3], const float* sA, const unsigned short* Wp,
+                         long wbs, int g0, int g1, int r, int h) {
+    const int gl = g1 - 1;
+    const float* ap = sA + (h * 32 + r) * 4;
+    bf16x8_t bh, bm, bl;
+    {
+        const float4 a0 = *(const float4*)(ap + (size_t)g0 * 512), a1 = *(const float4*)(ap + (size_t)g0 * 512 + 256);
+        split8(a0, a1, bh, bm, bl);
+    }
+    const size_t g1o = (size_t)min(g0 + 1, gl) * 512;
+    float4 n0 = *(const float4*)(ap + g1o), n1 = *(const float4*)(ap + g1o + 256);
+    int gb = g0;
+    for (; gb + D <= g1; gb += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int g = gb + d;
+            const bf16x8_t ch = bh, cm = bm, cl = bl;
+            split8(n0, n1, bh, bm, bl);                       // group g + 1 (the last one again past the end)
+            const size_t gn = (size_t)min(g + 2, gl) * 512;
+            n0 = *(const float4*)(ap + gn);
+            n1 = *(const float4*)(ap + gn + 256);
+            x6_mfma6<TN>(acc, wr[d], ch, cm, cl);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    wr[d][j][p] = *(const uint4*)(Wp + j * wbs + ((size_t)min(g + D, gl) * 3 + p) * 512);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) {
+        if (gb + d < g1) {
+            const bf16x8_t ch = bh, cm = bm, cl = bl;
+            split8(n0, n1, bh, bm, bl);
+            const size_t gn = (size_t)min(gb + d + 2, gl) * 512;
+            n0 = *(const float4*)(ap + gn);
+            n1 = *(const float4*)(ap + gn + 256);
+            x6_mfma6<TN>(acc, wr[d], ch, cm, cl);
         }
     }
 }
@@ -1356,6 +1425,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
     if constexpr (X6 == 2) ring6p_run<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n, lane);
+    else if constexpr (X6 == 1 && NW == 4 && X6_PIPE) ring6_run_pipe<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n, r, h);
     else if constexpr (X6 == 1) ring6_run<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n, r, h);
     else ring_run<TN, D>(acc, wr, sH, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3, r, h);
     // layer-2 weights in flight during the epilogue
@@ -1391,6 +1461,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
     if constexpr (X6 == 2) ring6p_run<TN, D>(acc, wx, sH, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n, lane);
+    else if constexpr (X6 == 1 && NW == 4 && X6_PIPE) ring6_run_pipe<TN, D>(acc, wx, sH, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n, r, h);
     else if constexpr (X6 == 1) ring6_run<TN, D>(acc, wx, sH, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n, r, h);
     else ring_run<TN, D>(acc, wr, sH, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3, r, h);
 #ifdef TDMPC_STAMPS
