@@ -69,3 +69,38 @@ def test_discount_pows_match_python_accumulation():
         ref.append(float(np.float32(d)))
         d *= 0.99
     assert _discount_pows(0.99, 5) == ref
+
+
+def test_entry_points_reject_null_arguments():
+    """Every compute entry point checks its required pointers before touching the device: TDMPC_E_NULL (-3)."""
+    L = _lib.lib()
+    cfg = make_cfg("humanoid")
+    d = _lib.dims_from_cfg(cfg)
+    prm = _lib.PlanParams()
+    prm.horizon, prm.iterations, prm.batch = 5, 6, 1
+    E_NULL = -3
+    assert L.tdmpc_plan(C.byref(d), C.byref(prm), None, None, 0, None, None, None, None, None, None, None, None,
+                        None, None, None, 0, None) == E_NULL
+    assert L.tdmpc_estimate_value(C.byref(d), C.byref(prm), None, None, None, None, 768, None, None, None, None, 0,
+                                  None) == E_NULL
+    assert L.tdmpc_pi_rollout(C.byref(d), C.byref(prm), None, None, None, None, None, 0, None) == E_NULL
+    assert L.tdmpc_cem_iter(C.byref(d), C.byref(prm), None, None, None, None, None, None, None, None, None, None,
+                            None, None, 0, None) == E_NULL
+    assert L.tdmpc_encode(C.byref(d), None, None, 0, 1, None, None, None) == E_NULL
+    assert L.tdmpc_pack_weights(C.byref(d), None, 0, None, 0, None) == E_NULL
+
+
+def test_packed_buffer_holds_the_x6_copy():
+    """The packed weight buffer carries the x6 (three bf16 planes) copy of the chain kernels' panels next to the
+    fp32 ones: at humanoid sizes 6 bytes per panel weight on top of the 4 (tdmpc_kernels.hip Layout::x6)."""
+    cfg = bench_cfg("humanoid-run")
+    d = _lib.dims_from_cfg(cfg, max_batch=1)
+    s = _lib.Sizes()
+    assert _lib.lib().tdmpc_sizes_for(C.byref(d), C.byref(s)) == 0
+    M, L, A = cfg.mlp_dim, cfg.latent_dim, cfg.action_dim
+    r32 = lambda x: -(-x // 32) * 32
+    r16 = lambda x: -(-x // 16) * 16
+    Ap, Lp = -(-A // 8) * 8, -(-L // 8) * 8
+    Kx = Ap + Lp
+    x6 = 3 * (2 * M * r16(Kx) + 3 * M * M + r32(L) * M + M * r16(Lp) + r32(A) * M + 2 * M * r16(Kx) + 2 * M * M)
+    assert s.packed_weight_bytes >= 2 * x6
