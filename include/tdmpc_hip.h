@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define TDMPC_ABI_VERSION 4
+#define TDMPC_ABI_VERSION 5
 
 #define TDMPC_OK 0
 #define TDMPC_E_DIMS (-1)     /* unsupported or inconsistent dims / params */
@@ -75,6 +75,11 @@ typedef struct tdmpc_plan_params {
                               (others layered), 6 = chain kernels with fp32 products from a three-way bf16
                               split (TDMPC_PATH_CHAIN_X6), 7 = path 5 with those products; results agree within
                               the fp32 tolerance */
+    /* ABI 5: per-call state read from device memory at run time, so one captured hipGraph serves every value */
+    const int32_t* warm_flags; /* optional device int32 [batch]: per-env warm start (tdmpc.py:124-125, `not t0`
+                                  for that env with a previous mean); NULL = warm_start for every env */
+    const float* std_floor_dev;/* optional device float scalar: self.std (tdmpc.py:148), which update() moves
+                                  every step during std_schedule (tdmpc.py:196); NULL = std_floor */
 } tdmpc_plan_params;
 
 #define TDMPC_PATH_AUTO 0

@@ -888,6 +888,7 @@ struct ChainProb {
 struct ChainArgs {
     ChainProb p[2];
     int rows, M, K1, q1;                 // logical rows; hidden width; first-layer K and its X quad offset
+    int k1_alg;                          // the first layer's real input width (L + A or L), for the profiler's FLOPs
     int rb;                              // row block: 32 (chain_kernel) or 16 (chain16_kernel)
     int nw;                              // waves per workgroup of chain_kernel: 8 or 16
     int hfl;                             // floats of the LDS activation block (max(K1, M) * rb, K1 to 16)
@@ -983,9 +984,16 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 #endif
 DEVI bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 
+// x = hi + mid + lo exactly for finite x. Non-finite inputs keep the fp32 semantics the reference's products
+// have (tdmpc.py:92 then maps them with nan_to_num): +-inf and NaN pass through whole in hi (mid = lo = 0, so
+// no inf - inf appears), and a finite x beyond bf16's largest value (whose round-to-nearest would be inf) takes
+// its truncated top half as hi, which is finite and leaves an exact residual.
 DEVI void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
-    hi = (__bf16)x;
-    const float r1 = __fsub_rn(x, (float)hi);
+    float h = (float)(__bf16)x;
+    const bool xfin = __builtin_isfinite(x);
+    if (!__builtin_isfinite(h)) h = xfin ? __uint_as_float(__float_as_uint(x) & 0xffff0000u) : x;
+    hi = (__bf16)h;
+    const float r1 = xfin ? __fsub_rn(x, h) : 0.f;
     mid = (__bf16)r1;
     lo = (__bf16)__fsub_rn(r1, (float)mid);
 }
@@ -2585,6 +2593,7 @@ struct CemArgs {
     const double* u;
     float* prev_mean; int eval_mode;
     float temperature, momentum, omm, std_floor;
+    const float* std_floor_p;           // optional device scalar overriding std_floor (graph-stable self.std)
     float* action; float* metrics;
     float* elite_out; float* score_out; float* mean_out; float* std_out;
     int no_pick; float* reward_out;     // tdmpc_cem_iter: stop after the refit; reward mean -> reward_out [B]
@@ -2711,6 +2720,7 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
     }
     __syncthreads();
     const float den = red[0];
+    const float std_floor = a.std_floor_p ? *a.std_floor_p : a.std_floor;
     for (int i = tid; i < HA; i += nt) {
         const int t = i / A, c = i % A;
         const float* ea = EA + (size_t)t * K * A + c;
@@ -2722,7 +2732,7 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
             const float dd = ea[(size_t)k * A] - mu;
             v = fadd(v, fmul(sc[k], fmul(dd, dd)));
         }
-        const float sd = tclamp(sqrtf(__fdiv_rn(v, den)), a.std_floor, 2.f);
+        const float sd = tclamp(sqrtf(__fdiv_rn(v, den)), std_floor, 2.f);
         const float nm = fadd(fmul(a.momentum, omean[i]), fmul(a.omm, mu));
         smean[i] = nm; sstd[i] = sd;
         gmean[i] = nm; gstd[i] = sd;
@@ -2796,6 +2806,7 @@ struct EncArgs {
     const float* w2t; const float* b2;
     float* z0;
     float* mean; float* stdv; const float* prev_mean; int warm, H, A, Hmax;
+    const int* warm_flags;                      // optional device [B]: per-env warm start (overrides warm)
     const float* ln_g; const float* ln_b;       // LayerNorm after the first Linear (or null)
     int warm_keep_last;                         // iCEM warm start: mean[-1] = prev_mean[-1] (else 0)
     float init_std;                             // 2 (TDMPC.plan) / 0.5 (iCEM)
@@ -2874,11 +2885,12 @@ __global__ void __launch_bounds__(1024) encode_kernel(const EncArgs a) {
     }
     if (a.mean) {
         const int HA = a.H * a.A;
+        const int warm = a.warm_flags ? a.warm_flags[e] : a.warm;
         for (int i = tid; i < HA; i += nt) {
             const int t = i / a.A;
             float mv = 0.f;
-            if (a.warm && t < a.H - 1) mv = a.prev_mean[(size_t)e * HA + i + a.A];  // mean[:-1] = prev[1:]
-            if (a.warm && t == a.H - 1 && a.warm_keep_last) mv = a.prev_mean[(size_t)e * HA + i];  // mean[-1] = prev[-1]
+            if (warm && t < a.H - 1) mv = a.prev_mean[(size_t)e * HA + i + a.A];  // mean[:-1] = prev[1:]
+            if (warm && t == a.H - 1 && a.warm_keep_last) mv = a.prev_mean[(size_t)e * HA + i];  // mean[-1] = prev[-1]
             a.mean[(size_t)e * a.Hmax * a.A + i] = mv;
             a.stdv[(size_t)e * a.Hmax * a.A + i] = a.init_std;
         }
@@ -3347,7 +3359,7 @@ bool chain16_shape_ok(const Layout& w) {
 // Algorithmic MACs per row of a chain launch (with the real widths, not the padded ones):
 // CH_STEP d + R = 2 (K1 M + M^2) + M L + M, CH_PI K1 M + M^2 + M A, CH_Q 2 (K1 M + M^2 + M).
 double chain_macs_per_row(int mode, const ChainArgs& a, int nprob) {
-    const double K1 = a.K1, M = a.M;
+    const double K1 = a.k1_alg > 0 ? a.k1_alg : a.K1, M = a.M;   // unpadded widths: algorithmic MACs
     if (mode == CH_STEP) return 2 * (K1 * M + M * M) + M * a.nvalid + M;
     if (mode == CH_PI) return K1 * M + M * M + M * a.nvalid;
     return nprob * (K1 * M + M * M + M);
@@ -3532,6 +3544,7 @@ ChainArgs chain0(const Ctx& c, int rows, RowMap map, int t, int K1, int q1, int 
     ChainArgs a;
     memset(&a, 0, sizeof a);
     a.rows = rows; a.M = c.M; a.K1 = K1; a.q1 = q1; a.amap = map;
+    a.k1_alg = K1 == c.Kx ? c.w.L + c.w.A : c.w.L;   // TOLD.next / Q take [z, a]; pi takes z
     a.rb = chain_rb(c, rows, nprob);
     a.x6 = a.rb == 32 ? use_x6(c) : (use_x6(c) ? 1 : 0);   // 16-row blocks: chain16_kernel<..., X6 = 1>
     // x6 mode 3: 4-wave workgroups, 128 columns per wave (the per-wave split amortised over twice the MFMAs); the pi
@@ -3876,7 +3889,7 @@ int terminal_q(const Ctx& c, float discH) {
 
 // TOLD.h for `batch` observations -> z0 [B][Lp]; optionally initialises the CEM mean/std.
 int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, const float* prev_mean, int warm,
-           int warm_keep_last = 0, float init_std = 2.f) {
+           int warm_keep_last = 0, float init_std = 2.f, const int* warm_flags = nullptr) {
     const Layout& w = c.w;
     const float* pw = c.pw;
     EncArgs a;
@@ -3940,7 +3953,7 @@ int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, const float*
         a.E = w.flat; a.w1t = nullptr; a.w2t = pw + w.pl_wt; a.b2 = pw + w.pl_b;
     }
     if (prev_mean) {
-        a.mean = c.k.mean; a.stdv = c.k.stdv; a.prev_mean = prev_mean; a.warm = warm;
+        a.mean = c.k.mean; a.stdv = c.k.stdv; a.prev_mean = prev_mean; a.warm = warm; a.warm_flags = warm_flags;
         a.warm_keep_last = warm_keep_last; a.init_std = init_std;
         a.H = c.H; a.A = c.A; a.Hmax = c.d->max_horizon;
     }
@@ -4149,7 +4162,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T;
     // z0 = h(obs) and mean = 0 (warm: prev_mean shifted), std = 2
-    if ((rc = encode(c, obs, obs_is_u8, B, prev_mean, prm->warm_start))) return rc;
+    if ((rc = encode(c, obs, obs_is_u8, B, prev_mean, prm->warm_start, 0, 2.f, prm->warm_flags))) return rc;
     if ((rc = prep(c, noise, 0, c.k.z0))) return rc;
 
     // pi pre-rollout (tdmpc.py:113-118) fused with CEM iteration 0: at each step t the policy rows get
@@ -4178,6 +4191,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     ca.eps_act_off = c.eps_act_off; ca.u = u; ca.prev_mean = prev_mean;
     ca.eval_mode = prm->eval_mode; ca.temperature = prm->temperature; ca.momentum = prm->momentum;
     ca.omm = prm->one_minus_momentum; ca.std_floor = prm->std_floor; ca.action = action; ca.metrics = metrics;
+    ca.std_floor_p = prm->std_floor_dev;
     ca.elite_out = elite_out; ca.score_out = score_out; ca.mean_out = mean_out; ca.std_out = std_out;
     ca.value_out = value_out;
     if (use_chain(c, B * T, 2, CK_Q)) {   // terminal_q leaves q1, q2 per row; cem_kernel forms the values
@@ -4429,7 +4443,7 @@ int tdmpc_cem_iter(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void
     ca.X = c.k.X; ca.x_stride = c.k.x_stride; ca.value = c.k.value; ca.rlast = c.k.rlast;
     ca.mean = c.k.mean; ca.stdv = c.k.stdv;
     ca.temperature = prm->temperature; ca.momentum = prm->momentum; ca.omm = prm->one_minus_momentum;
-    ca.std_floor = prm->std_floor;
+    ca.std_floor = prm->std_floor; ca.std_floor_p = prm->std_floor_dev;
     ca.elite_out = elite_actions; ca.score_out = score; ca.value_out = value; ca.reward_out = reward_mean;
     if (use_chain(c, B * T, 2, CK_Q)) { ca.G = c.k.G; ca.qv = c.k.qv; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H]; }
     hipLaunchKernelGGL(cem_kernel, dim3(B), dim3(1024), cem_lds_bytes(T, H, ca.K, A), c.s, ca);

@@ -59,7 +59,13 @@ class EnvShardedPlanner:
 
     @torch.no_grad()
     def plan(self, global_obs, step, t0=True):
-        """Plan this rank's envs of `global_obs` ([n_envs, ...]) and return every env's (actions, metrics)."""
+        """Plan this rank's envs of `global_obs` ([n_envs, ...]) and return every env's (actions, metrics).
+        `t0` is a bool for the whole batch or a sequence of n_envs per-env flags (global env order)."""
+        if not isinstance(t0, (bool, int)) and not (torch.is_tensor(t0) and t0.dim() == 0):
+            t0 = list(t0)
+            if len(t0) != self.n_envs:
+                raise ValueError(f"per-env t0 has {len(t0)} entries for {self.n_envs} envs")
+            t0 = t0[self.lo:self.hi]   # this rank's envs' flags
         a, m = self.plan_fn(self.local_obs(global_obs), step, t0)
         self._local[:, :self.A].copy_(a)
         self._local[:, self.A:].copy_(m)

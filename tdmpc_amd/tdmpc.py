@@ -99,6 +99,12 @@ class HipPlanner:
         self.prev_mean_flat = torch.zeros(max_batch * d.max_horizon * self.A, dtype=torch.float32, device=dev)
         self.action = torch.zeros(max_batch, self.A, dtype=torch.float32, device=dev)
         self.metrics = torch.zeros(max_batch, 2, dtype=torch.float32, device=dev)
+        # per-call state the kernels read from device memory (ABI 5), so one captured graph serves every value
+        # of self.std over std_schedule and every per-env t0 pattern
+        self.std_dev = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.warm_dev = torch.zeros(max_batch, dtype=torch.int32, device=dev)
+        self._std_host = None
+        self._warm_host = None
         if cfg.modality == "pixels":
             self.obs_buf = torch.zeros(max_batch, *cfg.obs_shape, dtype=torch.uint8, device=dev)
         else:
@@ -180,6 +186,24 @@ class HipPlanner:
         for t, v in enumerate(_discount_pows(cfg.discount, H)):
             p.discount_pow[t] = v
         return p
+
+    def set_call_state(self, std_floor: float, warm):
+        """Write self.std and the per-env warm flags into the device scalars the kernels read (stream-ordered
+        before the launch or graph replay that follows; skipped when unchanged)."""
+        s = float(np.float32(std_floor))
+        if s != self._std_host:
+            self.std_dev.fill_(s)
+            self._std_host = s
+        w = tuple(int(bool(x)) for x in warm)
+        if w != self._warm_host:
+            self.warm_dev[:len(w)].copy_(torch.tensor(w, dtype=torch.int32))
+            self._warm_host = w
+
+    def device_state_params(self, prm):
+        """Point prm at the device-resident std floor and warm flags (set_call_state)."""
+        prm.std_floor_dev = self.std_dev.data_ptr()
+        prm.warm_flags = self.warm_dev.data_ptr()
+        return prm
 
     def launch(self, prm, obs_is_u8: bool, trace: dict | None = None):
         L = self.L
@@ -379,6 +403,8 @@ class TDMPC:
             a = torch.empty(B, cfg.action_dim, dtype=torch.float32, device=self.device)
             for e in range(B):
                 a[e].uniform_(-1, 1)
+            if not sync_metrics:
+                return a, torch.zeros(B, 2, dtype=torch.float32, device=self.device)
             return a, [{"external_reward_mean": 0.0, "current_std": 0.0} for _ in range(B)]
         t0s = [t0] * B if isinstance(t0, (bool, int, np.bool_)) else list(t0)
         return self._plan_envs(obs, eval_mode, step, t0s, sync_metrics)
@@ -403,8 +429,6 @@ class TDMPC:
                 # the reference's `mean[:-1] = self._prev_mean[1:]` raises on a horizon change
                 raise RuntimeError(f"shape mismatch: prev_mean horizon {self._prev_H[e]} vs {H}")
             warm.append(w)
-        if len(set(warm)) > 1:
-            raise NotImplementedError("mixed warm/cold starts in one batch")
         pl.pack(self.model)
         if cfg.modality == "pixels":
             src = torch.as_tensor(obs).to(self.device, torch.uint8)
@@ -413,7 +437,8 @@ class TDMPC:
             src = torch.as_tensor(obs, dtype=torch.float32).to(self.device)
             pl.obs_buf[:B].copy_(src.view(B, -1))
         obs_u8 = cfg.modality == "pixels"
-        prm = pl.params(H, I, B, warm[0], eval_mode, self.std)
+        prm = pl.device_state_params(pl.params(H, I, B, warm[0], eval_mode, self.std))
+        pl.set_call_state(self.std, warm)
         if noise is not None:
             us = []
             for e, nb in enumerate(noise):
@@ -436,7 +461,7 @@ class TDMPC:
             pl.launch(prm, obs_u8, trace)
 
         if self.graph and noise is None and trace is None:
-            key = (H, I, B, bool(warm[0]), bool(eval_mode), float(self.std), self.rng)
+            key = (H, I, B, bool(eval_mode), self.rng)   # self.std and the warm flags live on the device
             g = pl._graphs.get(key)
             if g is None:
                 # No eager warm-up: the library has no lazy initialisation left after pack(), and an eager

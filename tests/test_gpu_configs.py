@@ -1,0 +1,207 @@
+"""GPU parity at BASELINE.json's full sizes for every GPU config, plus the drop-in's per-call state.
+
+* `test_plan_fullsize_configs`: whole `plan()` calls (N=512, H=5, 6 iterations, K=64) for cheetah-run,
+  humanoid-run with latent 512, quadruped-run pixels and dog-run, at one env per call (the drop-in) and at
+  8 envs per call (configs[3]'s per-GPU share of 64 dog envs), cold start, warm start and a mixed t0 batch,
+  every env against the oracle (the CPU restatement of tdmpc.py:94-163, pinned to the reference) on the same
+  noise. Tolerances as tests/test_gpu_plan.py (parity_util): values 1e-5 + 1e-4 |ref|, action / mean / std /
+  metrics 2e-5 while the elite sets agree; near-tie escapes are counted (tests/test_zz_parity_budget.py).
+* `test_mixed_t0_batch_equals_homogeneous`: per-env warm/cold starts in one batch (tdmpc.py:124-125 per env)
+  equal, bitwise, the same envs planned in all-warm and all-cold batches.
+* `test_graph_serves_std_schedule`: one captured HIP graph serves every self.std of std_schedule and every
+  t0 pattern (both read from device memory), bitwise equal to eager calls.
+* `test_estimate_value_nonfinite`: the NaN / inf guard (`G.nan_to_num_(0)`, tdmpc.py:92: NaN -> 0,
+  +-inf -> +-FLT_MAX) on every kernel path, including activations beyond bf16's range on the x6 products.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import tdmpc_ref
+from parity_util import close, compare_iterations, record
+from tdmpc_amd.config import make_cfg
+from tdmpc_amd.tdmpc import TDMPC
+from tdmpc_amd.told import synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+
+FULL = dict(num_samples=512, num_elites=64, iterations=6, horizon=5)
+CONFIGS = {
+    "cheetah-run": ("cheetah", dict(FULL)),
+    "humanoid-run-l512": ("humanoid", dict(FULL, latent_dim=512)),
+    "quadruped-run-pixels": ("quadruped", dict(FULL, modality="pixels")),
+    "dog-run": ("dog", dict(FULL)),
+}
+PATHS = ["layered", "chain16", "chain32", "split", "chain_x6", "split_x6", "chain"]
+
+
+def _agent(cfg, wseed, B=1, path="auto", **kw):
+    agent = TDMPC(cfg, max_batch=B, path=path, **kw)
+    agent.model.load_state_dict(synthetic_state_dict(cfg, wseed))
+    agent.std = 0.05
+    return agent
+
+
+def _obs(cfg, rs, B):
+    if cfg.modality == "pixels":
+        return rs.randint(0, 256, size=(B,) + tuple(cfg.obs_shape)).astype(np.uint8)
+    return rs.standard_normal((B,) + tuple(cfg.obs_shape)).astype(np.float32)
+
+
+@pytest.mark.parametrize("B", [1, 8])
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_plan_fullsize_configs(name, B):
+    task, ov = CONFIGS[name]
+    cfg = make_cfg(task, **ov)
+    agent = _agent(cfg, 21, B=B)
+    told = tdmpc_ref.RefTOLD(synthetic_state_dict(cfg, 21), cfg)
+    states = [tdmpc_ref.PlanState(0.05) for _ in range(B)]
+    diverged = [False] * B        # an env whose elite set swapped on a near tie is not compared while warm
+    rs = np.random.RandomState(5)
+    torch.manual_seed(8)
+    np.random.seed(8)
+    calls = [[True] * B, [False] * B]
+    if B > 1:
+        calls.append([e % 2 == 0 for e in range(B)])   # mixed: even envs restart, odd envs warm-start
+    for ci, t0s in enumerate(calls):
+        obs = _obs(cfg, rs, B)
+        noises = [tdmpc_ref.draw_noise(cfg, 10**6, False) for _ in range(B)]
+        tr = {}
+        a, m = agent._plan_envs(obs, False, 10**6, t0s, trace=tr, noise=noises)
+        a = a.cpu().numpy()
+        for e in range(B):
+            rtr = {}
+            ra, rm = tdmpc_ref.plan(told, cfg, states[e], obs[e], noises[e], eval_mode=False, step=10**6,
+                                    t0=t0s[e], trace=rtr)
+            if t0s[e]:
+                diverged[e] = False
+            if diverged[e]:
+                continue
+            ref_vals = torch.stack(rtr["value"]).squeeze(-1).numpy()
+            same = compare_iterations(tr["value"][e].cpu().numpy(), ref_vals, cfg.num_elites)
+            record(same, f"{name}/B{B}/call{ci}/env{e}")
+            if not same:
+                diverged[e] = True
+                continue
+            np.testing.assert_allclose(a[e], ra.numpy(), atol=2e-5, rtol=0, err_msg=f"call {ci} env {e}")
+            np.testing.assert_allclose(tr["mean"][e, -1].cpu().numpy(), rtr["mean"][-1].numpy(), atol=2e-5, rtol=0)
+            np.testing.assert_allclose(tr["std"][e, -1].cpu().numpy(), rtr["std"][-1].numpy(), atol=2e-5, rtol=0)
+            np.testing.assert_allclose([m[e]["external_reward_mean"], m[e]["current_std"]],
+                                       [rm["external_reward_mean"], rm["current_std"]], atol=2e-5, rtol=1e-4)
+            pm = agent.planner.prev_mean_view(5, B)[e].cpu().numpy()
+            np.testing.assert_allclose(pm, states[e].prev_mean.numpy(), atol=2e-5, rtol=0)
+
+
+@pytest.mark.parametrize("path", ["auto", "chain_x6", "layered"])
+def test_mixed_t0_batch_equals_homogeneous(path):
+    """A batch mixing warm and cold starts equals, env by env and bitwise, the same batch planned all-warm or
+    all-cold from the same previous means (same batch shape, so the same kernels run)."""
+    cfg = make_cfg("dog", **FULL)
+    B = 4
+    agent = _agent(cfg, 23, B=B, path=path)
+    pl = agent.planner
+    rs = np.random.RandomState(9)
+    obs0, obs1 = _obs(cfg, rs, B), _obs(cfg, rs, B)
+    torch.manual_seed(2)
+    n0 = [tdmpc_ref.draw_noise(cfg, 10**6, False) for _ in range(B)]
+    n1 = [tdmpc_ref.draw_noise(cfg, 10**6, False) for _ in range(B)]
+    agent._plan_envs(obs0, False, 10**6, [True] * B, noise=n0)
+    prev = pl.prev_mean_flat.clone()
+    outs = {}
+    for key, t0s in (("mixed", [True, False, False, True]), ("cold", [True] * B), ("warm", [False] * B)):
+        pl.prev_mean_flat.copy_(prev)
+        a, m = agent._plan_envs(obs1, False, 10**6, t0s, sync_metrics=False, noise=n1)
+        outs[key] = (a.clone(), m.clone(), pl.prev_mean_flat.clone())
+    HA = 5 * cfg.action_dim
+    for e, t0 in enumerate([True, False, False, True]):
+        ref = outs["cold" if t0 else "warm"]
+        assert torch.equal(outs["mixed"][0][e], ref[0][e]), e
+        assert torch.equal(outs["mixed"][1][e], ref[1][e]), e
+        assert torch.equal(outs["mixed"][2][e * HA:(e + 1) * HA], ref[2][e * HA:(e + 1) * HA]), e
+    assert not torch.equal(outs["cold"][0], outs["warm"][0])   # the warm start did change something
+
+
+def test_graph_serves_std_schedule():
+    """graph=True: std_schedule moves self.std on every update (tdmpc.py:196-197) and t0 changes per env; both
+    live in device memory, so ONE captured graph serves all calls, and each call equals an eager call."""
+    cfg = make_cfg("humanoid", **FULL)
+    B = 4
+    obs = np.random.RandomState(4).standard_normal((B, cfg.obs_shape[0])).astype(np.float32)
+    schedule = [(0.5, [True] * B), (0.4, [True, False, False, True]), (0.3, [False] * B), (0.05, [False, True] * 2)]
+    outs = []
+    for graph in (True, False):
+        agent = _agent(cfg, 2, B=B, rng="fused", graph=graph)
+        torch.manual_seed(11)
+        res = []
+        for std, t0s in schedule:
+            agent.std = std
+            a, m = agent.plan_batch(obs, step=10**6, t0=t0s, sync_metrics=False)
+            res.append((a.clone(), m.clone()))
+            assert bool((m[:, 1] >= np.float32(std) * (1 - 1e-6)).all()), "the CEM std floor (self.std) was not applied"
+        outs.append(res)
+        if graph:
+            assert len(agent.planner._graphs) == 1, list(agent.planner._graphs)
+    for (a1, m1), (a2, m2) in zip(*outs):
+        assert torch.equal(a1, a2) and torch.equal(m1, m2)
+
+
+FMAX = float(np.finfo(np.float32).max)
+
+
+def _nf_case(case, sd, z0):
+    """Weights / start latents that drive estimate_value outside the finite range."""
+    if case == "beyond_bf16":
+        # a latent above bf16's largest value (3.3895e38; rounds to inf in bf16) whose products stay finite:
+        # the x6 split must keep it finite (truncated top half + exact residual)
+        # (column weights ~1e-33: their bf16 mid / lo parts stay normal numbers, so the x6 products are exact)
+        z0[:, 3] = 3.4e38
+        for k in ("_dynamics.0.weight", "_reward.0.weight"):
+            sd[k][:, 3] *= 1e-32
+    elif case == "inf_latent":
+        z0[:, 3] = float("inf")
+    elif case == "nan_latent":
+        z0[:, 3] = float("nan")
+    elif case == "reward_pos_overflow":
+        sd["_reward.4.bias"][:] = 3e38            # G overflows to +inf -> +FLT_MAX
+    elif case == "reward_neg_overflow":
+        sd["_reward.4.bias"][:] = -3e38           # -> -FLT_MAX
+    elif case == "inf_minus_inf":
+        sd["_reward.4.bias"][:] = 3e38
+        sd["_Q1.6.bias"][:] = float("-inf")
+        sd["_Q2.6.bias"][:] = float("-inf")       # +inf + -inf = NaN -> 0
+    elif case == "large_finite":
+        sd["_reward.4.weight"].mul_(3e37)         # |G| ~ 1e37, finite
+
+
+@pytest.mark.parametrize("case", ["beyond_bf16", "inf_latent", "nan_latent", "reward_pos_overflow",
+                                  "reward_neg_overflow", "inf_minus_inf", "large_finite"])
+@pytest.mark.parametrize("path", PATHS)
+def test_estimate_value_nonfinite(case, path):
+    cfg = make_cfg("humanoid", num_samples=512, num_elites=64)
+    H = 5
+    sd = synthetic_state_dict(cfg, 7)
+    g = torch.Generator().manual_seed(3)
+    z0 = torch.randn(1, cfg.latent_dim, generator=g)
+    _nf_case(case, sd, z0)
+    agent = TDMPC(cfg, path=path)
+    agent.model.load_state_dict(sd)
+    pl = agent.planner
+    pl.pack(agent.model)
+    T, A = pl.T, cfg.action_dim
+    actions = torch.rand(1, H, T, A, generator=g) * 2 - 1
+    eps = torch.randn(1, T, A, generator=g)
+    v, _, _ = pl.estimate_value(z0, actions, eps, H)
+    gv = v[0].cpu().numpy()
+    told = tdmpc_ref.RefTOLD(sd, cfg)
+    rv = tdmpc_ref.estimate_value(told, cfg, z0.repeat(T, 1), actions[0], H, eps[0])[0][:, 0].numpy()
+    assert np.isfinite(gv).all(), "nan_to_num left a non-finite value"
+    special = (np.abs(rv) == FMAX) | (rv == 0)
+    np.testing.assert_array_equal(gv[special], rv[special])
+    # large_finite / beyond_bf16: G sums five rewards of ~1e37 / ~1e5 that partly cancel, so its rounding error
+    # follows the terms' scale, not |G|: absolute tolerance 1e-5 of the largest |G| there
+    atol = 1e-5 * float(np.abs(rv).max()) if case in ("large_finite", "beyond_bf16") else 1e-5
+    assert close(gv[~special], rv[~special], atol=atol).all(), np.abs(gv - rv)[~special].max()
+    if case in ("reward_pos_overflow", "reward_neg_overflow", "inf_minus_inf", "nan_latent", "inf_latent"):
+        assert special.all()   # the case does hit the guard's branches
+    if case in ("beyond_bf16", "large_finite"):
+        assert not special.any()

@@ -19,8 +19,8 @@ from tdmpc_amd.told import synthetic_state_dict
 
 pytestmark = pytest.mark.gpu
 
-RTOL, ATOL = 1e-4, 1e-5
-
+from parity_util import ATOL, RTOL, compare_iterations as _compare_iterations, close as _close, \
+    elites as _elites, near_tie as _near_tie, record
 
 PATHS = ["layered", "chain16", "chain32", "split", "chain_x6", "split_x6", "chain"]
 
@@ -30,36 +30,6 @@ def _agent(cfg, wseed, B=1, path="auto"):
     agent.model.load_state_dict(synthetic_state_dict(cfg, wseed))
     agent.std = 0.05
     return agent
-
-
-def _close(a, b, atol=ATOL, rtol=RTOL):
-    a = np.asarray(a, dtype=np.float64)
-    b = np.asarray(b, dtype=np.float64)
-    return np.abs(a - b) <= atol + rtol * np.abs(b)
-
-
-def _elites(v, K):
-    return set(np.argsort(-np.asarray(v), kind="stable")[:K].tolist())
-
-
-def _near_tie(ref_v, a, b, K):
-    """True when the symmetric difference of two elite sets only holds values next to the cut-off."""
-    v = np.asarray(ref_v, dtype=np.float64)
-    cut = np.sort(v)[::-1][K - 1]
-    diff = a ^ b
-    return all(abs(v[i] - cut) <= 1e-4 * (1 + abs(cut)) for i in diff)
-
-
-def _compare_iterations(gpu_vals, ref_vals, K):
-    """Compare per-iteration values; returns True if every iteration's elite set agreed."""
-    for i in range(ref_vals.shape[0]):
-        ok = _close(gpu_vals[i], ref_vals[i])
-        assert ok.all(), f"iteration {i}: max |dG| {np.abs(gpu_vals[i] - ref_vals[i]).max():.3e}"
-        eg, er = _elites(gpu_vals[i], K), _elites(ref_vals[i], K)
-        if eg != er:
-            assert _near_tie(ref_vals[i], eg, er, K), f"iteration {i}: elite sets differ away from the cut-off"
-            return False
-    return True
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -85,8 +55,9 @@ def test_plan_matches_reference_golden(name, path):
             np.testing.assert_allclose(agent._prev_mean.cpu().numpy(), d[f"c{ci}_prev_mean"], atol=2e-5, rtol=0)
             rm, cs = m[0]["external_reward_mean"], m[0]["current_std"]
             np.testing.assert_allclose([rm, cs], d[f"c{ci}_metrics"], atol=2e-5, rtol=1e-4)
-        else:
-            pytest.skip(f"{name} call {ci}: near-tie elite swap; trajectories diverge legitimately")
+        record(all_same, f"{name}/{path}/call{ci}")
+        if not all_same:
+            break   # near-tie swap: this and the later (warm-started) calls diverge legitimately
 
 
 @pytest.mark.parametrize("task,ov", [
@@ -210,8 +181,9 @@ def test_plan_fullsize_vs_oracle(path):
         ra, rm = tdmpc_ref.plan(told, cfg, st, obs, nb, eval_mode=False, step=10**6, t0=t0, trace=rtr)
         ref_vals = torch.stack(rtr["value"]).squeeze(-1).numpy()
         same = _compare_iterations(tr["value"][0].cpu().numpy(), ref_vals, cfg.num_elites)
+        record(same, f"fullsize/{path}/call{call}")
         if not same:
-            pytest.skip("near-tie elite swap")
+            break
         np.testing.assert_allclose(a[0].cpu().numpy(), ra.numpy(), atol=2e-5, rtol=0)
         np.testing.assert_allclose(tr["mean"][0, -1].cpu().numpy(), rtr["mean"][-1].numpy(), atol=2e-5, rtol=0)
         np.testing.assert_allclose(tr["std"][0, -1].cpu().numpy(), rtr["std"][-1].numpy(), atol=2e-5, rtol=0)
@@ -236,7 +208,9 @@ def test_plan_ragged_vs_oracle(path):
         st, rtr = tdmpc_ref.PlanState(0.05), {}
         ra, rm = tdmpc_ref.plan(told, cfg, st, obs[e], noises[e], eval_mode=False, step=10**6, t0=True, trace=rtr)
         ref_vals = torch.stack(rtr["value"]).squeeze(-1).numpy()
-        if _compare_iterations(tr["value"][e].cpu().numpy(), ref_vals, cfg.num_elites):
+        same = _compare_iterations(tr["value"][e].cpu().numpy(), ref_vals, cfg.num_elites)
+        record(same, f"ragged/{path}/env{e}")
+        if same:
             np.testing.assert_allclose(a[e].cpu().numpy(), ra.numpy(), atol=2e-5, rtol=0)
 
 
@@ -260,7 +234,9 @@ def test_bench_batch_vs_oracle():
         rtr = {}
         ra, rm = tdmpc_ref.plan(told, cfg, st, obs[e], noises[e], eval_mode=False, step=10**6, t0=True, trace=rtr)
         ref_vals = torch.stack(rtr["value"]).squeeze(-1).numpy()
-        if _compare_iterations(tr["value"][e].cpu().numpy(), ref_vals, cfg.num_elites):
+        same = _compare_iterations(tr["value"][e].cpu().numpy(), ref_vals, cfg.num_elites)
+        record(same, f"bench_batch/env{e}")
+        if same:
             np.testing.assert_allclose(a[e].cpu().numpy(), ra.numpy(), atol=2e-5, rtol=0)
             compared += 1
     assert compared >= B // 2, "too many near-tie elite swaps to compare actions"
@@ -356,6 +332,7 @@ def test_building_blocks_compose_plan(task, ov, path):
             if eg != er:
                 assert _near_tie(rv, eg, er, K)
                 diverged[e] = True
+                record(False, f"blocks/{task}/{path}/env{e}/iter{i}")
                 continue
             ref_elite = tr["actions"][i][:, ref_idx].numpy()
             np.testing.assert_allclose(elite[e].cpu().numpy(), ref_elite, atol=2e-5, rtol=0)
@@ -366,6 +343,7 @@ def test_building_blocks_compose_plan(task, ov, path):
     for e in range(B):
         if diverged[e]:
             continue
+        record(True)
         # the output pick of tdmpc.py:152-158 on the host from the last iteration's score / elites / std
         j = tdmpc_ref.choice_index(score[e].cpu().numpy(), us[e])
         a = elite[e, 0, j].cpu() + std[e, 0].cpu() * eps_act[e]

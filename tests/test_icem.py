@@ -10,6 +10,8 @@ import os
 
 import numpy as np
 import pytest
+
+from parity_util import near_tie, record
 import torch
 
 from icem_io import CALLS, icem_cfg
@@ -84,10 +86,12 @@ def test_gpu_icem_matches_oracle(path):
             K = cfg.num_elites
             eg = set(np.argsort(-gv, kind="stable")[:K]); er = set(np.argsort(-rv, kind="stable")[:K])
             if eg != er:
+                assert near_tie(rv, eg, er, K), (ci, i, "elite sets differ away from the cut-off")
                 same = False
                 break
+        record(same, f"icem/{path}/call{ci}")
         if not same:
-            pytest.skip(f"call {ci}: near-tie elite swap; trajectories diverge legitimately")
+            break   # near-tie swap: this and the later (warm-started) calls diverge legitimately
         np.testing.assert_allclose(ga.cpu().numpy(), ra.numpy(), atol=2e-5, rtol=0)
         np.testing.assert_allclose(agent._prev_mean.cpu().numpy(), st.prev_mean.numpy(), atol=2e-5, rtol=0)
         np.testing.assert_allclose(agent._elite_actions.cpu().numpy(), st.elite_actions.numpy(), atol=2e-5, rtol=0)
