@@ -984,10 +984,9 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 #endif
 DEVI bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 
-// x = hi + mid + lo exactly for finite x. Non-finite inputs keep the fp32 semantics the reference's products
-// have (tdmpc.py:92 then maps them with nan_to_num): +-inf and NaN pass through whole in hi (mid = lo = 0, so
-// no inf - inf appears), and a finite x beyond bf16's largest value (whose round-to-nearest would be inf) takes
-// its truncated top half as hi, which is finite and leaves an exact residual.
+// Weights (pack time, pack_x6_kernel): x = hi + mid + lo exactly, each part round-to-nearest (the smallest dropped
+// terms). A finite weight beyond bf16's largest value (whose rounding would be inf) takes its truncated top half as hi,
+// and a non-finite one passes through whole in hi (mid = lo = 0).
 DEVI void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
     float h = (float)(__bf16)x;
     const bool xfin = __builtin_isfinite(x);
@@ -998,12 +997,28 @@ DEVI void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
     lo = (__bf16)__fsub_rn(r1, (float)mid);
 }
 
+// Activations (in the hot loop, once per MFMA k group): hi = the truncated top half of x (one AND; finite for every
+// finite x, beyond bf16's largest value included), then mid / lo round-to-nearest: x = hi + mid + lo exactly for
+// finite x (the residual keeps <= 16 significant bits). The dropped terms (w_mid x_lo + w_lo x_mid + w_lo x_lo) are
+// <= 1.5 * 2^-23 of |w x|, the size of an fp32 product rounding. Same VALU cost as a round-to-nearest hi (the AND
+// replaces the bf16 -> fp32 unpack). A NaN stays NaN; an infinite activation gives NaN products (inf - inf in the
+// residual) where fp32 gives +-inf -- the reference's next mixed-sign layer or LayerNorm turns those into NaN too,
+// so G after nan_to_num (tdmpc.py:92) agrees (tests/test_gpu_configs.py::test_estimate_value_nonfinite).
+DEVI void split3_act(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
+    const uint32_t u = __float_as_uint(x);
+    const float h = __uint_as_float(u & 0xffff0000u);
+    hi = __builtin_bit_cast(__bf16, (unsigned short)(u >> 16));
+    const float r1 = __fsub_rn(x, h);
+    mid = (__bf16)r1;
+    lo = (__bf16)__fsub_rn(r1, (float)mid);
+}
+
 DEVI void split8(const float4& a0, const float4& a1, bf16x8_t& bh, bf16x8_t& bm, bf16x8_t& bl) {
     const float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         __bf16 h, m, l;
-        split3(x[e], h, m, l);
+        split3_act(x[e], h, m, l);
         bh[e] = h; bm[e] = m; bl[e] = l;
     }
 }
@@ -1375,7 +1390,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 __bf16 hh, mm, ll;
-                split3(xs[e], hh, mm, ll);
+                split3_act(xs[e], hh, mm, ll);
                 hb[e] = __builtin_bit_cast(unsigned short, hh);
                 mb[e] = __builtin_bit_cast(unsigned short, mm);
                 lb[e] = __builtin_bit_cast(unsigned short, ll);

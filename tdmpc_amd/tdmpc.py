@@ -12,7 +12,10 @@ Extensions beyond the reference API:
   * `plan_batch(obs[B], ...)` plans B independent environments in one call (one launch sequence, rows of
     all envs stacked), with per-env state (`_prev_mean` per env).
   * `rng="fused"` draws all of a call's Gaussian noise with one generator call instead of the reference's
-    18 separate draws (same distribution, different stream); `graph=True` replays the call from a HIP graph.
+    18 separate draws (same distribution, different stream).
+  * `graph=True` (the default) replays each call -- the reference-order draws included -- from one HIP graph per
+    (horizon, iterations, batch, eval_mode); self.std and the per-env warm starts are read from device memory,
+    so the graph serves every call. Equal, bitwise, to `graph=False` (eager launches).
   * `path` picks the kernel family: "auto" (by row count), "layered" (one fused GEMM per Linear) or "chain"
     (one row-block kernel per TOLD head); all agree within the fp32 parity tolerance.
 """
@@ -316,7 +319,7 @@ class HipPlanner:
 class TDMPC:
     """Drop-in for the reference `TDMPC` planning interface (tdmpc.py:53-163)."""
 
-    def __init__(self, cfg, max_batch: int = 1, rng: str = "reference", graph: bool = False, path: str = "auto"):
+    def __init__(self, cfg, max_batch: int = 1, rng: str = "reference", graph: bool = True, path: str = "auto"):
         self.cfg = cfg
         self.device = torch.device(cfg.device)
         self.std = linear_schedule(cfg.std_schedule, 0)      # tdmpc.py:59
