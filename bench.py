@@ -190,6 +190,21 @@ def replay_bench(cfg, dev, cpu=True, reps=200):
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t) / reps
         key = "without_replacement" if full else "with_replacement"
+        if not full:
+            # update_priorities at the learner's write-back size and at 50k (helper.py:487-488; duplicates: last wins)
+            upd = {}
+            for n in (B, 50_000):
+                ui = torch.from_numpy(rs.randint(0, total, n)).to(dev)
+                uv = torch.from_numpy(rs.exponential(1.0, (n, 1)).astype(np.float32)).to(dev)
+                for _ in range(3):
+                    buf.update_priorities(ui, uv)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                for _ in range(reps):
+                    buf.update_priorities(ui, uv)
+                torch.cuda.synchronize()
+                upd[str(n)] = round((time.perf_counter() - t1) / reps * 1e6, 2)
+            out["update_priorities_us"] = upd
         # algorithmic HBM bytes: priorities read, p**alpha write + read, probs write, float64 cdf write, window gather
         alg = total * (4 + 8 + 4 + 8) + B * (H + 2) * (obs_dim + A + 1) * 4
         out[key] = {"value": round(1.0 / dt, 1), "unit": "samples/s", "us_per_sample": round(dt * 1e6, 2),

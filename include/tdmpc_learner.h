@@ -36,6 +36,13 @@ int tdmpc_loss_forward(const tdmpc_loss_args* a, float* rows, float* scal, void*
 int tdmpc_loss_backward(const tdmpc_loss_args* a, const float* rows, const float* scal, const float* gw,
                         float* dzp, float* dq1, float* dq2, float* drp, void* stream);
 
+/* RandomShiftsAug (helper.py:250-283, the pixel learner's augmentation): out[k] = x[k] shifted by (shift[k][0],
+ * shift[k][1]) - pad pixels with replicate padding, i.e. the reference's pad + grid_sample at its (integer) sample
+ * points. x, out: float [n][c][h][w] (a 5-D [t][b] batch flattened to n = t * b, as the reference reshapes it);
+ * shift: float [n][2] integers in [0, 2 pad] (the reference's torch.randint draw, x then y). */
+int tdmpc_random_shift(const float* x, const float* shift, int32_t n, int32_t c, int32_t h, int32_t w, int32_t pad,
+                       float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -19,6 +19,7 @@ second); tests/test_learner.py requires this restatement to match it bit for bit
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -154,3 +155,19 @@ class RefLearner:
 
     def state_dicts(self):
         return {k: v.detach() for k, v in self.p.items()}, dict(self.pt)
+
+
+def random_shift(x: np.ndarray, shift: np.ndarray, pad: int) -> np.ndarray:
+    """RandomShiftsAug's arithmetic (helper.py:262-283) restated: replicate-pad by `pad`, then sample the padded
+    frame at base_grid + shift. linspace(-1 + 1/n, 1 - 1/n, n)[:h] unnormalises (align_corners=False) to the pixel
+    centres 0..h-1 and shift s * 2/n to s pixels, so the bilinear sample is the padded pixel (i + s_y, j + s_x).
+    The reference evaluates those coordinates in fp32 and lands within ~1e-5 px of them (its output blends that
+    much of a neighbour: <= 2.5e-3 on 0..255 frames, tests/test_learner.py against its recorded outputs).
+    x: [n, c, h, w] float32; shift: [n, 2] integers (x, y)."""
+    n, c, h, w = x.shape
+    xp = np.pad(x, ((0, 0), (0, 0), (pad, pad), (pad, pad)), mode="edge")
+    out = np.empty_like(x)
+    for k in range(n):
+        sx, sy = int(shift[k, 0]), int(shift[k, 1])
+        out[k] = xp[k, :, sy:sy + h, sx:sx + w]
+    return out

@@ -22,7 +22,7 @@ EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc
             "tdmpc_replay_workspace_bytes", "tdmpc_replay_add_priorities", "tdmpc_replay_update_priorities",
             "tdmpc_replay_sample",
             # include/tdmpc_learner.h
-            "tdmpc_loss_forward", "tdmpc_loss_backward")
+            "tdmpc_loss_forward", "tdmpc_loss_backward", "tdmpc_random_shift")
 
 
 class Dims(C.Structure):
@@ -109,11 +109,12 @@ def lib():
     L.tdmpc_replay_workspace_bytes.argtypes = [C.POINTER(ReplayDims)]
     L.tdmpc_replay_workspace_bytes.restype = sz
     L.tdmpc_replay_add_priorities.argtypes = [C.POINTER(ReplayDims), vp, i32, i32, vp, sz, vp]
-    L.tdmpc_replay_update_priorities.argtypes = [C.POINTER(ReplayDims), vp, vp, vp, i32, C.c_float, vp]
+    L.tdmpc_replay_update_priorities.argtypes = [C.POINTER(ReplayDims), vp, vp, vp, i32, C.c_float, vp, sz, vp]
     L.tdmpc_replay_sample.argtypes = [C.POINTER(ReplayDims), C.POINTER(ReplayStore), i32, i32, C.c_float,
                                       C.c_float, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
     L.tdmpc_loss_forward.argtypes = [C.POINTER(LossArgs), vp, vp, vp]
     L.tdmpc_loss_backward.argtypes = [C.POINTER(LossArgs), vp, vp, vp, vp, vp, vp, vp, vp]
+    L.tdmpc_random_shift.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp]
     for name in EXPORTED:
         if not hasattr(L, name):
             raise RuntimeError(f"{LIB_PATH} does not export {name}")

@@ -9,6 +9,8 @@
 
 #include <stdio.h>
 
+#include <algorithm>
+
 #include "../../include/tdmpc_hip.h"
 #include "../../include/tdmpc_learner.h"
 
@@ -129,9 +131,44 @@ bool args_ok(const tdmpc_loss_args* a) {
            a->B > 0 && a->L > 0;
 }
 
+// RandomShiftsAug (helper.py:250-283) as the gather it is: the reference pads by `pad` with replicate padding and
+// grid-samples (bilinear, zeros, align_corners=False) at base_grid + shift, whose points are exactly the integer
+// pixel centres (linspace(-1 + 1/n, 1 - 1/n, n)[:h] unnormalises to 0..h-1, shift s * 2/n to s pixels). So output
+// (i, j) of stacked image k is the padded image at (i + sy_k, j + sx_k) = the input at
+// (clamp(i + sy_k - pad), clamp(j + sx_k - pad)). One thread per output pixel, a row per 64 consecutive lanes
+// (coalesced, HBM-bound: 4 B read + 4 B written per pixel). shift: the reference's own draw, float [n][2] (x, y).
+__global__ void __launch_bounds__(256) random_shift_kernel(const float* x, const float* shift, int C, int h, int w,
+                                                           int pad, float* out) {
+    const int k = blockIdx.y;                        // stacked image
+    const int sx = (int)shift[2 * k], sy = (int)shift[2 * k + 1];
+    const size_t plane = (size_t)h * w;
+    const int total = C * h * w;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const int c = e / (h * w), r = e % (h * w), i = r / w, j = r % w;
+        const int si = min(max(i + sy - pad, 0), h - 1), sj = min(max(j + sx - pad, 0), w - 1);
+        out[(size_t)k * C * plane + e] = x[(size_t)k * C * plane + c * plane + (size_t)si * w + sj];
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int tdmpc_random_shift(const float* x, const float* shift, int32_t n, int32_t c, int32_t h, int32_t w, int32_t pad,
+                       float* out, void* stream) {
+    if (!x || !shift || !out) return TDMPC_E_NULL;
+    if (n <= 0 || c <= 0 || h <= 0 || w <= 0 || pad < 0 || (long)c * h * w >= (1L << 31)) return TDMPC_E_DIMS;
+    const int per = c * h * w;
+    hipLaunchKernelGGL(random_shift_kernel, dim3(std::min((per + 255) / 256, 64), n), dim3(256), 0,
+                       (hipStream_t)stream, x, shift, c, h, w, pad, out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        tdmpc_internal::set_error(hipGetErrorString(e));
+        return TDMPC_E_HIP;
+    }
+    return 0;
+}
+
 
 int tdmpc_loss_forward(const tdmpc_loss_args* a, float* rows, float* scal, void* stream) {
     if (!args_ok(a) || !rows || !scal) return TDMPC_E_NULL;

@@ -8,14 +8,14 @@
 // replacement, in rounds (found entries' p zeroed, cdf recomputed, duplicates of a round dropped keeping
 // first occurrences) without. This file does all of it on the device:
 //   rp_pow_kernel     p = powf(prio, alpha) and per-2048-block fp32 sums           (HBM: 4 B read + 4 B write)
-//   rp_total_kernel   S = sum of the block sums (fixed tree order)
-//   rp_scan_kernel    probs = p / S (fp32), float64 inclusive cdf per block         (4 B read, 4 + 8 B write)
+//   rp_scan_kernel    S = sum of the block sums (fixed tree order, recomputed per block), probs = p / S (fp32),
+//                     float64 inclusive cdf per block                               (4 B read, 4 + 8 B write)
 //   rp_offsets_kernel float64 block offsets, last = cdf[-1]
-//   rp_choice_kernel  with replacement: one wave per draw, 64-ary search on cdf/last
-//   rp_norepl_kernel  without replacement: numpy's rounds in one workgroup; the zeroed masses of the found
+//   rp_choice_kernel  with replacement (and round 1 without): one wave per draw, 64-ary search on cdf/last
+//   rp_norepl_kernel  without replacement: numpy's later rounds in one workgroup; the zeroed masses of the found
 //                     entries are subtracted from the cdf instead of recomputing it
-//   rp_weights_kernel (total * probs[idx])**-beta / max
-//   rp_gather_kernel  the H+1-step windows (state rows or pixel frame stacks), episode-end last_obs
+//   rp_gather_kernel  the H+1-step windows (state rows or pixel frame stacks), episode-end last_obs, and the
+//                     importance weights (total * probs[idx])**-beta / max
 // Exactness: the float64 cdf is a sum of float32 values; when every partial sum is exact in float64 (true
 // unless the probabilities span more than ~2^29 in ratio) any summation order -- numpy's sequential one,
 // this blocked scan, or cdf minus the found masses -- gives the same bits, so the chosen indices are
@@ -62,7 +62,9 @@ struct RWork {
     double* boff;    // [nb] float64 block offsets
     double* scal;    // [0] S (sum of p, as float), [1] last = cdf[-1]
     float* part;     // [nb] partial maxima (add_priorities)
-    int64_t* idx;    // [B] chosen indices
+    int64_t* idx;    // [B] chosen indices (without replacement: the first round's draws first)
+    unsigned long long* last;  // [cap] update_priorities: (generation << 32 | position) of the last writer
+    unsigned* gen;   // [1] update_priorities: generation counter
     size_t total;
 };
 
@@ -87,6 +89,8 @@ void make_rwork(const tdmpc_replay_dims* d, char* base, RWork* w) {
     w->scal = (double*)take(64);
     w->part = (float*)take(nb * 4);
     w->idx = (int64_t*)take(B * 8);
+    w->last = (unsigned long long*)take(cap * 8);
+    w->gen = (unsigned*)take(64);
     w->total = o;
 }
 
@@ -121,27 +125,37 @@ __global__ void __launch_bounds__(RT) rp_pow_kernel(const float* prio, int total
     if (t == 0) bsum[blockIdx.x] = red[0];
 }
 
-__global__ void __launch_bounds__(1024) rp_total_kernel(const float* bsum, int nb, double* scal) {
-    __shared__ float red[1024];
-    const int t = threadIdx.x;
-    float s = 0.f;
-    for (int i = t; i < nb; i += 1024) s += bsum[i];
-    red[t] = s;
+// S = sum of the fp32 block sums in a fixed order: slot i < 1024 holds bsum[i] + bsum[i + 1024] + ..., then a
+// halving tree over the 1024 slots. Every scan block recomputes it from the ~nb / 1024 floats (the same bits in each
+// block), so no separate launch is needed between the pow pass and the scan.
+DEVI float total_of(const float* bsum, int nb, float* red, int t) {   // 256 threads, red[256]
+    float v[4];
+    for (int q = 0; q < 4; ++q) {
+        float x = 0.f;
+        for (int i = t + 256 * q; i < nb; i += 1024) x += bsum[i];
+        v[q] = x;
+    }
+    v[0] += v[2];   // tree level 512: slot i += slot i + 512 (i = t, t + 256)
+    v[1] += v[3];
+    red[t] = v[0] + v[1];   // level 256
     __syncthreads();
-    for (int off = 512; off > 0; off >>= 1) {
+    for (int off = 128; off > 0; off >>= 1) {
         if (t < off) red[t] += red[t + off];
         __syncthreads();
     }
-    if (t == 0) scal[0] = (double)red[0];
+    const float S = red[0];
+    __syncthreads();
+    return S;
 }
 
 // probs = p / S (fp32, like `probs /= probs.sum()`), then the float64 inclusive cdf of each 2048-block:
 // 8 elements per thread sequentially, thread totals scanned across the block.
-__global__ void __launch_bounds__(RT) rp_scan_kernel(const float* p, int total, const double* scal, float* probs,
-                                                     float* probs_out, double* cdf, double* btot) {
+__global__ void __launch_bounds__(RT) rp_scan_kernel(const float* p, int total, const float* bsum, int nb,
+                                                     float* probs, float* probs_out, double* cdf, double* btot) {
     __shared__ double ts[RT];
+    __shared__ float red[RT];
     const int t = threadIdx.x, base = blockIdx.x * RB + t * 8;
-    const float S = (float)scal[0];
+    const float S = total_of(bsum, nb, red, t);
     double run = 0.0, loc[8];
     for (int k = 0; k < 8; ++k) {
         const int i = base + k;
@@ -220,9 +234,38 @@ __global__ void __launch_bounds__(64) rp_choice_kernel(const double* cdf, const 
     if (lane == 0) idx[b] = m ? lo + __ffsll(m) - 1 : hi - 1;
 }
 
-// Without replacement (numpy's rounds): one workgroup, one thread per draw of a round. The found set is kept
-// sorted in LDS with float64 prefix sums of its probabilities; cdf' = cdf - (mass of found entries <= i),
-// last' = last - (mass of all found).
+// Ascending bitonic sort of 1024 LDS keys by 1024 threads (callers sync before; returns synced).
+template <typename K>
+DEVI void bitonic1024(K* a, int t) {
+    for (int k = 2; k <= 1024; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const int o = t ^ j;
+            if (o > t) {
+                const K x = a[t], y = a[o];
+                const bool up = (t & k) == 0;
+                if ((x > y) == up) { a[t] = y; a[o] = x; }
+            }
+            __syncthreads();
+        }
+}
+
+// Uniform number k >= n_u of a without-replacement sample whose caller-supplied stream ran out: a splitmix64 hash of
+// the stream's last value and k, as a double in [0, 1) (53 bits). Deterministic, and only reached when numpy's
+// rounds need more than n_u uniforms (n_used then reports the total consumed, > n_u).
+DEVI double extra_uniform(const double* u, int n_u, int k) {
+    unsigned long long z = (unsigned long long)__double_as_longlong(u[n_u - 1]) + 0x9e3779b97f4a7c15ull * (unsigned)(k + 1);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    z ^= z >> 31;
+    return (double)(z >> 11) * 0x1.0p-53;
+}
+
+// Without replacement (numpy's rounds, RandomState.choice(replace=False, p)): round 1 has no found entries, so its
+// draws are rp_choice_kernel's (one wave per draw, in idx on entry); this workgroup keeps their first occurrences and
+// runs the later rounds -- usually zero or one, with a few draws -- itself: one wave per draw, 64-ary search of
+// u < cdf'(i) / last' where cdf' = cdf - (mass of found entries <= i) and last' = last - (mass of all found), the
+// found set kept sorted in LDS with float64 prefix masses. n_used: uniforms consumed; -2 when fewer than B entries
+// have non-zero probability (numpy raises "Fewer non-zero entries in p than size"; idx is then padded with 0).
 __global__ void __launch_bounds__(1024) rp_norepl_kernel(const double* cdf, const double* boff, const double* scal,
                                                          const float* probs, int total, int B, const double* u,
                                                          int n_u, int64_t* idx, int32_t* n_used) {
@@ -231,43 +274,56 @@ __global__ void __launch_bounds__(1024) rp_norepl_kernel(const double* cdf, cons
     __shared__ int order[1024];     // found indices in numpy's output order
     __shared__ int nv[1024];        // this round's draws
     __shared__ int pos[1024];
-    __shared__ int sh[4];
-    const int t = threadIdx.x;
+    __shared__ unsigned long long sk[1024];   // dedupe sort keys
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = blockDim.x >> 6;
     fs[t] = 0x7fffffff;
     int n_uniq = 0, used = 0, nf = 0;
     const double last = scal[1];
     bool ok = true;
+    if (t < B) nv[t] = (int)idx[t];   // round 1 (rp_choice_kernel)
     __syncthreads();
-    while (n_uniq < B) {
+    for (int round = 0; n_uniq < B; ++round) {
         const int m = B - n_uniq;
-        if (used + m > n_u) { ok = false; break; }
         const double lastp = last - (nf ? fm[nf - 1] : 0.0);
-        if (t < m) {
-            const double x = u[used + t];
-            int lo = 0, hi = total;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                // found mass at or below mid: fm of the last found index <= mid
-                int a = 0, bnd = nf;
-                while (a < bnd) {
-                    const int c = (a + bnd) >> 1;
-                    if (fs[c] <= mid) a = c + 1; else bnd = c;
+        if (round > 0) {
+            if (!(lastp > 0.0)) { ok = false; break; }   // every entry with mass is found already
+            for (int j = wave; j < m; j += nw) {
+                const int k = used + j;
+                const double x = k < n_u ? u[k] : extra_uniform(u, n_u, k);
+                int lo = 0, hi = total;   // answer in [lo, hi): the first i with x < cdf'(i) / last'
+                while (hi > lo) {
+                    const int len = hi - lo, step = (len + 63) / 64;
+                    const int i = min(lo + (lane + 1) * step - 1, hi - 1);
+                    int a = 0, bnd = nf;   // found entries <= i
+                    while (a < bnd) {
+                        const int c = (a + bnd) >> 1;
+                        if (fs[c] <= i) a = c + 1; else bnd = c;
+                    }
+                    const bool pred = x < (cdf_at(cdf, boff, i) - (a ? fm[a - 1] : 0.0)) / lastp;
+                    const unsigned long long bm = __ballot(pred);
+                    if (step == 1) {   // the probes were lo .. hi - 1 themselves
+                        lo = bm ? lo + __ffsll(bm) - 1 : hi - 1;
+                        break;
+                    }
+                    const int l = bm ? __ffsll(bm) - 1 : 63;
+                    const int il = min(lo + (l + 1) * step - 1, hi - 1);
+                    lo = l ? min(lo + l * step - 1, hi - 1) + 1 : lo;
+                    hi = il + 1;
                 }
-                const double cm = cdf_at(cdf, boff, mid) - (a ? fm[a - 1] : 0.0);
-                if (x < cm / lastp) hi = mid; else lo = mid + 1;
+                if (lane == 0) nv[j] = min(lo, total - 1);
             }
-            nv[t] = min(lo, total - 1);
         }
+        used += m;
         __syncthreads();
-        // keep the first occurrence of each value (np.unique(return_index) + sort), in draw order
-        int keep = 0;
-        if (t < m) {
-            keep = 1;
-            for (int s = 0; s < t; ++s)
-                if (nv[s] == nv[t]) { keep = 0; break; }
-        }
-        pos[t] = keep;
+        // keep the first occurrence of each value (np.unique(return_index) + sort), in draw order: bitonic sort
+        // of (value, draw) keys, a draw is kept when the key before it has another value
+        sk[t] = t < m ? ((unsigned long long)(unsigned)nv[t] << 32) | (unsigned)t : ~0ull;
+        pos[t] = 0;
         __syncthreads();
+        bitonic1024(sk, t);
+        if (t < m && (t == 0 || (sk[t - 1] >> 32) != (sk[t] >> 32))) pos[(int)(sk[t] & 0xffffffffu)] = 1;
+        __syncthreads();
+        const int keep = pos[t];
         for (int off = 1; off < 1024; off <<= 1) {
             const int add = t >= off ? pos[t - off] : 0;
             __syncthreads();
@@ -281,19 +337,10 @@ __global__ void __launch_bounds__(1024) rp_norepl_kernel(const double* cdf, cons
         }
         __syncthreads();
         n_uniq += kept;
-        used += m;
         nf += kept;
+        if (n_uniq >= B) break;
         // re-sort the found set (bitonic over 1024 slots) and rebuild its prefix masses
-        for (int k = 2; k <= 1024; k <<= 1)
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                const int o = t ^ j;
-                if (o > t) {
-                    const int a = fs[t], b = fs[o];
-                    const bool up = (t & k) == 0;
-                    if ((a > b) == up) { fs[t] = b; fs[o] = a; }
-                }
-                __syncthreads();
-            }
+        bitonic1024(fs, t);
         // prefix masses of the sorted found set (float64 block scan)
         fm[t] = t < nf ? (double)probs[fs[t]] : 0.0;
         __syncthreads();
@@ -305,28 +352,7 @@ __global__ void __launch_bounds__(1024) rp_norepl_kernel(const double* cdf, cons
         }
     }
     if (t < B) idx[t] = t < n_uniq ? order[t] : 0;
-    if (t == 0 && n_used) *n_used = ok ? used : -1;
-    (void)sh;
-}
-
-// ------------------------------------------------------------------------------------------------ weights
-__global__ void __launch_bounds__(1024) rp_weights_kernel(const int64_t* idx, const float* probs, int total, int B,
-                                                          float beta, int64_t* idxs_out, float* weights) {
-    __shared__ float red[1024];
-    const int t = threadIdx.x;
-    float w = 0.f;
-    if (t < B) {
-        const int64_t i = idx[t];
-        w = powf(__fmul_rn((float)total, probs[i]), -beta);
-        idxs_out[t] = i;
-    }
-    red[t] = t < B ? w : -INFINITY;
-    __syncthreads();
-    for (int off = 512; off > 0; off >>= 1) {
-        if (t < off) red[t] = nanmax(red[t], red[t + off]);
-        __syncthreads();
-    }
-    if (t < B) weights[t] = __fdiv_rn(w, red[0]);
+    if (t == 0 && n_used) *n_used = ok ? used : -2;
 }
 
 // ------------------------------------------------------------------------------------------------ gather
@@ -334,6 +360,8 @@ struct GatherArgs {
     int modality, F, S, fs, A, L, H, B;
     const void* obs; const void* last_obs; const float* action; const float* reward;
     const int64_t* idx;
+    // importance weights (helper.py:518-519): weights[b] = (total * probs[idx[b]])**-beta / max over the batch
+    const float* probs; int total; float beta; int64_t* idx_out; float* weights;
     float* o_obs; float* o_next; float* o_action; float* o_reward;
 };
 
@@ -360,6 +388,21 @@ __global__ void __launch_bounds__(256) rp_gather_kernel(const GatherArgs a) {
     const long i = a.idx[b];
     const int F = a.modality == 0 ? a.F : a.fs * 3 * a.S * a.S;
     if (y == 0) {
+        // the batch's largest weight (torch.max keeps NaN), recomputed by each row's block (B powf's from L2)
+        __shared__ float red[256];
+        const int t = threadIdx.x;
+        float m = -INFINITY;
+        for (int k = t; k < a.B; k += 256) m = nanmax(m, powf(__fmul_rn((float)a.total, a.probs[a.idx[k]]), -a.beta));
+        red[t] = m;
+        __syncthreads();
+        for (int off = 128; off > 0; off >>= 1) {
+            if (t < off) red[t] = nanmax(red[t], red[t + off]);
+            __syncthreads();
+        }
+        if (t == 0) {
+            a.weights[b] = __fdiv_rn(powf(__fmul_rn((float)a.total, a.probs[i]), -a.beta), red[0]);
+            a.idx_out[b] = i;
+        }
         stacked_obs(a, i, a.o_obs + (size_t)b * F);
         return;
     }
@@ -415,16 +458,28 @@ __global__ void __launch_bounds__(1024) rp_add_prio_kernel(float* prio, const fl
     for (int k = t; k < L; k += 1024) prio[idx + k] = k >= L - H ? 0.f : maxp;
 }
 
-// p[idxs[i]] = v[i] + eps; with duplicate indices the LAST occurrence wins, like a sequential index_put_
-// (the reference's CPU semantics; its GPU index_put_ leaves the winner unspecified)
-__global__ void rp_update_kernel(float* prio, const int64_t* idxs, const float* v, int n, float eps) {
+// p[idxs[i]] = v[i] + eps; with duplicate indices the LAST occurrence wins, like a sequential index_put_ (the
+// reference's CPU semantics; its GPU index_put_ leaves the winner unspecified). Last-writer-wins in O(n): every
+// position i posts (generation << 32 | i) to last[idxs[i]] with a 64-bit atomicMax; the position that finds its own
+// key there writes. The generation (a device counter bumped after each call) makes older calls' keys smaller, so
+// `last` never needs clearing (it starts zeroed with the workspace).
+__global__ void rp_update_post_kernel(unsigned long long* last, const unsigned* gen, const int64_t* idxs, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const int64_t k = idxs[i];
-    for (int j = i + 1; j < n; ++j)
-        if (idxs[j] == k) return;
-    prio[k] = __fadd_rn(v[i], eps);
+    const unsigned long long key = ((unsigned long long)(*gen + 1u) << 32) | (unsigned)i;
+    atomicMax(last + idxs[i], key);
 }
+
+__global__ void rp_update_write_kernel(float* prio, const unsigned long long* last, const unsigned* gen,
+                                       const int64_t* idxs, const float* v, int n, float eps) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long key = ((unsigned long long)(*gen + 1u) << 32) | (unsigned)i;
+    const int64_t k = idxs[i];
+    if (last[k] == key) prio[k] = __fadd_rn(v[i], eps);
+}
+
+__global__ void rp_update_bump_kernel(unsigned* gen) { *gen += 1u; }
 
 }  // namespace
 
@@ -458,12 +513,22 @@ int tdmpc_replay_add_priorities(const tdmpc_replay_dims* d, float* prio, int32_t
 }
 
 int tdmpc_replay_update_priorities(const tdmpc_replay_dims* d, float* prio, const int64_t* idxs,
-                                   const float* values, int32_t n, float eps, void* stream) {
-    if (!d || !prio || !idxs || !values) return TDMPC_E_NULL;
+                                   const float* values, int32_t n, float eps, void* ws, size_t ws_bytes,
+                                   void* stream) {
+    if (!d || !prio || !idxs || !values || !ws) return TDMPC_E_NULL;
     if (!dims_ok(d) || n < 0) return TDMPC_E_DIMS;
+    RWork w;
+    make_rwork(d, nullptr, &w);
+    if (ws_bytes < w.total) return TDMPC_E_SIZE;
+    make_rwork(d, (char*)ws, &w);
     if (!n) return 0;
-    hipLaunchKernelGGL(rp_update_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, prio, idxs,
-                       values, n, eps);
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid((n + 255) / 256);
+    hipLaunchKernelGGL(rp_update_post_kernel, grid, dim3(256), 0, s, w.last, w.gen, idxs, n);
+    RCHK(hipGetLastError());
+    hipLaunchKernelGGL(rp_update_write_kernel, grid, dim3(256), 0, s, prio, w.last, w.gen, idxs, values, n, eps);
+    RCHK(hipGetLastError());
+    hipLaunchKernelGGL(rp_update_bump_kernel, dim3(1), dim3(1), 0, s, w.gen);
     RCHK(hipGetLastError());
     return 0;
 }
@@ -485,26 +550,24 @@ int tdmpc_replay_sample(const tdmpc_replay_dims* d, const tdmpc_replay_store* st
     const int nb = (total + RB - 1) / RB;
     hipLaunchKernelGGL(rp_pow_kernel, dim3(nb), dim3(RT), 0, s, st->priorities, total, alpha, w.p, w.bsum);
     RCHK(hipGetLastError());
-    hipLaunchKernelGGL(rp_total_kernel, dim3(1), dim3(1024), 0, s, w.bsum, nb, w.scal);
-    RCHK(hipGetLastError());
-    hipLaunchKernelGGL(rp_scan_kernel, dim3(nb), dim3(RT), 0, s, w.p, total, w.scal, w.probs, probs_out, w.cdf, w.btot);
+    hipLaunchKernelGGL(rp_scan_kernel, dim3(nb), dim3(RT), 0, s, w.p, total, w.bsum, nb, w.probs, probs_out, w.cdf,
+                       w.btot);
     RCHK(hipGetLastError());
     hipLaunchKernelGGL(rp_offsets_kernel, dim3(1), dim3(1024), 0, s, w.btot, nb, w.boff, w.scal);
     RCHK(hipGetLastError());
-    if (!full) {
-        hipLaunchKernelGGL(rp_choice_kernel, dim3(B), dim3(64), 0, s, w.cdf, w.boff, w.scal, total, u, w.idx, n_used);
-        RCHK(hipGetLastError());
-    } else {
+    // round 1 of both forms: one wave per draw
+    hipLaunchKernelGGL(rp_choice_kernel, dim3(B), dim3(64), 0, s, w.cdf, w.boff, w.scal, total, u, w.idx, n_used);
+    RCHK(hipGetLastError());
+    if (full) {
         hipLaunchKernelGGL(rp_norepl_kernel, dim3(1), dim3(1024), 0, s, w.cdf, w.boff, w.scal, w.probs, total, B, u,
                            n_u, w.idx, n_used);
         RCHK(hipGetLastError());
     }
-    hipLaunchKernelGGL(rp_weights_kernel, dim3(1), dim3(1024), 0, s, w.idx, w.probs, total, B, beta, idxs, weights);
-    RCHK(hipGetLastError());
     GatherArgs g;
     g.modality = d->modality; g.F = d->obs_dim; g.S = d->img_hw; g.fs = d->frame_stack; g.A = d->action_dim;
     g.L = d->episode_length; g.H = d->horizon; g.B = B;
-    g.obs = st->obs; g.last_obs = st->last_obs; g.action = st->action; g.reward = st->reward; g.idx = idxs;
+    g.obs = st->obs; g.last_obs = st->last_obs; g.action = st->action; g.reward = st->reward; g.idx = w.idx;
+    g.probs = w.probs; g.total = total; g.beta = beta; g.idx_out = idxs; g.weights = weights;
     g.o_obs = obs; g.o_next = next_obs; g.o_action = action; g.o_reward = reward;
     hipLaunchKernelGGL(rp_gather_kernel, dim3(B, d->horizon + 2), dim3(256), 0, s, g);
     RCHK(hipGetLastError());

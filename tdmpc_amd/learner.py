@@ -33,34 +33,39 @@ METRICS = ("consistency_loss", "reward_loss", "value_loss", "pi_loss", "total_lo
 
 
 class RandomShiftsAug(torch.nn.Module):
-    """helper.py:250-283: random-shift augmentation of pixel observations (identity for state)."""
+    """helper.py:250-283: random-shift augmentation of pixel observations (identity for state). The shifts are
+    drawn exactly as the reference draws them (one torch.randint of [n, 1, 1, 2] on the input's device, so the
+    generator advances identically); the shift itself runs as one HIP gather kernel (tdmpc_random_shift,
+    include/tdmpc_learner.h): the reference's pad + grid_sample lands on integer pixel centres, so it is a
+    clamped-index copy (tests/test_learner.py holds it to the reference's outputs)."""
 
     def __init__(self, cfg):
         super().__init__()
         self.pad = int(cfg.img_size / 21) if cfg.modality == "pixels" else None
 
-    def forward(self, x):
+    def forward(self, x, shift=None):
+        """shift: optional explicit [n, 2] (x, y) integer shifts instead of the draw (parity tests)."""
         if not self.pad:
             return x
-        shape_len = len(x.size())
-        if shape_len == 5:
-            t, n, c, hh, ww = x.size()
-            x = x.reshape(t * n, c, hh, ww)
-        n_stacked, c, hh, ww = x.size()
-        padding = tuple([self.pad] * 4)
-        x = F.pad(x, padding, "replicate")
-        eps = 1.0 / (hh + 2 * self.pad)
-        arange = torch.linspace(-1.0 + eps, 1.0 - eps, hh + 2 * self.pad, device=x.device, dtype=x.dtype)[:hh]
-        arange = arange.unsqueeze(0).repeat(hh, 1).unsqueeze(2)
-        base_grid = torch.cat([arange, arange.transpose(1, 0)], dim=2)
-        base_grid = base_grid.unsqueeze(0).repeat(n_stacked, 1, 1, 1)
-        shift = torch.randint(0, 2 * self.pad + 1, size=(n_stacked, 1, 1, 2), device=x.device, dtype=x.dtype)
-        shift *= 2.0 / (hh + 2 * self.pad)
-        grid = base_grid + shift
-        shifted = F.grid_sample(x, grid, padding_mode="zeros", align_corners=False)
-        if shape_len == 5:
-            shifted = shifted.reshape(t, n, c, hh, ww)
-        return shifted
+        from . import _lib
+        shape = x.shape
+        if x.dim() == 5:
+            x = x.reshape(shape[0] * shape[1], *shape[2:])   # the same shift for a trajectory's frames
+        n, c, hh, ww = x.shape
+        if hh != ww or not x.is_cuda or x.dtype != torch.float32:
+            raise ValueError("RandomShiftsAug: square float32 frames on the GPU")
+        if shift is None:
+            shift = torch.randint(0, 2 * self.pad + 1, size=(n, 1, 1, 2), device=x.device, dtype=x.dtype)
+        else:
+            shift = torch.as_tensor(shift, dtype=torch.float32).to(x.device).reshape(n, 1, 1, 2)
+        x = x.contiguous()
+        out = torch.empty_like(x)
+        L = _lib.lib()
+        _lib.check(L.tdmpc_random_shift(C.c_void_p(x.data_ptr()), C.c_void_p(shift.data_ptr()), n, c, hh, ww,
+                                        self.pad, C.c_void_p(out.data_ptr()),
+                                        C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)),
+                   "tdmpc_random_shift")
+        return out.reshape(shape)
 
 
 class _FusedLoss(torch.autograd.Function):

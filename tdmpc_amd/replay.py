@@ -62,7 +62,7 @@ class ReplayBuffer:
         ws = self._L.tdmpc_replay_workspace_bytes(C.byref(d))
         if ws == 0:
             raise ValueError("unsupported replay buffer dims")
-        self._ws = torch.empty(ws, dtype=torch.uint8, device=dev)
+        self._ws = torch.zeros(ws, dtype=torch.uint8, device=dev)   # zero-filled once (update_priorities' keys)
         B, H = self.batch_size, self.horizon
         obs_shape = tuple(cfg.obs_shape)
         self._out_idx = torch.empty(B, dtype=torch.int64, device=dev)
@@ -107,8 +107,9 @@ class ReplayBuffer:
             raise ValueError("priorities and idxs differ in length")
         _lib.check(self._L.tdmpc_replay_update_priorities(
             C.byref(self._dims), C.c_void_p(self._priorities.data_ptr()), C.c_void_p(idxs.data_ptr()),
-            C.c_void_p(vals.data_ptr()), idxs.numel(), C.c_float(self._eps), self._stream()),
-            "tdmpc_replay_update_priorities")
+            C.c_void_p(vals.data_ptr()), idxs.numel(), C.c_float(self._eps), C.c_void_p(self._ws.data_ptr()),
+            self._ws.numel(), self._stream()), "tdmpc_replay_update_priorities")
+        self._keep_upd = (idxs, vals)   # read asynchronously by the kernels
 
     def sample(self, u=None, keep_probs: bool = False):
         """helper.py:504-528 -> (obs, next_obs, action, reward [H+1, B, 1], idxs, weights). The returned
@@ -137,5 +138,12 @@ class ReplayBuffer:
 
     @property
     def uniforms_used(self) -> int:
-        """Uniforms the last sample consumed (-1: the supplied stream ran out). Synchronises."""
+        """Uniforms the last sample consumed (> the supplied count: the rounds continued on the hash stream;
+        -2: fewer than batch_size non-zero priorities without replacement). Synchronises."""
         return int(self._n_used.item())
+
+    def check_sample(self):
+        """Raise like the reference's np.random.choice(replace=False) when the last sample could not find
+        batch_size distinct non-zero-probability transitions (device flag; synchronises)."""
+        if self.uniforms_used == -2:
+            raise ValueError("Fewer non-zero entries in p than size")

@@ -161,25 +161,64 @@ def test_cpu_batched_learner_matches_oracle():
         _params_close(agent.model_target.state_dict(), sdt, cfg.lr)
 
 
-def test_random_shifts_aug_matches_reference():
-    """tdmpc_amd.learner.RandomShiftsAug (helper.py:250-283) against the reference module's outputs on the same
-    frames and torch seed (tests/golden/learner_aug_pixels.npz, make_aug_golden.py): 4-D and 5-D (horizon) batches."""
-    from types import SimpleNamespace
-    from tdmpc_amd.learner import RandomShiftsAug
+AUG_ATOL = 2.5e-3   # the reference's fp32 grid coordinates sit within ~1e-5 px of the pixel centres
+
+
+def _aug_golden():
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "learner_aug_pixels.npz"))
-    aug = RandomShiftsAug(SimpleNamespace(img_size=84, modality="pixels"))
     for k in ("4", "5"):
-        torch.manual_seed(11)
-        y = aug(torch.from_numpy(g["x" + k].astype(np.float32))).numpy()
-        assert np.array_equal(y, g["y" + k]), k
+        x = g["x" + k].astype(np.float32)
+        n = x.shape[0] * x.shape[1] if x.ndim == 5 else x.shape[0]
+        torch.manual_seed(11)   # the reference's draw in make_aug_golden.py
+        shift = torch.randint(0, 9, size=(n, 1, 1, 2), dtype=torch.float32).view(n, 2).numpy()
+        yield k, x, g["y" + k], shift
+
+
+def test_random_shift_oracle_matches_reference():
+    """oracle.learner_ref.random_shift (the integer-shift restatement of RandomShiftsAug, helper.py:250-283) against
+    the reference module's recorded outputs (tests/golden/learner_aug_pixels.npz, make_aug_golden.py): 4-D and 5-D
+    (horizon) batches, within AUG_ATOL."""
+    from oracle.learner_ref import random_shift
+    for k, x, y, shift in _aug_golden():
+        xs = x.reshape(-1, *x.shape[-3:])
+        r = random_shift(xs, shift, 4).reshape(y.shape)
+        assert np.abs(r - y).max() <= AUG_ATOL, k
+
+
+@pytest.mark.gpu
+def test_gpu_random_shifts_aug_matches_reference():
+    """tdmpc_amd.learner.RandomShiftsAug on the device (tdmpc_random_shift gather kernel): same torch draw as the
+    reference module, output equal to the oracle's integer shift bitwise and within AUG_ATOL of the reference's
+    recorded outputs, 4-D and 5-D batches."""
+    from types import SimpleNamespace
+    from oracle.learner_ref import random_shift
+    from tdmpc_amd.learner import RandomShiftsAug
+    aug = RandomShiftsAug(SimpleNamespace(img_size=84, modality="pixels"))
+    for k, x, y, shift in _aug_golden():
+        # the golden's shifts came from the CPU generator (make_aug_golden.py); on the GPU the module draws from
+        # torch's CUDA generator with the reference's call (shape, dtype, device), checked below
+        out = aug(torch.from_numpy(x).cuda(), shift=shift).cpu().numpy()
+        assert out.shape == y.shape
+        assert np.abs(out - y).max() <= AUG_ATOL, k
+        xs = x.reshape(-1, *x.shape[-3:])
+        assert np.array_equal(out.reshape(xs.shape), random_shift(xs, shift, 4)), k
+        n = xs.shape[0]
+        torch.manual_seed(12)
+        out = aug(torch.from_numpy(x).cuda()).cpu().numpy()
+        torch.manual_seed(12)
+        drawn = torch.randint(0, 9, size=(n, 1, 1, 2), device="cuda", dtype=torch.float32).view(n, 2).cpu().numpy()
+        assert np.array_equal(out.reshape(xs.shape), random_shift(xs, drawn, 4)), k
 
 
 @pytest.mark.gpu
 def test_gpu_pixel_update_graph_equals_eager():
     """Pixel TOLD (quadruped frames, conv encoder, RandomShiftsAug on the device): 4 updates from a fixed batch,
     3 eager warm-ups + 1 graph replay vs 4 eager updates; metrics finite. Not bitwise: MIOpen's convolution
-    backward (the encoder's weight gradient) may sum in a different order between calls, so the comparison is
-    at the learner tolerance (rtol 2e-5 on the metrics, parameters within 1e-6 + 1e-4 |x|)."""
+    backward (the encoder's weight gradient) may sum in a different order between calls (deterministic mode is
+    requested, not guaranteed), and Adam turns a last-bit gradient difference on a ~0 gradient into a step of up
+    to lr, which the next update's losses see. So: the first update's metrics at rtol 2e-5, the later ones at
+    rtol 2e-3, parameters as the learner parity tests (_params_close: <= 2 lr everywhere, 1e-6 + 1e-4 |x| on
+    99.9 % of the elements)."""
     from tdmpc_amd.config import make_cfg
     from tdmpc_amd.tdmpc import TDMPC
     cfg = make_cfg("quadruped", modality="pixels", num_samples=32, num_elites=8, iterations=2, horizon=3,
@@ -197,6 +236,8 @@ def test_gpu_pixel_update_graph_equals_eager():
         graph_safe, idx, _full = True, 0, False
 
     outs = []
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
     for warm in (3, 100):
         agent = TDMPC(cfg)
         agent.model.load_state_dict(synthetic_state_dict(cfg, 4))
@@ -206,12 +247,13 @@ def test_gpu_pixel_update_graph_equals_eager():
         torch.manual_seed(9)
         ms = [agent.update(buf, s + 1, sync_metrics=False).clone() for s in range(4)]
         outs.append((agent, torch.stack(ms)))
+    torch.backends.cudnn.deterministic = det
     (a1, m1), (a2, m2) = outs
     assert a1.learner()._graphs and not a2.learner()._graphs
     assert torch.isfinite(m1).all()
-    torch.testing.assert_close(m1, m2, rtol=2e-5, atol=1e-6)
-    for x, y in zip(a1.model.parameters(), a2.model.parameters()):
-        torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(m1[0], m2[0], rtol=2e-5, atol=1e-6)
+    torch.testing.assert_close(m1, m2, rtol=2e-3, atol=1e-5)
+    _params_close(a1.model.state_dict(), {k: v.cpu() for k, v in a2.model.state_dict().items()}, cfg.lr)
 
 
 @pytest.mark.gpu

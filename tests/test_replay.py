@@ -142,3 +142,73 @@ def test_gpu_choice_large_buffer(full):
     st = buf._obs.cpu()
     assert torch.equal(obs.cpu(), st[idxs.cpu()])
     assert torch.equal(next_obs[2].cpu(), st[idxs.cpu() + 3])
+
+
+def _big_buffer(full, cap=250_000, L=500):
+    from types import SimpleNamespace
+    from tdmpc_amd.replay import ReplayBuffer
+    c = SimpleNamespace(modality="state", obs_shape=(67,), action_dim=21, episode_length=L, capacity=cap,
+                        batch_size=512, horizon=5, per_alpha=0.6, per_beta=0.4, frame_stack=1)
+    buf = ReplayBuffer(_gpu_cfg(c), latent_plan=True)
+    rs = np.random.RandomState(1)
+    ep = _Ep(rs.standard_normal((L + 1, 67)).astype(np.float32), rs.uniform(-1, 1, (L, 21)).astype(np.float32),
+             rs.standard_normal(L).astype(np.float32))
+    for _ in range(cap // L if full else cap // L // 2):
+        buf.add(ep)
+    return buf
+
+
+@pytest.mark.gpu
+def test_gpu_update_priorities_last_writer_wins():
+    """helper.py:487-488 with duplicate indices, at the bench's size (50k updates): the last occurrence wins,
+    as a sequential index_put_ on the CPU; repeated calls (generation-tagged keys, never cleared) included."""
+    buf = _big_buffer(False)
+    total = buf.idx
+    rs = np.random.RandomState(5)
+    ref = buf._priorities.cpu().numpy().copy()
+    for n, span in ((50_000, 3000), (700, 50), (50_000, total)):
+        idx = rs.randint(0, span, size=n)
+        v = rs.exponential(1.0, size=(n, 1)).astype(np.float32)
+        buf.update_priorities(torch.from_numpy(idx), torch.from_numpy(v))
+        for i, k in enumerate(idx):   # the reference's CPU index_put_: sequential
+            ref[k] = np.float32(v[i, 0] + np.float32(1e-6))
+        assert np.array_equal(buf._priorities.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+def test_gpu_norepl_concentrated_priorities():
+    """Without replacement on a full buffer whose mass sits on a few hundred transitions (one of them 1e6 times
+    the rest): several of numpy's rounds, each after zeroing the found masses -- the device's picks equal the
+    oracle's choice on the device's probabilities and the same uniforms, and the uniforms consumed agree."""
+    buf = _big_buffer(True)
+    rs = np.random.RandomState(2)
+    buf._priorities.zero_()
+    hot = rs.choice(buf.capacity, 700, replace=False)
+    p = rs.exponential(1.0, size=700).astype(np.float32)
+    p[0] = 1e6
+    buf.update_priorities(torch.from_numpy(hot), torch.from_numpy(p[:, None]))
+    u = rs.random_sample(64 * 512)
+    *_, idxs, weights = buf.sample(u=u, keep_probs=True)
+    probs = buf.last_probs.cpu().numpy()
+    want, used = choice(probs, 512, False, u)
+    assert np.array_equal(idxs.cpu().numpy(), want)
+    assert buf.uniforms_used == used and used > 512   # more than one round
+    # the same with only batch_size uniforms: the rounds continue on the hash stream, still distinct picks
+    *_, idxs, _ = buf.sample(u=u[:512])
+    got = idxs.cpu().numpy()
+    assert len(set(got.tolist())) == 512 and (probs[got] > 0).all() and buf.uniforms_used > 512
+    buf.check_sample()
+
+
+@pytest.mark.gpu
+def test_gpu_norepl_fewer_nonzero_than_batch_raises():
+    """numpy's choice(replace=False) raises when fewer than `size` entries have mass; the device flags it and
+    check_sample() raises the same ValueError."""
+    buf = _big_buffer(True)
+    buf._priorities.zero_()
+    hot = torch.arange(0, 300, dtype=torch.int64) * 7
+    buf.update_priorities(hot, torch.ones(300, 1))
+    *_, idxs, _ = buf.sample()
+    with pytest.raises(ValueError, match="Fewer non-zero"):
+        buf.check_sample()
+    assert set(idxs.cpu().numpy().tolist()[:300]) == set(hot.tolist())
