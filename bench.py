@@ -188,7 +188,20 @@ def replay_bench(cfg, dev, cpu=True, reps=200):
         for _ in range(reps):
             buf.sample()
         torch.cuda.synchronize()
-        dt = (time.perf_counter() - t) / reps
+        dt_eager = (time.perf_counter() - t) / reps
+        # as the learner runs it: captured in its HIP graph (device time, no per-call host launch cost)
+        g = torch.cuda.CUDAGraph()
+        per = 20
+        with torch.cuda.graph(g):
+            for _ in range(per):
+                buf.sample()
+        g.replay()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(reps // per):
+            g.replay()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / (reps // per * per)
         key = "without_replacement" if full else "with_replacement"
         if not full:
             # update_priorities at the learner's write-back size and at 50k (helper.py:487-488; duplicates: last wins)
@@ -208,6 +221,9 @@ def replay_bench(cfg, dev, cpu=True, reps=200):
         # algorithmic HBM bytes: priorities read, p**alpha write + read, probs write, float64 cdf write, window gather
         alg = total * (4 + 8 + 4 + 8) + B * (H + 2) * (obs_dim + A + 1) * 4
         out[key] = {"value": round(1.0 / dt, 1), "unit": "samples/s", "us_per_sample": round(dt * 1e6, 2),
+                    "us_per_sample_eager": round(dt_eager * 1e6, 2),
+                    "note": "sample() (device uniforms included) replayed from a HIP graph of 20 samples, as the "
+                            "learner's captured update runs it; eager = one Python call per sample",
                     "total": total, "hbm_gbs_algorithmic": round(alg / dt / 1e9, 1)}
         if cpu:
             from oracle.replay_ref import RefReplay

@@ -234,19 +234,43 @@ __global__ void __launch_bounds__(64) rp_choice_kernel(const double* cdf, const 
     if (lane == 0) idx[b] = m ? lo + __ffsll(m) - 1 : hi - 1;
 }
 
-// Ascending bitonic sort of 1024 LDS keys by 1024 threads (callers sync before; returns synced).
+// Ascending bitonic sort of 1024 keys, one per thread of a 1024-thread block, returned in the thread's register
+// (thread t holds the t-th smallest). Partner distances below 64 run in the wave (xor shuffles, no barrier); only
+// the 10 steps with j >= 64 go through LDS (`buf`, 1024 keys).
 template <typename K>
-DEVI void bitonic1024(K* a, int t) {
+DEVI K bitonic1024(K v, K* buf, int t) {
     for (int k = 2; k <= 1024; k <<= 1)
         for (int j = k >> 1; j > 0; j >>= 1) {
-            const int o = t ^ j;
-            if (o > t) {
-                const K x = a[t], y = a[o];
-                const bool up = (t & k) == 0;
-                if ((x > y) == up) { a[t] = y; a[o] = x; }
+            K o;
+            if (j >= 64) {
+                buf[t] = v;
+                __syncthreads();
+                o = buf[t ^ j];
+                __syncthreads();
+            } else {
+                o = __shfl_xor(v, j, 64);
             }
-            __syncthreads();
+            const bool lower = (t & j) == 0, up = (t & k) == 0;
+            // the lower partner keeps the min when ascending, the max when descending
+            v = (lower == up) ? (o < v ? o : v) : (o < v ? v : o);
         }
+    return v;
+}
+
+// Inclusive prefix sum over a 1024-thread block: wave scans by shuffles, then the 16 wave totals (2 barriers).
+template <typename T>
+DEVI T block_scan1024(T v, T* wsum, int t) {
+    const int lane = t & 63, w = t >> 6;
+    for (int o = 1; o < 64; o <<= 1) {
+        const T u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    if (lane == 63) wsum[w] = v;
+    __syncthreads();
+    T add = 0;
+    for (int i = 0; i < w; ++i) add += wsum[i];
+    __syncthreads();
+    return v + add;
 }
 
 // Uniform number k >= n_u of a without-replacement sample whose caller-supplied stream ran out: a splitmix64 hash of
@@ -264,19 +288,25 @@ DEVI double extra_uniform(const double* u, int n_u, int k) {
 // draws are rp_choice_kernel's (one wave per draw, in idx on entry); this workgroup keeps their first occurrences and
 // runs the later rounds -- usually zero or one, with a few draws -- itself: one wave per draw, 64-ary search of
 // u < cdf'(i) / last' where cdf' = cdf - (mass of found entries <= i) and last' = last - (mass of all found), the
-// found set kept sorted in LDS with float64 prefix masses. n_used: uniforms consumed; -2 when fewer than B entries
-// have non-zero probability (numpy raises "Fewer non-zero entries in p than size"; idx is then padded with 0).
+// found set kept sorted in LDS with float64 prefix masses. First occurrences per round (np.unique(return_index))
+// come from an LDS hash set; the found set is re-sorted only when another round follows (a draw never repeats a
+// found entry: those have no mass left). n_used: uniforms consumed;
+// -2 when fewer than B entries have non-zero probability (numpy raises "Fewer non-zero entries in p than size";
+// idx is then padded with 0).
 __global__ void __launch_bounds__(1024) rp_norepl_kernel(const double* cdf, const double* boff, const double* scal,
                                                          const float* probs, int total, int B, const double* u,
                                                          int n_u, int64_t* idx, int32_t* n_used) {
-    __shared__ int fs[1024];        // found indices, sorted ascending (INT_MAX padding)
+    __shared__ int fs[1024];        // found indices, sorted ascending, [0, nf)
     __shared__ double fm[1024];     // fm[k] = mass of fs[0..k]
     __shared__ int order[1024];     // found indices in numpy's output order
     __shared__ int nv[1024];        // this round's draws
-    __shared__ int pos[1024];
-    __shared__ unsigned long long sk[1024];   // dedupe sort keys
+    __shared__ int newv[1024];      // this round's new found values
+    __shared__ int hkey[2048];      // hash set of the round's values
+    __shared__ int hpos[2048];      // smallest draw position per value
+    __shared__ int sk[1024];        // sort exchange buffer
+    __shared__ int iws[16];
+    __shared__ double dws[16];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = blockDim.x >> 6;
-    fs[t] = 0x7fffffff;
     int n_uniq = 0, used = 0, nf = 0;
     const double last = scal[1];
     bool ok = true;
@@ -312,44 +342,45 @@ __global__ void __launch_bounds__(1024) rp_norepl_kernel(const double* cdf, cons
                 }
                 if (lane == 0) nv[j] = min(lo, total - 1);
             }
+            __syncthreads();
         }
         used += m;
+        // first occurrences (np.unique(return_index)): an LDS hash set of the round's values, each slot keeping
+        // the smallest draw position that holds its value
+        hkey[t] = -1; hkey[t + 1024] = -1;
+        hpos[t] = 0x7fffffff; hpos[t + 1024] = 0x7fffffff;
         __syncthreads();
-        // keep the first occurrence of each value (np.unique(return_index) + sort), in draw order: bitonic sort
-        // of (value, draw) keys, a draw is kept when the key before it has another value
-        sk[t] = t < m ? ((unsigned long long)(unsigned)nv[t] << 32) | (unsigned)t : ~0ull;
-        pos[t] = 0;
-        __syncthreads();
-        bitonic1024(sk, t);
-        if (t < m && (t == 0 || (sk[t - 1] >> 32) != (sk[t] >> 32))) pos[(int)(sk[t] & 0xffffffffu)] = 1;
-        __syncthreads();
-        const int keep = pos[t];
-        for (int off = 1; off < 1024; off <<= 1) {
-            const int add = t >= off ? pos[t - off] : 0;
-            __syncthreads();
-            pos[t] += add;
-            __syncthreads();
-        }
-        const int kept = pos[1023];
-        if (keep) {
-            order[n_uniq + pos[t] - 1] = nv[t];
-            fs[nf + pos[t] - 1] = nv[t];
+        int slot = 0;
+        if (t < m) {
+            const int v = nv[t];
+            slot = (int)(((unsigned)v * 2654435761u) >> 21);   // 11 bits
+            while (true) {
+                const int old = atomicCAS(&hkey[slot], -1, v);
+                if (old == -1 || old == v) break;
+                slot = (slot + 1) & 2047;
+            }
+            atomicMin(&hpos[slot], t);
         }
         __syncthreads();
-        n_uniq += kept;
-        nf += kept;
+        const bool first = t < m && hpos[slot] == t;
+        const int rank = block_scan1024(first ? 1 : 0, iws, t) - (first ? 1 : 0);
+        int nnew = 0;
+        for (int i = 0; i < 16; ++i) nnew += iws[i];
+        if (first) {
+            order[n_uniq + rank] = nv[t];
+            newv[rank] = nv[t];
+        }
+        n_uniq += nnew;
+        __syncthreads();
         if (n_uniq >= B) break;
-        // re-sort the found set (bitonic over 1024 slots) and rebuild its prefix masses
-        bitonic1024(fs, t);
-        // prefix masses of the sorted found set (float64 block scan)
-        fm[t] = t < nf ? (double)probs[fs[t]] : 0.0;
+        // the next round searches cdf - (found masses): found set = previous found + this round's, sorted
+        int v2 = t < nf ? fs[t] : (t < nf + nnew ? newv[t - nf] : 0x7fffffff);
+        v2 = bitonic1024(v2, sk, t);
+        fs[t] = v2;
+        nf += nnew;
+        const double fmv = block_scan1024(t < nf ? (double)probs[v2] : 0.0, dws, t);
+        fm[t] = fmv;
         __syncthreads();
-        for (int off = 1; off < 1024; off <<= 1) {
-            const double add = t >= off ? fm[t - off] : 0.0;
-            __syncthreads();
-            fm[t] += add;
-            __syncthreads();
-        }
     }
     if (t < B) idx[t] = t < n_uniq ? order[t] : 0;
     if (t == 0 && n_used) *n_used = ok ? used : -2;

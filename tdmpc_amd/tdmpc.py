@@ -366,7 +366,10 @@ class TDMPC:
         m = self.learner().update(replay_buffer, step, noise=noise)
         if not sync_metrics:
             return m
-        return {k: float(v) for k, v in zip(METRICS, m.double().cpu().tolist())}
+        out = {k: float(v) for k, v in zip(METRICS, m.double().cpu().tolist())}
+        if getattr(replay_buffer, "_full", False) and hasattr(replay_buffer, "check_sample"):
+            replay_buffer.check_sample()   # numpy's choice(replace=False) error, raised at this existing sync
+        return out
 
     def update_pi(self, zs):
         """tdmpc.py:165-182."""
