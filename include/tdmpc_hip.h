@@ -73,8 +73,9 @@ typedef struct tdmpc_plan_params {
                               kernels wherever the shape allows (row block by launch size), 3 / 4 = chain
                               kernels on 32- / 16-row blocks only, 5 = TOLD.next on the column-split step kernel
                               (others layered), 6 = chain kernels with fp32 products from a three-way bf16
-                              split (TDMPC_PATH_CHAIN_X6), 7 = path 5 with those products; results agree within
-                              the fp32 tolerance */
+                              split (TDMPC_PATH_CHAIN_X6), 7 = path 5 with those products, 8 = path 2 with
+                              TOLD.next / helper.q on 64-row x6 blocks (chain64); results agree within the fp32
+                              tolerance */
     /* ABI 5: per-call state read from device memory at run time, so one captured hipGraph serves every value */
     const int32_t* warm_flags; /* optional device int32 [batch]: per-env warm start (tdmpc.py:124-125, `not t0`
                                   for that env with a previous mean); NULL = warm_start for every env */
@@ -90,6 +91,7 @@ typedef struct tdmpc_plan_params {
 #define TDMPC_PATH_SPLIT 5
 #define TDMPC_PATH_CHAIN_X6 6   /* chain kernels, fp32 products from a three-way bf16 split (M = 512) */
 #define TDMPC_PATH_SPLIT_X6 7   /* the split path (5) with the x6 products (M = 512) */
+#define TDMPC_PATH_CHAIN64 8    /* chain kernels with TOLD.next / helper.q on 64-row x6 blocks at any width (M = 512) */
 
 /* Byte sizes the caller must allocate (all 256-byte aligned). */
 typedef struct tdmpc_sizes {

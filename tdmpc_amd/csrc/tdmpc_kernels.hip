@@ -1661,6 +1661,320 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
 #endif
 }
 
+#ifndef CHAIN64_DIAG
+#define CHAIN64_DIAG 0   // diagnostic builds only (tools/gpu/chain64_diag.sh): 1 = hi.hi term only, 2 = no weight refill
+#endif
+// ------------------------------------------------------------------------------------------------ chain64
+// 64-row blocks for the wide x6 launches (TOLD.next and helper.q at >= one workgroup per CU): one 8-wave workgroup
+// per CU carries TWO 32-row tiles through the head, and every 1 KiB weight fragment it streams from L2 feeds both
+// tiles' MFMAs. Why: the x6 products run the bf16 MFMA at 16x the f32 rate, so a 32-row block needs
+// 6 B x 32 cols per 16-deep k group per MFMA pass -- at full MFMA rate 64 B/cycle of weights per CU, the whole L2
+// share of a CU (34.5 TB/s / 256 CUs ~ 62 B/cycle); the 32-row chain kernel sat at ~0.5 MFMA busy behind it.
+// Two tiles per fragment halve that to 32 B/cycle. Wave w owns output columns [64w, 64w + 64) (TN = 2) of the
+// M = 512 layers for both tiles (4 accumulators); the activation block is [2][K/4][32][4] fp32 (128 KB at M = 512),
+// so one workgroup per CU with two waves per SIMD. The math per row is the 32-row x6 kernel's (same k order, same
+// split, same epilogues), so results equal chain_kernel<..., X6 = 1> bitwise row for row.
+template <int TN, int D>
+DEVI void ring6x2_run(floatx16 (&acc)[TN][2], uint4 (&wr)[D][TN][3], const float* sA, long tile_fl,
+                      const unsigned short* Wp, long wbs, int g0, int g1, int r, int h) {
+    const int gl = g1 - 1;
+    const float* ap = sA + (h * 32 + r) * 4;
+    const float* bp = ap + tile_fl;
+    float4 n0 = *(const float4*)(ap + (size_t)g0 * 512), n1 = *(const float4*)(ap + (size_t)g0 * 512 + 256);
+    float4 m0 = *(const float4*)(bp + (size_t)g0 * 512), m1 = *(const float4*)(bp + (size_t)g0 * 512 + 256);
+    int gb = g0;
+    for (; gb < g1; gb += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int g = gb + d;
+            if (g >= g1) break;
+            const float4 a0 = n0, a1 = n1, b0 = m0, b1 = m1;
+            const size_t gn = (size_t)min(g + 1, gl) * 512;
+            n0 = *(const float4*)(ap + gn);
+            n1 = *(const float4*)(ap + gn + 256);
+            m0 = *(const float4*)(bp + gn);
+            m1 = *(const float4*)(bp + gn + 256);
+            __builtin_amdgcn_sched_barrier(0);
+            bf16x8_t ah, am, al, bh, bm, bl;
+            split8(a0, a1, ah, am, al);
+            split8(b0, b1, bh, bm, bl);
+#if CHAIN64_DIAG == 1
+            // diagnostic: the hi.hi term only (1 MFMA per product instead of 6; results inexact)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), ah, acc[j][0], 0, 0, 0);
+                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bh, acc[j][1], 0, 0, 0);
+            }
+            if (0)
+#endif
+            {
+            // small terms first, the hi.hi term last (x6_group's order), both tiles per weight fragment
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), am, acc[j][0], 0, 0, 0);
+                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), bm, acc[j][1], 0, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][2]), ah, acc[j][0], 0, 0, 0);
+                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][2]), bh, acc[j][1], 0, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), al, acc[j][0], 0, 0, 0);
+                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bl, acc[j][1], 0, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), ah, acc[j][0], 0, 0, 0);
+                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), bh, acc[j][1], 0, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), am, acc[j][0], 0, 0, 0);
+                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bm, acc[j][1], 0, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), ah, acc[j][0], 0, 0, 0);
+                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bh, acc[j][1], 0, 0, 0);
+            }
+            }
+            // refill this slot D groups ahead (past the end: the last group again, never used)
+#if CHAIN64_DIAG != 2   // diagnostic 2: no refill (the first D groups' weights reused; results inexact)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    wr[d][j][p] = *(const uint4*)(Wp + j * wbs + ((size_t)min(g + D, gl) * 3 + p) * 512);
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
+template <int TN>
+DEVI void zero_acc2(floatx16 (&acc)[TN][2]) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[j][t][e] = 0.f;
+}
+
+// per-tile copies of the chain helpers' register tile
+template <int TN>
+DEVI void take_tile(floatx16 (&dst)[TN], const floatx16 (&acc)[TN][2], int t) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) dst[j] = acc[j][t];
+}
+
+template <int MODE, int D = 2, int D3 = 2>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) chain64_kernel(const ChainArgs a) {
+    constexpr int NW = 8, NTH = 512, TN = 2;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int pb = blockIdx.y;
+    const ChainProb& P = a.p[pb];
+    const int M = a.M;
+    const int m0 = blockIdx.x * 64;
+    float* sH = smem;                       // activation block [2 tiles][max(K1, M)/4][32][4]
+    const long tfl = a.hfl / 2;             // floats per tile
+    float* red0 = smem + a.hfl;             // [NW][64]
+    float* red1 = red0 + 64 * NW;           // [NW][64]
+    float* sp = red1 + 64 * NW;             // parameter vectors (chain_param_floats)
+    float* sb1 = sp;
+    float* sb2 = sp + M;
+    float* sw3 = sp + 2 * M;
+    float* sb3 = sp + 3 * M;
+    float* sg1 = sp + 3 * M;
+    float* sbe1 = sp + 4 * M;
+    float* sg2 = sp + 5 * M;
+    float* sbe2 = sp + 6 * M;
+    const int g1n = (int)(rup(a.K1, 16) >> 4), g2n = M >> 4;
+    const long wb1 = (long)g1n * 1536, wb2 = (long)g2n * 1536;
+    const int cw0 = wave * TN;
+    const bool head_dot = MODE == CH_Q || (MODE == CH_STEP && pb == 1);
+
+    uint4 wx[D][TN][3];
+    ring6_fill<TN, D>(wx, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n);
+    // input rows: both tiles, K1 rounded to 16 with zero quads (64 consecutive threads = 32 rows of a quad x 2 tiles)
+    const int q1n = g1n * 4;
+    for (int i = tid; i < q1n * 64; i += NTH) {
+        const int rr = i & 31, t = (i >> 5) & 1, q = i >> 6;
+        const int lm = m0 + t * 32 + rr;
+        const int xr = map_row(a.amap, lm < a.rows ? lm : 0);
+        const float4 x = q < (a.K1 >> 2)
+            ? *(const float4*)(a.X + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.q1 + q) * 128 + (xr & 31) * 4)
+            : make_float4(0.f, 0.f, 0.f, 0.f);
+        *(float4*)(sH + t * tfl + (q * 32 + rr) * 4) = x;
+    }
+    for (int i = tid; i < M / 4; i += NTH) {
+        ((float4*)sb1)[i] = ((const float4*)P.b1)[i];
+        ((float4*)sb2)[i] = ((const float4*)P.b2)[i];
+        if (head_dot) ((float4*)sw3)[i] = ((const float4*)P.w3v)[i];
+        if (MODE == CH_Q) {
+            ((float4*)sg1)[i] = ((const float4*)P.g1)[i];
+            ((float4*)sbe1)[i] = ((const float4*)P.be1)[i];
+            ((float4*)sg2)[i] = ((const float4*)P.g2)[i];
+            ((float4*)sbe2)[i] = ((const float4*)P.be2)[i];
+        }
+    }
+    if (!head_dot)
+        for (int i = tid; i < a.n3 / 4; i += NTH) ((float4*)sb3)[i] = ((const float4*)a.b3)[i];
+    float g_old = 0.f;   // the running return of this thread's row (reward workgroups, tid < 64)
+    if (MODE == CH_STEP && pb == 1 && tid < 64 && !a.first && m0 + tid < a.rows)
+        g_old = a.G[map_row(a.amap, m0 + tid)];
+    lds_barrier();
+
+    // ---- layer 1
+    floatx16 acc[TN][2];
+    zero_acc2<TN>(acc);
+    ring6x2_run<TN, D>(acc, wx, sH, tfl, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n, r, h);
+    ring6_fill<TN, D>(wx, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n);
+    lds_barrier();   // every wave is done with the input tiles: sH becomes h1
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        floatx16 at[TN];
+        take_tile<TN>(at, acc, t);
+        float v[TN * 16];
+        chain_bias<TN>(v, at, sb1, cw0, h);
+        if (MODE == CH_Q) {
+            float mean, rs;
+            chain_row_moments<TN, NW>(v, red0 + t * 32 * NW, red1 + t * 32 * NW, wave, r, h, M, mean, rs);
+            chain_ln<TN>(v, rs, -rs * mean, sg1, sbe1, cw0, h);
+#pragma unroll
+            for (int i = 0; i < TN * 16; ++i) v[i] = tanh_f(v[i]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < TN * 16; ++i) v[i] = elu_f(v[i]);
+        }
+        chain_store_lds<TN>(sH + t * tfl, v, cw0, r, h);
+    }
+    lds_barrier();
+
+    // ---- layer 2
+    zero_acc2<TN>(acc);
+    ring6x2_run<TN, D>(acc, wx, sH, tfl, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n, r, h);
+    const int nb3 = a.n3 >> 5;
+    const int ks = nb3 >= NW ? 1 : NW / nb3;
+    const int items = nb3 * ks;
+    const int gper = g2n / ks;
+    uint4 w3x[D3][1][3];
+    if (!head_dot && wave < items)
+        ring6_fill<1, D3>(w3x, a.X3 + (size_t)(wave / ks) * wb2 + lane * 8, wb2, (wave % ks) * gper, (wave % ks + 1) * gper);
+    if (head_dot) {
+        float s[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            floatx16 at[TN];
+            take_tile<TN>(at, acc, t);
+            float v[TN * 16];
+            chain_bias<TN>(v, at, sb2, cw0, h);
+            if (MODE == CH_Q) {
+                float mean, rs;
+                chain_row_moments<TN, NW>(v, red0 + t * 32 * NW, red1 + t * 32 * NW, wave, r, h, M, mean, rs);
+                chain_ln<TN>(v, rs, -rs * mean, sg2, sbe2, cw0, h);
+            }
+            float d = 0.f;
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 w4 = *(const float4*)(sw3 + (cw0 + j) * 32 + 8 * q + 4 * h);
+                    const float* x = v + j * 16 + 4 * q;
+                    d += (elu_f(x[0]) * w4.x + elu_f(x[1]) * w4.y) + (elu_f(x[2]) * w4.z + elu_f(x[3]) * w4.w);
+                }
+            s[t] = d + __shfl_xor(d, 32);
+        }
+        lds_barrier();   // red0 is free again (the LayerNorm moments are read)
+        if (h == 0) {
+            red0[wave * 64 + r] = s[0];
+            red0[wave * 64 + 32 + r] = s[1];
+        }
+        lds_barrier();
+        if (tid < 64) {
+            const int lm = m0 + tid;
+            if (lm < a.rows) {
+                const int xr = map_row(a.amap, lm);
+                float tot = 0.f;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) tot += red0[w * 64 + tid];
+                const float o = tot + P.b3v[0];
+                if (MODE == CH_Q) {
+                    a.q[(size_t)pb * a.q_ld + xr] = o;
+                } else {
+                    const float dr = fmul(a.disc, o);
+                    a.G[xr] = a.first ? dr : fadd(g_old, dr);
+                    if (a.last) a.rlast[xr] = o;
+                }
+            }
+        }
+        return;
+    }
+    // dynamics: h2 = ELU(y2) into the activation block once every wave is done reading h1
+    {
+        float v0[TN * 16], v1[TN * 16];
+        floatx16 at[TN];
+        take_tile<TN>(at, acc, 0);
+        chain_bias<TN>(v0, at, sb2, cw0, h);
+        take_tile<TN>(at, acc, 1);
+        chain_bias<TN>(v1, at, sb2, cw0, h);
+#pragma unroll
+        for (int i = 0; i < TN * 16; ++i) { v0[i] = elu_f(v0[i]); v1[i] = elu_f(v1[i]); }
+        lds_barrier();
+        chain_store_lds<TN>(sH, v0, cw0, r, h);
+        chain_store_lds<TN>(sH + tfl, v1, cw0, r, h);
+    }
+    lds_barrier();
+
+    // ---- layer 3: [64 x M] . W3^T -> [64 x n3]; items = (32-column block, K part), both tiles each
+    floatx16 p3[2][1][2];
+    int nit = 0;
+    for (int it = wave; it < items && nit < 2; it += NW, ++nit) {
+        const int blk = it / ks, kp = it % ks;
+        if (nit > 0)
+            ring6_fill<1, D3>(w3x, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper);
+        floatx16 a3[1][2];
+        zero_acc2<1>(a3);
+        ring6x2_run<1, D3>(a3, w3x, sH, tfl, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, r, h);
+        p3[nit][0][0] = a3[0][0];
+        p3[nit][0][1] = a3[0][1];
+    }
+    lds_barrier();   // partial tiles overwrite h2: item it, tile t at sH + (it * 2 + t) * 1024
+    for (int k = 0; k < nit; ++k) {
+        const int it = wave + k * NW;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *(float4*)(sH + (size_t)(it * 2 + t) * 1024 + ((2 * q + h) * 32 + r) * 4) =
+                    make_float4(p3[k][0][t][4 * q], p3[k][0][t][4 * q + 1], p3[k][0][t][4 * q + 2], p3[k][0][t][4 * q + 3]);
+    }
+    lds_barrier();
+    for (int i = tid; i < (a.nstore >> 2) * 64; i += NTH) {
+        const int rr = i & 31, t = (i >> 5) & 1, cq = i >> 6;
+        const int lm = m0 + t * 32 + rr;
+        if (lm >= a.rows) continue;
+        const int blk = cq >> 3, qi = cq & 7;
+        float4 sv = *(const float4*)(sH + (size_t)(blk * ks * 2 + t) * 1024 + (qi * 32 + rr) * 4);
+        for (int kp = 1; kp < ks; ++kp) {
+            const float4 u = *(const float4*)(sH + (size_t)((blk * ks + kp) * 2 + t) * 1024 + (qi * 32 + rr) * 4);
+            sv.x += u.x; sv.y += u.y; sv.z += u.z; sv.w += u.w;
+        }
+        const int c = 4 * cq;
+        const float4 bb = *(const float4*)(sb3 + c);
+        float o[4] = {sv.x + bb.x, sv.y + bb.y, sv.z + bb.z, sv.w + bb.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (c + k >= a.nvalid) o[k] = 0.f;
+        const int xr = map_row(a.amap, lm);
+        *(float4*)(a.Xo + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.out_q0 + cq) * 128 + (xr & 31) * 4) =
+            make_float4(o[0], o[1], o[2], o[3]);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------ chain16
 // Row-block chain kernel on 16-row blocks (v_mfma_f32_16x16x4_f32), the same three modes as chain_kernel.
 // Why a second block size: a 32-row chain launch of the B = 8 bench shape is exactly one workgroup per CU
@@ -3139,6 +3453,12 @@ int init_attrs() {
     HIPCHK(hipFuncSetAttribute((const void*)chain16_kernel<CH_PI, 4, 4, 4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain16_kernel<CH_Q, 4, 4, 4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 #undef CHAIN16_ATTR
+#define C64_ATTR(MODE, D, D3) \
+    HIPCHK(hipFuncSetAttribute((const void*)chain64_kernel<MODE, D, D3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+#define C64_ATTRS(MODE) C64_ATTR(MODE, 2, 2)
+    C64_ATTRS(CH_STEP) C64_ATTRS(CH_Q)
+#undef C64_ATTRS
+#undef C64_ATTR
     if (rc) return TDMPC_E_HIP;
     done = 1;
     return 0;
@@ -3407,6 +3727,22 @@ int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
     Profiler& pf = g_prof;
     const bool prof = pf.armed && pf.cfg == 4 + mode && pf.n + 2 <= pf.cap && (pf.rows == 0 || a.rows == pf.rows);
     if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], s));
+    if (a.rb == 64) {
+        const size_t lds64 = ((size_t)a.hfl + 2 * 64 * 8 + chain_param_floats(mode, a.M, a.n3)) * 4;
+        const dim3 g64((a.rows + 63) / 64, nprob);
+        a.il = 0;
+        // (weight-ring depths D / D3 of 3-4 / 6 measured 1-3 % slower than 2 / 2 on MI355X)
+        if (mode == CH_STEP) hipLaunchKernelGGL((chain64_kernel<CH_STEP, 2, 2>), g64, dim3(512), lds64, s, a);
+        else if (mode == CH_Q) hipLaunchKernelGGL((chain64_kernel<CH_Q, 2, 2>), g64, dim3(512), lds64, s, a);
+        else { snprintf(g_err, sizeof g_err, "chain64: unsupported mode %d", mode); return TDMPC_E_DIMS; }
+        HIPCHK(hipGetLastError());
+        if (prof) {
+            HIPCHK(hipEventRecord(pf.ev[pf.n + 1], s));
+            pf.n += 2;
+            pf.flops += 2.0 * a.rows * chain_macs_per_row(mode, a, nprob);
+        }
+        return 0;
+    }
     if (a.rb == 16) {
         const int nt = a.M / 128;
 #define CHAIN16_LAUNCH(MODE, NT) \
@@ -3555,6 +3891,27 @@ int chain_rb(const Ctx& c, int rows, int nprob) {
     return (rows + 31) / 32 * nprob > num_cus() / 2 ? 32 : 16;
 }
 
+// 64-row x6 blocks (chain64_kernel) for TOLD.next / helper.q launches wide enough to give every CU a workgroup:
+// TDMPC_CHAIN64=1 on the auto / chain paths, every such launch on TDMPC_PATH_CHAIN64 (parity tests). Off by default:
+// measured on MI355X (humanoid-run B = 32, rocprofv3): step 137.1 vs 136.9 us, Q 181.8 vs 180.2 us for the 32-row x6
+// kernel -- halving the weight bytes per MFMA changed nothing, i.e. the L2 weight stream is not what bounds these
+// kernels.
+void maybe_rb64(const Ctx& c, ChainArgs& a, int mode, int nprob) {
+    static int en = -1;
+    if (en < 0) {
+        const char* e = getenv("TDMPC_CHAIN64");
+        en = e ? atoi(e) : 0;
+    }
+    if (c.w.M != 512 || (mode != CH_STEP && mode != CH_Q)) return;
+    const bool forced = c.path == TDMPC_PATH_CHAIN64;
+    if (!forced && (!en || !a.x6 || a.rb != 32 || (c.path != TDMPC_PATH_AUTO && c.path != TDMPC_PATH_CHAIN) ||
+                    (a.rows + 63) / 64 * nprob < num_cus()))
+        return;
+    const int hfl = std::max((int)rup(c.Kx, 32), c.M) * 64;
+    if (((size_t)hfl + 2 * 64 * 8 + chain_param_floats(mode, c.M, a.n3)) * 4 > 160 * 1024) return;
+    a.rb = 64; a.nw = 8; a.x6 = 1; a.hfl = hfl;
+}
+
 ChainArgs chain0(const Ctx& c, int rows, RowMap map, int t, int K1, int q1, int nprob) {
     ChainArgs a;
     memset(&a, 0, sizeof a);
@@ -3661,6 +4018,12 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         }
         a.Xo = Xt(c, t + 1); a.out_q0 = w.Ap / 4;
         a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
+        maybe_rb64(c, a, CH_STEP, 2);
+        if (a.rb == 64) {
+            const size_t rb1 = (size_t)(M / 32) * (rup(c.Kx, 16) / 16) * 1536;
+            d.X1 = x6p(c, X6_W1X); r.X1 = x6p(c, X6_W1X) + rb1;
+            d.X2 = x6p(c, X6_W2D); r.X2 = x6p(c, X6_W2R); a.X3 = x6p(c, X6_W3D);
+        }
         return launch_chain(CH_STEP, a, 2, c.s);
     }
     if (use_split(c, rows)) {
@@ -3848,6 +4211,12 @@ int q_chain(const Ctx& c, int rows, RowMap map) {
         }
     }
     a.q = c.k.qv; a.q_ld = c.k.xrows;
+    maybe_rb64(c, a, CH_Q, 2);
+    if (a.rb == 64)
+        for (int q = 0; q < 2; ++q) {
+            a.p[q].X1 = x6p(c, X6_WQ1X) + (size_t)q * (M / 32) * (rup(c.Kx, 16) / 16) * 1536;
+            a.p[q].X2 = x6p(c, X6_WQ2) + (size_t)q * (M / 32) * (M / 16) * 1536;
+        }
     return launch_chain(CH_Q, a, 2, c.s);
 }
 
@@ -4173,7 +4542,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     int rc;
     const int H = prm->horizon, I = prm->iterations, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 7) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 8) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T;
     // z0 = h(obs) and mean = 0 (warm: prev_mean shifted), std = 2
@@ -4256,7 +4625,7 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
     const int H = prm->horizon, I = prm->iterations, B = prm->batch, K = d->num_elites;
     if (I <= 0 || I > 16) { snprintf(g_err, sizeof g_err, "iCEM: 1..16 iterations"); return TDMPC_E_DIMS; }
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream, K))) return rc;
-    if (prm->path < 0 || prm->path > 7) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 8) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = d->num_samples, Pmax = d->num_pi, Tw = N + K + Pmax, pi_base = N + K, P0 = prm->n_pi0;
     c.T = Tw;
@@ -4354,7 +4723,7 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 7) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 8) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     if (rows != c.T) { snprintf(g_err, sizeof g_err, "rows must equal N+P"); return TDMPC_E_DIMS; }
     const int T = c.T, L = c.w.L;
@@ -4399,7 +4768,7 @@ int tdmpc_pi_rollout(const tdmpc_dims* d, const tdmpc_plan_params* prm, const vo
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 7) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 8) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T;
     const long A = c.A;
@@ -4428,7 +4797,7 @@ int tdmpc_cem_iter(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 7) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > 8) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T, A = c.A, HA = H * A;
     if (P > 0 && !pi_actions) return TDMPC_E_NULL;
