@@ -156,6 +156,13 @@ def cpu_baselines(cfg, budget_s: float):
     return out
 
 
+def sampleable(rs, total, n, L=500, H=5):
+    """n random storage indices outside the masked last H steps of each episode (helper.py:468-470): the
+    positions a learner's priority write-back can touch, so every sampled window stays inside its episode."""
+    r = rs.randint(0, total // L * (L - H), n)
+    return (r // (L - H)) * L + r % (L - H)
+
+
 def replay_bench(cfg, dev, cpu=True, reps=200):
     """one prioritized-replay sample() (batch 512, H+1 = 6-step windows) from a buffer of the
     task's capacity (train_steps 500000 / action_repeat 2 = 250k transitions, 500-step episodes), random
@@ -179,7 +186,7 @@ def replay_bench(cfg, dev, cpu=True, reps=200):
         for _ in range(cap // L if full else cap // L - 1):
             buf.add(ep)
         total = cap if full else buf.idx
-        buf.update_priorities(torch.from_numpy(rs.randint(0, total, 50_000)),
+        buf.update_priorities(torch.from_numpy(sampleable(rs, total, 50_000)),
                               torch.from_numpy(rs.exponential(1.0, (50_000, 1)).astype(np.float32)))
         for _ in range(5):
             buf.sample()
@@ -207,7 +214,7 @@ def replay_bench(cfg, dev, cpu=True, reps=200):
             # update_priorities at the learner's write-back size and at 50k (helper.py:487-488; duplicates: last wins)
             upd = {}
             for n in (B, 50_000):
-                ui = torch.from_numpy(rs.randint(0, total, n)).to(dev)
+                ui = torch.from_numpy(sampleable(rs, total, n)).to(dev)
                 uv = torch.from_numpy(rs.exponential(1.0, (n, 1)).astype(np.float32)).to(dev)
                 for _ in range(3):
                     buf.update_priorities(ui, uv)

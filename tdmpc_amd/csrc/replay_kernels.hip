@@ -389,6 +389,7 @@ __global__ void __launch_bounds__(1024) rp_norepl_kernel(const double* cdf, cons
 // ------------------------------------------------------------------------------------------------ gather
 struct GatherArgs {
     int modality, F, S, fs, A, L, H, B;
+    long cap;   // storage rows: action/reward [cap], obs [cap + 1]
     const void* obs; const void* last_obs; const float* action; const float* reward;
     const int64_t* idx;
     // importance weights (helper.py:518-519): weights[b] = (total * probs[idx[b]])**-beta / max over the batch
@@ -399,6 +400,13 @@ struct GatherArgs {
 // stacked observation of storage index j into dst: state = row j; pixels = frame_stack frames back from j
 // that do not cross the episode start (helper.py:490-502), oldest first, as floats.
 DEVI void stacked_obs(const GatherArgs& a, long j, float* dst) {
+    if (j > a.cap) {
+        // a window past the storage end (only reachable when a caller gave a masked episode tail a non-zero
+        // priority; the reference raises IndexError there): NaN rows instead of an out-of-bounds read
+        const int F = a.modality == 0 ? a.F : a.fs * 3 * a.S * a.S;
+        for (int k = threadIdx.x; k < F; k += blockDim.x) dst[k] = NAN;
+        return;
+    }
     if (a.modality == 0) {
         const float* src = (const float*)a.obs + (size_t)j * a.F;
         for (int k = threadIdx.x; k < a.F; k += blockDim.x) dst[k] = src[k];
@@ -439,7 +447,7 @@ __global__ void __launch_bounds__(256) rp_gather_kernel(const GatherArgs a) {
     }
     const int t = y - 1;
     float* dst = a.o_next + ((size_t)t * a.B + b) * F;
-    if (t == a.H && (i + a.H + 1) % a.L == 0) {
+    if (t == a.H && (i + a.H + 1) % a.L == 0 && i + a.H < a.cap) {
         // episode end: the stored final observation (helper.py:525-526)
         const long e = (i + a.H) / a.L;
         if (a.modality == 0) {
@@ -452,9 +460,10 @@ __global__ void __launch_bounds__(256) rp_gather_kernel(const GatherArgs a) {
     } else {
         stacked_obs(a, i + t + 1, dst);
     }
+    const bool in = i + t < a.cap;
     for (int k = threadIdx.x; k < a.A; k += blockDim.x)
-        a.o_action[((size_t)t * a.B + b) * a.A + k] = a.action[(size_t)(i + t) * a.A + k];
-    if (threadIdx.x == 0) a.o_reward[(size_t)t * a.B + b] = a.reward[i + t];
+        a.o_action[((size_t)t * a.B + b) * a.A + k] = in ? a.action[(size_t)(i + t) * a.A + k] : NAN;
+    if (threadIdx.x == 0) a.o_reward[(size_t)t * a.B + b] = in ? a.reward[i + t] : NAN;
 }
 
 // ------------------------------------------------------------------------------------------------ add
@@ -597,6 +606,7 @@ int tdmpc_replay_sample(const tdmpc_replay_dims* d, const tdmpc_replay_store* st
     GatherArgs g;
     g.modality = d->modality; g.F = d->obs_dim; g.S = d->img_hw; g.fs = d->frame_stack; g.A = d->action_dim;
     g.L = d->episode_length; g.H = d->horizon; g.B = B;
+    g.cap = d->capacity;
     g.obs = st->obs; g.last_obs = st->last_obs; g.action = st->action; g.reward = st->reward; g.idx = w.idx;
     g.probs = w.probs; g.total = total; g.beta = beta; g.idx_out = idxs; g.weights = weights;
     g.o_obs = obs; g.o_next = next_obs; g.o_action = action; g.o_reward = reward;
