@@ -74,8 +74,8 @@ typedef struct tdmpc_plan_params {
                               kernels on 32- / 16-row blocks only, 5 = TOLD.next on the column-split step kernel
                               (others layered), 6 = chain kernels with fp32 products from a three-way bf16
                               split (TDMPC_PATH_CHAIN_X6), 7 = path 5 with those products, 8 = path 2 with
-                              TOLD.next / helper.q on 64-row x6 blocks (chain64); results agree within the fp32
-                              tolerance */
+                              TOLD.next / helper.q on 64-row x6 blocks (chain64), 9 = the persistent one-env plan
+                              (plan1: one launch after the encoder); results agree within the fp32 tolerance */
     /* ABI 5: per-call state read from device memory at run time, so one captured hipGraph serves every value */
     const int32_t* warm_flags; /* optional device int32 [batch]: per-env warm start (tdmpc.py:124-125, `not t0`
                                   for that env with a previous mean); NULL = warm_start for every env */
@@ -92,6 +92,9 @@ typedef struct tdmpc_plan_params {
 #define TDMPC_PATH_CHAIN_X6 6   /* chain kernels, fp32 products from a three-way bf16 split (M = 512) */
 #define TDMPC_PATH_SPLIT_X6 7   /* the split path (5) with the x6 products (M = 512) */
 #define TDMPC_PATH_CHAIN64 8    /* chain kernels with TOLD.next / helper.q on 64-row x6 blocks at any width (M = 512) */
+#define TDMPC_PATH_PERSIST 9    /* one env: the whole plan after the encoder as ONE persistent launch (x6 products,
+                                   weight-stationary; batch 1, M = 512, >= 256 CUs; the auto path's choice there);
+                                   calls it does not apply to run the auto path */
 
 /* Byte sizes the caller must allocate (all 256-byte aligned). */
 typedef struct tdmpc_sizes {
@@ -241,6 +244,11 @@ int tdmpc_cem_iter(const tdmpc_dims* dims, const tdmpc_plan_params* params, cons
  * head's MACs per row at the real, unpadded widths). Eager use only (events are not graph-capturable). */
 int tdmpc_profile_begin(int32_t cfg, int32_t pro, int32_t kdim, int32_t rows, int32_t max_launches);
 int tdmpc_profile_end(int32_t* launches, double* total_ms, double* flops);
+
+/* Diagnostic: persistent one-env plans (TDMPC_PATH_PERSIST) launched after this call record, for workgroups 0 and
+ * 255, the 100 MHz realtime clock at every hand-off's arrival and release into `dev` (device, 2048 uint64:
+ * [workgroup 0: 1024][workgroup 255: 1024], entry 2*k / 2*k + 1 for hand-off k). NULL turns it off. */
+int tdmpc_debug_plan1_stamps(void* dev);
 
 /* Last HIP error string seen by this thread (for diagnostics). */
 const char* tdmpc_last_error(void);

@@ -12,11 +12,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDMPC_LIB_PATH") or os.path.join(HERE, "libtdmpc_hip.so")   # override: A/B of builds
 
 ABI_VERSION = 5
-PATHS = {"auto": 0, "layered": 1, "chain": 2, "chain32": 3, "chain16": 4, "split": 5, "chain_x6": 6, "split_x6": 7, "chain64": 8}
+PATHS = {"auto": 0, "layered": 1, "chain": 2, "chain32": 3, "chain16": 4, "split": 5, "chain_x6": 6, "split_x6": 7, "chain64": 8, "persist": 9}
 
 EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc_num_param_tensors",
             "tdmpc_pack_weights", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_pi_rollout",
-            "tdmpc_cem_iter", "tdmpc_last_error",
+            "tdmpc_cem_iter", "tdmpc_last_error", "tdmpc_debug_plan1_stamps",
             "tdmpc_profile_begin", "tdmpc_profile_end", "tdmpc_icem_sizes_for", "tdmpc_plan_icem",
             # include/tdmpc_replay.h
             "tdmpc_replay_workspace_bytes", "tdmpc_replay_add_priorities", "tdmpc_replay_update_priorities",
@@ -87,6 +87,7 @@ def lib():
     L = C.CDLL(LIB_PATH)
     vp, i32, sz = C.c_void_p, C.c_int32, C.c_size_t
     L.tdmpc_abi_version.restype = C.c_int
+    L.tdmpc_debug_plan1_stamps.argtypes = [vp]
     L.tdmpc_sizes_for.argtypes = [C.POINTER(Dims), C.POINTER(Sizes)]
     L.tdmpc_noise_floats.argtypes = [C.POINTER(Dims), i32, i32]
     L.tdmpc_noise_floats.restype = sz

@@ -25,7 +25,7 @@ def hipcc() -> str:
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
-    deps = SRCS + [os.path.join(REPO, "include", h) for h in ("tdmpc_hip.h", "tdmpc_replay.h", "tdmpc_learner.h")]
+    deps = SRCS + [os.path.join(HERE, "csrc", "plan1.inc")] + [os.path.join(REPO, "include", h) for h in ("tdmpc_hip.h", "tdmpc_replay.h", "tdmpc_learner.h")]
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
     tmp = OUT + ".tmp"

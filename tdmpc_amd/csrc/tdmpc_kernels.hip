@@ -29,6 +29,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "../../include/tdmpc_hip.h"
 
@@ -198,6 +199,8 @@ struct Work {
     float* enc_tmp;  // pixel conv activations
     size_t x_stride; // floats per X_t
     int xrows;       // rup(B*T, 32)
+    char* p1;        // exchange region of the persistent one-env plan (plan1.inc), p1_bytes (0: not eligible)
+    size_t p1_bytes;
     size_t total;
 };
 
@@ -205,6 +208,73 @@ size_t pixel_act_floats(const Layout& w) {
     size_t m = 0;
     for (int i = 1; i <= 4; ++i) m = std::max(m, (size_t)w.nch * w.conv_hw[i] * w.conv_hw[i]);
     return m;
+}
+
+// ---- persistent one-env plan (plan1.inc): its exchange region and shape limits
+constexpr int P1_NG = 8;      // row groups
+constexpr int P1_WPG = 32;    // workgroups per group: 2 heads x 16 column slices
+constexpr int P1_RTM = 3;     // 32-row tiles per group at most
+constexpr int P1_ROWS = 32 * P1_RTM;
+// hidden-activation exchange row stride (floats): 512 + 32, so the 16 rows a wave reads per k-step do not all map to
+// one L2 channel (a 2 KB stride puts every row's 128 B line of a k-step on the same channel)
+constexpr int P1_H1LD = 544;
+constexpr unsigned P1_XCC_TAB = P1_NG * 256 + 256;   // sync block: per-workgroup XCD ids (placement census)
+constexpr unsigned P1_SPIN_MAX = 400000;   // ~0.3-0.5 s of polling before a workgroup gives up
+
+// exchange region bytes (all offsets 256-aligned) for dims; 0 = not eligible
+struct P1Region {
+    unsigned o_sync, o_xb, o_h1, o_zp, o_rp, o_pp, o_qm, o_qp, o_val, o_rl, xb_t, xb_g, total;
+};
+
+// the first layer's 32-k steps the kernel instantiation runs (4 or 6; steps past K meet zero activations)
+inline int p1_ks(const Layout& w) { return (w.Kx + 31) / 32 <= 4 ? 4 : 6; }
+// XB row floats: [a | 0 | z | 0] zero-padded past both first layers' KS 32-k steps (the policy's starts at Ap)
+inline int p1_kxs(const Layout& w) { return (int)rup(w.Ap + 32 * p1_ks(w), 16); }
+
+inline P1Region p1_region(const tdmpc_dims* d, const Layout& w) {
+    P1Region r;
+    memset(&r, 0, sizeof r);
+    const size_t T = d->num_samples + d->num_pi, Hm = d->max_horizon;
+    size_t o = 0;
+    auto take = [&](size_t b) { size_t x = o; o += rup(b, 256); return (unsigned)x; };
+    r.o_sync = take(P1_NG * 256 + 256 + 4 * P1_NG * P1_WPG);   // counters, error word, XCD census
+    r.xb_t = (unsigned)((size_t)P1_ROWS * p1_kxs(w) * 4);
+    r.xb_g = (unsigned)((Hm + 1) * r.xb_t);
+    r.o_xb = take((size_t)P1_NG * r.xb_g);
+    r.o_h1 = take((size_t)P1_NG * 2 * P1_ROWS * P1_H1LD * 4);
+    r.o_zp = take((size_t)P1_NG * 16 * P1_ROWS * w.Lr * 4);
+    r.o_rp = take((size_t)P1_NG * 16 * P1_ROWS * 4);
+    r.o_pp = take((size_t)P1_NG * 16 * P1_ROWS * w.Ar * 4);
+    r.o_qm = take((size_t)P1_NG * 2 * 16 * P1_ROWS * 8);
+    r.o_qp = take((size_t)P1_NG * 2 * 16 * P1_ROWS * 4);
+    r.o_val = take(2 * T * 4);
+    r.o_rl = take(T * 4);
+    r.total = (unsigned)o;
+    return r;
+}
+
+// LDS of plan1_kernel: the hidden-layer weight slice (96 KB), a layer's 32-column slice of the group's rows (+ per-row
+// LayerNorm scalars), the CEM step's top-k keys and elite actions, mean / std / scores / bias slices
+__host__ __device__ inline size_t p1_cem_floats(int H, int K, int A, int T) {   // top-k keys + elites | K-half partials
+    const size_t c = (size_t)(T + 63) / 64 * 64 * 2 + rup((size_t)H * K * A, 4);
+    return c > 4 * 2 * 64 * 4 ? c : 4 * 2 * 64 * 4;
+}
+inline size_t p1_lds_bytes(int H, int K, int A, int T) {
+    const size_t HA = (size_t)H * A;
+    return ((size_t)32 * 3 * 64 * 4 + (size_t)P1_ROWS * 36 + 2 * P1_ROWS + p1_cem_floats(H, K, A, T) +
+            3 * rup(HA, 4) + 64 + 64 + 16 + 32 + 648) * 4;
+}
+
+// plan1_kernel's shape limits (dims only; the call adds batch == 1 and >= 256 CUs): mlp_dim 512, at most 96 rows
+// (three 32-row tiles) per row group, first-layer K <= 192 and latent K <= 192 (three 16-k groups per wave), latent
+// and action heads <= 128 / 64 columns, LDS within 160 KB.
+inline bool p1_dims_ok(const tdmpc_dims* d, const Layout& w) {
+    if (w.M != 512 || d->num_elites > 64) return false;
+    const int N = d->num_samples, P = d->num_pi, T = N + P;
+    const int sr = (N + P1_NG - 1) / P1_NG, pr = (P + P1_NG - 1) / P1_NG;
+    if (sr + pr > P1_ROWS || T > 1024) return false;
+    if ((w.Kx + 15) / 16 > 12 || (w.Lp + 15) / 16 > 12 || w.Lr > 128 || w.Ar > 128) return false;
+    return p1_lds_bytes(d->max_horizon, d->num_elites, w.A, T) <= 160 * 1024;
 }
 
 // extra: rows per env beyond N + P (the iCEM planner keeps up to K reused elite trajectories per env)
@@ -232,6 +302,8 @@ void make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k, int ex
     k->mean = (float*)take(B * H * w.A * 4);
     k->stdv = (float*)take(B * H * w.A * 4);
     k->enc_tmp = (float*)take(d->modality ? 2 * B * pixel_act_floats(w) * 4 : 256);
+    k->p1_bytes = p1_dims_ok(d, w) && !extra ? p1_region(d, w).total : 0;
+    k->p1 = k->p1_bytes ? (char*)take(k->p1_bytes) : nullptr;
     k->total = o;
 }
 
@@ -978,7 +1050,7 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 #endif
 #ifndef X6_PIPE
 // 1: 4-wave x6 chain workgroups split group g + 1 under group g's MFMAs (ring6_run_pipe). Off: measured 3 % slower
-// (6.56 vs 6.35 ms per B = 32 plan, 2.31 vs 2.22 at B = 8, tools/gpu92.sh) -- the other wave on the SIMD already
+// (6.56 vs 6.35 ms per B = 32 plan, 2.31 vs 2.22 at B = 8, round-1 run) -- the other wave on the SIMD already
 // fills the split's VALU slots, and the extra live operands cost more than the overlap gains
 #define X6_PIPE 0
 #endif
@@ -1247,7 +1319,7 @@ DEVI void chain_store_planes(float* sH, const float (&v)[TN * 16], int cw0, int 
 // Workgroup barrier for the chain kernels' LDS hand-offs: waits for this wave's LDS traffic only. HIP's
 // __syncthreads() carries a fence that drains vmcnt, i.e. it also waits for every global load in flight (the next
 // layer's weight ring prefetched before the epilogue, the ring's tail refills). No chain-kernel barrier orders
-// global memory between waves. Measured neutral on MI355X (stamps, tools/gpu48.sh: the layer-boundary cost is
+// global memory between waves. Measured neutral on MI355X (stamps, round-1 run: the layer-boundary cost is
 // the MFMA pipe draining before each epilogue, not the load wait), kept as the precise primitive.
 DEVI void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
@@ -1339,10 +1411,14 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     constexpr int NTH = 64 * NW;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-    const int pb = a.il ? blockIdx.x % a.il : blockIdx.y;
+    // il > 0: heads interleaved along x; il < 0: XCD-grouped heads (blocks b, b + 8, ... share an XCD: dispatch
+    // groups 0-3 run head 0, 4-7 head 1, so each XCD's L2 holds one head's weights); else head = blockIdx.y
+    const int bx = blockIdx.x;
+    const int pb = a.il > 0 ? bx % a.il : a.il < 0 ? (bx & 7) >> 2 : blockIdx.y;
     const ChainProb& P = a.p[pb];
     const int M = a.M;
-    const int m0 = (a.il ? blockIdx.x / a.il : blockIdx.x) * 32;
+    const int m0 = (a.il > 0 ? bx / a.il : a.il < 0 ? (bx >> 3) * 4 + (bx & 3) : bx) * 32;
+    if (m0 >= a.rows) return;   // (XCD-grouped grids are padded to a multiple of 4 blocks per head)
     float* sH = smem;                       // activation block [max(K1, M)/4][32][4]
     float* red0 = smem + a.hfl;             // [NW][32]
     float* red1 = red0 + 32 * NW;           // [NW][32]
@@ -3402,6 +3478,8 @@ int set_lds_attr() {
     return 0;
 }
 
+#include "plan1.inc"
+
 #define FOR_EACH_LINEAR(X)                                                                          \
     X(1, 1, 1, 1, 0, 32, false) X(1, 1, 1, 1, 0, 64, false) X(1, 1, 1, 1, 0, 128, false)              \
     X(1, 2, 1, 1, 0, 32, false) X(1, 2, 1, 1, 0, 64, false) X(1, 2, 1, 1, 0, 128, false)              \
@@ -3418,6 +3496,8 @@ int init_attrs() {
     FOR_EACH_LINEAR(SET_ATTR)
 #undef SET_ATTR
     HIPCHK(hipFuncSetAttribute((const void*)cem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)plan1_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)plan1_kernel<6>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -3650,7 +3730,7 @@ int launch_lin(const LinArgs& a, int nprob, int nmax, int wide64, int pro, hipSt
 // 32-row-block equivalents x problems (TDMPC_CHAIN_WGS, default 64, 0 disables). Narrow launches run on 16-row
 // blocks (chain_rb), so from 64 32-row blocks on they still spread over 128+ CUs; below that the layered
 // GEMMs, whose K-split tiles spread the same rows over more CUs, finish first. Measured on MI355X (humanoid
-// plan, tools/gpu38.sh): threshold 64 vs 128: B = 2 envs 1.65 vs 1.87 ms, B = 4 1.88 vs 1.98 ms; 32 loses
+// plan, round-1 run): threshold 64 vs 128: B = 2 envs 1.65 vs 1.87 ms, B = 4 1.88 vs 1.98 ms; 32 loses
 // at one env (1.56 vs 1.38 ms).
 int chain_wgs() {
     static int v = -1;
@@ -3702,13 +3782,22 @@ double chain_macs_per_row(int mode, const ChainArgs& a, int nprob) {
 
 // TDMPC_CHAIN_IL=1: the two problems of a launch (dynamics / reward, Q1 / Q2) alternate along blockIdx.x, so a
 // CU's co-resident workgroups are one of each (different layer-3 phases) instead of two of the same head. Off by
-// default: measured on MI355X (humanoid-run, tools/gpu68.sh) 9.50 vs 8.99 ms per B = 32 plan, 3.08 vs 3.04 at
+// default: measured on MI355X (humanoid-run, round-1 run) 9.50 vs 8.99 ms per B = 32 plan, 3.08 vs 3.04 at
 // B = 8 -- two workgroups of the same head on a CU stream the same weight panels at about the same time and
 // share them through the CU's L1, which the mixed pair loses.
 int chain_il() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("TDMPC_CHAIN_IL");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+
+int chain_xcd() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("TDMPC_CHAIN_XCD");
         v = e ? atoi(e) : 0;
     }
     return v;
@@ -3721,7 +3810,12 @@ int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
     const size_t lds = ((size_t)a.hfl + (a.rb == 16 ? 256 : 64 * nw) + chain_param_floats(mode, a.M, a.n3)) * 4;
     const int nblk = (a.rows + a.rb - 1) / a.rb;
     a.il = nprob > 1 && chain_il() ? nprob : 0;
-    const dim3 grid(a.il ? nblk * nprob : nblk, a.il ? 1 : nprob), block(64 * nw);
+    // XCD-grouped heads for two-head 32-row launches (TDMPC_CHAIN_XCD=1): each XCD streams one head's (x6: 2.15 MB)
+    // weights instead of both (4.3 MB). Off by default: measured on MI355X (humanoid-run B = 32) 6.41 vs 6.09 ms per
+    // plan -- co-resident same-head workgroups on a CU already share the weight stream, and halving the heads per
+    // XCD halves the workgroups that stream each weight line at the same time
+    if (!a.il && nprob == 2 && a.rb == 32 && chain_xcd()) a.il = -1;
+    const dim3 grid(a.il > 0 ? nblk * nprob : a.il < 0 ? (unsigned)rup(nblk, 4) * 2 : nblk, a.il ? 1 : nprob), block(64 * nw);
     const int tn = a.M / (32 * nw);
     // diagnostic timer (tdmpc_profile_begin cfg 4 + mode): HIP events around matching chain launches
     Profiler& pf = g_prof;
@@ -3811,7 +3905,7 @@ float* Xt(const Ctx& c, int t) { return c.k.X + (size_t)t * c.k.x_stride; }
 const unsigned short* x6p(const Ctx& c, int i) { return (const unsigned short*)(c.pw + c.w.x6[i]); }
 // Per-head thresholds (TDMPC_CHAIN_WGS_STEP / _PI / _Q override). The Q heads' layered form is four launches
 // (two GEMMs with LayerNorm partial moments, the LN+tanh pass, the value kernel), so the chain form wins from half
-// the step threshold: one env's 768 terminal rows 1.42 -> 1.32 ms per plan (tools/gpu52.sh); the step and pi
+// the step threshold: one env's 768 terminal rows 1.42 -> 1.32 ms per plan (round-1 run); the step and pi
 // heads keep chain_wgs() (lower thresholds measured slower for them).
 enum { CK_STEP = 0, CK_PI = 1, CK_Q = 2 };
 int chain_wgs_kind(int kind) {
@@ -3857,10 +3951,10 @@ int chain_nw() {
 // x6 chain kernels (fp32 products from a three-way bf16 split, chain_kernel<..., X6>) for 32-row chain launches:
 // forced by TDMPC_PATH_CHAIN_X6, the default of the auto / chain paths (TDMPC_X6=0 turns it off there); the
 // chain32 / chain16 paths keep the exact f32 MFMA. M = 512 only (the one instantiated width). Measured on MI355X
-// (humanoid-run, tools/gpu72.sh): 8.89 -> 6.52 ms per B = 32 plan, 3.03 -> 2.19 ms at B = 8.
+// (humanoid-run, round-1 run): 8.89 -> 6.52 ms per B = 32 plan, 3.03 -> 2.19 ms at B = 8.
 // Returns the x6 mode of a chain launch (0 = f32 MFMA; 1 = 8-wave workgroups, activations split as read; 2 = split
 // planes in LDS; 3 = mode 1 on 4-wave workgroups of 128 columns per wave, the default: the per-wave split serves
-// twice the MFMAs -- measured 6.37 vs 6.60 ms per B = 32 plan, 2.23 vs 2.28 at B = 8, tools/gpu83.sh). TDMPC_X6
+// twice the MFMAs -- measured 6.37 vs 6.60 ms per B = 32 plan, 2.23 vs 2.28 at B = 8, round-1 run). TDMPC_X6
 // picks the mode, 0 turns x6 off on the auto / chain paths.
 int use_x6(const Ctx& c) {
     if (c.w.M != 512) return 0;
@@ -4347,6 +4441,56 @@ int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, const float*
     return 0;
 }
 
+// The persistent one-env plan (plan1.inc) for this call? Auto path (and TDMPC_PATH_PERSIST) when the shape fits,
+// batch 1, >= 256 CUs (every workgroup of its 256-block grid must be resident); TDMPC_PERSIST=0 turns it off.
+unsigned long long* g_p1_stamps = nullptr;   // tdmpc_debug_plan1_stamps (diagnostic)
+
+bool use_plan1(const Ctx& c) {
+    static int en = -1;
+    if (en < 0) {
+        const char* e = getenv("TDMPC_PERSIST");
+        en = e ? atoi(e) : 1;
+    }
+    if (c.path != TDMPC_PATH_PERSIST && (c.path != TDMPC_PATH_AUTO || !en)) return false;
+    return c.B == 1 && c.k.p1 && num_cus() >= P1_NG * P1_WPG && c.H <= 16;
+}
+
+// encode_kernel has written z0 and the initial mean / std; one memset node (the hand-off counters) + one launch.
+int plan1_launch(const Ctx& c, const tdmpc_plan_params* prm, const float* noise, const double* u, float* prev_mean,
+                 float* action, float* metrics, float* elite_out, float* score_out, float* value_out, float* mean_out,
+                 float* std_out) {
+    const Layout& w = c.w;
+    const float* pw = c.pw;
+    const P1Region rg = p1_region(c.d, w);
+    P1Args a;
+    memset(&a, 0, sizeof a);
+    a.A = w.A; a.L = w.L; a.Ap = w.Ap; a.Lp = w.Lp; a.KG1 = (w.Kx + 15) / 16; a.KGP = (w.Lp + 15) / 16;
+    a.KXS = p1_kxs(w); a.Lr = w.Lr; a.Ar = w.Ar; a.H = c.H; a.I = prm->iterations; a.N = c.N; a.P = c.P; a.T = c.T;
+    a.K = c.d->num_elites; a.sr = (c.N + P1_NG - 1) / P1_NG; a.pr = (c.P + P1_NG - 1) / P1_NG;
+    a.x1x = x6p(c, X6_W1X); a.x2d = x6p(c, X6_W2D); a.x2r = x6p(c, X6_W2R); a.x3d = x6p(c, X6_W3D);
+    a.xp1 = x6p(c, X6_WP1); a.xp2 = x6p(c, X6_WP2); a.xp3 = x6p(c, X6_WP3); a.xq1 = x6p(c, X6_WQ1X); a.xq2 = x6p(c, X6_WQ2);
+    a.b1x = pw + w.b1x; a.b2d = pw + w.b2d; a.b2r = pw + w.b2r; a.b3d = pw + w.b3d; a.w3r = pw + w.w3r; a.b3r = pw + w.b3r;
+    a.bp1 = pw + w.bp1; a.bp2 = pw + w.bp2; a.bp3 = pw + w.bp3; a.bq1 = pw + w.bq1x; a.g1 = pw + w.g1; a.be1 = pw + w.be1;
+    a.bq2 = pw + w.bq2; a.g2 = pw + w.g2; a.be2 = pw + w.be2; a.wq3 = pw + w.wq3; a.bq3 = pw + w.bq3;
+    a.z0 = c.k.z0; a.mean0 = c.k.mean; a.std0 = c.k.stdv;
+    a.noise = noise; a.cem_off = c.eps_cem_off; a.iter_len = c.eps_iter; a.term_off = c.eps_term_off; a.act_off = c.eps_act_off;
+    a.u = u; a.prev_mean = prev_mean; a.action = action; a.metrics = metrics;
+    a.elite_out = elite_out; a.score_out = score_out; a.value_out = value_out; a.mean_out = mean_out; a.std_out = std_out;
+    a.eval_mode = prm->eval_mode; a.min_std = prm->min_std; a.temperature = prm->temperature; a.momentum = prm->momentum;
+    a.omm = prm->one_minus_momentum; a.std_floor = prm->std_floor; a.std_floor_p = prm->std_floor_dev;
+    for (int t = 0; t <= c.H && t < 17; ++t) a.disc[t] = prm->discount_pow[t];
+    a.base = c.k.p1; a.bytes = (unsigned)c.k.p1_bytes;
+    a.o_sync = rg.o_sync; a.o_xb = rg.o_xb; a.o_h1 = rg.o_h1; a.o_zp = rg.o_zp; a.o_rp = rg.o_rp; a.o_pp = rg.o_pp;
+    a.o_qm = rg.o_qm; a.o_qp = rg.o_qp; a.o_val = rg.o_val; a.o_rl = rg.o_rl; a.xb_t = rg.xb_t; a.xb_g = rg.xb_g;
+    a.stamps = g_p1_stamps;
+    HIPCHK(hipMemsetAsync(c.k.p1 + rg.o_sync, 0, P1_NG * 256 + 256, c.s));   // counters + error word
+    const size_t lds = p1_lds_bytes(c.H, a.K, w.A, c.T);
+    if (p1_ks(w) == 4) hipLaunchKernelGGL(plan1_kernel<4>, dim3(P1_NG * P1_WPG), dim3(P1_NT), lds, c.s, a);
+    else hipLaunchKernelGGL(plan1_kernel<6>, dim3(P1_NG * P1_WPG), dim3(P1_NT), lds, c.s, a);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 int setup_ctx(Ctx& c, const tdmpc_dims* d, const void* packed, void* ws, size_t ws_bytes, int batch, int H,
               int I, hipStream_t s, int extra_rows = 0) {
     if (!check_dims(d)) { snprintf(g_err, sizeof g_err, "bad dims"); return TDMPC_E_DIMS; }
@@ -4398,6 +4542,12 @@ void set_error(const char* msg) { snprintf(g_err, sizeof g_err, "%s", msg); }
 extern "C" {
 
 int tdmpc_abi_version(void) { return TDMPC_ABI_VERSION; }
+
+// Diagnostic: later persistent plans record per-hand-off realtime stamps into `dev` (device, 2048 uint64; NULL off).
+int tdmpc_debug_plan1_stamps(void* dev) {
+    g_p1_stamps = (unsigned long long*)dev;
+    return 0;
+}
 
 const char* tdmpc_last_error(void) { return g_err; }
 
@@ -4542,11 +4692,15 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     int rc;
     const int H = prm->horizon, I = prm->iterations, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 8) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path;
     const int N = c.N, P = c.P, T = c.T;
+    // TDMPC_PATH_PERSIST: the persistent plan where it applies (one env, supported shape), the auto path elsewhere
+    if (c.path == TDMPC_PATH_PERSIST && !use_plan1(c)) c.path = TDMPC_PATH_AUTO;
     // z0 = h(obs) and mean = 0 (warm: prev_mean shifted), std = 2
     if ((rc = encode(c, obs, obs_is_u8, B, prev_mean, prm->warm_start, 0, 2.f, prm->warm_flags))) return rc;
+    if (use_plan1(c))
+        return plan1_launch(c, prm, noise, u, prev_mean, action, metrics, elite_out, score_out, value_out, mean_out, std_out);
     if ((rc = prep(c, noise, 0, c.k.z0))) return rc;
 
     // pi pre-rollout (tdmpc.py:113-118) fused with CEM iteration 0: at each step t the policy rows get
@@ -4625,8 +4779,8 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
     const int H = prm->horizon, I = prm->iterations, B = prm->batch, K = d->num_elites;
     if (I <= 0 || I > 16) { snprintf(g_err, sizeof g_err, "iCEM: 1..16 iterations"); return TDMPC_E_DIMS; }
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream, K))) return rc;
-    if (prm->path < 0 || prm->path > 8) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
-    c.path = prm->path;
+    if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path;   // (persist: whole plans only)
     const int N = d->num_samples, Pmax = d->num_pi, Tw = N + K + Pmax, pi_base = N + K, P0 = prm->n_pi0;
     c.T = Tw;
     if (P0 <= 0 || P0 > Pmax || prm->n_samples[0] != N) { snprintf(g_err, sizeof g_err, "iCEM: bad counts"); return TDMPC_E_DIMS; }
@@ -4723,8 +4877,8 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 8) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
-    c.path = prm->path;
+    if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path;   // (persist: whole plans only)
     if (rows != c.T) { snprintf(g_err, sizeof g_err, "rows must equal N+P"); return TDMPC_E_DIMS; }
     const int T = c.T, L = c.w.L;
     HIPCHK(hipMemsetAsync(c.k.z0, 0, (size_t)B * c.w.Lp * 4, c.s));
@@ -4768,8 +4922,8 @@ int tdmpc_pi_rollout(const tdmpc_dims* d, const tdmpc_plan_params* prm, const vo
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 8) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
-    c.path = prm->path;
+    if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path;   // (persist: whole plans only)
     const int N = c.N, P = c.P, T = c.T;
     const long A = c.A;
     if (P <= 0) { snprintf(g_err, sizeof g_err, "num_pi is 0"); return TDMPC_E_DIMS; }
@@ -4797,8 +4951,8 @@ int tdmpc_cem_iter(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > 8) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
-    c.path = prm->path;
+    if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path;   // (persist: whole plans only)
     const int N = c.N, P = c.P, T = c.T, A = c.A, HA = H * A;
     if (P > 0 && !pi_actions) return TDMPC_E_NULL;
     // the caller's mean/std [B][H][A] -> the workspace's [B][Hmax][A]
