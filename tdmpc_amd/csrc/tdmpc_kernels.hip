@@ -4443,15 +4443,15 @@ int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, const float*
 
 unsigned long long* g_p1_stamps = nullptr;   // tdmpc_debug_plan1_stamps (diagnostic)
 
-// The persistent one-env plan (plan1.inc) for this call? TDMPC_PATH_PERSIST (or TDMPC_PERSIST=1 on the auto path)
-// when the shape fits, batch 1, >= 256 CUs (every workgroup of its 256-block grid must be resident). Off on the auto
-// path by default: measured on MI355X (humanoid-run, one env) it ties the launch chain -- 1.11-1.15 vs 1.10-1.18 ms
-// per plan_batch call, 1.26 vs 1.23-1.24 ms per literal plan() -- see DESIGN.md §4 for its per-phase timeline.
+// The persistent one-env plan (plan1.inc) for this call? The auto path's choice (TDMPC_PERSIST=0 turns it off) and
+// TDMPC_PATH_PERSIST, when the shape fits, batch 1, >= 256 CUs (every workgroup of its 256-block grid must be
+// resident). Measured on MI355X (humanoid-run, one env, same box, alternating): 1.083-1.087 vs 1.142-1.144 ms per
+// plan_batch call, 1.185-1.198 vs 1.237-1.251 ms per literal plan() -- see DESIGN.md §4 for its per-phase timeline.
 bool use_plan1(const Ctx& c) {
     static int en = -1;
     if (en < 0) {
         const char* e = getenv("TDMPC_PERSIST");
-        en = e ? atoi(e) : 0;
+        en = e ? atoi(e) : 1;
     }
     if (c.path != TDMPC_PATH_PERSIST && (c.path != TDMPC_PATH_AUTO || !en)) return false;
     return c.B == 1 && c.k.p1 && num_cus() >= P1_NG * P1_WPG && c.H <= 16;

@@ -54,3 +54,10 @@ for w, base in (("wg0", 0), ("wg255", 1024)):
 mk, ck = s[900:906], s[920:926]
 print("local hand-offs:", s[950], " step i1 t0 L2 (us): mm", (mk[1]-mk[0])/100, "put+barrier", (mk[2]-mk[1])/100,
       "last layer", (mk[3]-mk[2])/100, "| cycles", ck[1]-ck[0], ck[2]-ck[1], ck[3]-ck[2])
+mk = s[900:920]
+print("CEM i1 (us): sort+merge", (mk[11]-mk[10])/100, "elite gather", (mk[12]-mk[11])/100, "refit", (mk[13]-mk[12])/100,
+      "-> next sync arrival", (s[2 * (1 + 30 + 3 + 5 + 1 + 1) ] - mk[13]) / 100 if False else "")
+ga = s[1400:1656].astype(np.float64)
+ga = (ga - ga.min()) / 100
+print("grid arrival spread i1 (us): per group max", [round(float(ga[g::8].max()), 1) for g in range(8)],
+      "per group min", [round(float(ga[g::8].min()), 1) for g in range(8)])
