@@ -43,6 +43,92 @@ int tdmpc_loss_backward(const tdmpc_loss_args* a, const float* rows, const float
 int tdmpc_random_shift(const float* x, const float* shift, int32_t n, int32_t c, int32_t h, int32_t w, int32_t pad,
                        float* out, void* stream);
 
+/* ---------------------------------------------------------------------------------------------------------------
+ * The learner engine: TDMPC.update / update_pi / _td_target (tdmpc.py:165-245) as explicit forward and backward
+ * passes over the TOLD heads (tdmpc_amd/learner_engine.py drives them). Every pointer is a device
+ * pointer to float32; strides in elements. Stream-ordered, no allocation, graph-capturable; 0 or TDMPC_E*.
+ * ------------------------------------------------------------------------------------------------------------- */
+
+/* One K segment of a GEMM: C[m][n] (+)= sum_k A(m, k) B(k, n), k < k_len.
+ *   amode 0: A(m, k) = a[m * lda + k]   (activations, row-major)   amode 1: A(m, k) = a[k * lda + m]  (dY^T)
+ *   bmode 0: B(k, n) = b[n * ldb + k]   (Linear weight [N][K])     bmode 1: B(k, n) = b[k * ldb + n]
+ *   ones_col >= 0: B(k, ones_col) = 1 (the bias column of a weight gradient: db = colsum(dY)). */
+typedef struct tdmpc_lg_seg {
+    const float* a; const float* b;
+    int32_t lda, ldb, k, amode, bmode, ones_col;
+} tdmpc_lg_seg;
+
+enum { TDMPC_LG_EPI_NONE = 0, TDMPC_LG_EPI_ELU = 1, TDMPC_LG_EPI_PI = 2, TDMPC_LG_EPI_ELU_BWD = 3,
+       TDMPC_LG_EPI_PI_BWD = 4 };
+
+/* One GEMM of a grouped launch: C = epi(sum over segments + bias[n] + res[m][n]).
+ *   EPI_ELU:     elu(x)                                   (nn.ELU)
+ *   EPI_PI:      mu = tanh(x); c = clamp(mu + clamp(std * aux, -0.3, 0.3), -1 + 1e-6, 1 - 1e-6); c2 = mu
+ *                (TOLD.pi + TruncatedNormal.sample, helper.py:71-96; aux = the standard normal draws)
+ *   EPI_ELU_BWD: x * (aux > 0 ? 1 : aux + 1)              (aux = the ELU's output)
+ *   EPI_PI_BWD:  x * (1 - aux^2)                          (aux = mu: tanh' with the straight-through clamp)
+ *   c2 (EPI_NONE): a second copy of C (ldc2).
+ * splits > 1: split-K over workgroups; slice s of the raw sum goes to c + s * slice (no bias / res / epi). */
+typedef struct tdmpc_lg_job {
+    tdmpc_lg_seg seg[3];
+    int32_t nseg, m, n, epi;
+    float* c; float* c2; const float* bias; const float* aux; const float* res;
+    int32_t ldc, ldc2, ldaux, ldres;
+    float std_; int32_t splits; int64_t slice;
+} tdmpc_lg_job;
+
+/* Up to 12 GEMMs in one launch; tile 1: 32x32 output tiles, 2: 64x64 (4 waves split K inside a workgroup). */
+int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* stream);
+
+/* Row kernels over [rows][m] activations (one wave per row; m in {256, 512, 1024}), up to 3 heads.
+ * Forward, per head: v = x (ln: v = layer_norm(x) * g + beta, saving xhat [rows][m] and rstd [rows]); y = act(v)
+ * (act 1 tanh, 2 elu) -> y (ldy); tail: out[r] = y . w3 + b3[0]. td != null: td[r] = reward[r] + gamma *
+ * min(out_0[r], out_1[r]) (TDMPC._td_target, tdmpc.py:184-190).
+ * Backward, per head: d = tail ? dq[r] * w3 : x (dA, ldx); d *= act'(yact); ln: d = layer_norm backward (xhat, rstd,
+ * g) -> y (dP, ldy). part != null: per-workgroup column sums [nwg][..] of (ln: d*xhat, d) then (tail: dq*yact, dq),
+ * i.e. the partial gradients of the LayerNorm affine and of the scalar output layer. pi mode (q1 != null): dq of
+ * head h is d(-sum_t rho^t mean_b min(q1, q2)) / dq_h (ties split in half, as torch.min's backward). */
+typedef struct tdmpc_lg_rowhead {
+    const float* x; float* y; float* xhat; float* rstd; const float* yact;
+    const float* g; const float* beta; const float* w3; const float* b3; float* out; const float* dq; float* part;
+    int32_t ldx, ldy, ln, act, tail;
+} tdmpc_lg_rowhead;
+
+typedef struct tdmpc_lg_rows {
+    tdmpc_lg_rowhead hd[3];
+    int32_t nh, rows, m, bsz;
+    const float* reward; float* td; float gamma;
+    const float* q1; const float* q2; const float* rho;
+} tdmpc_lg_rows;
+
+int tdmpc_lg_rows_fwd(const tdmpc_lg_rows* a, void* stream);
+int tdmpc_lg_rows_bwd(const tdmpc_lg_rows* a, int32_t nwg, void* stream);
+
+/* pi_loss = sum_t rho^t * -(mean_b min(q1, q2)) over rows t * bsz + b, t < nt (TDMPC.update_pi) -> out[0]. */
+int tdmpc_lg_pi_loss(const float* q1, const float* q2, const float* rho, int32_t nt, int32_t bsz, float* out,
+                     void* stream);
+
+/* Gradient finalisation: parameter tensor i occupies g[dst, dst + rows * cols); its gradient is the sum of
+ * nslices slices src + s * sstride, element (r, c) at src[r * ld + c]. Writes g, per-workgroup sums of squares to
+ * normp (one workgroup per 2048 elements of a tensor; nblk = the capacity of normp, whose unused tail must hold
+ * zeros) and step[0] += 1 (the optimiser's step count). */
+typedef struct tdmpc_lg_gsrc {
+    const float* src; int64_t dst; int64_t sstride;
+    int32_t rows, cols, ld, nslices;
+} tdmpc_lg_gsrc;
+
+int tdmpc_lg_finalize(const tdmpc_lg_gsrc* t, int32_t nt, float* g, float* normp, int32_t nblk, int32_t* step,
+                      void* stream);
+
+/* clip_grad_norm_ (total norm = sqrt of the sum of normp [nblk]) + Adam (torch.optim.Adam, no weight decay) over n contiguous parameters;
+ * norm_out[0] = the total norm (clip_grad_norm_'s return value). */
+int tdmpc_lg_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* normp, int32_t nblk,
+                  const int32_t* step, float lr, float beta1, float beta2, float eps, float max_norm,
+                  float* norm_out, void* stream);
+
+/* t <- lerp(t, p, w) elementwise (helper.ema, helper.py:48-52). */
+int tdmpc_lg_lerp(float* t, const float* p, int64_t n, float w, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,7 +22,9 @@ EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc
             "tdmpc_replay_workspace_bytes", "tdmpc_replay_add_priorities", "tdmpc_replay_update_priorities",
             "tdmpc_replay_sample",
             # include/tdmpc_learner.h
-            "tdmpc_loss_forward", "tdmpc_loss_backward", "tdmpc_random_shift")
+            "tdmpc_loss_forward", "tdmpc_loss_backward", "tdmpc_random_shift",
+            "tdmpc_lg_gemm", "tdmpc_lg_rows_fwd", "tdmpc_lg_rows_bwd", "tdmpc_lg_pi_loss", "tdmpc_lg_finalize",
+            "tdmpc_lg_adam", "tdmpc_lg_lerp")
 
 
 class Dims(C.Structure):
@@ -65,6 +67,35 @@ class LossArgs(C.Structure):   # tdmpc_loss_args (include/tdmpc_learner.h)
     _fields_ = [(n, C.c_void_p) for n in ("zp", "nz", "q1", "q2", "rp", "rw", "td", "w", "rho")] + \
                [("H", C.c_int32), ("B", C.c_int32), ("L", C.c_int32), ("consistency_coef", C.c_float),
                 ("reward_coef", C.c_float), ("value_coef", C.c_float)]
+
+
+class LgSeg(C.Structure):       # tdmpc_lg_seg (include/tdmpc_learner.h)
+    _fields_ = [("a", C.c_void_p), ("b", C.c_void_p)] + \
+               [(n, C.c_int32) for n in ("lda", "ldb", "k", "amode", "bmode", "ones_col")]
+
+
+class LgJob(C.Structure):       # tdmpc_lg_job
+    _fields_ = [("seg", LgSeg * 3)] + [(n, C.c_int32) for n in ("nseg", "m", "n", "epi")] + \
+               [(n, C.c_void_p) for n in ("c", "c2", "bias", "aux", "res")] + \
+               [(n, C.c_int32) for n in ("ldc", "ldc2", "ldaux", "ldres")] + \
+               [("std_", C.c_float), ("splits", C.c_int32), ("slice", C.c_int64)]
+
+
+class LgRowHead(C.Structure):   # tdmpc_lg_rowhead
+    _fields_ = [(n, C.c_void_p) for n in ("x", "y", "xhat", "rstd", "yact", "g", "beta", "w3", "b3", "out", "dq",
+                                          "part")] + \
+               [(n, C.c_int32) for n in ("ldx", "ldy", "ln", "act", "tail")]
+
+
+class LgRows(C.Structure):      # tdmpc_lg_rows
+    _fields_ = [("hd", LgRowHead * 3)] + [(n, C.c_int32) for n in ("nh", "rows", "m", "bsz")] + \
+               [("reward", C.c_void_p), ("td", C.c_void_p), ("gamma", C.c_float),
+                ("q1", C.c_void_p), ("q2", C.c_void_p), ("rho", C.c_void_p)]
+
+
+class LgGsrc(C.Structure):      # tdmpc_lg_gsrc
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_int64), ("sstride", C.c_int64)] + \
+               [(n, C.c_int32) for n in ("rows", "cols", "ld", "nslices")]
 
 
 class Sizes(C.Structure):
@@ -116,6 +147,14 @@ def lib():
     L.tdmpc_loss_forward.argtypes = [C.POINTER(LossArgs), vp, vp, vp]
     L.tdmpc_loss_backward.argtypes = [C.POINTER(LossArgs), vp, vp, vp, vp, vp, vp, vp, vp]
     L.tdmpc_random_shift.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp]
+    L.tdmpc_lg_gemm.argtypes = [C.POINTER(LgJob), i32, i32, vp]
+    L.tdmpc_lg_rows_fwd.argtypes = [C.POINTER(LgRows), vp]
+    L.tdmpc_lg_rows_bwd.argtypes = [C.POINTER(LgRows), i32, vp]
+    L.tdmpc_lg_pi_loss.argtypes = [vp, vp, vp, i32, i32, vp, vp]
+    L.tdmpc_lg_finalize.argtypes = [C.POINTER(LgGsrc), i32, vp, vp, i32, vp, vp]
+    L.tdmpc_lg_adam.argtypes = [vp, vp, vp, vp, C.c_int64, vp, i32, vp, C.c_float, C.c_float, C.c_float,
+                                C.c_float, C.c_float, vp, vp]
+    L.tdmpc_lg_lerp.argtypes = [vp, vp, C.c_int64, C.c_float, vp]
     for name in EXPORTED:
         if not hasattr(L, name):
             raise RuntimeError(f"{LIB_PATH} does not export {name}")

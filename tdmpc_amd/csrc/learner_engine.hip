@@ -1,0 +1,644 @@
+// learner_engine.hip -- the learner's forward / backward passes over the TOLD heads for MI355X (gfx950).
+//
+// Reference: TDMPC.update / update_pi / _td_target, /root/reference/src/algorithm/tdmpc.py:165-245, over the
+// TOLD heads of helper.py:150-176 (enc, mlp, q) and TruncatedNormal.sample (helper.py:71-96). The reference
+// runs them as ~1,500 one-op launches through autograd; tdmpc_amd/learner_engine.py runs the same math as ~80
+// launches of four kernel families (include/tdmpc_learner.h):
+//   * lg_gemm_kernel: grouped fp32 GEMM on v_mfma_f32_32x32x2_f32 (exact f32 products, as the reference's
+//     fp32 Linear layers) with the bias, a residual, ELU / policy-sampling / activation-backward epilogues fused.
+//     Operands are read straight from L2 into the MFMA lane layout (each lane loads 4 consecutive k of its row /
+//     column; the MFMA's two k slots per step are then k and k + 4, a permutation of the sum), four waves of a
+//     workgroup split K and add through LDS, and up to 12 GEMMs of one pass (the heads, or every weight gradient
+//     of an update) share one launch.
+//   * lg_rows_fwd / lg_rows_bwd: one wave per row of 256 / 512 / 1024 features: LayerNorm + Tanh / ELU (+ the
+//     scalar output layer of the Q and reward heads as a row dot), and their backward, with the column sums that
+//     are the LayerNorm-affine and scalar-layer weight gradients written as per-workgroup partials.
+//   * lg_finalize / lg_adam: the gradient slices summed in a fixed order into one flat gradient, the global
+//     norm (clip_grad_norm_), Adam (torch.optim.Adam's update) over the flat parameter range; lg_lerp: the EMA.
+// Every reduction runs in a fixed order (no float atomics), so a graph replay equals the eager pass bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "../../include/tdmpc_hip.h"
+#include "../../include/tdmpc_learner.h"
+
+namespace tdmpc_internal {
+void set_error(const char* msg);
+}
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int LG_MAXJ = 12;
+constexpr unsigned LG_OOB = 0x7ffffff0u;   // buffer range of the operand descriptors; offsets >= it read 0
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+struct KJob {
+    tdmpc_lg_job j;
+    int tiles_m, block0, nb_mem[3];
+};
+struct KArgs {
+    KJob job[LG_MAXJ];
+    int njobs;
+};
+
+__device__ __forceinline__ float wsum(float v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
+
+// One K segment [k_lo, k_hi) of a wave's 32TM x 32TN tile: lane (r = lane & 31, h = lane >> 5) holds k0 + 4h ..
+// k0 + 4h + 3 of its rows / columns; MFMA step e then sums k0 + e and k0 + 4 + e. Waves take every fourth group
+// of 8 k. Out-of-range rows / columns / k read a clamped (valid) address and are replaced by 0; the next group
+// is loaded before the current one is multiplied.
+template <int AM, int BM, bool AV, bool BV, int TM, int TN>
+__device__ __forceinline__ void seg_loop(const tdmpc_lg_seg& S, int nb_mem, int k_lo, int k_hi, int m0, int n0,
+                                         int M, int N, floatx16 (&acc)[TM][TN], int wave, int r, int h) {
+    const int kb0 = k_lo + 8 * wave;
+    if (kb0 >= k_hi) return;
+    const int nit = (k_hi - kb0 + 31) / 32;
+    const float* __restrict__ A = S.a;
+    const float* __restrict__ B = S.b;
+    const int lda = S.lda, ldb = S.ldb;
+    int mrow[TM], ncol[TN];
+    bool mok[TM], nok[TN], one[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + 32 * i + r;
+        mok[i] = m < M;
+        mrow[i] = mok[i] ? m : M - 1;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + 32 * j + r;
+        nok[j] = n < N;
+        one[j] = n == S.ones_col;
+        ncol[j] = min(n, nb_mem - 1);
+    }
+    // buffer loads: an out-of-range offset returns 0 without a branch (a guarded plain load makes the compiler
+    // branch around it and wait for every load in flight)
+    const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)LG_OOB, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)LG_OOB, 0x00020000);
+    auto load = [&](int kb, float4 (&a)[TM], float4 (&b)[TN]) {
+        const bool kin = kb < k_hi;     // vector paths: whole groups of 8 (K % 8 == 0); past the end -> zeros
+        const int kc = kb;
+        const int k = kb + 4 * h;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            if constexpr (AM == 0 && AV) {
+                const unsigned off = (mok[i] && kin) ? (unsigned)(mrow[i] * lda + kc + 4 * h) * 4u : LG_OOB;
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsa, (int)off, 0, 0);
+                a[i] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                                   __uint_as_float(v.w));
+            } else {
+                float e[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const unsigned idx = AM == 0 ? (unsigned)(mrow[i] * lda + k + q) : (unsigned)((k + q) * lda + mrow[i]);
+                    const unsigned off = (mok[i] && k + q < k_hi) ? idx * 4u : LG_OOB;
+                    e[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsa, (int)off, 0, 0));
+                }
+                a[i] = make_float4(e[0], e[1], e[2], e[3]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            if constexpr (BM == 0 && BV) {
+                const unsigned off = (nok[j] && kin) ? (unsigned)(ncol[j] * ldb + kc + 4 * h) * 4u : LG_OOB;
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsb, (int)off, 0, 0);
+                b[j] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                                   __uint_as_float(v.w));
+            } else {
+                float e[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const bool kv = k + q < k_hi;
+                    const unsigned idx = BM == 0 ? (unsigned)(ncol[j] * ldb + k + q) : (unsigned)((k + q) * ldb + ncol[j]);
+                    const unsigned off = (nok[j] && !one[j] && kv) ? idx * 4u : LG_OOB;
+                    e[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsb, (int)off, 0, 0));
+                }
+                b[j] = make_float4(e[0], e[1], e[2], e[3]);
+            }
+        }
+    };
+    // a ring of D groups in flight: the loads of group g + D - 1 are issued (sched_barrier keeps them ahead of
+    // the MFMAs) before group g is multiplied; groups past the end load zeros, so the trip count needs no tail
+    constexpr int D = TM * TN >= 4 ? 2 : 4;
+    float4 ra[D][TM], rb[D][TN];
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) load(kb0 + 32 * d, ra[d], rb[d]);
+    for (int it = 0; it < nit; it += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            load(kb0 + 32 * (it + d + D - 1), ra[(d + D - 1) % D], rb[(d + D - 1) % D]);
+            __builtin_amdgcn_sched_barrier(0);
+            // (no arithmetic on freshly loaded registers before the barrier: it would wait for those loads)
+            float4 bu[TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                bu[j] = rb[d][j];
+                if constexpr (AM == 1) {   // weight gradients: the bias column of ones, inside K only
+                    const int k = kb0 + 32 * (it + d) + 4 * h;
+                    bu[j].x += (one[j] && k < k_hi) ? 1.f : 0.f;
+                    bu[j].y += (one[j] && k + 1 < k_hi) ? 1.f : 0.f;
+                    bu[j].z += (one[j] && k + 2 < k_hi) ? 1.f : 0.f;
+                    bu[j].w += (one[j] && k + 3 < k_hi) ? 1.f : 0.f;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[d][i].x, bu[j].x, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[d][i].y, bu[j].y, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[d][i].z, bu[j].z, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[d][i].w, bu[j].w, acc[i][j], 0, 0, 0);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
+__device__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+template <int TM, int TN>
+__global__ void __launch_bounds__(256) lg_gemm_kernel(const KArgs P) {
+    __shared__ float red[4][TM * TN * 16][64];
+    int jb = 0;
+    for (int q = 1; q < P.njobs; ++q)
+        if ((int)blockIdx.x >= P.job[q].block0) jb = q;
+    const KJob& J = P.job[jb];
+    const int local = (int)blockIdx.x - J.block0;
+    const int splits = J.j.splits, split = local % splits, tile = local / splits;
+    const int m0 = (tile % J.tiles_m) * 32 * TM, n0 = (tile / J.tiles_m) * 32 * TN;
+    const int M = J.j.m, N = J.j.n;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    for (int s = 0; s < J.j.nseg; ++s) {
+        const tdmpc_lg_seg& S = J.j.seg[s];
+        int k_lo = 0, k_hi = S.k;
+        if (splits > 1) {
+            const int chunk = ((S.k + splits - 1) / splits + 7) & ~7;
+            k_lo = min(S.k, split * chunk);
+            k_hi = min(S.k, k_lo + chunk);
+        }
+        if (k_hi <= k_lo) continue;
+        const int nbm = J.nb_mem[s];
+        const bool av = S.amode == 0 && S.lda % 4 == 0 && S.k % 8 == 0 && al16(S.a);
+        const bool bv = S.bmode == 0 && S.ldb % 4 == 0 && S.k % 8 == 0 && al16(S.b);
+        if (S.amode == 1) {
+            seg_loop<1, 1, false, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
+        } else if (S.bmode == 1) {
+            if (av) seg_loop<0, 1, true, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
+            else seg_loop<0, 1, false, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
+        } else {
+            if (av && bv) seg_loop<0, 0, true, true, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
+            else if (av) seg_loop<0, 0, true, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
+            else if (bv) seg_loop<0, 0, false, true, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
+            else seg_loop<0, 0, false, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
+        }
+    }
+
+    // the four waves' K partials -> LDS; each wave finishes a quarter of the tile (C/D map of the 32x32 MFMA:
+    // col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5))
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) red[wave][(i * TN + j) * 16 + e][lane] = acc[i][j][e];
+    __syncthreads();
+    constexpr int QN = TM * TN * 4;
+    const tdmpc_lg_job& JJ = J.j;
+    for (int q = wave * QN; q < (wave + 1) * QN; ++q) {
+        const float v = red[0][q][lane] + red[1][q][lane] + red[2][q][lane] + red[3][q][lane];
+        const int i = q / (TN * 16), j = (q / 16) % TN, e = q % 16;
+        const int row = m0 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h, col = n0 + 32 * j + r;
+        if (row >= M || col >= N) continue;
+        if (splits > 1) {
+            JJ.c[(size_t)split * JJ.slice + (size_t)row * JJ.ldc + col] = v;
+            continue;
+        }
+        float x = v;
+        if (JJ.bias) x += JJ.bias[col];
+        if (JJ.res) x += JJ.res[(size_t)row * JJ.ldres + col];
+        switch (JJ.epi) {
+        case TDMPC_LG_EPI_ELU: x = elu_f(x); break;
+        case TDMPC_LG_EPI_PI: {
+            const float mu = tanhf(x);
+            const float e2 = fminf(fmaxf(JJ.std_ * JJ.aux[(size_t)row * JJ.ldaux + col], -0.3f), 0.3f);
+            x = fminf(fmaxf(mu + e2, -1.0f + 1e-6f), 1.0f - 1e-6f);
+            JJ.c2[(size_t)row * JJ.ldc2 + col] = mu;
+            break;
+        }
+        case TDMPC_LG_EPI_ELU_BWD: {
+            const float y = JJ.aux[(size_t)row * JJ.ldaux + col];
+            x *= y > 0.f ? 1.f : y + 1.f;
+            break;
+        }
+        case TDMPC_LG_EPI_PI_BWD: {
+            const float mu = JJ.aux[(size_t)row * JJ.ldaux + col];
+            x *= 1.f - mu * mu;
+            break;
+        }
+        default:
+            if (JJ.c2) JJ.c2[(size_t)row * JJ.ldc2 + col] = x;
+        }
+        JJ.c[(size_t)row * JJ.ldc + col] = x;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------- rows
+template <int NC>
+__global__ void __launch_bounds__(256) lg_rows_fwd_kernel(const tdmpc_lg_rows a) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= a.rows) return;
+    const int m = a.m;
+    const float inv_m = 1.f / (float)m;
+    float outv[3] = {0.f, 0.f, 0.f};
+    for (int hh = 0; hh < a.nh; ++hh) {
+        const tdmpc_lg_rowhead& H = a.hd[hh];
+        float x[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) x[c] = H.x[(size_t)r * H.ldx + lane + 64 * c];
+        if (H.ln) {
+            float s = 0.f;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) s += x[c];
+            const float mean = wsum(s) * inv_m;
+            float d = 0.f;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) d += (x[c] - mean) * (x[c] - mean);
+            const float rs = 1.f / sqrtf(wsum(d) * inv_m + 1e-5f);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int n = lane + 64 * c;
+                const float xh = (x[c] - mean) * rs;
+                if (H.xhat) H.xhat[(size_t)r * m + n] = xh;
+                x[c] = xh * H.g[n] + H.beta[n];
+            }
+            if (H.rstd && lane == 0) H.rstd[r] = rs;
+        }
+        float dot = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int n = lane + 64 * c;
+            const float y = H.act == 1 ? tanhf(x[c]) : H.act == 2 ? elu_f(x[c]) : x[c];
+            if (H.y) H.y[(size_t)r * H.ldy + n] = y;
+            if (H.tail) dot += y * H.w3[n];
+        }
+        if (H.tail) {
+            const float o = wsum(dot) + H.b3[0];
+            outv[hh] = o;
+            if (H.out && lane == 0) H.out[r] = o;
+        }
+    }
+    if (a.td && lane == 0) a.td[r] = a.reward[r] + a.gamma * fminf(outv[0], outv[1]);
+}
+
+template <int NC>
+__global__ void __launch_bounds__(256) lg_rows_bwd_kernel(const tdmpc_lg_rows a) {
+    __shared__ float red[4][3 * NC * 64 + 1];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int m = a.m;
+    const float inv_m = 1.f / (float)m;
+    const int stride = gridDim.x * 4;
+    for (int hh = 0; hh < a.nh; ++hh) {
+        const tdmpc_lg_rowhead& H = a.hd[hh];
+        float pg[NC], pb[NC], pw[NC], pq = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) pg[c] = pb[c] = pw[c] = 0.f;
+        for (int r = blockIdx.x * 4 + wave; r < a.rows; r += stride) {
+            float d[NC], y[NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) y[c] = H.yact[(size_t)r * m + lane + 64 * c];
+            if (H.tail) {
+                float dq;
+                if (a.q1) {   // update_pi: d(-sum_t rho^t mean_b min(q1, q2)) / dq_head
+                    const float q1 = a.q1[r], q2 = a.q2[r];
+                    const float base = -a.rho[r / a.bsz] / (float)a.bsz;
+                    dq = q1 == q2 ? 0.5f * base : ((q1 < q2) == (hh == 0) ? base : 0.f);
+                } else {
+                    dq = H.dq[r];
+                }
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    d[c] = dq * H.w3[lane + 64 * c];
+                    pw[c] += dq * y[c];
+                }
+                pq += dq;
+            } else {
+#pragma unroll
+                for (int c = 0; c < NC; ++c) d[c] = H.x[(size_t)r * H.ldx + lane + 64 * c];
+            }
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                d[c] *= H.act == 1 ? 1.f - y[c] * y[c] : H.act == 2 ? (y[c] > 0.f ? 1.f : y[c] + 1.f) : 1.f;
+            if (H.ln) {
+                const float rs = H.rstd[r];
+                float xh[NC], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    const int n = lane + 64 * c;
+                    xh[c] = H.xhat[(size_t)r * m + n];
+                    pb[c] += d[c];
+                    pg[c] += d[c] * xh[c];
+                    d[c] *= H.g[n];
+                    s1 += d[c];
+                    s2 += d[c] * xh[c];
+                }
+                s1 = wsum(s1) * inv_m;
+                s2 = wsum(s2) * inv_m;
+#pragma unroll
+                for (int c = 0; c < NC; ++c) d[c] = rs * (d[c] - s1 - xh[c] * s2);
+            }
+#pragma unroll
+            for (int c = 0; c < NC; ++c) H.y[(size_t)r * H.ldy + lane + 64 * c] = d[c];
+        }
+        if (!H.part) continue;
+        // partial column sums of this workgroup: [dg (m), dbeta (m)] if ln, then [dW3 (m), db3] if tail
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            red[wave][c * 64 + lane] = pg[c];
+            red[wave][(NC + c) * 64 + lane] = pb[c];
+            red[wave][(2 * NC + c) * 64 + lane] = pw[c];
+        }
+        if (lane == 0) red[wave][3 * NC * 64] = pq;   // the same in every lane (dq is a per-row scalar)
+        __syncthreads();
+        const int pw_n = (H.ln ? 2 * m : 0) + (H.tail ? m + 1 : 0);
+        float* out = H.part + (size_t)blockIdx.x * pw_n;
+        for (int i = threadIdx.x; i < pw_n; i += 256) {
+            int src;
+            if (H.ln && i < 2 * m) src = i;                       // dg | dbeta
+            else {
+                const int t = i - (H.ln ? 2 * m : 0);
+                src = t < m ? 2 * m + t : 3 * NC * 64;          // dW3 | db3
+            }
+            out[i] = red[0][src] + red[1][src] + red[2][src] + red[3][src];
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(256) lg_pi_loss_kernel(const float* q1, const float* q2, const float* rho,
+                                                         int nt, int bsz, float* out) {
+    __shared__ float red[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float loss = 0.f;
+    for (int t = 0; t < nt; ++t) {
+        float s = 0.f;
+        for (int b = threadIdx.x; b < bsz; b += 256) s += fminf(q1[t * bsz + b], q2[t * bsz + b]);
+        s = wsum(s);
+        if (lane == 0) red[wave] = s;
+        __syncthreads();
+        const float tot = red[0] + red[1] + red[2] + red[3];
+        __syncthreads();
+        loss += -(tot / (float)bsz) * rho[t];
+    }
+    if (threadIdx.x == 0) out[0] = loss;
+}
+
+// ------------------------------------------------------------------------------------------ optimiser
+constexpr int LG_MAXT = 48;
+constexpr int LG_FIN_PER = 2048;   // gradient elements per lg_finalize workgroup (8 per thread)
+struct FArgs {
+    tdmpc_lg_gsrc t[LG_MAXT];
+    int block0[LG_MAXT];
+    int nt;
+};
+
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+    v = wsum(v);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+}
+
+// workgroup -> (tensor, chunk of 2048 elements); each element sums its slices in order
+__global__ void __launch_bounds__(256) lg_finalize_kernel(const FArgs F, float* g, float* normp, int* step) {
+    __shared__ float red[4];
+    int ti = 0;
+    for (int q = 1; q < F.nt; ++q)
+        if ((int)blockIdx.x >= F.block0[q]) ti = q;
+    const tdmpc_lg_gsrc& T = F.t[ti];
+    const long n = (long)T.rows * T.cols;
+    const long e0 = (long)(blockIdx.x - F.block0[ti]) * LG_FIN_PER;
+    float sq = 0.f;
+#pragma unroll
+    for (int u = 0; u < LG_FIN_PER / 256; ++u) {
+        const long loc = e0 + u * 256 + threadIdx.x;
+        if (loc < n) {
+            const int rr = (int)(loc / T.cols), cc = (int)(loc % T.cols);
+            const float* p = T.src + (size_t)rr * T.ld + cc;
+            float v = 0.f;
+            for (int k = 0; k < T.nslices; ++k) v += p[(size_t)k * T.sstride];
+            g[T.dst + loc] = v;
+            sq += v * v;
+        }
+    }
+    const float tot = block_sum256(sq, red);
+    if (threadIdx.x == 0) {
+        normp[blockIdx.x] = tot;
+        if (blockIdx.x == 0 && step) step[0] += 1;
+    }
+}
+
+__global__ void __launch_bounds__(256) lg_adam_kernel(float* p, const float* g, float* m, float* v, long n,
+                                                      const float* normp, int nblk, const int* step, float lr,
+                                                      float b1, float b2, float eps, float max_norm,
+                                                      float* norm_out) {
+    __shared__ float red[4];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < nblk; i += 256) s += normp[i];
+    const float total = sqrtf(block_sum256(s, red));
+    const float coef = fminf(max_norm / (total + 1e-6f), 1.0f);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = total;
+    const int t = step[0];
+    const double bc1 = 1.0 - pow((double)b1, (double)t), bc2 = 1.0 - pow((double)b2, (double)t);
+    const float step_size = (float)(lr / bc1);
+    const float bc2_sqrt = (float)sqrt(bc2);
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const float gi = g[i] * coef;
+        const float mi = m[i] + (1.f - b1) * (gi - m[i]);     // exp_avg.lerp_(grad, 1 - beta1)
+        const float vi = v[i] * b2 + (1.f - b2) * gi * gi;  // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        p[i] = p[i] - step_size * (mi / denom);
+    }
+}
+
+__global__ void __launch_bounds__(256) lg_lerp_kernel(float* t, const float* p, long n, float w) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const float a = t[i], b = p[i];
+        t[i] = w < 0.5f ? a + w * (b - a) : b - (b - a) * (1.f - w);
+    }
+}
+
+int fail(hipError_t e, const char* what) {
+    char msg[256];
+    snprintf(msg, sizeof msg, "learner_engine %s: %s", what, hipGetErrorString(e));
+    tdmpc_internal::set_error(msg);
+    return TDMPC_E_HIP;
+}
+
+int bad(const char* what) {
+    tdmpc_internal::set_error(what);
+    return TDMPC_E_DIMS;
+}
+
+int launched(const char* what) {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(e, what);
+}
+
+}  // namespace
+
+extern "C" {
+
+int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* stream) {
+    if (!jobs) return TDMPC_E_NULL;
+    if (njobs <= 0 || njobs > LG_MAXJ || (tile != 1 && tile != 2)) return bad("tdmpc_lg_gemm: njobs / tile");
+    KArgs P;
+    memset(&P, 0, sizeof P);
+    const int tw = 32 * tile;
+    long blocks = 0;
+    for (int q = 0; q < njobs; ++q) {
+        const tdmpc_lg_job& j = jobs[q];
+        if (!j.c || j.m <= 0 || j.n <= 0 || j.nseg < 1 || j.nseg > 3 || j.splits < 1 || j.splits > 64)
+            return bad("tdmpc_lg_gemm: job shape");
+        if (j.splits > 1 && (j.bias || j.res || j.epi != TDMPC_LG_EPI_NONE || j.c2))
+            return bad("tdmpc_lg_gemm: split-K job with an epilogue");
+        if ((j.epi == TDMPC_LG_EPI_PI && (!j.aux || !j.c2)) ||
+            ((j.epi == TDMPC_LG_EPI_ELU_BWD || j.epi == TDMPC_LG_EPI_PI_BWD) && !j.aux))
+            return bad("tdmpc_lg_gemm: epilogue operand missing");
+        P.job[q].j = j;
+        for (int s = 0; s < j.nseg; ++s) {
+            const tdmpc_lg_seg& S = j.seg[s];
+            if (!S.a || (!S.b && S.ones_col < 0) || S.k <= 0) return bad("tdmpc_lg_gemm: segment");
+            if (S.amode == 1 && S.bmode != 1) return bad("tdmpc_lg_gemm: amode 1 needs bmode 1");
+            // columns of B that exist in memory: all N, or those before the ones column
+            P.job[q].nb_mem[s] = S.ones_col >= 0 ? S.ones_col : j.n;
+            if (P.job[q].nb_mem[s] < 1) return bad("tdmpc_lg_gemm: ones column");
+        }
+        const int tm = (j.m + tw - 1) / tw, tn = (j.n + tw - 1) / tw;
+        P.job[q].tiles_m = tm;
+        P.job[q].block0 = (int)blocks;
+        blocks += (long)tm * tn * j.splits;
+    }
+    P.njobs = njobs;
+    if (blocks >= (1L << 31)) return bad("tdmpc_lg_gemm: grid");
+    if (tile == 1)
+        hipLaunchKernelGGL((lg_gemm_kernel<1, 1>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, P);
+    else
+        hipLaunchKernelGGL((lg_gemm_kernel<2, 2>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, P);
+    return launched("gemm");
+}
+
+static int rows_ok(const tdmpc_lg_rows* a) {
+    if (!a) return TDMPC_E_NULL;
+    if (a->nh < 1 || a->nh > 3 || a->rows <= 0 || (a->m != 256 && a->m != 512 && a->m != 1024))
+        return bad("tdmpc_lg_rows: nh / rows / m");
+    return 0;
+}
+
+int tdmpc_lg_rows_fwd(const tdmpc_lg_rows* a, void* stream) {
+    if (int rc = rows_ok(a)) return rc;
+    if (a->td && (a->nh < 2 || !a->reward)) return bad("tdmpc_lg_rows_fwd: td needs two tail heads");
+    const dim3 g((a->rows + 3) / 4);
+    hipStream_t s = (hipStream_t)stream;
+    if (a->m == 256) hipLaunchKernelGGL(lg_rows_fwd_kernel<4>, g, dim3(256), 0, s, *a);
+    else if (a->m == 512) hipLaunchKernelGGL(lg_rows_fwd_kernel<8>, g, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL(lg_rows_fwd_kernel<16>, g, dim3(256), 0, s, *a);
+    return launched("rows_fwd");
+}
+
+int tdmpc_lg_rows_bwd(const tdmpc_lg_rows* a, int32_t nwg, void* stream) {
+    if (int rc = rows_ok(a)) return rc;
+    if (nwg < 1 || nwg > 4096) return bad("tdmpc_lg_rows_bwd: nwg");
+    for (int h = 0; h < a->nh; ++h) {
+        const tdmpc_lg_rowhead& H = a->hd[h];
+        if (!H.y || !H.yact || (H.ln && (!H.xhat || !H.rstd || !H.g)) || (H.tail && (!H.w3 || (!H.dq && !a->q1))) ||
+            (!H.tail && !H.x))
+            return TDMPC_E_NULL;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (a->m == 256) hipLaunchKernelGGL(lg_rows_bwd_kernel<4>, dim3(nwg), dim3(256), 0, s, *a);
+    else if (a->m == 512) hipLaunchKernelGGL(lg_rows_bwd_kernel<8>, dim3(nwg), dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL(lg_rows_bwd_kernel<16>, dim3(nwg), dim3(256), 0, s, *a);
+    return launched("rows_bwd");
+}
+
+int tdmpc_lg_pi_loss(const float* q1, const float* q2, const float* rho, int32_t nt, int32_t bsz, float* out,
+                     void* stream) {
+    if (!q1 || !q2 || !rho || !out) return TDMPC_E_NULL;
+    if (nt <= 0 || bsz <= 0) return bad("tdmpc_lg_pi_loss: dims");
+    hipLaunchKernelGGL(lg_pi_loss_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, q1, q2, rho, nt, bsz, out);
+    return launched("pi_loss");
+}
+
+int tdmpc_lg_finalize(const tdmpc_lg_gsrc* t, int32_t nt, float* g, float* normp, int32_t nblk, int32_t* step,
+                      void* stream) {
+    if (!t || !g || !normp) return TDMPC_E_NULL;
+    if (nt <= 0 || nt > LG_MAXT || nblk <= 0) return bad("tdmpc_lg_finalize: nt / nblk");
+    FArgs F;
+    memset(&F, 0, sizeof F);
+    long off = 0;
+    int blocks = 0;
+    for (int i = 0; i < nt; ++i) {
+        if (!t[i].src || t[i].dst != off || t[i].rows <= 0 || t[i].cols <= 0 || t[i].nslices <= 0 ||
+            t[i].ld < t[i].cols)
+            return bad("tdmpc_lg_finalize: tensors must tile [0, total) in order");
+        F.t[i] = t[i];
+        F.block0[i] = blocks;
+        const long n = (long)t[i].rows * t[i].cols;
+        off += n;
+        blocks += (int)((n + LG_FIN_PER - 1) / LG_FIN_PER);
+    }
+    if (blocks > nblk) return bad("tdmpc_lg_finalize: normp holds fewer entries than workgroups");
+    F.nt = nt;
+    hipLaunchKernelGGL(lg_finalize_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, F, g, normp, step);
+    return launched("finalize");
+}
+
+int tdmpc_lg_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* normp, int32_t nblk,
+                  const int32_t* step, float lr, float beta1, float beta2, float eps, float max_norm,
+                  float* norm_out, void* stream) {
+    if (!p || !g || !m || !v || !normp || !step) return TDMPC_E_NULL;
+    if (n <= 0 || nblk <= 0) return bad("tdmpc_lg_adam: dims");
+    const unsigned blocks = (unsigned)std::min<long>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(lg_adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (long)n, normp,
+                       nblk, step, lr, beta1, beta2, eps, max_norm, norm_out);
+    return launched("adam");
+}
+
+int tdmpc_lg_lerp(float* t, const float* p, int64_t n, float w, void* stream) {
+    if (!t || !p) return TDMPC_E_NULL;
+    if (n <= 0) return bad("tdmpc_lg_lerp: n");
+    const unsigned blocks = (unsigned)std::min<long>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(lg_lerp_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, t, p, (long)n, w);
+    return launched("lerp");
+}
+
+}  // extern "C"

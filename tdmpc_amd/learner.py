@@ -131,9 +131,17 @@ class Learner:
         self.params = list(model.parameters())
         self.pi_params = list(model._pi.parameters())
         self.target_params = list(agent.model_target.parameters())
-        # tdmpc.py:62-63 (Adam over all TOLD parameters; the policy's own Adam, both at cfg.lr)
-        agent.optim = torch.optim.Adam(self.params, lr=self.cfg.lr, capturable=graph, fused=True)
-        agent.pi_optim = torch.optim.Adam(self.pi_params, lr=self.cfg.lr, capturable=graph, fused=True)
+        from . import learner_engine
+        self.engine = None
+        if str(agent.device).startswith("cuda") and learner_engine.supported(self.cfg):
+            # explicit forward / backward kernels over flat parameters (tdmpc_amd/learner_engine.py); its two
+            # Adam states stand in for the reference's optimisers
+            self.engine = learner_engine.Engine(agent)
+            agent.optim, agent.pi_optim = self.engine.opt_main, self.engine.opt_pi
+        else:
+            # tdmpc.py:62-63 (Adam over all TOLD parameters; the policy's own Adam, both at cfg.lr)
+            agent.optim = torch.optim.Adam(self.params, lr=self.cfg.lr, capturable=graph, fused=True)
+            agent.pi_optim = torch.optim.Adam(self.pi_params, lr=self.cfg.lr, capturable=graph, fused=True)
         self.calls = 0
         self._graphs = {}
         H = self.cfg.horizon
@@ -152,6 +160,8 @@ class Learner:
     def update_pi(self, zs, eps=None):
         """tdmpc.py:165-182 -> pi_loss (tensor): the H+1 latents in one pass, sum_t -mean(min Q_t) rho^t."""
         a, cfg = self.agent, self.cfg
+        if self.engine is not None:
+            return self.engine.update_pi(zs, eps)
         a.pi_optim.zero_grad(set_to_none=True)
         a.model.track_q_grad(False)
         n = len(zs)
@@ -168,6 +178,8 @@ class Learner:
     def step(self, buffer, noise=None):
         """One TDMPC.update without the EMA (tdmpc.py:192-241) -> metrics tensor [7] (METRICS order).
         noise: optional list of 2H+1 [B, A] TruncatedNormal draws (H for the TD targets, H+1 for update_pi)."""
+        if self.engine is not None:
+            return self.engine.update(buffer, noise)
         a, cfg = self.agent, self.cfg
         m = a.model
         H = cfg.horizon
@@ -226,6 +238,8 @@ class Learner:
     @torch.no_grad()
     def ema(self):
         """helper.py:48-52: target <- lerp(target, model, tau)."""
+        if self.engine is not None:
+            return self.engine.ema(self.cfg.tau)
         torch._foreach_lerp_(self.target_params, self.params, self.cfg.tau)
 
     # ------------------------------------------------------------------ graph driver

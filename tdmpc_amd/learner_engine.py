@@ -1,0 +1,480 @@
+"""The learner engine: one TDMPC.update (tdmpc.py:192-245) as explicit forward and backward passes of HIP kernels.
+
+Reference: /root/reference/src/algorithm/tdmpc.py:165-245 (update_pi, _td_target, update), helper.py:150-176
+(TOLD heads), helper.py:71-96 (TruncatedNormal.sample), helper.py:48-52 (ema), torch.optim.Adam and
+clip_grad_norm_ as the reference calls them (tdmpc.py:62-63, 180, 236). The math is the reference's; what is
+different is that no autograd graph is built: the backward of every head is written out (include/tdmpc_learner.h
+documents each kernel), so an update is ~80 launches instead of ~400 autograd / hipBLASLt kernels (ours before)
+or ~1,500 (the reference).
+
+Layout (device, float32):
+  * every TOLD parameter is a view into ONE flat buffer P (likewise the target into PT), ordered encoder, dynamics,
+    reward, Q1, Q2 | pi, so the main optimiser is one Adam pass over P[:n_main] and the policy optimiser one over
+    P[n_main:]; gradients go to the flat G, Adam moments to flat M / V;
+  * X0 [(H+1) B][L+A]: rows t*B..t*B+B-1 hold (z_t, a_t) -- the encoder writes z_0, dynamics step t writes z_{t+1}
+    into block t+1 -- so the Q / reward heads read all H steps as one [H B][L+A] operand and the policy update reads
+    the H+1 latents in place (stride L+A);
+  * activations saved for the backward: each hidden layer's output (ELU / Tanh output; the derivative is a function
+    of it), the LayerNorm's xhat and 1/std per row.
+Weight gradients: one grouped split-K GEMM launch per optimiser (every dW with the bias as a column of ones), the
+LayerNorm affine and scalar output layers as per-workgroup column sums; lg_finalize sums the slices in a fixed order
+(so graph replay == eager, bitwise), lg_adam clips by the global norm and applies Adam.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+
+ELU, TANH = 2, 1
+EPI_NONE, EPI_ELU, EPI_PI, EPI_ELU_BWD, EPI_PI_BWD = 0, 1, 2, 3, 4
+NBLK = 2048         # capacity of the norm partials (one per lg_finalize workgroup of 2048 gradients)
+ROWS_NWG = 80       # lg_rows_bwd workgroups (column-sum partials per head)
+
+
+def supported(cfg) -> bool:
+    """State observations, the plain encoder, hidden width 256 / 512 / 1024 (one wave per row in the row kernels)."""
+    return (getattr(cfg, "modality", "state") == "state" and not getattr(cfg, "enc_norm", False)
+            and int(cfg.mlp_dim) in (256, 512, 1024))
+
+
+def _p(t, off: int = 0) -> int:
+    return t.data_ptr() + 4 * off
+
+
+def _seg(a, lda, b, ldb, k, amode=0, bmode=0, ones=-1):
+    return (a, b, lda, ldb, k, amode, bmode, ones)
+
+
+class _Adam:
+    """Adam state of one flat parameter range (the engine's counterpart of agent.optim / agent.pi_optim)."""
+
+    def __init__(self, params, lo, hi, lr, device):
+        self.lo, self.hi, self.lr = lo, hi, lr
+        self.exp_avg = torch.zeros(hi - lo, device=device)
+        self.exp_avg_sq = torch.zeros(hi - lo, device=device)
+        self.step_t = torch.zeros(1, dtype=torch.int32, device=device)
+        self.param_groups = [{"params": params, "lr": lr, "betas": (0.9, 0.999), "eps": 1e-8}]
+
+    def state_dict(self):
+        return {"step": self.step_t, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
+
+
+class Engine:
+    def __init__(self, agent):
+        self.agent = agent
+        cfg = self.cfg = agent.cfg
+        self.dev = torch.device(agent.device)
+        self.O, self.E, self.L = int(cfg.obs_shape[0]), int(cfg.enc_dim), int(cfg.latent_dim)
+        self.A, self.M, self.H = int(cfg.action_dim), int(cfg.mlp_dim), int(cfg.horizon)
+        self.LA = self.L + self.A
+        order = ["_encoder", "_dynamics", "_reward", "_Q1", "_Q2", "_pi"]
+        self.off = {}
+        sd = agent.model.state_dict()
+        names = [k for pre in order for k in sd if k.startswith(pre + ".")]
+        assert len(names) == len(sd), "unexpected TOLD parameters"
+        total = sum(sd[k].numel() for k in names)
+        self.P = torch.empty(total, device=self.dev)
+        self.PT = torch.empty(total, device=self.dev)
+        self.G = torch.zeros(total, device=self.dev)
+        off = 0
+        for k in names:
+            self.off[k] = (off, tuple(sd[k].shape))
+            off += sd[k].numel()
+        self.n_main = self.off["_pi.0.weight"][0]
+        self._alias(agent.model, self.P)
+        self._alias(agent.model_target, self.PT)
+        lr = float(cfg.lr)
+        params = dict(agent.model.named_parameters())
+        self.opt_main = _Adam([params[k] for k in names if not k.startswith("_pi.")], 0, self.n_main, lr, self.dev)
+        self.opt_pi = _Adam([params[k] for k in names if k.startswith("_pi.")], self.n_main, total, lr, self.dev)
+        self.normp = torch.zeros(2, NBLK, device=self.dev)
+        self.rho = torch.tensor([cfg.rho ** t for t in range(self.H + 1)], dtype=torch.float32, device=self.dev)
+        self.gw = torch.full((1,), 1.0, dtype=torch.float32, device=self.dev) * (1 / self.H)   # the 1/H hook
+        self._bufs = {}
+        self.lib = _lib.lib()
+
+    def _alias(self, model, flat):
+        """Make every parameter of `model` a view into `flat` (values kept)."""
+        with torch.no_grad():
+            for k, p in model.named_parameters():
+                o, shape = self.off[k]
+                n = p.numel()
+                flat[o:o + n].copy_(p.detach().reshape(-1))
+                p.data = flat[o:o + n].view(shape)
+
+    # ---------------------------------------------------------------------------------------------- helpers
+    def w(self, k, target=False):
+        o, _ = self.off[k]
+        return _p(self.PT if target else self.P, o)
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def gemm(self, jobs, tile=None):
+        """jobs: dicts (segs, m, n, c, ldc, bias, epi, aux, ldaux, res, ldres, c2, ldc2, std, splits, slice)."""
+        arr = (_lib.LgJob * len(jobs))()
+        tiles64 = 0
+        for i, j in enumerate(jobs):
+            J = arr[i]
+            segs = j["segs"]
+            for s, sg in enumerate(segs):
+                a, b, lda, ldb, k, am, bm, ones = sg
+                J.seg[s].a, J.seg[s].b = a, b
+                J.seg[s].lda, J.seg[s].ldb, J.seg[s].k = lda, ldb, k
+                J.seg[s].amode, J.seg[s].bmode, J.seg[s].ones_col = am, bm, ones
+            J.nseg, J.m, J.n, J.epi = len(segs), j["m"], j["n"], j.get("epi", EPI_NONE)
+            J.c, J.ldc = j["c"], j["ldc"]
+            J.c2, J.ldc2 = j.get("c2"), j.get("ldc2", 0)
+            J.bias = j.get("bias")
+            J.aux, J.ldaux = j.get("aux"), j.get("ldaux", 0)
+            J.res, J.ldres = j.get("res"), j.get("ldres", 0)
+            J.std_ = j.get("std", 0.0)
+            J.splits, J.slice = j.get("splits", 1), j.get("slice", 0)
+            tiles64 += -(-j["m"] // 64) * -(-j["n"] // 64) * J.splits
+        if tile is None:
+            tile = 2 if tiles64 >= 240 else 1
+        _lib.check(self.lib.tdmpc_lg_gemm(arr, len(jobs), tile, self._stream()), "tdmpc_lg_gemm")
+
+    def rows(self, heads, n, bwd=False, **kw):
+        a = _lib.LgRows()
+        for i, h in enumerate(heads):
+            H = a.hd[i]
+            for f in ("x", "y", "xhat", "rstd", "yact", "g", "beta", "w3", "b3", "out", "dq", "part"):
+                setattr(H, f, h.get(f))
+            H.ldx, H.ldy = h.get("ldx", self.M), h.get("ldy", self.M)
+            H.ln, H.act, H.tail = int(h.get("ln", 0)), h["act"], int(h.get("tail", 0))
+        a.nh, a.rows, a.m, a.bsz = len(heads), n, self.M, kw.get("bsz", 1)
+        a.reward, a.td, a.gamma = kw.get("reward"), kw.get("td"), kw.get("gamma", 0.0)
+        a.q1, a.q2, a.rho = kw.get("q1"), kw.get("q2"), kw.get("rho")
+        if bwd:
+            _lib.check(self.lib.tdmpc_lg_rows_bwd(C.byref(a), ROWS_NWG, self._stream()), "tdmpc_lg_rows_bwd")
+        else:
+            _lib.check(self.lib.tdmpc_lg_rows_fwd(C.byref(a), self._stream()), "tdmpc_lg_rows_fwd")
+
+    def bufs(self, B):
+        b = self._bufs.get(B)
+        if b is not None:
+            return b
+        H, L, A, M, E, O, LA = self.H, self.L, self.A, self.M, self.E, self.O, self.LA
+        R, R1 = H * B, (H + 1) * B
+        z = lambda *s: torch.zeros(*s, device=self.dev)  # noqa: E731
+        b = dict(
+            eps=z((2 * H + 1) * B, A),
+            # TD target
+            Yt1=z(R, E), Yo1=z(R, E), NZ=z(R, L), Xtd=z(R, LA), T1=z(R, M), T2=z(R, M), MUtd=z(R, A),
+            TQ=z(2, R), TD=z(R),
+            # main forward
+            Ye1=z(B, E), X0=z(R1, LA), Yd1=z(R, M), Yd2=z(R, M), ZP=z(R, L),
+            PA=z(3, R1, M), PB=z(3, R1, M), Y1=z(2, R1, M), Y2=z(3, R1, M), XH1=z(2, R1, M), XH2=z(2, R1, M),
+            RS1=z(2, R1), RS2=z(2, R1), Q=z(3, R1),
+            lrows=z(5, B), scal=z(6), dZP=z(R1, L), dq=z(3, R),
+            # main backward
+            dP2=z(3, R1, M), dA=z(2, R1, M), dP1=z(3, R1, M), S=z(R, L), DG=z(max(R - B, 1), L), DZ0=z(B, L),
+            dP2d=z(R, M), dP1d=z(R, M), dP1e=z(B, E),
+            # pi
+            Yp1=z(R1, M), Yp2=z(R1, M), ACT=z(R1, A), MU=z(R1, A), dACT=z(R1, A), dPp2=z(R1, M), dPp1=z(R1, M),
+            piloss=z(1), gnorm=z(1),
+        )
+        # weight-gradient slots: (name, out, in, dY, X, K) resolved per pass; sized for the largest pass
+        self._bufs[B] = b
+        b["slots"] = {}
+        return b
+
+    def slot(self, b, key, numel):
+        s = b["slots"].get(key)
+        if s is None:
+            s = b["slots"][key] = torch.zeros(numel, device=self.dev)
+        return s
+
+    # ------------------------------------------------------------------------------------------- passes
+    def td_target(self, b, nxo, rew, R, eps):
+        """tdmpc.py:184-190 for all H steps: online encoder + pi (TruncatedNormal draws `eps`), target Q, and the
+        target encoder's next_z (tdmpc.py:206-207) -> b["TD"], b["NZ"]."""
+        O, E, L, A, M, LA = self.O, self.E, self.L, self.A, self.M, self.LA
+        w, wt = self.w, (lambda k: self.w(k, True))
+        self.gemm([dict(segs=[_seg(nxo, O, wt("_encoder.0.weight"), O, O)], m=R, n=E, c=_p(b["Yt1"]), ldc=E,
+                        bias=wt("_encoder.0.bias"), epi=EPI_ELU),
+                   dict(segs=[_seg(nxo, O, w("_encoder.0.weight"), O, O)], m=R, n=E, c=_p(b["Yo1"]), ldc=E,
+                        bias=w("_encoder.0.bias"), epi=EPI_ELU)])
+        self.gemm([dict(segs=[_seg(_p(b["Yt1"]), E, wt("_encoder.2.weight"), E, E)], m=R, n=L, c=_p(b["NZ"]),
+                        ldc=L, bias=wt("_encoder.2.bias")),
+                   dict(segs=[_seg(_p(b["Yo1"]), E, w("_encoder.2.weight"), E, E)], m=R, n=L, c=_p(b["Xtd"]),
+                        ldc=LA, bias=w("_encoder.2.bias"))])
+        self.gemm([dict(segs=[_seg(_p(b["Xtd"]), LA, w("_pi.0.weight"), L, L)], m=R, n=M, c=_p(b["T1"]), ldc=M,
+                        bias=w("_pi.0.bias"), epi=EPI_ELU)])
+        self.gemm([dict(segs=[_seg(_p(b["T1"]), M, w("_pi.2.weight"), M, M)], m=R, n=M, c=_p(b["T2"]), ldc=M,
+                        bias=w("_pi.2.bias"), epi=EPI_ELU)])
+        self.gemm([dict(segs=[_seg(_p(b["T2"]), M, w("_pi.4.weight"), M, M)], m=R, n=A, c=_p(b["Xtd"], L),
+                        ldc=LA, bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MUtd"]), ldc2=A,
+                        std=float(self.cfg.min_std))])
+        PA, PB = b["PA"], b["PB"]
+        self.gemm([dict(segs=[_seg(_p(b["Xtd"]), LA, wt(f"_Q{h + 1}.0.weight"), LA, LA)], m=R, n=M,
+                        c=_p(PA[h]), ldc=M, bias=wt(f"_Q{h + 1}.0.bias")) for h in range(2)])
+        self.rows([dict(x=_p(PA[h]), y=_p(PB[h]), ln=1, g=wt(f"_Q{h + 1}.1.weight"), beta=wt(f"_Q{h + 1}.1.bias"),
+                        act=TANH) for h in range(2)], R)
+        self.gemm([dict(segs=[_seg(_p(PB[h]), M, wt(f"_Q{h + 1}.3.weight"), M, M)], m=R, n=M, c=_p(PA[h]), ldc=M,
+                        bias=wt(f"_Q{h + 1}.3.bias")) for h in range(2)])
+        self.rows([dict(x=_p(PA[h]), ln=1, g=wt(f"_Q{h + 1}.4.weight"), beta=wt(f"_Q{h + 1}.4.bias"), act=ELU,
+                        tail=1, w3=wt(f"_Q{h + 1}.6.weight"), b3=wt(f"_Q{h + 1}.6.bias"), out=_p(b["TQ"][h]))
+                   for h in range(2)], R, reward=rew, td=_p(b["TD"]), gamma=float(self.cfg.discount))
+
+    def q_forward(self, b, n, x_segs, save=True):
+        """helper.q for both Q heads over n rows: layer 1 from the segments x_segs(h) -> Q values b["Q"][0:2]."""
+        M = self.M
+        w = self.w
+        PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = (b[k] for k in ("PA", "PB", "Y1", "Y2", "XH1", "XH2", "RS1", "RS2"))
+        self.gemm([dict(segs=x_segs(h), m=n, n=M, c=_p(PA[h]), ldc=M, bias=w(f"_Q{h + 1}.0.bias"))
+                   for h in range(2)])
+        self.rows([dict(x=_p(PA[h]), y=_p(Y1[h]), xhat=_p(XH1[h]), rstd=_p(RS1[h]), ln=1,
+                        g=w(f"_Q{h + 1}.1.weight"), beta=w(f"_Q{h + 1}.1.bias"), act=TANH) for h in range(2)], n)
+        return PA, PB, Y1, Y2, XH1, XH2, RS1, RS2
+
+    def update(self, buffer, noise=None):
+        """One TDMPC.update without the EMA -> metrics [7] (learner.METRICS order)."""
+        cfg, dev = self.cfg, self.dev
+        H, O, E, L, A, M, LA = self.H, self.O, self.E, self.L, self.A, self.M, self.LA
+        obs, next_obses, action, reward, idxs, weights = buffer.sample()
+        B = obs.shape[0]
+        R, R1 = H * B, (H + 1) * B
+        b = self.bufs(B)
+        obs = obs.contiguous()
+        nxo_t = next_obses[:H].contiguous()
+        rew_t = reward[:H].contiguous()
+        weights = weights.contiguous()
+        if noise is None:
+            b["eps"].normal_()
+        else:
+            b["eps"].copy_(torch.cat([x.reshape(B, A) for x in noise]).to(dev))
+        eps = b["eps"]
+        nxo, rew = _p(nxo_t), _p(rew_t)
+        w = self.w
+
+        # ---- TD targets and target latents (no gradient) ----
+        self.td_target(b, nxo, rew, R, _p(eps))
+
+        # ---- forward: encoder, latent rollout, heads ----
+        X0 = b["X0"]
+        self.gemm([dict(segs=[_seg(_p(obs), O, w("_encoder.0.weight"), O, O)], m=B, n=E, c=_p(b["Ye1"]), ldc=E,
+                        bias=w("_encoder.0.bias"), epi=EPI_ELU)])
+        self.gemm([dict(segs=[_seg(_p(b["Ye1"]), E, w("_encoder.2.weight"), E, E)], m=B, n=L, c=_p(X0), ldc=LA,
+                        bias=w("_encoder.2.bias"))])
+        X0.view(H + 1, B, LA)[:H, :, L:].copy_(action[:H])
+        for t in range(H):
+            self.gemm([dict(segs=[_seg(_p(X0, t * B * LA), LA, w("_dynamics.0.weight"), LA, LA)], m=B, n=M,
+                            c=_p(b["Yd1"], t * B * M), ldc=M, bias=w("_dynamics.0.bias"), epi=EPI_ELU)])
+            self.gemm([dict(segs=[_seg(_p(b["Yd1"], t * B * M), M, w("_dynamics.2.weight"), M, M)], m=B, n=M,
+                            c=_p(b["Yd2"], t * B * M), ldc=M, bias=w("_dynamics.2.bias"), epi=EPI_ELU)])
+            self.gemm([dict(segs=[_seg(_p(b["Yd2"], t * B * M), M, w("_dynamics.4.weight"), M, M)], m=B, n=L,
+                            c=_p(X0, (t + 1) * B * LA), ldc=LA, bias=w("_dynamics.4.bias"),
+                            c2=_p(b["ZP"], t * B * L), ldc2=L)])
+        PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(
+            b, R, lambda h: [_seg(_p(X0), LA, w(f"_Q{h + 1}.0.weight"), LA, LA)])
+        # reward head layer 1 (ELU) rides in its own slot 2 of PA / Y2 buffers
+        self.gemm([dict(segs=[_seg(_p(X0), LA, w("_reward.0.weight"), LA, LA)], m=R, n=M, c=_p(PA[2]), ldc=M,
+                        bias=w("_reward.0.bias"), epi=EPI_ELU)]
+                  + [dict(segs=[_seg(_p(Y1[h]), M, w(f"_Q{h + 1}.3.weight"), M, M)], m=R, n=M, c=_p(PB[h]), ldc=M,
+                          bias=w(f"_Q{h + 1}.3.bias")) for h in range(2)])
+        self.gemm([dict(segs=[_seg(_p(PA[2]), M, w("_reward.2.weight"), M, M)], m=R, n=M, c=_p(PB[2]), ldc=M,
+                        bias=w("_reward.2.bias"))])
+        Q = b["Q"]
+        heads = [dict(x=_p(PB[h]), y=_p(Y2[h]), xhat=_p(XH2[h]), rstd=_p(RS2[h]), ln=1, g=w(f"_Q{h + 1}.4.weight"),
+                      beta=w(f"_Q{h + 1}.4.bias"), act=ELU, tail=1, w3=w(f"_Q{h + 1}.6.weight"),
+                      b3=w(f"_Q{h + 1}.6.bias"), out=_p(Q[h])) for h in range(2)]
+        heads.append(dict(x=_p(PB[2]), y=_p(Y2[2]), act=ELU, tail=1, w3=w("_reward.4.weight"),
+                          b3=w("_reward.4.bias"), out=_p(Q[2])))
+        self.rows(heads, R)
+
+        # ---- losses (fused HIP loss, include/tdmpc_learner.h) ----
+        la = _lib.LossArgs(_p(b["ZP"]), _p(b["NZ"]), _p(Q[0]), _p(Q[1]), _p(Q[2]), rew, _p(b["TD"]), _p(weights),
+                           _p(self.rho), H, B, L, float(cfg.consistency_coef), float(cfg.reward_coef),
+                           float(cfg.value_coef))
+        st = self._stream()
+        _lib.check(self.lib.tdmpc_loss_forward(C.byref(la), _p(b["lrows"]), _p(b["scal"]), st), "loss_forward")
+        dq = b["dq"]
+        _lib.check(self.lib.tdmpc_loss_backward(C.byref(la), _p(b["lrows"]), _p(b["scal"]), _p(self.gw),
+                                                _p(b["dZP"], B * L), _p(dq[0]), _p(dq[1]), _p(dq[2]), st),
+                   "loss_backward")
+
+        # ---- backward through the heads ----
+        dP2, dA, dP1 = b["dP2"], b["dA"], b["dP1"]
+        PW2, PWr, PW1 = 3 * M + 1, M + 1, 2 * M
+        part2 = [self.slot(b, f"pq2_{h}", ROWS_NWG * PW2) for h in range(2)]
+        partr = self.slot(b, "pr", ROWS_NWG * PWr)
+        part1 = [self.slot(b, f"pq1_{h}", ROWS_NWG * PW1) for h in range(2)]
+        heads = [dict(y=_p(dP2[h]), yact=_p(Y2[h]), xhat=_p(XH2[h]), rstd=_p(RS2[h]), ln=1,
+                      g=w(f"_Q{h + 1}.4.weight"), act=ELU, tail=1, w3=w(f"_Q{h + 1}.6.weight"), dq=_p(dq[h]),
+                      part=_p(part2[h])) for h in range(2)]
+        heads.append(dict(y=_p(dP2[2]), yact=_p(Y2[2]), act=ELU, tail=1, w3=w("_reward.4.weight"), dq=_p(dq[2]),
+                          part=_p(partr)))
+        self.rows(heads, R, bwd=True)
+        self.gemm([dict(segs=[_seg(_p(dP2[h]), M, w(f"_Q{h + 1}.3.weight"), M, M, bmode=1)], m=R, n=M,
+                        c=_p(dA[h]), ldc=M) for h in range(2)]
+                  + [dict(segs=[_seg(_p(dP2[2]), M, w("_reward.2.weight"), M, M, bmode=1)], m=R, n=M,
+                          c=_p(dP1[2]), ldc=M, epi=EPI_ELU_BWD, aux=_p(PA[2]), ldaux=M)])
+        self.rows([dict(x=_p(dA[h]), y=_p(dP1[h]), yact=_p(Y1[h]), xhat=_p(XH1[h]), rstd=_p(RS1[h]), ln=1,
+                        g=w(f"_Q{h + 1}.1.weight"), act=TANH, part=_p(part1[h])) for h in range(2)], R, bwd=True)
+        # gradient of z_t from the three heads (+ the consistency term on z_t): S = sum_h dP1_h W1_h[:, :L] + dZP
+        S, dZP = b["S"], b["dZP"]
+        self.gemm([dict(segs=[_seg(_p(dP1[0]), M, w("_Q1.0.weight"), LA, M, bmode=1),
+                              _seg(_p(dP1[1]), M, w("_Q2.0.weight"), LA, M, bmode=1),
+                              _seg(_p(dP1[2]), M, w("_reward.0.weight"), LA, M, bmode=1)],
+                         m=R, n=L, c=_p(S), ldc=L, res=_p(dZP), ldres=L)])
+        # ---- backward through the latent rollout (tdmpc.py:203-205), newest step first ----
+        DG, dP2d, dP1d, DZ0 = b["DG"], b["dP2d"], b["dP1d"], b["DZ0"]
+        for t in range(H - 1, -1, -1):
+            g_t = _p(dZP, H * B * L) if t == H - 1 else _p(DG, t * B * L)     # d loss / d z_{t+1}
+            self.gemm([dict(segs=[_seg(g_t, L, w("_dynamics.4.weight"), M, L, bmode=1)], m=B, n=M,
+                            c=_p(dP2d, t * B * M), ldc=M, epi=EPI_ELU_BWD, aux=_p(b["Yd2"], t * B * M), ldaux=M)])
+            self.gemm([dict(segs=[_seg(_p(dP2d, t * B * M), M, w("_dynamics.2.weight"), M, M, bmode=1)], m=B, n=M,
+                            c=_p(dP1d, t * B * M), ldc=M, epi=EPI_ELU_BWD, aux=_p(b["Yd1"], t * B * M), ldaux=M)])
+            out = _p(DG, (t - 1) * B * L) if t > 0 else _p(DZ0)
+            self.gemm([dict(segs=[_seg(_p(dP1d, t * B * M), M, w("_dynamics.0.weight"), LA, M, bmode=1)], m=B,
+                            n=L, c=out, ldc=L, res=_p(S, t * B * L), ldres=L)])
+        self.gemm([dict(segs=[_seg(_p(DZ0), L, w("_encoder.2.weight"), E, L, bmode=1)], m=B, n=E,
+                        c=_p(b["dP1e"]), ldc=E, epi=EPI_ELU_BWD, aux=_p(b["Ye1"]), ldaux=E)])
+
+        # ---- weight gradients (one grouped launch) ----
+        sp = 2 if R >= 1024 else 1
+        g_dyn3 = ([_seg(_p(DG), L, _p(b["Yd2"]), M, R - B, 1, 1, M)] if H > 1 else []) + \
+            [_seg(_p(dZP, H * B * L), L, _p(b["Yd2"], (H - 1) * B * M), M, B, 1, 1, M)]
+        dw = [("_encoder.2", L, E, [_seg(_p(DZ0), L, _p(b["Ye1"]), E, B, 1, 1, E)], 1),
+              ("_encoder.0", E, O, [_seg(_p(b["dP1e"]), E, _p(obs), O, B, 1, 1, O)], 1),
+              ("_dynamics.4", L, M, g_dyn3, sp),
+              ("_dynamics.2", M, M, [_seg(_p(dP2d), M, _p(b["Yd1"]), M, R, 1, 1, M)], sp),
+              ("_dynamics.0", M, LA, [_seg(_p(dP1d), M, _p(X0), LA, R, 1, 1, LA)], sp),
+              ("_reward.2", M, M, [_seg(_p(dP2[2]), M, _p(PA[2]), M, R, 1, 1, M)], sp),
+              ("_reward.0", M, LA, [_seg(_p(dP1[2]), M, _p(X0), LA, R, 1, 1, LA)], sp)]
+        for h in range(2):
+            dw += [(f"_Q{h + 1}.3", M, M, [_seg(_p(dP2[h]), M, _p(Y1[h]), M, R, 1, 1, M)], sp),
+                   (f"_Q{h + 1}.0", M, LA, [_seg(_p(dP1[h]), M, _p(X0), LA, R, 1, 1, LA)], sp)]
+        slots = self._dw(b, "main", dw)
+
+        # ---- finalize (sum slices, global norm), clip + Adam ----
+        src = {}
+        for name, o, i, _, s in dw:
+            src[name + ".weight"] = (slots[name], o, i, i + 1, s, o * (i + 1))
+            src[name + ".bias"] = (slots[name] + 4 * i, o, 1, i + 1, s, o * (i + 1))
+        for h in range(2):
+            q = f"_Q{h + 1}"
+            src[q + ".1.weight"] = (_p(part1[h]), 1, M, M, ROWS_NWG, PW1)
+            src[q + ".1.bias"] = (_p(part1[h], M), 1, M, M, ROWS_NWG, PW1)
+            src[q + ".4.weight"] = (_p(part2[h]), 1, M, M, ROWS_NWG, PW2)
+            src[q + ".4.bias"] = (_p(part2[h], M), 1, M, M, ROWS_NWG, PW2)
+            src[q + ".6.weight"] = (_p(part2[h], 2 * M), 1, M, M, ROWS_NWG, PW2)
+            src[q + ".6.bias"] = (_p(part2[h], 3 * M), 1, 1, 1, ROWS_NWG, PW2)
+        src["_reward.4.weight"] = (_p(partr), 1, M, M, ROWS_NWG, PWr)
+        src["_reward.4.bias"] = (_p(partr, M), 1, 1, 1, ROWS_NWG, PWr)
+        self._optimise(self.opt_main, src, 0, _p(b["gnorm"]))
+        buffer.update_priorities(idxs, b["lrows"][3].view(B, 1))
+
+        # ---- update_pi on the detached latents z_0..z_H (tdmpc.py:165-182) ----
+        pi_loss = self._update_pi(b, _p(X0), LA, H + 1, B, _p(eps, R * A))
+        scal = b["scal"]
+        return torch.cat([scal[0:3], pi_loss, scal[3:5], b["gnorm"]])
+
+    def _dw(self, b, tag, dw):
+        """One grouped launch of every weight gradient of a pass -> {name: slot pointer}."""
+        jobs, slots = [], {}
+        for name, o, i, segs, s in dw:
+            buf = self.slot(b, f"{tag}:{name}", s * o * (i + 1))
+            slots[name] = _p(buf)
+            jobs.append(dict(segs=segs, m=o, n=i + 1, c=_p(buf), ldc=i + 1, splits=s, slice=o * (i + 1)))
+        self.gemm(jobs, tile=2)
+        return slots
+
+    def _optimise(self, opt, src, g_lo, norm_out):
+        """lg_finalize over the optimiser's tensors (in flat order), then lg_adam over its flat range."""
+        names = [k for k in self.off if (k in src)]
+        names.sort(key=lambda k: self.off[k][0])
+        arr = (_lib.LgGsrc * len(names))()
+        for i, k in enumerate(names):
+            p, rows, cols, ld, ns, ss = src[k]
+            o, shape = self.off[k]
+            assert rows * cols == int(torch.Size(shape).numel()), k
+            T = arr[i]
+            T.src, T.dst, T.sstride, T.rows, T.cols, T.ld, T.nslices = p, o - opt.lo, ss, rows, cols, ld, ns
+        assert self.off[names[0]][0] == opt.lo
+        which = 0 if opt is self.opt_main else 1
+        normp = _p(self.normp[which])
+        st = self._stream()
+        _lib.check(self.lib.tdmpc_lg_finalize(arr, len(names), _p(self.G, opt.lo), normp, NBLK, _p(opt.step_t), st),
+                   "tdmpc_lg_finalize")
+        _lib.check(self.lib.tdmpc_lg_adam(_p(self.P, opt.lo), _p(self.G, opt.lo), _p(opt.exp_avg),
+                                          _p(opt.exp_avg_sq), opt.hi - opt.lo, normp, NBLK, _p(opt.step_t),
+                                          opt.lr, 0.9, 0.999, 1e-8, float(self.cfg.grad_clip_norm), norm_out, st),
+                   "tdmpc_lg_adam")
+
+    def _update_pi(self, b, z, ldz, nt, B, eps):
+        """TDMPC.update_pi over nt latent blocks of B rows at z (row stride ldz) -> pi_loss tensor [1]."""
+        L, A, M, LA = self.L, self.A, self.M, self.LA
+        n = nt * B
+        w = self.w
+        self.gemm([dict(segs=[_seg(z, ldz, w("_pi.0.weight"), L, L)], m=n, n=M, c=_p(b["Yp1"]), ldc=M,
+                        bias=w("_pi.0.bias"), epi=EPI_ELU)])
+        self.gemm([dict(segs=[_seg(_p(b["Yp1"]), M, w("_pi.2.weight"), M, M)], m=n, n=M, c=_p(b["Yp2"]), ldc=M,
+                        bias=w("_pi.2.bias"), epi=EPI_ELU)])
+        self.gemm([dict(segs=[_seg(_p(b["Yp2"]), M, w("_pi.4.weight"), M, M)], m=n, n=A, c=_p(b["ACT"]), ldc=A,
+                        bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MU"]), ldc2=A,
+                        std=float(self.cfg.min_std))])
+        PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(
+            b, n, lambda h: [_seg(z, ldz, w(f"_Q{h + 1}.0.weight"), LA, L),
+                             _seg(_p(b["ACT"]), A, w(f"_Q{h + 1}.0.weight") + 4 * L, LA, A)])
+        self.gemm([dict(segs=[_seg(_p(Y1[h]), M, w(f"_Q{h + 1}.3.weight"), M, M)], m=n, n=M, c=_p(PB[h]), ldc=M,
+                        bias=w(f"_Q{h + 1}.3.bias")) for h in range(2)])
+        Q = b["Q"]
+        self.rows([dict(x=_p(PB[h]), y=_p(Y2[h]), xhat=_p(XH2[h]), rstd=_p(RS2[h]), ln=1, g=w(f"_Q{h + 1}.4.weight"),
+                        beta=w(f"_Q{h + 1}.4.bias"), act=ELU, tail=1, w3=w(f"_Q{h + 1}.6.weight"),
+                        b3=w(f"_Q{h + 1}.6.bias"), out=_p(Q[h])) for h in range(2)], n)
+        st = self._stream()
+        _lib.check(self.lib.tdmpc_lg_pi_loss(_p(Q[0]), _p(Q[1]), _p(self.rho), nt, B, _p(b["piloss"]), st),
+                   "tdmpc_lg_pi_loss")
+        # backward to the action (Q weights frozen: no weight gradients), then through pi
+        dP2, dA, dP1 = b["dP2"], b["dA"], b["dP1"]
+        self.rows([dict(y=_p(dP2[h]), yact=_p(Y2[h]), xhat=_p(XH2[h]), rstd=_p(RS2[h]), ln=1,
+                        g=w(f"_Q{h + 1}.4.weight"), act=ELU, tail=1, w3=w(f"_Q{h + 1}.6.weight"))
+                   for h in range(2)], n, bwd=True, q1=_p(Q[0]), q2=_p(Q[1]), rho=_p(self.rho), bsz=B)
+        self.gemm([dict(segs=[_seg(_p(dP2[h]), M, w(f"_Q{h + 1}.3.weight"), M, M, bmode=1)], m=n, n=M,
+                        c=_p(dA[h]), ldc=M) for h in range(2)])
+        self.rows([dict(x=_p(dA[h]), y=_p(dP1[h]), yact=_p(Y1[h]), xhat=_p(XH1[h]), rstd=_p(RS1[h]), ln=1,
+                        g=w(f"_Q{h + 1}.1.weight"), act=TANH) for h in range(2)], n, bwd=True)
+        self.gemm([dict(segs=[_seg(_p(dP1[h]), M, w(f"_Q{h + 1}.0.weight") + 4 * L, LA, M, bmode=1)
+                              for h in range(2)],
+                        m=n, n=A, c=_p(b["dACT"]), ldc=A, epi=EPI_PI_BWD, aux=_p(b["MU"]), ldaux=A)])
+        self.gemm([dict(segs=[_seg(_p(b["dACT"]), A, w("_pi.4.weight"), M, A, bmode=1)], m=n, n=M,
+                        c=_p(b["dPp2"]), ldc=M, epi=EPI_ELU_BWD, aux=_p(b["Yp2"]), ldaux=M)])
+        self.gemm([dict(segs=[_seg(_p(b["dPp2"]), M, w("_pi.2.weight"), M, M, bmode=1)], m=n, n=M,
+                        c=_p(b["dPp1"]), ldc=M, epi=EPI_ELU_BWD, aux=_p(b["Yp1"]), ldaux=M)])
+        sp = 2 if n >= 1024 else 1
+        dw = [("_pi.4", A, M, [_seg(_p(b["dACT"]), A, _p(b["Yp2"]), M, n, 1, 1, M)], sp),
+              ("_pi.2", M, M, [_seg(_p(b["dPp2"]), M, _p(b["Yp1"]), M, n, 1, 1, M)], sp),
+              ("_pi.0", M, L, [_seg(_p(b["dPp1"]), M, z, ldz, n, 1, 1, L)], sp)]
+        slots = self._dw(b, f"pi{n}", dw)
+        src = {}
+        for name, o, i, _, s in dw:
+            src[name + ".weight"] = (slots[name], o, i, i + 1, s, o * (i + 1))
+            src[name + ".bias"] = (slots[name] + 4 * i, o, 1, i + 1, s, o * (i + 1))
+        self._optimise(self.opt_pi, src, self.n_main, None)
+        return b["piloss"]
+
+    def update_pi(self, zs, eps=None):
+        """The public TDMPC.update_pi(zs): zs a list of [B, L] latents (detached) -> pi_loss tensor [1]."""
+        B = zs[0].shape[0]
+        nt = len(zs)
+        b = self.bufs(B)
+        if nt > self.H + 1:
+            raise ValueError(f"update_pi: at most horizon + 1 = {self.H + 1} latent blocks")
+        Z = torch.cat([z.detach().reshape(B, self.L) for z in zs]).contiguous()
+        e = b["eps"][self.H * B:(self.H + nt) * B]
+        if eps is None:
+            e.normal_()
+        else:
+            e.copy_(torch.cat([x.reshape(B, self.A) for x in list(eps)[:nt]]).to(self.dev))
+        b["zpi"] = Z          # kept alive until the kernels have run
+        return self._update_pi(b, _p(Z), self.L, nt, B, _p(e)).clone()
+
+    def ema(self, tau):
+        _lib.check(self.lib.tdmpc_lg_lerp(_p(self.PT), _p(self.P), self.P.numel(), float(tau), self._stream()),
+                   "tdmpc_lg_lerp")

@@ -88,6 +88,35 @@ def test_gpu_update_matches_oracle():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("task", ["humanoid", "dog"])
+def test_gpu_update_matches_oracle_full_size(task):
+    """The bench's learner shape (batch 512, horizon 5, mlp 512; humanoid L100 A21 / dog L100 A38 obs 223):
+    two updates (EMA on the second) against the oracle, same batch and TruncatedNormal draws, same tolerances."""
+    from tdmpc_amd.config import make_cfg
+    from tdmpc_amd.tdmpc import TDMPC
+    cfg = make_cfg(task, num_samples=64, num_elites=32, iterations=3, horizon=5, batch_size=512)
+    agent = TDMPC(cfg)
+    agent.model.load_state_dict(synthetic_state_dict(cfg, 31))
+    agent.model_target.load_state_dict(synthetic_state_dict(cfg, 32))
+    assert agent.learner().engine is not None
+    ref = RefLearner(cfg, synthetic_state_dict(cfg, 31), synthetic_state_dict(cfg, 32))
+    b = batch(cfg, seed=9)
+    buf = _DeviceBatchBuffer(b)
+    H, B, A = cfg.horizon, cfg.batch_size, cfg.action_dim
+    torch.manual_seed(1)
+    noise = [[torch.empty(B, A).normal_() for _ in range(2 * H + 1)] for _ in range(2)]
+    torch.manual_seed(1)
+    for k, step in enumerate((1, 2)):
+        m = agent.update(buf, step, noise=noise[k])
+        rm, rprio = ref.update(b, step)
+        np.testing.assert_allclose([m[n] for n in METRICS], [rm[n] for n in METRICS], rtol=2e-5, atol=1e-7)
+        np.testing.assert_allclose(buf.prio.cpu().numpy(), rprio.numpy(), rtol=2e-5, atol=1e-6)
+        sd, sdt = ref.state_dicts()
+        _params_close(agent.model.state_dict(), sd, cfg.lr)
+        _params_close(agent.model_target.state_dict(), sdt, cfg.lr)
+
+
+@pytest.mark.gpu
 def test_graph_replay_equals_eager():
     """6 updates from a device replay buffer: 3 eager warm-ups + 3 graph replays == 6 eager updates, bitwise
     (same kernels, same philox offsets), including the buffer's priorities and the EMA target."""
