@@ -420,6 +420,7 @@ __global__ void __launch_bounds__(256) lg_pi_loss_kernel(const float* q1, const 
 // ------------------------------------------------------------------------------------------ optimiser
 constexpr int LG_MAXT = 48;
 constexpr int LG_FIN_PER = 2048;   // gradient elements per lg_finalize workgroup (8 per thread)
+constexpr int LG_FIN_MANY = 32;    // from this many slices a workgroup sums 64 elements with all its threads
 struct FArgs {
     tdmpc_lg_gsrc t[LG_MAXT];
     int block0[LG_MAXT];
@@ -435,26 +436,54 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
     return red[0] + red[1] + red[2] + red[3];
 }
 
-// workgroup -> (tensor, chunk of 2048 elements); each element sums its slices in order
+// workgroup -> (tensor, chunk): 2048 elements of a tensor with few slices (8 per thread), or 64 elements of one
+// with many (the row kernels' per-workgroup column sums: 4 thread groups split the slices, 8 loads in flight
+// each, combined in a fixed order)
 __global__ void __launch_bounds__(256) lg_finalize_kernel(const FArgs F, float* g, float* normp, int* step) {
     __shared__ float red[4];
+    __shared__ float part[4][64];
     int ti = 0;
     for (int q = 1; q < F.nt; ++q)
         if ((int)blockIdx.x >= F.block0[q]) ti = q;
     const tdmpc_lg_gsrc& T = F.t[ti];
-    const long n = (long)T.rows * T.cols;
-    const long e0 = (long)(blockIdx.x - F.block0[ti]) * LG_FIN_PER;
+    const int n = T.rows * T.cols;
     float sq = 0.f;
+    if (T.nslices < LG_FIN_MANY) {
+        const int e0 = (blockIdx.x - F.block0[ti]) * LG_FIN_PER;
 #pragma unroll
-    for (int u = 0; u < LG_FIN_PER / 256; ++u) {
-        const long loc = e0 + u * 256 + threadIdx.x;
+        for (int u = 0; u < LG_FIN_PER / 256; ++u) {
+            const int loc = e0 + u * 256 + threadIdx.x;
+            if (loc < n) {
+                const int rr = loc / T.cols, cc = loc - rr * T.cols;
+                const float* p = T.src + (size_t)rr * T.ld + cc;
+                float v = 0.f;
+                for (int k = 0; k < T.nslices; ++k) v += p[(size_t)k * T.sstride];
+                g[T.dst + loc] = v;
+                sq += v * v;
+            }
+        }
+    } else {
+        const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
+        const int loc = (blockIdx.x - F.block0[ti]) * 64 + e;
+        float v = 0.f;
         if (loc < n) {
-            const int rr = (int)(loc / T.cols), cc = (int)(loc % T.cols);
+            const int rr = loc / T.cols, cc = loc - rr * T.cols;
             const float* p = T.src + (size_t)rr * T.ld + cc;
-            float v = 0.f;
-            for (int k = 0; k < T.nslices; ++k) v += p[(size_t)k * T.sstride];
-            g[T.dst + loc] = v;
-            sq += v * v;
+            float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            int k = grp;
+            for (; k + 28 < T.nslices; k += 32) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc[u] += p[(size_t)(k + 4 * u) * T.sstride];
+            }
+            for (int u = 0; k < T.nslices; k += 4, ++u) acc[u & 7] += p[(size_t)k * T.sstride];
+            v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+        }
+        part[grp][e] = v;
+        __syncthreads();
+        if (grp == 0 && loc < n) {
+            const float t = (part[0][e] + part[1][e]) + (part[2][e] + part[3][e]);
+            g[T.dst + loc] = t;
+            sq = t * t;
         }
     }
     const float tot = block_sum256(sq, red);
@@ -614,7 +643,8 @@ int tdmpc_lg_finalize(const tdmpc_lg_gsrc* t, int32_t nt, float* g, float* normp
         F.block0[i] = blocks;
         const long n = (long)t[i].rows * t[i].cols;
         off += n;
-        blocks += (int)((n + LG_FIN_PER - 1) / LG_FIN_PER);
+        const int per = t[i].nslices < LG_FIN_MANY ? LG_FIN_PER : 64;
+        blocks += (int)((n + per - 1) / per);
     }
     if (blocks > nblk) return bad("tdmpc_lg_finalize: normp holds fewer entries than workgroups");
     F.nt = nt;

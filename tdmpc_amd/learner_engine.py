@@ -31,7 +31,7 @@ from . import _lib
 ELU, TANH = 2, 1
 EPI_NONE, EPI_ELU, EPI_PI, EPI_ELU_BWD, EPI_PI_BWD = 0, 1, 2, 3, 4
 NBLK = 2048         # capacity of the norm partials (one per lg_finalize workgroup of 2048 gradients)
-ROWS_NWG = 80       # lg_rows_bwd workgroups (column-sum partials per head)
+ROWS_NWG = 256      # lg_rows_bwd workgroups (column-sum partials per head)
 
 
 def supported(cfg) -> bool:
