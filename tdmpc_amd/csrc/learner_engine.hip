@@ -133,6 +133,7 @@ __device__ __forceinline__ void seg_loop(const tdmpc_lg_seg& S, int nb_mem, int 
     };
     // a ring of D groups in flight: the loads of group g + D - 1 are issued (sched_barrier keeps them ahead of
     // the MFMAs) before group g is multiplied; groups past the end load zeros, so the trip count needs no tail
+    // (deeper rings, 4 / 8 groups, measured 15-20 % slower on MI355X: the loads are throughput-, not latency-bound)
     constexpr int D = TM * TN >= 4 ? 2 : 4;
     float4 ra[D][TM], rb[D][TN];
 #pragma unroll
@@ -169,10 +170,46 @@ __device__ __forceinline__ void seg_loop(const tdmpc_lg_seg& S, int nb_mem, int 
     }
 }
 
+// One output element of a job: the split-K partial as is, else bias / residual / epilogue (tdmpc_lg_job).
+__device__ __forceinline__ void lg_store(const tdmpc_lg_job& JJ, int splits, int split, int row, int col, float v) {
+    if (splits > 1) {
+        JJ.c[(size_t)split * JJ.slice + (size_t)row * JJ.ldc + col] = v;
+        return;
+    }
+    float x = v;
+    if (JJ.bias) x += JJ.bias[col];
+    if (JJ.res) x += JJ.res[(size_t)row * JJ.ldres + col];
+    switch (JJ.epi) {
+    case TDMPC_LG_EPI_ELU: x = elu_f(x); break;
+    case TDMPC_LG_EPI_PI: {
+        const float mu = tanhf(x);
+        const float e2 = fminf(fmaxf(JJ.std_ * JJ.aux[(size_t)row * JJ.ldaux + col], -0.3f), 0.3f);
+        x = fminf(fmaxf(mu + e2, -1.0f + 1e-6f), 1.0f - 1e-6f);
+        JJ.c2[(size_t)row * JJ.ldc2 + col] = mu;
+        break;
+    }
+    case TDMPC_LG_EPI_ELU_BWD: {
+        const float y = JJ.aux[(size_t)row * JJ.ldaux + col];
+        x *= y > 0.f ? 1.f : y + 1.f;
+        break;
+    }
+    case TDMPC_LG_EPI_PI_BWD: {
+        const float mu = JJ.aux[(size_t)row * JJ.ldaux + col];
+        x *= 1.f - mu * mu;
+        break;
+    }
+    default:
+        if (JJ.c2) JJ.c2[(size_t)row * JJ.ldc2 + col] = x;
+    }
+    JJ.c[(size_t)row * JJ.ldc + col] = x;
+}
+
 __device__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// (amdgpu_waves_per_eu(2): left to itself the compiler gave the 64 x 64 form 224 VGPRs + 128 AGPRs, one wave per SIMD;
+// bounded, 210 VGPRs and no spills: two)
 template <int TM, int TN>
-__global__ void __launch_bounds__(256) lg_gemm_kernel(const KArgs P) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) lg_gemm_kernel(const KArgs P) {
     __shared__ float red[4][TM * TN * 16][64];
     int jb = 0;
     for (int q = 1; q < P.njobs; ++q)
@@ -233,36 +270,7 @@ __global__ void __launch_bounds__(256) lg_gemm_kernel(const KArgs P) {
         const int i = q / (TN * 16), j = (q / 16) % TN, e = q % 16;
         const int row = m0 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h, col = n0 + 32 * j + r;
         if (row >= M || col >= N) continue;
-        if (splits > 1) {
-            JJ.c[(size_t)split * JJ.slice + (size_t)row * JJ.ldc + col] = v;
-            continue;
-        }
-        float x = v;
-        if (JJ.bias) x += JJ.bias[col];
-        if (JJ.res) x += JJ.res[(size_t)row * JJ.ldres + col];
-        switch (JJ.epi) {
-        case TDMPC_LG_EPI_ELU: x = elu_f(x); break;
-        case TDMPC_LG_EPI_PI: {
-            const float mu = tanhf(x);
-            const float e2 = fminf(fmaxf(JJ.std_ * JJ.aux[(size_t)row * JJ.ldaux + col], -0.3f), 0.3f);
-            x = fminf(fmaxf(mu + e2, -1.0f + 1e-6f), 1.0f - 1e-6f);
-            JJ.c2[(size_t)row * JJ.ldc2 + col] = mu;
-            break;
-        }
-        case TDMPC_LG_EPI_ELU_BWD: {
-            const float y = JJ.aux[(size_t)row * JJ.ldaux + col];
-            x *= y > 0.f ? 1.f : y + 1.f;
-            break;
-        }
-        case TDMPC_LG_EPI_PI_BWD: {
-            const float mu = JJ.aux[(size_t)row * JJ.ldaux + col];
-            x *= 1.f - mu * mu;
-            break;
-        }
-        default:
-            if (JJ.c2) JJ.c2[(size_t)row * JJ.ldc2 + col] = x;
-        }
-        JJ.c[(size_t)row * JJ.ldc + col] = x;
+        lg_store(JJ, splits, split, row, col, v);
     }
 }
 

@@ -95,6 +95,10 @@ class Engine:
         self.gw = torch.full((1,), 1.0, dtype=torch.float32, device=self.dev) * (1 / self.H)   # the 1/H hook
         self._bufs = {}
         self.lib = _lib.lib()
+        # independent passes run on a second stream (forked from and joined back into the caller's; captured into
+        # the learner's HIP graph as parallel branches): the TD target beside the encoder + latent rollout, the
+        # heads' weight gradients beside the rollout's backward. Both pairs touch disjoint buffers.
+        self.side = torch.cuda.Stream(self.dev)
 
     def _alias(self, model, flat):
         """Make every parameter of `model` a view into `flat` (values kept)."""
@@ -165,7 +169,7 @@ class Engine:
             eps=z((2 * H + 1) * B, A),
             # TD target
             Yt1=z(R, E), Yo1=z(R, E), NZ=z(R, L), Xtd=z(R, LA), T1=z(R, M), T2=z(R, M), MUtd=z(R, A),
-            TQ=z(2, R), TD=z(R),
+            TQ=z(2, R), TD=z(R), PAt=z(2, R, M), PBt=z(2, R, M),
             # main forward
             Ye1=z(B, E), X0=z(R1, LA), Yd1=z(R, M), Yd2=z(R, M), ZP=z(R, L),
             PA=z(3, R1, M), PB=z(3, R1, M), Y1=z(2, R1, M), Y2=z(3, R1, M), XH1=z(2, R1, M), XH2=z(2, R1, M),
@@ -210,7 +214,7 @@ class Engine:
         self.gemm([dict(segs=[_seg(_p(b["T2"]), M, w("_pi.4.weight"), M, M)], m=R, n=A, c=_p(b["Xtd"], L),
                         ldc=LA, bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MUtd"]), ldc2=A,
                         std=float(self.cfg.min_std))])
-        PA, PB = b["PA"], b["PB"]
+        PA, PB = b["PAt"], b["PBt"]
         self.gemm([dict(segs=[_seg(_p(b["Xtd"]), LA, wt(f"_Q{h + 1}.0.weight"), LA, LA)], m=R, n=M,
                         c=_p(PA[h]), ldc=M, bias=wt(f"_Q{h + 1}.0.bias")) for h in range(2)])
         self.rows([dict(x=_p(PA[h]), y=_p(PB[h]), ln=1, g=wt(f"_Q{h + 1}.1.weight"), beta=wt(f"_Q{h + 1}.1.bias"),
@@ -252,8 +256,11 @@ class Engine:
         nxo, rew = _p(nxo_t), _p(rew_t)
         w = self.w
 
-        # ---- TD targets and target latents (no gradient) ----
-        self.td_target(b, nxo, rew, R, _p(eps))
+        # ---- TD targets and target latents (no gradient), on the side stream ----
+        main = torch.cuda.current_stream(dev)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            self.td_target(b, nxo, rew, R, _p(eps))
 
         # ---- forward: encoder, latent rollout, heads ----
         X0 = b["X0"]
@@ -287,6 +294,7 @@ class Engine:
                           b3=w("_reward.4.bias"), out=_p(Q[2])))
         self.rows(heads, R)
 
+        main.wait_stream(self.side)   # TD / NZ ready
         # ---- losses (fused HIP loss, include/tdmpc_learner.h) ----
         la = _lib.LossArgs(_p(b["ZP"]), _p(b["NZ"]), _p(Q[0]), _p(Q[1]), _p(Q[2]), rew, _p(b["TD"]), _p(weights),
                            _p(self.rho), H, B, L, float(cfg.consistency_coef), float(cfg.reward_coef),
@@ -322,6 +330,16 @@ class Engine:
                               _seg(_p(dP1[1]), M, w("_Q2.0.weight"), LA, M, bmode=1),
                               _seg(_p(dP1[2]), M, w("_reward.0.weight"), LA, M, bmode=1)],
                          m=R, n=L, c=_p(S), ldc=L, res=_p(dZP), ldres=L)])
+        # ---- the heads' weight gradients (side stream) beside the latent rollout's backward ----
+        sp = 2 if R >= 1024 else 1
+        dw_h = [("_reward.2", M, M, [_seg(_p(dP2[2]), M, _p(PA[2]), M, R, 1, 1, M)], sp),
+                ("_reward.0", M, LA, [_seg(_p(dP1[2]), M, _p(X0), LA, R, 1, 1, LA)], sp)]
+        for h in range(2):
+            dw_h += [(f"_Q{h + 1}.3", M, M, [_seg(_p(dP2[h]), M, _p(Y1[h]), M, R, 1, 1, M)], sp),
+                     (f"_Q{h + 1}.0", M, LA, [_seg(_p(dP1[h]), M, _p(X0), LA, R, 1, 1, LA)], sp)]
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            slots = self._dw(b, "mainh", dw_h)
         # ---- backward through the latent rollout (tdmpc.py:203-205), newest step first ----
         DG, dP2d, dP1d, DZ0 = b["DG"], b["dP2d"], b["dP1d"], b["DZ0"]
         for t in range(H - 1, -1, -1):
@@ -336,21 +354,17 @@ class Engine:
         self.gemm([dict(segs=[_seg(_p(DZ0), L, w("_encoder.2.weight"), E, L, bmode=1)], m=B, n=E,
                         c=_p(b["dP1e"]), ldc=E, epi=EPI_ELU_BWD, aux=_p(b["Ye1"]), ldaux=E)])
 
-        # ---- weight gradients (one grouped launch) ----
-        sp = 2 if R >= 1024 else 1
+        # ---- the rollout's weight gradients (one grouped launch) ----
         g_dyn3 = ([_seg(_p(DG), L, _p(b["Yd2"]), M, R - B, 1, 1, M)] if H > 1 else []) + \
             [_seg(_p(dZP, H * B * L), L, _p(b["Yd2"], (H - 1) * B * M), M, B, 1, 1, M)]
         dw = [("_encoder.2", L, E, [_seg(_p(DZ0), L, _p(b["Ye1"]), E, B, 1, 1, E)], 1),
               ("_encoder.0", E, O, [_seg(_p(b["dP1e"]), E, _p(obs), O, B, 1, 1, O)], 1),
               ("_dynamics.4", L, M, g_dyn3, sp),
               ("_dynamics.2", M, M, [_seg(_p(dP2d), M, _p(b["Yd1"]), M, R, 1, 1, M)], sp),
-              ("_dynamics.0", M, LA, [_seg(_p(dP1d), M, _p(X0), LA, R, 1, 1, LA)], sp),
-              ("_reward.2", M, M, [_seg(_p(dP2[2]), M, _p(PA[2]), M, R, 1, 1, M)], sp),
-              ("_reward.0", M, LA, [_seg(_p(dP1[2]), M, _p(X0), LA, R, 1, 1, LA)], sp)]
-        for h in range(2):
-            dw += [(f"_Q{h + 1}.3", M, M, [_seg(_p(dP2[h]), M, _p(Y1[h]), M, R, 1, 1, M)], sp),
-                   (f"_Q{h + 1}.0", M, LA, [_seg(_p(dP1[h]), M, _p(X0), LA, R, 1, 1, LA)], sp)]
-        slots = self._dw(b, "main", dw)
+              ("_dynamics.0", M, LA, [_seg(_p(dP1d), M, _p(X0), LA, R, 1, 1, LA)], sp)]
+        slots.update(self._dw(b, "main", dw))
+        main.wait_stream(self.side)   # the heads' slices ready
+        dw += dw_h
 
         # ---- finalize (sum slices, global norm), clip + Adam ----
         src = {}
