@@ -139,7 +139,10 @@ class Engine:
             J.splits, J.slice = j.get("splits", 1), j.get("slice", 0)
             tiles64 += -(-j["m"] // 64) * -(-j["n"] // 64) * J.splits
         if tile is None:
-            tile = 2 if tiles64 >= 240 else 1
+            # 64 x 64 tiles only for wide launches of row-major operands; a transposed weight operand (the
+            # backward's dX) runs 15-25 % faster on 32 x 32 tiles (tools/lg_gemm_bench.py)
+            tbw = any(sg[6] == 1 for j in jobs for sg in j["segs"])
+            tile = 2 if tiles64 >= 240 and not tbw else 1
         _lib.check(self.lib.tdmpc_lg_gemm(arr, len(jobs), tile, self._stream()), "tdmpc_lg_gemm")
 
     def rows(self, heads, n, bwd=False, **kw):
@@ -331,7 +334,7 @@ class Engine:
                               _seg(_p(dP1[2]), M, w("_reward.0.weight"), LA, M, bmode=1)],
                          m=R, n=L, c=_p(S), ldc=L, res=_p(dZP), ldres=L)])
         # ---- the heads' weight gradients (side stream) beside the latent rollout's backward ----
-        sp = 2 if R >= 1024 else 1
+        sp = 4 if R >= 1024 else 1
         dw_h = [("_reward.2", M, M, [_seg(_p(dP2[2]), M, _p(PA[2]), M, R, 1, 1, M)], sp),
                 ("_reward.0", M, LA, [_seg(_p(dP1[2]), M, _p(X0), LA, R, 1, 1, LA)], sp)]
         for h in range(2):
@@ -396,7 +399,9 @@ class Engine:
             buf = self.slot(b, f"{tag}:{name}", s * o * (i + 1))
             slots[name] = _p(buf)
             jobs.append(dict(segs=segs, m=o, n=i + 1, c=_p(buf), ldc=i + 1, splits=s, slice=o * (i + 1)))
-        self.gemm(jobs, tile=2)
+        # 32 x 32 tiles, K (the rows) split 4 ways: 2-3x faster than 64 x 64 tiles for these narrow-N / long-K
+        # products on MI355X (tools/lg_gemm_bench.py --dw: 512 x 122 x 2560 12 vs 38 us)
+        self.gemm(jobs, tile=1)
         return slots
 
     def _optimise(self, opt, src, g_lo, norm_out):
@@ -461,7 +466,7 @@ class Engine:
                         c=_p(b["dPp2"]), ldc=M, epi=EPI_ELU_BWD, aux=_p(b["Yp2"]), ldaux=M)])
         self.gemm([dict(segs=[_seg(_p(b["dPp2"]), M, w("_pi.2.weight"), M, M, bmode=1)], m=n, n=M,
                         c=_p(b["dPp1"]), ldc=M, epi=EPI_ELU_BWD, aux=_p(b["Yp1"]), ldaux=M)])
-        sp = 2 if n >= 1024 else 1
+        sp = 4 if n >= 1024 else 1
         dw = [("_pi.4", A, M, [_seg(_p(b["dACT"]), A, _p(b["Yp2"]), M, n, 1, 1, M)], sp),
               ("_pi.2", M, M, [_seg(_p(b["dPp2"]), M, _p(b["Yp1"]), M, n, 1, 1, M)], sp),
               ("_pi.0", M, L, [_seg(_p(b["dPp1"]), M, z, ldz, n, 1, 1, L)], sp)]
