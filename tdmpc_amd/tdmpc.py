@@ -116,6 +116,14 @@ class HipPlanner:
         self._packed_model = None
         self._packed_params = []
         self._graphs = {}
+        # pinned host staging for the per-call traffic of the drop-in plan(): the observation and numpy's
+        # uniform go up, the metrics come down, each as one async copy (a pageable copy blocks the host and an
+        # intermediate device tensor costs a copy kernel)
+        pin = dev.type == "cuda"
+        self._pin_obs = torch.zeros(self.obs_buf.shape, dtype=self.obs_buf.dtype, pin_memory=pin)
+        self._pin_u = torch.zeros(max_batch, dtype=torch.float64, pin_memory=pin)
+        self._pin_met = torch.zeros(max_batch, 2, dtype=torch.float32, pin_memory=pin)
+        self._h2d_done = torch.cuda.Event() if pin else None
 
     # ------------------------------------------------------------------ weights
     def pack(self, model: TOLD):
@@ -436,7 +444,13 @@ class TDMPC:
                 raise RuntimeError(f"shape mismatch: prev_mean horizon {self._prev_H[e]} vs {H}")
             warm.append(w)
         pl.pack(self.model)
-        if cfg.modality == "pixels":
+        host = not torch.is_tensor(obs) or obs.device.type == "cpu"
+        if host and pl._h2d_done is not None:
+            # host observations through the pinned staging buffer (the previous call's copy has drained first)
+            pl._h2d_done.synchronize()
+            pl._pin_obs[:B].view(B, -1).copy_(torch.as_tensor(obs).reshape(B, -1))
+            pl.obs_buf[:B].copy_(pl._pin_obs[:B], non_blocking=True)
+        elif cfg.modality == "pixels":
             src = torch.as_tensor(obs).to(self.device, torch.uint8)
             pl.obs_buf[:B].copy_(src.view(B, *cfg.obs_shape))
         else:
@@ -453,8 +467,15 @@ class TDMPC:
             pl.u[:B].copy_(torch.tensor(us, dtype=torch.float64))
         elif self.rng == "reference":
             # np.random.choice's uniform, drawn on the host from numpy's global generator (tdmpc.py:153)
-            pl.u[:B].copy_(torch.tensor([float(np.random.random_sample()) for _ in range(B)],
-                                        dtype=torch.float64))
+            us = [float(np.random.random_sample()) for _ in range(B)]
+            if pl._h2d_done is not None:
+                for e in range(B):
+                    pl._pin_u[e] = us[e]
+                pl.u[:B].copy_(pl._pin_u[:B], non_blocking=True)
+            else:
+                pl.u[:B].copy_(torch.tensor(us, dtype=torch.float64))
+        if pl._h2d_done is not None:
+            pl._h2d_done.record()
 
         def device_work():
             if noise is None:
@@ -484,5 +505,10 @@ class TDMPC:
         actions = pl.action[:B]
         if not sync_metrics:
             return actions, pl.metrics[:B]
-        m = pl.metrics[:B].double().cpu().numpy()
+        if pl._h2d_done is not None:
+            pl._pin_met[:B].copy_(pl.metrics[:B], non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            m = pl._pin_met[:B].tolist()
+        else:
+            m = pl.metrics[:B].double().cpu().tolist()
         return actions, [{"external_reward_mean": float(r), "current_std": float(s)} for r, s in m]
