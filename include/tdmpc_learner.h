@@ -129,6 +129,10 @@ int tdmpc_lg_adam(float* p, const float* g, float* m, float* v, int64_t n, const
 /* t <- lerp(t, p, w) elementwise (helper.ema, helper.py:48-52). */
 int tdmpc_lg_lerp(float* t, const float* p, int64_t n, float w, void* stream);
 
+/* In place over n elements: mode 0 x <- ELU(x) (nn.ELU, helper.py:172); mode 1 x <- x * ELU'(y) with y the saved
+ * ELU output (y > 0 ? 1 : y + 1) -- the activation epilogues of a library GEMM's output. */
+int tdmpc_lg_act(float* x, const float* y, int64_t n, int32_t mode, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,7 +24,7 @@ EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc
             # include/tdmpc_learner.h
             "tdmpc_loss_forward", "tdmpc_loss_backward", "tdmpc_random_shift",
             "tdmpc_lg_gemm", "tdmpc_lg_rows_fwd", "tdmpc_lg_rows_bwd", "tdmpc_lg_pi_loss", "tdmpc_lg_finalize",
-            "tdmpc_lg_adam", "tdmpc_lg_lerp")
+            "tdmpc_lg_adam", "tdmpc_lg_lerp", "tdmpc_lg_act")
 
 
 class Dims(C.Structure):
@@ -155,6 +155,7 @@ def lib():
     L.tdmpc_lg_adam.argtypes = [vp, vp, vp, vp, C.c_int64, vp, i32, vp, C.c_float, C.c_float, C.c_float,
                                 C.c_float, C.c_float, vp, vp]
     L.tdmpc_lg_lerp.argtypes = [vp, vp, C.c_int64, C.c_float, vp]
+    L.tdmpc_lg_act.argtypes = [vp, vp, C.c_int64, i32, vp]
     for name in EXPORTED:
         if not hasattr(L, name):
             raise RuntimeError(f"{LIB_PATH} does not export {name}")

@@ -533,6 +533,22 @@ __global__ void __launch_bounds__(256) lg_lerp_kernel(float* t, const float* p, 
     }
 }
 
+__global__ void __launch_bounds__(256) lg_act_kernel(float4* x, const float4* y, long n4, int mode) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        float4 v = x[i];
+        if (mode == 0) {
+            v = make_float4(elu_f(v.x), elu_f(v.y), elu_f(v.z), elu_f(v.w));
+        } else {
+            const float4 a = y[i];
+            v.x *= a.x > 0.f ? 1.f : a.x + 1.f;
+            v.y *= a.y > 0.f ? 1.f : a.y + 1.f;
+            v.z *= a.z > 0.f ? 1.f : a.z + 1.f;
+            v.w *= a.w > 0.f ? 1.f : a.w + 1.f;
+        }
+        x[i] = v;
+    }
+}
+
 int fail(hipError_t e, const char* what) {
     char msg[256];
     snprintf(msg, sizeof msg, "learner_engine %s: %s", what, hipGetErrorString(e));
@@ -677,6 +693,16 @@ int tdmpc_lg_lerp(float* t, const float* p, int64_t n, float w, void* stream) {
     const unsigned blocks = (unsigned)std::min<long>((n + 255) / 256, 2048);
     hipLaunchKernelGGL(lg_lerp_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, t, p, (long)n, w);
     return launched("lerp");
+}
+
+int tdmpc_lg_act(float* x, const float* y, int64_t n, int32_t mode, void* stream) {
+    if (!x || (mode == 1 && !y)) return TDMPC_E_NULL;
+    if (n <= 0 || n % 4 || (mode != 0 && mode != 1)) return bad("tdmpc_lg_act: n / mode");
+    if (((uintptr_t)x & 15) || (y && ((uintptr_t)y & 15))) return bad("tdmpc_lg_act: alignment");
+    const unsigned blocks = (unsigned)std::min<long>((n / 4 + 255) / 256, 2048);
+    hipLaunchKernelGGL(lg_act_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (float4*)x, (const float4*)y,
+                       (long)(n / 4), mode);
+    return launched("act");
 }
 
 }  // extern "C"

@@ -114,6 +114,28 @@ class Engine:
         o, _ = self.off[k]
         return _p(self.PT if target else self.P, o)
 
+    def wv(self, k, target=False):
+        """The parameter `k` as a tensor view of the flat buffer."""
+        o, shape = self.off[k]
+        n = int(torch.Size(shape).numel())
+        return (self.PT if target else self.P)[o:o + n].view(shape)
+
+    def mm(self, x, k, out, bias=None, target=False, transpose=False):
+        """out = x @ W^T (+ bias) -- or x @ W with transpose=True (the backward's dX) -- for the plain M x M
+        products of a pass on hipBLASLt (no epilogue to fuse: 20-30 % faster than lg_gemm at these shapes,
+        tools/mm_calibrate.py vs tools/lg_gemm_bench.py)."""
+        w = self.wv(k, target)
+        w = w if transpose else w.t()
+        if bias is None:
+            torch.mm(x, w, out=out)
+        else:
+            torch.addmm(self.wv(bias, target), x, w, out=out)
+
+    def act(self, x, y=None):
+        """x <- ELU(x) (y None) or x <- x * ELU'(y) in place (tdmpc_lg_act)."""
+        _lib.check(self.lib.tdmpc_lg_act(_p(x), None if y is None else _p(y), x.numel(), 0 if y is None else 1,
+                                         self._stream()), "tdmpc_lg_act")
+
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
 
@@ -212,8 +234,8 @@ class Engine:
                         ldc=LA, bias=w("_encoder.2.bias"))])
         self.gemm([dict(segs=[_seg(_p(b["Xtd"]), LA, w("_pi.0.weight"), L, L)], m=R, n=M, c=_p(b["T1"]), ldc=M,
                         bias=w("_pi.0.bias"), epi=EPI_ELU)])
-        self.gemm([dict(segs=[_seg(_p(b["T1"]), M, w("_pi.2.weight"), M, M)], m=R, n=M, c=_p(b["T2"]), ldc=M,
-                        bias=w("_pi.2.bias"), epi=EPI_ELU)])
+        self.mm(b["T1"], "_pi.2.weight", b["T2"], bias="_pi.2.bias")
+        self.act(b["T2"])
         self.gemm([dict(segs=[_seg(_p(b["T2"]), M, w("_pi.4.weight"), M, M)], m=R, n=A, c=_p(b["Xtd"], L),
                         ldc=LA, bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MUtd"]), ldc2=A,
                         std=float(self.cfg.min_std))])
@@ -222,8 +244,8 @@ class Engine:
                         c=_p(PA[h]), ldc=M, bias=wt(f"_Q{h + 1}.0.bias")) for h in range(2)])
         self.rows([dict(x=_p(PA[h]), y=_p(PB[h]), ln=1, g=wt(f"_Q{h + 1}.1.weight"), beta=wt(f"_Q{h + 1}.1.bias"),
                         act=TANH) for h in range(2)], R)
-        self.gemm([dict(segs=[_seg(_p(PB[h]), M, wt(f"_Q{h + 1}.3.weight"), M, M)], m=R, n=M, c=_p(PA[h]), ldc=M,
-                        bias=wt(f"_Q{h + 1}.3.bias")) for h in range(2)])
+        for h in range(2):
+            self.mm(PB[h, :R], f"_Q{h + 1}.3.weight", PA[h, :R], bias=f"_Q{h + 1}.3.bias", target=True)
         self.rows([dict(x=_p(PA[h]), ln=1, g=wt(f"_Q{h + 1}.4.weight"), beta=wt(f"_Q{h + 1}.4.bias"), act=ELU,
                         tail=1, w3=wt(f"_Q{h + 1}.6.weight"), b3=wt(f"_Q{h + 1}.6.bias"), out=_p(b["TQ"][h]))
                    for h in range(2)], R, reward=rew, td=_p(b["TD"]), gamma=float(self.cfg.discount))
@@ -284,11 +306,10 @@ class Engine:
             b, R, lambda h: [_seg(_p(X0), LA, w(f"_Q{h + 1}.0.weight"), LA, LA)])
         # reward head layer 1 (ELU) rides in its own slot 2 of PA / Y2 buffers
         self.gemm([dict(segs=[_seg(_p(X0), LA, w("_reward.0.weight"), LA, LA)], m=R, n=M, c=_p(PA[2]), ldc=M,
-                        bias=w("_reward.0.bias"), epi=EPI_ELU)]
-                  + [dict(segs=[_seg(_p(Y1[h]), M, w(f"_Q{h + 1}.3.weight"), M, M)], m=R, n=M, c=_p(PB[h]), ldc=M,
-                          bias=w(f"_Q{h + 1}.3.bias")) for h in range(2)])
-        self.gemm([dict(segs=[_seg(_p(PA[2]), M, w("_reward.2.weight"), M, M)], m=R, n=M, c=_p(PB[2]), ldc=M,
-                        bias=w("_reward.2.bias"))])
+                        bias=w("_reward.0.bias"), epi=EPI_ELU)])
+        for h in range(2):
+            self.mm(Y1[h, :R], f"_Q{h + 1}.3.weight", PB[h, :R], bias=f"_Q{h + 1}.3.bias")
+        self.mm(PA[2, :R], "_reward.2.weight", PB[2, :R], bias="_reward.2.bias")
         Q = b["Q"]
         heads = [dict(x=_p(PB[h]), y=_p(Y2[h]), xhat=_p(XH2[h]), rstd=_p(RS2[h]), ln=1, g=w(f"_Q{h + 1}.4.weight"),
                       beta=w(f"_Q{h + 1}.4.bias"), act=ELU, tail=1, w3=w(f"_Q{h + 1}.6.weight"),
@@ -321,10 +342,10 @@ class Engine:
         heads.append(dict(y=_p(dP2[2]), yact=_p(Y2[2]), act=ELU, tail=1, w3=w("_reward.4.weight"), dq=_p(dq[2]),
                           part=_p(partr)))
         self.rows(heads, R, bwd=True)
-        self.gemm([dict(segs=[_seg(_p(dP2[h]), M, w(f"_Q{h + 1}.3.weight"), M, M, bmode=1)], m=R, n=M,
-                        c=_p(dA[h]), ldc=M) for h in range(2)]
-                  + [dict(segs=[_seg(_p(dP2[2]), M, w("_reward.2.weight"), M, M, bmode=1)], m=R, n=M,
-                          c=_p(dP1[2]), ldc=M, epi=EPI_ELU_BWD, aux=_p(PA[2]), ldaux=M)])
+        for h in range(2):
+            self.mm(dP2[h, :R], f"_Q{h + 1}.3.weight", dA[h, :R], transpose=True)
+        self.gemm([dict(segs=[_seg(_p(dP2[2]), M, w("_reward.2.weight"), M, M, bmode=1)], m=R, n=M,
+                        c=_p(dP1[2]), ldc=M, epi=EPI_ELU_BWD, aux=_p(PA[2]), ldaux=M)])
         self.rows([dict(x=_p(dA[h]), y=_p(dP1[h]), yact=_p(Y1[h]), xhat=_p(XH1[h]), rstd=_p(RS1[h]), ln=1,
                         g=w(f"_Q{h + 1}.1.weight"), act=TANH, part=_p(part1[h])) for h in range(2)], R, bwd=True)
         # gradient of z_t from the three heads (+ the consistency term on z_t): S = sum_h dP1_h W1_h[:, :L] + dZP
@@ -433,16 +454,16 @@ class Engine:
         w = self.w
         self.gemm([dict(segs=[_seg(z, ldz, w("_pi.0.weight"), L, L)], m=n, n=M, c=_p(b["Yp1"]), ldc=M,
                         bias=w("_pi.0.bias"), epi=EPI_ELU)])
-        self.gemm([dict(segs=[_seg(_p(b["Yp1"]), M, w("_pi.2.weight"), M, M)], m=n, n=M, c=_p(b["Yp2"]), ldc=M,
-                        bias=w("_pi.2.bias"), epi=EPI_ELU)])
+        self.mm(b["Yp1"][:n], "_pi.2.weight", b["Yp2"][:n], bias="_pi.2.bias")
+        self.act(b["Yp2"][:n])
         self.gemm([dict(segs=[_seg(_p(b["Yp2"]), M, w("_pi.4.weight"), M, M)], m=n, n=A, c=_p(b["ACT"]), ldc=A,
                         bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MU"]), ldc2=A,
                         std=float(self.cfg.min_std))])
         PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(
             b, n, lambda h: [_seg(z, ldz, w(f"_Q{h + 1}.0.weight"), LA, L),
                              _seg(_p(b["ACT"]), A, w(f"_Q{h + 1}.0.weight") + 4 * L, LA, A)])
-        self.gemm([dict(segs=[_seg(_p(Y1[h]), M, w(f"_Q{h + 1}.3.weight"), M, M)], m=n, n=M, c=_p(PB[h]), ldc=M,
-                        bias=w(f"_Q{h + 1}.3.bias")) for h in range(2)])
+        for h in range(2):
+            self.mm(Y1[h, :n], f"_Q{h + 1}.3.weight", PB[h, :n], bias=f"_Q{h + 1}.3.bias")
         Q = b["Q"]
         self.rows([dict(x=_p(PB[h]), y=_p(Y2[h]), xhat=_p(XH2[h]), rstd=_p(RS2[h]), ln=1, g=w(f"_Q{h + 1}.4.weight"),
                         beta=w(f"_Q{h + 1}.4.bias"), act=ELU, tail=1, w3=w(f"_Q{h + 1}.6.weight"),
@@ -455,8 +476,8 @@ class Engine:
         self.rows([dict(y=_p(dP2[h]), yact=_p(Y2[h]), xhat=_p(XH2[h]), rstd=_p(RS2[h]), ln=1,
                         g=w(f"_Q{h + 1}.4.weight"), act=ELU, tail=1, w3=w(f"_Q{h + 1}.6.weight"))
                    for h in range(2)], n, bwd=True, q1=_p(Q[0]), q2=_p(Q[1]), rho=_p(self.rho), bsz=B)
-        self.gemm([dict(segs=[_seg(_p(dP2[h]), M, w(f"_Q{h + 1}.3.weight"), M, M, bmode=1)], m=n, n=M,
-                        c=_p(dA[h]), ldc=M) for h in range(2)])
+        for h in range(2):
+            self.mm(dP2[h, :n], f"_Q{h + 1}.3.weight", dA[h, :n], transpose=True)
         self.rows([dict(x=_p(dA[h]), y=_p(dP1[h]), yact=_p(Y1[h]), xhat=_p(XH1[h]), rstd=_p(RS1[h]), ln=1,
                         g=w(f"_Q{h + 1}.1.weight"), act=TANH) for h in range(2)], n, bwd=True)
         self.gemm([dict(segs=[_seg(_p(dP1[h]), M, w(f"_Q{h + 1}.0.weight") + 4 * L, LA, M, bmode=1)
@@ -464,8 +485,8 @@ class Engine:
                         m=n, n=A, c=_p(b["dACT"]), ldc=A, epi=EPI_PI_BWD, aux=_p(b["MU"]), ldaux=A)])
         self.gemm([dict(segs=[_seg(_p(b["dACT"]), A, w("_pi.4.weight"), M, A, bmode=1)], m=n, n=M,
                         c=_p(b["dPp2"]), ldc=M, epi=EPI_ELU_BWD, aux=_p(b["Yp2"]), ldaux=M)])
-        self.gemm([dict(segs=[_seg(_p(b["dPp2"]), M, w("_pi.2.weight"), M, M, bmode=1)], m=n, n=M,
-                        c=_p(b["dPp1"]), ldc=M, epi=EPI_ELU_BWD, aux=_p(b["Yp1"]), ldaux=M)])
+        self.mm(b["dPp2"][:n], "_pi.2.weight", b["dPp1"][:n], transpose=True)
+        self.act(b["dPp1"][:n], b["Yp1"][:n])
         sp = 4 if n >= 1024 else 1
         dw = [("_pi.4", A, M, [_seg(_p(b["dACT"]), A, _p(b["Yp2"]), M, n, 1, 1, M)], sp),
               ("_pi.2", M, M, [_seg(_p(b["dPp2"]), M, _p(b["Yp1"]), M, n, 1, 1, M)], sp),

@@ -45,6 +45,12 @@ def run(m, n, k, amode, bmode, tile, splits=1, reps=50):
 
 
 import sys as _s
+if "--small" in _s.argv:
+    for (m, n, k, am, bm) in [(512, 512, 512, 0, 0), (512, 512, 121, 0, 0), (512, 100, 512, 0, 0),
+                              (512, 512, 100, 0, 1), (512, 512, 512, 0, 1), (512, 100, 512, 0, 1)]:
+        for tile in (1, 3):
+            run(m, n, k, am, bm, tile)
+    _s.exit(0)
 for (m, n, k) in ([] if "--dw" in _s.argv else [(2560, 512, 512), (3072, 512, 512), (512, 512, 512), (2560, 512, 121), (2560, 21, 512)]):
     for amode, bmode in [(0, 0), (0, 1), (1, 1)]:
         for tile in (1, 2):
