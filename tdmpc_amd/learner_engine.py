@@ -120,13 +120,18 @@ class Engine:
         n = int(torch.Size(shape).numel())
         return (self.PT if target else self.P)[o:o + n].view(shape)
 
-    def mm(self, x, k, out, bias=None, target=False, transpose=False):
-        """out = x @ W^T (+ bias) -- or x @ W with transpose=True (the backward's dX) -- for the plain M x M
-        products of a pass on hipBLASLt (no epilogue to fuse: 20-30 % faster than lg_gemm at these shapes,
-        tools/mm_calibrate.py vs tools/lg_gemm_bench.py)."""
+    def mm(self, x, k, out, bias=None, target=False, transpose=False, cols=None, acc=False):
+        """out = x @ W^T (+ bias) -- or x @ W with transpose=True (the backward's dX) -- for the products of a
+        pass with no epilogue to fuse, on hipBLASLt (20-30 % faster than lg_gemm at the learner's 2560-3072-row
+        shapes, tools/mm_calibrate.py vs tools/lg_gemm_bench.py). cols: W's input columns [c0, c1) only (a
+        layer whose input is split over two tensors); acc: out += x @ W^T."""
         w = self.wv(k, target)
+        if cols is not None:
+            w = w[:, cols[0]:cols[1]]
         w = w if transpose else w.t()
-        if bias is None:
+        if acc:
+            out.addmm_(x, w)
+        elif bias is None:
             torch.mm(x, w, out=out)
         else:
             torch.addmm(self.wv(bias, target), x, w, out=out)
@@ -232,16 +237,16 @@ class Engine:
                         ldc=L, bias=wt("_encoder.2.bias")),
                    dict(segs=[_seg(_p(b["Yo1"]), E, w("_encoder.2.weight"), E, E)], m=R, n=L, c=_p(b["Xtd"]),
                         ldc=LA, bias=w("_encoder.2.bias"))])
-        self.gemm([dict(segs=[_seg(_p(b["Xtd"]), LA, w("_pi.0.weight"), L, L)], m=R, n=M, c=_p(b["T1"]), ldc=M,
-                        bias=w("_pi.0.bias"), epi=EPI_ELU)])
+        self.mm(b["Xtd"][:, :L], "_pi.0.weight", b["T1"], bias="_pi.0.bias")
+        self.act(b["T1"])
         self.mm(b["T1"], "_pi.2.weight", b["T2"], bias="_pi.2.bias")
         self.act(b["T2"])
         self.gemm([dict(segs=[_seg(_p(b["T2"]), M, w("_pi.4.weight"), M, M)], m=R, n=A, c=_p(b["Xtd"], L),
                         ldc=LA, bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MUtd"]), ldc2=A,
                         std=float(self.cfg.min_std))])
         PA, PB = b["PAt"], b["PBt"]
-        self.gemm([dict(segs=[_seg(_p(b["Xtd"]), LA, wt(f"_Q{h + 1}.0.weight"), LA, LA)], m=R, n=M,
-                        c=_p(PA[h]), ldc=M, bias=wt(f"_Q{h + 1}.0.bias")) for h in range(2)])
+        for h in range(2):
+            self.mm(b["Xtd"], f"_Q{h + 1}.0.weight", PA[h, :R], bias=f"_Q{h + 1}.0.bias", target=True)
         self.rows([dict(x=_p(PA[h]), y=_p(PB[h]), ln=1, g=wt(f"_Q{h + 1}.1.weight"), beta=wt(f"_Q{h + 1}.1.bias"),
                         act=TANH) for h in range(2)], R)
         for h in range(2):
@@ -250,13 +255,14 @@ class Engine:
                         tail=1, w3=wt(f"_Q{h + 1}.6.weight"), b3=wt(f"_Q{h + 1}.6.bias"), out=_p(b["TQ"][h]))
                    for h in range(2)], R, reward=rew, td=_p(b["TD"]), gamma=float(self.cfg.discount))
 
-    def q_forward(self, b, n, x_segs, save=True):
-        """helper.q for both Q heads over n rows: layer 1 from the segments x_segs(h) -> Q values b["Q"][0:2]."""
-        M = self.M
+    def q_forward(self, b, n, parts):
+        """helper.q layer 1 + LayerNorm + Tanh for both Q heads over n rows; the input is the concatenation of
+        parts [(tensor [n, c1 - c0], c0, c1)] along the feature axis."""
         w = self.w
         PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = (b[k] for k in ("PA", "PB", "Y1", "Y2", "XH1", "XH2", "RS1", "RS2"))
-        self.gemm([dict(segs=x_segs(h), m=n, n=M, c=_p(PA[h]), ldc=M, bias=w(f"_Q{h + 1}.0.bias"))
-                   for h in range(2)])
+        for h in range(2):
+            for i, (x, c0, c1) in enumerate(parts):
+                self.mm(x, f"_Q{h + 1}.0.weight", PA[h, :n], bias=f"_Q{h + 1}.0.bias", cols=(c0, c1), acc=i > 0)
         self.rows([dict(x=_p(PA[h]), y=_p(Y1[h]), xhat=_p(XH1[h]), rstd=_p(RS1[h]), ln=1,
                         g=w(f"_Q{h + 1}.1.weight"), beta=w(f"_Q{h + 1}.1.bias"), act=TANH) for h in range(2)], n)
         return PA, PB, Y1, Y2, XH1, XH2, RS1, RS2
@@ -302,11 +308,10 @@ class Engine:
             self.gemm([dict(segs=[_seg(_p(b["Yd2"], t * B * M), M, w("_dynamics.4.weight"), M, M)], m=B, n=L,
                             c=_p(X0, (t + 1) * B * LA), ldc=LA, bias=w("_dynamics.4.bias"),
                             c2=_p(b["ZP"], t * B * L), ldc2=L)])
-        PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(
-            b, R, lambda h: [_seg(_p(X0), LA, w(f"_Q{h + 1}.0.weight"), LA, LA)])
+        PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(b, R, [(X0[:R], 0, LA)])
         # reward head layer 1 (ELU) rides in its own slot 2 of PA / Y2 buffers
-        self.gemm([dict(segs=[_seg(_p(X0), LA, w("_reward.0.weight"), LA, LA)], m=R, n=M, c=_p(PA[2]), ldc=M,
-                        bias=w("_reward.0.bias"), epi=EPI_ELU)])
+        self.mm(X0[:R], "_reward.0.weight", PA[2, :R], bias="_reward.0.bias")
+        self.act(PA[2, :R])
         for h in range(2):
             self.mm(Y1[h, :R], f"_Q{h + 1}.3.weight", PB[h, :R], bias=f"_Q{h + 1}.3.bias")
         self.mm(PA[2, :R], "_reward.2.weight", PB[2, :R], bias="_reward.2.bias")
@@ -409,7 +414,7 @@ class Engine:
         buffer.update_priorities(idxs, b["lrows"][3].view(B, 1))
 
         # ---- update_pi on the detached latents z_0..z_H (tdmpc.py:165-182) ----
-        pi_loss = self._update_pi(b, _p(X0), LA, H + 1, B, _p(eps, R * A))
+        pi_loss = self._update_pi(b, X0[:, :L], H + 1, B, _p(eps, R * A))
         scal = b["scal"]
         return torch.cat([scal[0:3], pi_loss, scal[3:5], b["gnorm"]])
 
@@ -447,21 +452,21 @@ class Engine:
                                           opt.lr, 0.9, 0.999, 1e-8, float(self.cfg.grad_clip_norm), norm_out, st),
                    "tdmpc_lg_adam")
 
-    def _update_pi(self, b, z, ldz, nt, B, eps):
-        """TDMPC.update_pi over nt latent blocks of B rows at z (row stride ldz) -> pi_loss tensor [1]."""
+    def _update_pi(self, b, zt, nt, B, eps):
+        """TDMPC.update_pi over the nt latent blocks of B rows of zt ([nt B, L], rows may be strided) -> pi_loss
+        tensor [1]."""
         L, A, M, LA = self.L, self.A, self.M, self.LA
         n = nt * B
         w = self.w
-        self.gemm([dict(segs=[_seg(z, ldz, w("_pi.0.weight"), L, L)], m=n, n=M, c=_p(b["Yp1"]), ldc=M,
-                        bias=w("_pi.0.bias"), epi=EPI_ELU)])
+        z, ldz = _p(zt), zt.stride(0)
+        self.mm(zt, "_pi.0.weight", b["Yp1"][:n], bias="_pi.0.bias")
+        self.act(b["Yp1"][:n])
         self.mm(b["Yp1"][:n], "_pi.2.weight", b["Yp2"][:n], bias="_pi.2.bias")
         self.act(b["Yp2"][:n])
         self.gemm([dict(segs=[_seg(_p(b["Yp2"]), M, w("_pi.4.weight"), M, M)], m=n, n=A, c=_p(b["ACT"]), ldc=A,
                         bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MU"]), ldc2=A,
                         std=float(self.cfg.min_std))])
-        PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(
-            b, n, lambda h: [_seg(z, ldz, w(f"_Q{h + 1}.0.weight"), LA, L),
-                             _seg(_p(b["ACT"]), A, w(f"_Q{h + 1}.0.weight") + 4 * L, LA, A)])
+        PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(b, n, [(zt, 0, L), (b["ACT"][:n], L, LA)])
         for h in range(2):
             self.mm(Y1[h, :n], f"_Q{h + 1}.3.weight", PB[h, :n], bias=f"_Q{h + 1}.3.bias")
         Q = b["Q"]
@@ -513,7 +518,7 @@ class Engine:
         else:
             e.copy_(torch.cat([x.reshape(B, self.A) for x in list(eps)[:nt]]).to(self.dev))
         b["zpi"] = Z          # kept alive until the kernels have run
-        return self._update_pi(b, _p(Z), self.L, nt, B, _p(e)).clone()
+        return self._update_pi(b, Z, nt, B, _p(e)).clone()
 
     def ema(self, tau):
         _lib.check(self.lib.tdmpc_lg_lerp(_p(self.PT), _p(self.P), self.P.numel(), float(tau), self._stream()),
