@@ -1,0 +1,72 @@
+"""src/train.py's loop on the drop-in agent (reference: /root/reference/src/train.py:80-110): plan() (HIP graph,
+reference-order RNG) -> buffer.add -> update() (the learner's captured HIP graph) -> plan() again. A replayed graph
+writes the parameters in place without bumping their tensor versions, so the learner tells the planner to repack;
+this test holds the next plan to the oracle evaluated on the agent's CURRENT weights."""
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+from learner_io import learner_cfg
+from oracle import tdmpc_ref
+from tdmpc_amd.told import synthetic_state_dict
+
+
+def _oracle_first_values(agent, cfg, obs, step):
+    """First-iteration candidate values of a cold plan() traced on the GPU, and the oracle's on the same noise and
+    the agent's current state_dict (the recipe of __graft_entry__.smoke)."""
+    trace = {}
+    std = float(agent.std)
+    agent._plan_envs(obs[None], False, step, [True], trace=trace)
+    pl = agent.planner
+    H, I = agent.horizon(step), cfg.iterations
+    lay = pl.noise_layout(H, I)
+    buf = pl.noise_view(H, I, 1)[0].cpu()
+    P, N, A, T = pl.P, pl.N, pl.A, pl.T
+    nb = tdmpc_ref.NoiseBundle(eps_pi=buf[:H * P * A].view(H, P, A))
+    for i in range(I):
+        o = lay["cem_off"] + i * lay["iter"]
+        nb.eps_cem.append(buf[o:o + H * N * A].view(H, N, A))
+        nb.eps_term.append(buf[o + H * N * A:o + H * N * A + T * A].view(T, A))
+    nb.u = float(pl.u[0].cpu())
+    nb.eps_act = buf[lay["act_off"]:lay["act_off"] + A]
+    sd = {k: v.detach().cpu() for k, v in agent.model.state_dict().items()}
+    told = tdmpc_ref.RefTOLD(sd, cfg)
+    ref_trace = {}
+    tdmpc_ref.plan(told, cfg, tdmpc_ref.PlanState(std), obs, nb, eval_mode=False, step=step, t0=True,
+                   trace=ref_trace)
+    return trace["value"][0, 0].cpu(), ref_trace["value"][0].squeeze(1)
+
+
+@pytest.mark.gpu
+def test_train_loop_plans_with_updated_weights():
+    from tdmpc_amd.replay import ReplayBuffer
+    from tdmpc_amd.tdmpc import TDMPC
+    cfg = learner_cfg()
+    rc = SimpleNamespace(**{**vars(cfg), "device": "cuda", "train_steps": 2000, "max_buffer_size": 10**6,
+                            "episode_length": 200, "env_horizon": cfg.horizon})
+    rs = np.random.RandomState(3)
+    agent = TDMPC(cfg)
+    agent.model.load_state_dict(synthetic_state_dict(cfg, 41))
+    agent.model_target.load_state_dict(synthetic_state_dict(cfg, 42))
+    agent.learner(graph=True, warmup=2)
+    buf = ReplayBuffer(rc, latent_plan=True)
+    for _ in range(3):
+        buf.add(SimpleNamespace(obs=torch.from_numpy(rs.standard_normal((201, 5)).astype(np.float32)),
+                                action=torch.from_numpy(rs.uniform(-1, 1, (200, 1)).astype(np.float32)),
+                                reward=torch.from_numpy(rs.standard_normal(200).astype(np.float32))))
+    w0 = [p.detach().clone() for p in agent.model.parameters()]
+    obs = rs.standard_normal(cfg.obs_shape).astype(np.float32)
+    torch.manual_seed(0)
+    np.random.seed(0)
+    step = 10**6
+    for k in range(6):
+        a, m = agent.plan(obs, step=step, t0=(k == 0))
+        assert torch.isfinite(a).all()   # (not clamped: the reference adds std * randn to the mean, tdmpc.py:161)
+        agent.update(buf, k + 1)
+    assert agent.learner()._graphs, "the learner never replayed its captured graph"
+    assert any(not torch.equal(p, q) for p, q in zip(agent.model.parameters(), w0)), "no update reached the model"
+    v_gpu, v_ref = _oracle_first_values(agent, cfg, obs, step)
+    err = (v_gpu - v_ref).abs().max().item()
+    assert err < 1e-4 * (1 + v_ref.abs().max().item()), f"plan after graph-replayed updates: max|dG| {err}"
