@@ -88,6 +88,26 @@ def test_entry_points_reject_null_arguments():
                             None, None, 0, None) == E_NULL
     assert L.tdmpc_encode(C.byref(d), None, None, 0, 1, None, None, None) == E_NULL
     assert L.tdmpc_pack_weights(C.byref(d), None, 0, None, 0, None) == E_NULL
+    # learner engine (include/tdmpc_learner.h)
+    assert L.tdmpc_lg_gemm(None, 1, 1, None) == E_NULL
+    assert L.tdmpc_lg_lerp(None, None, 16, 0.5, None) == E_NULL
+    assert L.tdmpc_lg_act(None, None, 16, 0, None) == E_NULL
+    assert L.tdmpc_lg_adam(None, None, None, None, 16, None, 1, None, 1e-3, 0.9, 0.999, 1e-8, 10.0, None,
+                           None) == E_NULL
+
+
+def test_learner_entry_points_reject_bad_shapes():
+    """Shape / mode checks run before any launch: TDMPC_E_DIMS (-1), the message in tdmpc_last_error."""
+    L = _lib.lib()
+    E_DIMS = -1
+    x = C.c_void_p(16)   # never dereferenced: the checks fail first
+    assert L.tdmpc_lg_act(x, None, 6, 0, None) == E_DIMS            # n not a multiple of 4
+    assert L.tdmpc_lg_act(x, None, 16, 2, None) == E_DIMS           # unknown mode
+    assert L.tdmpc_lg_act(x, None, 16, 1, None) == -3               # mode 1 needs the activation
+    jobs = (_lib.LgJob * 1)()
+    assert L.tdmpc_lg_gemm(jobs, 0, 1, None) == E_DIMS              # no jobs
+    assert L.tdmpc_lg_gemm(jobs, 1, 7, None) == E_DIMS              # unknown tile
+    assert L.tdmpc_lg_gemm(jobs, 1, 1, None) == E_DIMS              # job without an output / shape
 
 
 def test_packed_buffer_holds_the_x6_copy():
