@@ -4,8 +4,9 @@
 // TOLD heads of helper.py:150-176 (enc, mlp, q) and TruncatedNormal.sample (helper.py:71-96). The reference
 // runs them as ~1,500 one-op launches through autograd; tdmpc_amd/learner_engine.py runs the same math as ~80
 // launches of four kernel families (include/tdmpc_learner.h):
-//   * lg_gemm_kernel: grouped fp32 GEMM on v_mfma_f32_32x32x2_f32 (exact f32 products, as the reference's
-//     fp32 Linear layers) with the bias, a residual, ELU / policy-sampling / activation-backward epilogues fused.
+//   * lg_gemm_kernel: grouped fp32 GEMM -- fp32-accurate x6 products on v_mfma_f32_32x32x16_bf16 by default (see
+//     seg_loop_x6), exact v_mfma_f32_32x32x2_f32 products with TDMPC_LG_X6=0 -- with the bias, a residual, ELU /
+//     policy-sampling / activation-backward epilogues fused.
 //     Operands are read straight from L2 into the MFMA lane layout (each lane loads 4 consecutive k of its row /
 //     column; the MFMA's two k slots per step are then k and k + 4, a permutation of the sum), four waves of a
 //     workgroup split K and add through LDS, and up to 12 GEMMs of one pass (the heads, or every weight gradient
@@ -20,10 +21,12 @@
 
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "../../include/tdmpc_hip.h"
 #include "../../include/tdmpc_learner.h"
@@ -40,6 +43,10 @@ constexpr int LG_MAXJ = 12;
 constexpr unsigned LG_OOB = 0x7ffffff0u;   // buffer range of the operand descriptors; offsets >= it read 0
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float4 u2f4(const u32x4 v) {
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
 
 struct KJob {
     tdmpc_lg_job j;
@@ -170,6 +177,125 @@ __device__ __forceinline__ void seg_loop(const tdmpc_lg_seg& S, int nb_mem, int 
     }
 }
 
+// ---- x6 products (tdmpc_kernels.hip's chain kernels): both fp32 operands split exactly into three
+// round-to-nearest bf16 parts x = hi + mid + lo, six v_mfma_f32_32x32x16_bf16 per product pair (hi.hi, hi.mid,
+// mid.hi, hi.lo, lo.hi, mid.mid; the dropped mid.lo, lo.mid, lo.lo are <= 2^-25 of |a b| each), fp32 accumulation:
+// fp32-accurate products at 6/16 of the f32 MFMA's cycles. (A non-finite operand gives NaN products, where an
+// fp32 GEMM gives +-inf: the learner's losses are NaN either way.)
+typedef __bf16 lg_bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void lg_split8(const float4& a0, const float4& a1, lg_bf16x8& bh, lg_bf16x8& bm,
+                                          lg_bf16x8& bl) {
+    const float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const __bf16 hi = (__bf16)x[e];
+        const float r1 = __fsub_rn(x[e], (float)hi);
+        const __bf16 mid = (__bf16)r1;
+        bh[e] = hi;
+        bm[e] = mid;
+        bl[e] = (__bf16)__fsub_rn(r1, (float)mid);
+    }
+}
+
+// One K segment of a wave's 32TM x 32TN tile on x6 products: lane (r, h) holds k0 + 8h .. k0 + 8h + 7 of its rows /
+// columns (the 16-deep k group of one v_mfma_f32_32x32x16_bf16); waves take every NW-th group of 16 k.
+template <int AM, int BM, bool AV, bool BV, int TM, int TN, int NW>
+__device__ __forceinline__ void seg_loop_x6(const tdmpc_lg_seg& S, int nb_mem, int k_lo, int k_hi, int m0, int n0,
+                                            int M, int N, floatx16 (&acc)[TM][TN], int wave, int r, int h) {
+    constexpr int KS = 16 * NW;
+    const int kb0 = k_lo + 16 * wave;
+    if (kb0 >= k_hi) return;
+    const int nit = (k_hi - kb0 + KS - 1) / KS;
+    const int lda = S.lda, ldb = S.ldb;
+    int mrow[TM], ncol[TN];
+    bool mok[TM], nok[TN], one[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + 32 * i + r;
+        mok[i] = m < M;
+        mrow[i] = mok[i] ? m : M - 1;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + 32 * j + r;
+        nok[j] = n < N;
+        one[j] = n == S.ones_col;
+        ncol[j] = min(n, nb_mem - 1);
+    }
+    const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)S.a, (short)0, (int)LG_OOB, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)S.b, (short)0, (int)LG_OOB, 0x00020000);
+    // 8 consecutive k of one row (MODE 0: element (x, k) at x * ld + k) or column (MODE 1: at k * ld + x)
+    auto load8 = [&](auto MODE_, auto VEC_, const __amdgpu_buffer_rsrc_t& rs, int ld, int x, bool xok, bool zero,
+                     int k, float4& v0, float4& v1) {
+        constexpr int MODE = decltype(MODE_)::value;
+        constexpr bool VEC = decltype(VEC_)::value;
+        if constexpr (MODE == 0 && VEC) {   // (K % 8 == 0: a group's 8 k are all in or all out)
+            const bool in = xok && !zero && k < k_hi;
+            v0 = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)(in ? (unsigned)(x * ld + k) * 4u : LG_OOB), 0, 0));
+            v1 = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)(in ? (unsigned)(x * ld + k + 4) * 4u : LG_OOB), 0, 0));
+        } else {
+            float e[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const unsigned idx = MODE == 0 ? (unsigned)(x * ld + k + q) : (unsigned)((k + q) * ld + x);
+                const unsigned off = (xok && !zero && k + q < k_hi) ? idx * 4u : LG_OOB;
+                e[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0));
+            }
+            v0 = make_float4(e[0], e[1], e[2], e[3]);
+            v1 = make_float4(e[4], e[5], e[6], e[7]);
+        }
+    };
+    using IA = std::integral_constant<int, AM>;
+    using IB = std::integral_constant<int, BM>;
+    using VA = std::integral_constant<bool, AV>;
+    using VB = std::integral_constant<bool, BV>;
+    auto load = [&](int kb, float4 (&a)[TM][2], float4 (&b)[TN][2]) {
+        const int k = kb + 8 * h;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) load8(IA{}, VA{}, rsa, lda, mrow[i], mok[i], false, k, a[i][0], a[i][1]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) load8(IB{}, VB{}, rsb, ldb, ncol[j], nok[j], one[j], k, b[j][0], b[j][1]);
+    };
+    constexpr int D = 2;
+    float4 ra[D][TM][2], rb[D][TN][2];
+    load(kb0, ra[0], rb[0]);
+    for (int it = 0; it < nit; it += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            load(kb0 + KS * (it + d + 1), ra[(d + 1) % D], rb[(d + 1) % D]);
+            __builtin_amdgcn_sched_barrier(0);
+            lg_bf16x8 ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) lg_split8(ra[d][i][0], ra[d][i][1], ah[i], am[i], al[i]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                float4 b0 = rb[d][j][0], b1 = rb[d][j][1];
+                if constexpr (AM == 1) {   // weight gradients: the bias column of ones, inside K only
+                    const int k = kb0 + KS * (it + d) + 8 * h;
+                    if (one[j]) {
+                        b0 = make_float4(k < k_hi, k + 1 < k_hi, k + 2 < k_hi, k + 3 < k_hi);
+                        b1 = make_float4(k + 4 < k_hi, k + 5 < k_hi, k + 6 < k_hi, k + 7 < k_hi);
+                    }
+                }
+                lg_split8(b0, b1, bh[j], bm[j], bl[j]);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
 // One output element of a job: the split-K partial as is, else bias / residual / epilogue (tdmpc_lg_job).
 __device__ __forceinline__ void lg_store(const tdmpc_lg_job& JJ, int splits, int split, int row, int col, float v) {
     if (splits > 1) {
@@ -208,7 +334,7 @@ __device__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15)
 
 // (amdgpu_waves_per_eu(2): left to itself the compiler gave the 64 x 64 form 224 VGPRs + 128 AGPRs, one wave per SIMD;
 // bounded, 210 VGPRs and no spills: two)
-template <int TM, int TN>
+template <int TM, int TN, bool X6 = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) lg_gemm_kernel(const KArgs P) {
     __shared__ float red[4][TM * TN * 16][64];
     int jb = 0;
@@ -242,15 +368,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
         const bool av = S.amode == 0 && S.lda % 4 == 0 && S.k % 8 == 0 && al16(S.a);
         const bool bv = S.bmode == 0 && S.ldb % 4 == 0 && S.k % 8 == 0 && al16(S.b);
         if (S.amode == 1) {
-            seg_loop<1, 1, false, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
+            { if constexpr (X6) seg_loop_x6<1, 1, false, false, TM, TN, 4>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); else seg_loop<1, 1, false, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); }
         } else if (S.bmode == 1) {
-            if (av) seg_loop<0, 1, true, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
-            else seg_loop<0, 1, false, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
+            if (av) { if constexpr (X6) seg_loop_x6<0, 1, true, false, TM, TN, 4>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); else seg_loop<0, 1, true, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); }
+            else { if constexpr (X6) seg_loop_x6<0, 1, false, false, TM, TN, 4>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); else seg_loop<0, 1, false, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); }
         } else {
-            if (av && bv) seg_loop<0, 0, true, true, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
-            else if (av) seg_loop<0, 0, true, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
-            else if (bv) seg_loop<0, 0, false, true, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
-            else seg_loop<0, 0, false, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h);
+            if (av && bv) { if constexpr (X6) seg_loop_x6<0, 0, true, true, TM, TN, 4>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); else seg_loop<0, 0, true, true, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); }
+            else if (av) { if constexpr (X6) seg_loop_x6<0, 0, true, false, TM, TN, 4>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); else seg_loop<0, 0, true, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); }
+            else if (bv) { if constexpr (X6) seg_loop_x6<0, 0, false, true, TM, TN, 4>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); else seg_loop<0, 0, false, true, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); }
+            else { if constexpr (X6) seg_loop_x6<0, 0, false, false, TM, TN, 4>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); else seg_loop<0, 0, false, false, TM, TN>(S, nbm, k_lo, k_hi, m0, n0, M, N, acc, wave, r, h); }
         }
     }
 
@@ -602,10 +728,16 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
     }
     P.njobs = njobs;
     if (blocks >= (1L << 31)) return bad("tdmpc_lg_gemm: grid");
-    if (tile == 1)
-        hipLaunchKernelGGL((lg_gemm_kernel<1, 1>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, P);
-    else
-        hipLaunchKernelGGL((lg_gemm_kernel<2, 2>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, P);
+    static int x6 = -1;   // x6 products by default; TDMPC_LG_X6=0: the exact f32 MFMA products
+    if (x6 < 0) {
+        const char* e = getenv("TDMPC_LG_X6");
+        x6 = e ? atoi(e) : 1;
+    }
+    const dim3 g((unsigned)blocks), b(256);
+    if (tile == 1 && x6) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, true>), g, b, 0, (hipStream_t)stream, P);
+    else if (tile == 1) hipLaunchKernelGGL((lg_gemm_kernel<1, 1>), g, b, 0, (hipStream_t)stream, P);
+    else if (x6) hipLaunchKernelGGL((lg_gemm_kernel<2, 2, true>), g, b, 0, (hipStream_t)stream, P);
+    else hipLaunchKernelGGL((lg_gemm_kernel<2, 2>), g, b, 0, (hipStream_t)stream, P);
     return launched("gemm");
 }
 
