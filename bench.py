@@ -386,21 +386,38 @@ def make_agent(cfg, B, rng, graph, seed, path="auto"):
     return agent
 
 
+def _sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
 def time_steps(step_fn, warmup, steps, dist):
+    """W untimed steps, then exactly `steps` timed ones bracketed by a barrier + device sync on both sides."""
     for i in range(warmup):
         step_fn(i)
-    torch.cuda.synchronize()
+    _sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync()
     t0 = time.perf_counter()
     for i in range(steps):
         step_fn(warmup + i)
-    torch.cuda.synchronize()
+    _sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync()
     return time.perf_counter() - t0
+
+
+def job_rate(elapsed, units_per_rank, dist, device):
+    """Whole-job throughput: the slowest rank's time (MAX over ranks) and every rank's units over it."""
+    world = 1
+    if dist is not None:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        world = dist.get_world_size()
+    return elapsed, world * units_per_rank / elapsed
 
 
 def main():
@@ -451,12 +468,8 @@ def main():
         return sharded.plan(global_obs, step, t0=(i % 100 == 0))
 
     elapsed = time_steps(one_step, args.warmup, args.steps, dist)
-    if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, value = job_rate(elapsed, B * args.steps, dist, dev)
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * B * args.steps / elapsed
 
     # ---- roofline of the dominant kernel class: HIP events around each launch, eager replay of the same
     # steps on the same stream (graph replays cannot carry the events)

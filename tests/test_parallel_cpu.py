@@ -111,3 +111,48 @@ def test_sharded_plan_gloo_world2():
         assert same, f"rank {rank} weights not synchronised"
         assert torch.equal(torch.from_numpy(a), a_ref), rank
         assert torch.equal(torch.from_numpy(m), m_ref), rank
+
+
+def _bench_worker(rank, world, port, out_q):
+    try:
+        import time as _t
+        import bench
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        calls = []
+
+        def step(i):   # rank 1 is the slow one
+            calls.append(i)
+            _t.sleep(0.002 * (1 + rank))
+
+        el = bench.time_steps(step, 2, 5, dist)
+        el_max, value = bench.job_rate(el, 3 * 5, dist, torch.device("cpu"))
+        out_q.put((rank, calls, el, el_max, value))
+        dist.destroy_process_group()
+    except Exception as e:
+        out_q.put((rank, repr(e), None, None, None))
+
+
+def test_bench_timing_contract_gloo_world2():
+    """bench.py's multi-rank contract (the driver's N > 1 runs): W untimed + exactly K timed steps per rank between
+    barriers, the slowest rank's time (MAX over ranks) on every rank, value = all ranks' units / that time."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=120)
+        res[r[0]] = r
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(world):
+        assert isinstance(res[r][1], list), res[r][1]
+        assert res[r][1] == list(range(7))            # 2 warm-up + 5 timed steps, in order
+    el_max = max(res[r][2] for r in range(world))
+    for r in range(world):
+        assert res[r][3] == pytest.approx(el_max)      # every rank reports the slowest rank's time
+        assert res[r][4] == pytest.approx(world * 3 * 5 / el_max)
+    assert res[1][2] >= 5 * 0.004                      # rank 1's own timed region holds its slower steps
