@@ -88,9 +88,9 @@ def test_gpu_update_matches_oracle():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("task", ["humanoid", "dog"])
+@pytest.mark.parametrize("task", ["humanoid", "dog", "cheetah"])
 def test_gpu_update_matches_oracle_full_size(task):
-    """The bench's learner shape (batch 512, horizon 5, mlp 512; humanoid L100 A21 / dog L100 A38 obs 223):
+    """The bench's learner shape (batch 512, horizon 5, mlp 512; humanoid L100 A21 / dog L100 A38 obs 223 / cheetah L50 A6):
     two updates (EMA on the second) against the oracle, same batch and TruncatedNormal draws, same tolerances."""
     from tdmpc_amd.config import make_cfg
     from tdmpc_amd.tdmpc import TDMPC
