@@ -52,7 +52,7 @@ for w, base in (("wg0", 0), ("wg255", 1024)):
         print(f"{lab:18s} work {wk:7.2f} us  wait {wt:7.2f} us")
     print(f"total work {tot_work:.1f} us, wait {tot_wait:.1f} us")
 mk, ck = s[900:906], s[920:926]
-print("local hand-offs:", s[950], " step i1 t0 L2 (us): mm", (mk[1]-mk[0])/100, "put+barrier", (mk[2]-mk[1])/100,
+print("local hand-offs per group:", list(s[950:958]), " step i1 t0 L2 (us): mm", (mk[1]-mk[0])/100, "put+barrier", (mk[2]-mk[1])/100,
       "last layer", (mk[3]-mk[2])/100, "| cycles", ck[1]-ck[0], ck[2]-ck[1], ck[3]-ck[2])
 mk = s[900:920]
 print("CEM i1 (us): sort+merge", (mk[11]-mk[10])/100, "elite gather", (mk[12]-mk[11])/100, "refit", (mk[13]-mk[12])/100,
