@@ -9,7 +9,7 @@ from tdmpc_amd.told import synthetic_state_dict
 name = sys.argv[1] if len(sys.argv) > 1 else "humanoid-run"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 cfg = bench_cfg(name)
-agent = TDMPC(cfg, max_batch=B, rng="fused")
+agent = TDMPC(cfg, max_batch=B, rng="fused", path=os.environ.get("QT_PATH", "auto"))
 agent.model.load_state_dict(synthetic_state_dict(cfg, 0)); agent.std = 0.05
 obs = np.random.RandomState(0).standard_normal((B,) + tuple(cfg.obs_shape)).astype(np.float32)
 if cfg.modality == "pixels":
