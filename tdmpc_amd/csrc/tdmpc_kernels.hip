@@ -3988,8 +3988,10 @@ int chain_rb(const Ctx& c, int rows, int nprob) {
 // 64-row x6 blocks (chain64_kernel) for TOLD.next / helper.q launches wide enough to give every CU a workgroup:
 // TDMPC_CHAIN64=1 on the auto / chain paths, every such launch on TDMPC_PATH_CHAIN64 (parity tests). Off by default:
 // measured on MI355X (humanoid-run B = 32, rocprofv3): step 137.1 vs 136.9 us, Q 181.8 vs 180.2 us for the 32-row x6
-// kernel -- halving the weight bytes per MFMA changed nothing, i.e. the L2 weight stream is not what bounds these
-// kernels.
+// kernel. In the M x M loop alone the 64-row form is faster (0.66-0.70 vs 0.55-0.60 MFMA busy,
+// tools/mb/x6_stream.hip: the CUs' vector-memory path carries the weight stream), but its 128 KB activation block
+// allows one workgroup per CU, and the staging / layer-1 / layer-3 / epilogue phases it can no longer overlap with a
+// co-resident workgroup eat the gain.
 void maybe_rb64(const Ctx& c, ChainArgs& a, int mode, int nprob) {
     static int en = -1;
     if (en < 0) {
