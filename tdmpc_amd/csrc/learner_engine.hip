@@ -698,6 +698,8 @@ extern "C" {
 
 int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* stream) {
     if (!jobs) return TDMPC_E_NULL;
+    const bool x6 = !(tile & TDMPC_LG_TILE_EXACT);   // x6 products unless the caller asks for the exact f32 MFMA
+    tile &= ~TDMPC_LG_TILE_EXACT;
     if (njobs <= 0 || njobs > LG_MAXJ || (tile != 1 && tile != 2)) return bad("tdmpc_lg_gemm: njobs / tile");
     KArgs P;
     memset(&P, 0, sizeof P);
@@ -728,11 +730,6 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
     }
     P.njobs = njobs;
     if (blocks >= (1L << 31)) return bad("tdmpc_lg_gemm: grid");
-    static int x6 = -1;   // x6 products by default; TDMPC_LG_X6=0: the exact f32 MFMA products
-    if (x6 < 0) {
-        const char* e = getenv("TDMPC_LG_X6");
-        x6 = e ? atoi(e) : 1;
-    }
     const dim3 g((unsigned)blocks), b(256);
     if (tile == 1 && x6) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, true>), g, b, 0, (hipStream_t)stream, P);
     else if (tile == 1) hipLaunchKernelGGL((lg_gemm_kernel<1, 1>), g, b, 0, (hipStream_t)stream, P);

@@ -23,6 +23,7 @@ LayerNorm affine and scalar output layers as per-workgroup column sums; lg_final
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -32,6 +33,7 @@ ELU, TANH = 2, 1
 EPI_NONE, EPI_ELU, EPI_PI, EPI_ELU_BWD, EPI_PI_BWD = 0, 1, 2, 3, 4
 NBLK = 2048         # capacity of the norm partials (one per lg_finalize workgroup of 2048 gradients)
 ROWS_NWG = 256      # lg_rows_bwd workgroups (column-sum partials per head)
+TILE_EXACT = 0x100  # TDMPC_LG_TILE_EXACT (include/tdmpc_learner.h)
 
 
 def supported(cfg) -> bool:
@@ -99,6 +101,9 @@ class Engine:
         # the learner's HIP graph as parallel branches): the TD target beside the encoder + latent rollout, the
         # heads' weight gradients beside the rollout's backward. Both pairs touch disjoint buffers.
         self.side = torch.cuda.Stream(self.dev)
+        # lg_gemm's products: fp32-accurate x6 (default) or the exact f32 MFMA (TDMPC_LG_X6=0, or set before the
+        # first update: the captured graph keeps the choice)
+        self.x6 = os.environ.get("TDMPC_LG_X6", "1") != "0"
 
     def _alias(self, model, flat):
         """Make every parameter of `model` a view into `flat` (values kept)."""
@@ -170,6 +175,7 @@ class Engine:
             # backward's dX) runs 15-25 % faster on 32 x 32 tiles (tools/lg_gemm_bench.py)
             tbw = any(sg[6] == 1 for j in jobs for sg in j["segs"])
             tile = 2 if tiles64 >= 240 and not tbw else 1
+        tile |= 0 if self.x6 else TILE_EXACT
         _lib.check(self.lib.tdmpc_lg_gemm(arr, len(jobs), tile, self._stream()), "tdmpc_lg_gemm")
 
     def rows(self, heads, n, bwd=False, **kw):
