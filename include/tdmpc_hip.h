@@ -117,6 +117,18 @@ int tdmpc_sizes_for(const tdmpc_dims* dims, tdmpc_sizes* out);
  * laid out in exactly that (reference draw) order. */
 size_t tdmpc_noise_floats(const tdmpc_dims* dims, int32_t horizon, int32_t iterations);
 
+/* Fill the noise streams of `batch` envs (env e at noise + e*env_stride floats, layout above) with exactly the
+ * values the reference's per-env draw sequence takes from torch's device Philox generator (tdmpc.py:117, 131, 91,
+ * 158 -- each a separate normal_/randn launch there), in ONE launch: element li of a draw of n values is
+ * component (li / S) % 4 of the (li / S / 4 + 1)-th normal4 of Philox subsequence li % S at the draw's counter
+ * offset, S = 256 * min(grid_cap, ceil(n / 256)) (ATen's distribution_elementwise_grid_stride_kernel, block
+ * 256, unroll 4). Draw k of env e starts at `offset` + the counter advance of every earlier draw;
+ * `*offset_advance` receives the total the caller adds to the generator. grid_cap = CUs * (max threads per
+ * CU / 256), as ATen's calc_execution_policy. eval_mode skips the final action draw. */
+int tdmpc_reference_normals(const tdmpc_dims* dims, float* noise, int32_t batch, int64_t env_stride,
+                            int32_t horizon, int32_t iterations, int32_t eval_mode, uint64_t seed, uint64_t offset,
+                            int32_t grid_cap, uint64_t* offset_advance, void* stream);
+
 /* Number of parameter tensors tdmpc_pack_weights expects: the reference state_dict order
  * (TOLD, tdmpc.py:9-23): _encoder.*, _dynamics.{0,2,4}.{weight,bias}, _reward.{0,2,4}.*, _pi.{0,2,4}.*,
  * _Q1.{0,1,3,4,6}.*, _Q2.{0,1,3,4,6}.*  (state encoder: 4 tensors, 6 with enc_norm -- 0.w 0.b 1.w 1.b 3.w

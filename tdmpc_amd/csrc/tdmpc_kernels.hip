@@ -21,6 +21,7 @@
 //                  on the last iteration the elite choice (np.random.choice cdf) and the output action.
 //   encode_kernel / conv_relu_kernel   TOLD.h (state MLP or pixel conv stack) + CEM mean/std init.
 #include <hip/hip_runtime.h>
+#include <hiprand/hiprand_kernel.h>
 
 #include <math.h>
 #include <stdint.h>
@@ -4572,6 +4573,123 @@ size_t tdmpc_noise_floats(const tdmpc_dims* d, int32_t H, int32_t I) {
     if (!d) return 0;
     const size_t A = d->action_dim, N = d->num_samples, P = d->num_pi, T = N + P;
     return (size_t)H * P * A + (size_t)I * ((size_t)H * N * A + T * A) + A;
+}
+
+// ---------------------------------------------------------------- reference-order draws in one launch
+// The reference takes its planning noise from torch's global device generator, one normal_/randn launch per
+// draw (tdmpc.py:117 per horizon step, 131 and 91 per iteration, 158): at humanoid sizes 18 launches per env.
+// Each of those is ATen's grid-stride Philox kernel, so the value of element li of a draw is a pure function of
+// (seed, draw's counter offset, li, the draw's grid): this kernel recomputes every element of every draw of
+// every env in one pass, one thread per stream float.
+struct RefNormalsArgs {
+    float* noise;
+    int64_t env_stride, per_env;       // floats between env streams; floats written per env
+    int64_t n_pi, n_cem, n_term, n_act; // elements per draw of each kind
+    int64_t s_pi, s_cem, s_term, s_act; // ATen grid stride (threads) of each draw kind
+    uint64_t c_pi, c_cem, c_term, c_act; // counter advance of each draw kind
+    uint64_t seed, offset, env_adv;
+    int32_t H, I, has_pi, batch;
+};
+
+// rocrand's Box-Muller (normal_distribution4 on one Philox output) with the instruction sequence of the
+// normal_ kernel in the installed torch build (its code object, disassembled): logf as v_log_f32 plus the
+// two-product ln2 scaling finished by a separate ADD, which a newer compiler fuses into one FMA (a 1-2 ulp
+// difference in ~15% of values); sqrtf correctly rounded; sin/cos native on v / 2pi. Fused multiply-adds are
+// written out, everything else is kept unfused.
+DEVI float torch_bm_log(float u) {
+#pragma clang fp contract(off)
+    const bool tiny = u < 0x1p-126f;
+    const float L = __builtin_amdgcn_logf(tiny ? ldexpf(u, 32) : u);   // log2
+    const float hi = L * 0x1.62e42ep-1f;                                  // ln2 (hi)
+    float e = fmaf(L, 0x1.62e42ep-1f, -hi);
+    e = fmaf(0x1.efa39ep-25f, L, e);                                      // ln2 (lo)
+    const float r = fabsf(L) < INFINITY ? hi + e : L;
+    return r - (tiny ? 0x1.62e430p+4f : 0.f);                             // 32 ln2
+}
+
+DEVI float torch_normal_component(uint4 r, int c) {
+#pragma clang fp contract(off)
+    const unsigned x = c < 2 ? r.x : r.z, y = c < 2 ? r.y : r.w;
+    const float u = fmaf((float)x, 0x1p-32f, 0x1p-32f);                   // ROCRAND_2POW32_INV
+    const float v = fmaf((float)y, 0x1.921fb6p-30f, 0x1.921fb6p-30f);     // ROCRAND_2POW32_INV_2PI
+    const float s = sqrtf(-2.0f * torch_bm_log(u));
+    const float t = v * 0x1.45f306p-3f;
+    return ((c & 1) ? __builtin_amdgcn_cosf(t) : __builtin_amdgcn_sinf(t)) * s;
+}
+
+__global__ void __launch_bounds__(256) ref_normals_kernel(RefNormalsArgs a) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= (int64_t)a.batch * a.per_env) return;
+    const int64_t e = g / a.per_env;
+    int64_t p = g - e * a.per_env, li, S;
+    uint64_t off = a.offset + e * a.env_adv;
+    const int64_t pi_tot = a.has_pi ? a.H * a.n_pi : 0;
+    if (p < pi_tot) {   // H x normal_([P, A])
+        const int64_t d = p / a.n_pi;
+        li = p - d * a.n_pi;
+        S = a.s_pi;
+        off += d * a.c_pi;
+    } else {
+        p -= pi_tot;
+        off += a.has_pi ? a.H * a.c_pi : 0;
+        const int64_t it_len = a.n_cem + a.n_term;
+        const int64_t it = p / it_len;
+        const int64_t r = p - it * it_len;
+        off += it * (a.c_cem + a.c_term);
+        if (it >= a.I) {               // randn(A) after the last iteration
+            li = p - (int64_t)a.I * it_len;
+            S = a.s_act;
+        } else if (r < a.n_cem) {      // randn(H, N, A)
+            li = r;
+            S = a.s_cem;
+        } else {                       // normal_([T, A]) at the horizon
+            li = r - a.n_cem;
+            S = a.s_term;
+            off += a.c_cem;
+        }
+    }
+    const int64_t j = li / S;
+    hiprandStatePhilox4_32_10_t st;
+    hiprand_init(a.seed, (unsigned long long)(li - j * S), off, &st);
+    uint4 r = hiprand4(&st);
+    for (int64_t k = 0; k < j / 4; ++k) r = hiprand4(&st);
+    const float x = torch_normal_component(r, (int)(j & 3));
+    a.noise[e * a.env_stride + (g - e * a.per_env)] = x * 1.0f + 0.0f;   // transformation::normal(x, 0, 1)
+}
+
+int tdmpc_reference_normals(const tdmpc_dims* d, float* noise, int32_t B, int64_t env_stride, int32_t H,
+                            int32_t I, int32_t eval_mode, uint64_t seed, uint64_t offset, int32_t grid_cap,
+                            uint64_t* offset_advance, void* stream) {
+    if (!d || !noise || !offset_advance) return TDMPC_E_NULL;
+    if (!check_dims(d)) return TDMPC_E_DIMS;
+    const int64_t A = d->action_dim, N = d->num_samples, P = d->num_pi, T = N + P;
+    const int64_t per_env = (int64_t)tdmpc_noise_floats(d, H, I) - (eval_mode ? A : 0);
+    if (B < 1 || H < 1 || I < 1 || grid_cap < 1 || env_stride < (int64_t)tdmpc_noise_floats(d, H, I)) {
+        snprintf(g_err, sizeof g_err, "reference_normals: batch %d horizon %d iterations %d grid_cap %d stride %lld",
+                 B, H, I, grid_cap, (long long)env_stride);
+        return TDMPC_E_DIMS;
+    }
+    RefNormalsArgs a{};
+    // ATen calc_execution_policy: block 256, grid min(cap, ceil(n/256)), advance 4 per unrolled pass
+    auto stride = [&](int64_t n) { return 256 * std::min<int64_t>(grid_cap, (n + 255) / 256); };
+    auto adv = [&](int64_t n) { return (uint64_t)(((n - 1) / (stride(n) * 4) + 1) * 4); };
+    a.noise = noise;
+    a.env_stride = env_stride;
+    a.per_env = per_env;
+    a.n_pi = P * A, a.n_cem = H * N * A, a.n_term = T * A, a.n_act = A;
+    a.has_pi = P > 0;
+    a.s_pi = a.has_pi ? stride(a.n_pi) : 1, a.s_cem = stride(a.n_cem), a.s_term = stride(a.n_term);
+    a.s_act = stride(A);
+    a.c_pi = a.has_pi ? adv(a.n_pi) : 0, a.c_cem = adv(a.n_cem), a.c_term = adv(a.n_term);
+    a.c_act = eval_mode ? 0 : adv(A);
+    a.env_adv = H * a.c_pi + I * (a.c_cem + a.c_term) + a.c_act;
+    a.seed = seed, a.offset = offset;
+    a.H = H, a.I = I, a.batch = B;
+    *offset_advance = (uint64_t)B * a.env_adv;
+    const int64_t n = (int64_t)B * per_env;
+    hipLaunchKernelGGL(ref_normals_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
+    HIPCHK(hipGetLastError());
+    return 0;
 }
 
 int tdmpc_num_param_tensors(const tdmpc_dims* d) {

@@ -22,6 +22,7 @@ Extensions beyond the reference API:
 from __future__ import annotations
 
 import ctypes as C
+import os
 from copy import deepcopy
 
 import numpy as np
@@ -124,6 +125,12 @@ class HipPlanner:
         self._pin_u = torch.zeros(max_batch, dtype=torch.float64, pin_memory=pin)
         self._pin_met = torch.zeros(max_batch, 2, dtype=torch.float32, pin_memory=pin)
         self._h2d_done = torch.cuda.Event() if pin else None
+        # reference-order draws: "device" = one tdmpc_reference_normals launch per call, "torch" = the
+        # reference's own normal_ launches (18 per env at humanoid sizes); equal bitwise
+        self.ref_draws = os.environ.get("TDMPC_REF_DRAWS", "device")
+        if self.ref_draws not in ("device", "torch"):
+            raise ValueError(f"TDMPC_REF_DRAWS must be device or torch, not {self.ref_draws!r}")
+        self._grid_cap = None
 
     # ------------------------------------------------------------------ weights
     def pack(self, model: TOLD):
@@ -166,6 +173,25 @@ class HipPlanner:
             buf[o + H * N * A:o + H * N * A + T * A].view(T, A).normal_()
         if not eval_mode:
             buf[lay["act_off"]:lay["act_off"] + A].normal_()
+
+    def draw_reference_device(self, B: int, H: int, I: int, eval_mode: bool):
+        """The same values as B successive `draw_reference_torch` calls (env 0 first), recomputed by one kernel
+        (tdmpc_reference_normals) from the global generator's seed and Philox offset, which then advances
+        exactly as the B x 18 normal_ launches would have advanced it. Launched on the current stream, outside
+        any graph capture (the offset is read on the host)."""
+        gen = torch.cuda.default_generators[self.device.index or 0]
+        if self._grid_cap is None:
+            prop = torch.cuda.get_device_properties(self.device)
+            per_cu = getattr(prop, "max_threads_per_multi_processor", 2048) // 256
+            self._grid_cap = prop.multi_processor_count * per_cu   # ATen calc_execution_policy's grid cap
+        buf = self.noise_view(H, I, B)
+        off = gen.get_offset()
+        adv = C.c_uint64(0)
+        rc = self.L.tdmpc_reference_normals(C.byref(self.dims), C.c_void_p(buf.data_ptr()), B, buf.stride(0), H, I,
+                                            int(eval_mode), gen.initial_seed(), off, self._grid_cap, C.byref(adv),
+                                            C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+        _lib.check(rc, "tdmpc_reference_normals")
+        gen.set_offset(off + adv.value)
 
     def load_noise(self, e: int, H: int, I: int, eps_pi, eps_cem, eps_term, eps_act):
         """Write an explicit noise stream for env e (parity tests feed the oracle's / the reference's draws)."""
@@ -477,8 +503,12 @@ class TDMPC:
         if pl._h2d_done is not None:
             pl._h2d_done.record()
 
+        one_launch = noise is None and self.rng == "reference" and pl.ref_draws == "device"
+        if one_launch:
+            pl.draw_reference_device(B, H, I, eval_mode)
+
         def device_work():
-            if noise is None:
+            if noise is None and not one_launch:
                 if self.rng == "reference":
                     for e in range(B):
                         pl.draw_reference_torch(e, H, I, eval_mode)
@@ -488,7 +518,7 @@ class TDMPC:
             pl.launch(prm, obs_u8, trace)
 
         if self.graph and noise is None and trace is None:
-            key = (H, I, B, bool(eval_mode), self.rng)   # self.std and the warm flags live on the device
+            key = (H, I, B, bool(eval_mode), self.rng, one_launch)   # self.std and the warm flags live on the device
             g = pl._graphs.get(key)
             if g is None:
                 # No eager warm-up: the library has no lazy initialisation left after pack(), and an eager

@@ -162,6 +162,62 @@ def test_reference_rng_order_on_device():
     assert torch.equal(buf[lay["act_off"]:lay["act_off"] + A], nb.eps_act)
 
 
+@pytest.mark.parametrize("task,ov,B,ev", [
+    ("cartpole", dict(num_samples=64, num_elites=32, iterations=3), 1, False),
+    ("humanoid", dict(num_samples=512, num_elites=64, iterations=6, horizon=5), 3, False),
+    ("humanoid", dict(num_samples=512, num_elites=64, iterations=6, horizon=5), 2, True),
+    ("dog", dict(num_samples=77, num_elites=13, iterations=3, horizon=4), 3, False),
+    # no pi trajectories, and a randn(H,N,A) of 622,592 > 2048 x 256 values: ATen's grid-stride loop takes
+    # two passes, elements past the first pass come from the 2nd normal4 and its components .y/.z/.w
+    ("dog", dict(num_samples=2048, num_elites=64, mixture_coef=0.0, iterations=2, horizon=8), 2, False),
+])
+def test_reference_normals_one_launch(task, ov, B, ev):
+    """tdmpc_reference_normals (one kernel for all of a call's draws, every env) writes bitwise the values of the
+    reference's separate normal_ launches, and leaves torch's generator where those launches leave it."""
+    cfg = make_cfg(task, **ov)
+    pl = TDMPC(cfg, max_batch=B).planner
+    H, I = cfg.horizon, cfg.iterations
+    gen = torch.cuda.default_generators[0]
+    torch.manual_seed(77)
+    torch.randn(5, device="cuda")   # a nonzero starting offset
+    for e in range(B):
+        pl.draw_reference_torch(e, H, I, ev)
+    want = pl.noise_view(H, I, B).clone()
+    off_want = gen.get_offset()
+    next_want = torch.randn(1000, device="cuda")
+    pl.noise_flat.fill_(7.0)
+    torch.manual_seed(77)
+    torch.randn(5, device="cuda")
+    pl.draw_reference_device(B, H, I, ev)
+    got = pl.noise_view(H, I, B)
+    assert gen.get_offset() == off_want
+    assert torch.equal(torch.randn(1000, device="cuda"), next_want)
+    if ev:   # the final action draw is not taken in eval mode: the slot is left alone
+        A = pl.A
+        assert (got[:, -A:] == 7.0).all()
+        got, want = got[:, :-A], want[:, :-A]
+    bad = (got != want).nonzero()
+    assert bad.numel() == 0, f"{bad.shape[0]} of {got.numel()} differ, first at {bad[0].tolist()}"
+
+
+def test_plan_reference_draws_device_equals_torch(monkeypatch):
+    """plan() with the one-launch draws (default, outside the captured graph) equals plan() with the reference's
+    own normal_ launches captured in the graph, bitwise, over warm-started calls."""
+    cfg = make_cfg("humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5)
+    obs = np.random.RandomState(4).standard_normal((3, cfg.obs_shape[0])).astype(np.float32)
+    outs = []
+    for mode in ("device", "torch"):
+        monkeypatch.setenv("TDMPC_REF_DRAWS", mode)
+        agent = _agent(cfg, 2)
+        assert agent.planner.ref_draws == mode
+        torch.manual_seed(11)
+        np.random.seed(11)
+        outs.append([agent.plan(obs[k], step=10**6, t0=(k == 0))[0].clone() for k in range(3)])
+        outs[-1].append(torch.randn(4, device="cuda"))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("path", PATHS)
 def test_plan_fullsize_vs_oracle(path):
     """Full humanoid-run plan (N=512, H=5, 6 iterations, T=768): GPU vs oracle on identical noise, warm
