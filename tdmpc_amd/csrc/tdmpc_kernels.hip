@@ -4581,14 +4581,19 @@ size_t tdmpc_noise_floats(const tdmpc_dims* d, int32_t H, int32_t I) {
 // Each of those is ATen's grid-stride Philox kernel, so the value of element li of a draw is a pure function of
 // (seed, draw's counter offset, li, the draw's grid): this kernel recomputes every element of every draw of
 // every env in one pass, one thread per stream float.
+// Per call a table of the env's draws (the same for every env): draw k covers blocks [blk[k], blk[k+1]) of the
+// env's grid row, so a block belongs to one draw and finds it with a scalar search.
+constexpr int REF_MAX_DRAWS = 96;
 struct RefNormalsArgs {
     float* noise;
-    int64_t env_stride, per_env;       // floats between env streams; floats written per env
-    int64_t n_pi, n_cem, n_term, n_act; // elements per draw of each kind
-    int64_t s_pi, s_cem, s_term, s_act; // ATen grid stride (threads) of each draw kind
-    uint64_t c_pi, c_cem, c_term, c_act; // counter advance of each draw kind
-    uint64_t seed, offset, env_adv;
-    int32_t H, I, has_pi, batch;
+    int64_t env_stride;
+    uint64_t seed, offset, env_adv;   // generator state at the call; counter advance per env
+    int32_t ndraw;
+    int32_t blk[REF_MAX_DRAWS + 1];   // first block of each draw
+    int32_t n[REF_MAX_DRAWS];         // elements
+    int32_t out[REF_MAX_DRAWS];       // float offset in the env stream
+    int32_t S[REF_MAX_DRAWS];         // ATen grid stride (threads)
+    uint32_t coff[REF_MAX_DRAWS];     // counter offset from the env's first draw
 };
 
 // rocrand's Box-Muller (normal_distribution4 on one Philox output) with the instruction sequence of the
@@ -4618,43 +4623,19 @@ DEVI float torch_normal_component(uint4 r, int c) {
 }
 
 __global__ void __launch_bounds__(256) ref_normals_kernel(RefNormalsArgs a) {
-    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (g >= (int64_t)a.batch * a.per_env) return;
-    const int64_t e = g / a.per_env;
-    int64_t p = g - e * a.per_env, li, S;
-    uint64_t off = a.offset + e * a.env_adv;
-    const int64_t pi_tot = a.has_pi ? a.H * a.n_pi : 0;
-    if (p < pi_tot) {   // H x normal_([P, A])
-        const int64_t d = p / a.n_pi;
-        li = p - d * a.n_pi;
-        S = a.s_pi;
-        off += d * a.c_pi;
-    } else {
-        p -= pi_tot;
-        off += a.has_pi ? a.H * a.c_pi : 0;
-        const int64_t it_len = a.n_cem + a.n_term;
-        const int64_t it = p / it_len;
-        const int64_t r = p - it * it_len;
-        off += it * (a.c_cem + a.c_term);
-        if (it >= a.I) {               // randn(A) after the last iteration
-            li = p - (int64_t)a.I * it_len;
-            S = a.s_act;
-        } else if (r < a.n_cem) {      // randn(H, N, A)
-            li = r;
-            S = a.s_cem;
-        } else {                       // normal_([T, A]) at the horizon
-            li = r - a.n_cem;
-            S = a.s_term;
-            off += a.c_cem;
-        }
-    }
-    const int64_t j = li / S;
+    const int e = blockIdx.y, bx = blockIdx.x;
+    int k = 0;
+    while (k + 1 < a.ndraw && a.blk[k + 1] <= bx) ++k;
+    const int li = (bx - a.blk[k]) * 256 + (int)threadIdx.x;
+    if (li >= a.n[k]) return;
+    const int S = a.S[k];
+    const int j = li < S ? 0 : li / S;   // ATen grid-stride pass (0 unless the draw exceeds the grid cap)
     hiprandStatePhilox4_32_10_t st;
-    hiprand_init(a.seed, (unsigned long long)(li - j * S), off, &st);
+    hiprand_init(a.seed, (unsigned long long)(li - j * S), a.offset + (uint64_t)e * a.env_adv + a.coff[k], &st);
     uint4 r = hiprand4(&st);
-    for (int64_t k = 0; k < j / 4; ++k) r = hiprand4(&st);
-    const float x = torch_normal_component(r, (int)(j & 3));
-    a.noise[e * a.env_stride + (g - e * a.per_env)] = x * 1.0f + 0.0f;   // transformation::normal(x, 0, 1)
+    for (int p = 0; p < j / 4; ++p) r = hiprand4(&st);
+    const float x = torch_normal_component(r, j & 3);
+    a.noise[e * a.env_stride + a.out[k] + li] = x * 1.0f + 0.0f;   // transformation::normal(x, 0, 1)
 }
 
 int tdmpc_reference_normals(const tdmpc_dims* d, float* noise, int32_t B, int64_t env_stride, int32_t H,
@@ -4673,21 +4654,33 @@ int tdmpc_reference_normals(const tdmpc_dims* d, float* noise, int32_t B, int64_
     // ATen calc_execution_policy: block 256, grid min(cap, ceil(n/256)), advance 4 per unrolled pass
     auto stride = [&](int64_t n) { return 256 * std::min<int64_t>(grid_cap, (n + 255) / 256); };
     auto adv = [&](int64_t n) { return (uint64_t)(((n - 1) / (stride(n) * 4) + 1) * 4); };
+    int64_t out = 0, blk = 0;
+    uint64_t coff = 0;
+    auto draw = [&](int64_t n) {
+        const int k = a.ndraw++;
+        a.blk[k] = (int32_t)blk, a.n[k] = (int32_t)n, a.out[k] = (int32_t)out, a.S[k] = (int32_t)stride(n);
+        a.coff[k] = (uint32_t)coff;
+        blk += (n + 255) / 256, out += n, coff += adv(n);
+    };
+    const int64_t D = (P > 0 ? H : 0) + 2 * I + (eval_mode ? 0 : 1);
+    if (D > REF_MAX_DRAWS || per_env >= (1ll << 31)) {
+        snprintf(g_err, sizeof g_err, "reference_normals: %lld draws (max %d), %lld floats per env", (long long)D,
+                 REF_MAX_DRAWS, (long long)per_env);
+        return TDMPC_E_DIMS;
+    }
+    if (P > 0)
+        for (int t = 0; t < H; ++t) draw(P * A);   // tdmpc.py:117 (helper.py:88), one per horizon step
+    for (int i = 0; i < I; ++i) {
+        draw((int64_t)H * N * A);                   // tdmpc.py:131
+        draw(T * A);                                // tdmpc.py:91 (pi at the horizon)
+    }
+    if (!eval_mode) draw(A);                        // tdmpc.py:158
+    a.blk[a.ndraw] = (int32_t)blk;
     a.noise = noise;
     a.env_stride = env_stride;
-    a.per_env = per_env;
-    a.n_pi = P * A, a.n_cem = H * N * A, a.n_term = T * A, a.n_act = A;
-    a.has_pi = P > 0;
-    a.s_pi = a.has_pi ? stride(a.n_pi) : 1, a.s_cem = stride(a.n_cem), a.s_term = stride(a.n_term);
-    a.s_act = stride(A);
-    a.c_pi = a.has_pi ? adv(a.n_pi) : 0, a.c_cem = adv(a.n_cem), a.c_term = adv(a.n_term);
-    a.c_act = eval_mode ? 0 : adv(A);
-    a.env_adv = H * a.c_pi + I * (a.c_cem + a.c_term) + a.c_act;
-    a.seed = seed, a.offset = offset;
-    a.H = H, a.I = I, a.batch = B;
-    *offset_advance = (uint64_t)B * a.env_adv;
-    const int64_t n = (int64_t)B * per_env;
-    hipLaunchKernelGGL(ref_normals_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
+    a.seed = seed, a.offset = offset, a.env_adv = coff;
+    *offset_advance = (uint64_t)B * coff;
+    hipLaunchKernelGGL(ref_normals_kernel, dim3((unsigned)blk, (unsigned)B), dim3(256), 0, (hipStream_t)stream, a);
     HIPCHK(hipGetLastError());
     return 0;
 }
