@@ -590,7 +590,8 @@ def main():
         el1 = time_steps(lambda i: a1.plan(o1, step=step, t0=(i % 100 == 0)), 3, ks, None)
         single = {"value": round(ks / el1, 3), "unit": "plan-steps/s", "ms_per_step": round(el1 / ks * 1e3, 4),
                   "note": "agent.plan(obs, step, t0) exactly as src/train.py:95 calls it: TDMPC(cfg) defaults "
-                          "(reference-order RNG on torch's / numpy's global generators, no graph), numpy obs "
+                          "(reference-order RNG on torch's / numpy's global generators -- the torch draws as one "
+                          "tdmpc_reference_normals launch, bitwise torch's -- HIP graph replay), numpy obs "
                           "copied to the device, metrics synced to the host; same GPU, same run"}
         # the same env through the batch API with device RNG and graph replay (no host sync)
         ab1 = make_agent(cfg, 1, args.rng, graph, 7)
