@@ -27,3 +27,20 @@ for i in range(K):
 torch.cuda.synchronize()
 pr.disable()
 pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+
+# GPU time of one call's device work alone: the cached graph replayed back to back (draws included when they are
+# captured, i.e. TDMPC_REF_DRAWS=torch) vs the wall time of a whole plan() call
+pl = agent.planner
+g = next(iter(pl._graphs.values()))
+torch.cuda.synchronize()
+t = time.perf_counter()
+for i in range(K):
+    g.replay()
+    torch.cuda.current_stream().synchronize()
+print(f"graph replay + sync alone: {(time.perf_counter() - t) / K * 1e3:.3f} ms/call")
+t = time.perf_counter()
+for i in range(K):
+    pl.draw_reference_device(1, 5, 6, False)
+    g.replay()
+    torch.cuda.current_stream().synchronize()
+print(f"one-launch draws + graph replay + sync: {(time.perf_counter() - t) / K * 1e3:.3f} ms/call")
