@@ -124,10 +124,12 @@ size_t tdmpc_noise_floats(const tdmpc_dims* dims, int32_t horizon, int32_t itera
  * offset, S = 256 * min(grid_cap, ceil(n / 256)) (ATen's distribution_elementwise_grid_stride_kernel, block
  * 256, unroll 4). Draw k of env e starts at `offset` + the counter advance of every earlier draw;
  * `*offset_advance` receives the total the caller adds to the generator. grid_cap = CUs * (max threads per
- * CU / 256), as ATen's calc_execution_policy. eval_mode skips the final action draw. */
+ * CU / 256), as ATen's calc_execution_policy. eval_mode skips the final action draw. gen_state: NULL, or a device
+ * pointer to {seed, offset} read by the kernel when it runs instead of `seed` / `offset` -- so one captured graph
+ * serves every call: the host stages the generator's state into it before each replay. */
 int tdmpc_reference_normals(const tdmpc_dims* dims, float* noise, int32_t batch, int64_t env_stride,
                             int32_t horizon, int32_t iterations, int32_t eval_mode, uint64_t seed, uint64_t offset,
-                            int32_t grid_cap, uint64_t* offset_advance, void* stream);
+                            const uint64_t* gen_state, int32_t grid_cap, uint64_t* offset_advance, void* stream);
 
 /* Number of parameter tensors tdmpc_pack_weights expects: the reference state_dict order
  * (TOLD, tdmpc.py:9-23): _encoder.*, _dynamics.{0,2,4}.{weight,bias}, _reward.{0,2,4}.*, _pi.{0,2,4}.*,

@@ -124,7 +124,7 @@ def lib():
     L.tdmpc_noise_floats.restype = sz
     L.tdmpc_num_param_tensors.argtypes = [C.POINTER(Dims)]
     L.tdmpc_reference_normals.argtypes = [C.POINTER(Dims), vp, i32, C.c_int64, i32, i32, i32, C.c_uint64,
-                                          C.c_uint64, i32, C.POINTER(C.c_uint64), vp]
+                                          C.c_uint64, vp, i32, C.POINTER(C.c_uint64), vp]
     L.tdmpc_pack_weights.argtypes = [C.POINTER(Dims), C.POINTER(vp), i32, vp, sz, vp]
     L.tdmpc_encode.argtypes = [C.POINTER(Dims), vp, vp, i32, i32, vp, vp, vp]
     L.tdmpc_plan.argtypes = [C.POINTER(Dims), C.POINTER(PlanParams), vp, vp, i32, vp, vp, vp, vp, vp,

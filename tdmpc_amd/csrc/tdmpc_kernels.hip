@@ -4588,6 +4588,7 @@ struct RefNormalsArgs {
     float* noise;
     int64_t env_stride;
     uint64_t seed, offset, env_adv;   // generator state at the call; counter advance per env
+    const uint64_t* gen_state;        // non-null: {seed, offset} read from device memory when the kernel runs
     int32_t ndraw;
     int32_t blk[REF_MAX_DRAWS + 1];   // first block of each draw
     int32_t n[REF_MAX_DRAWS];         // elements
@@ -4630,8 +4631,10 @@ __global__ void __launch_bounds__(256) ref_normals_kernel(RefNormalsArgs a) {
     if (li >= a.n[k]) return;
     const int S = a.S[k];
     const int j = li < S ? 0 : li / S;   // ATen grid-stride pass (0 unless the draw exceeds the grid cap)
+    uint64_t seed = a.seed, off = a.offset;
+    if (a.gen_state) seed = a.gen_state[0], off = a.gen_state[1];
     hiprandStatePhilox4_32_10_t st;
-    hiprand_init(a.seed, (unsigned long long)(li - j * S), a.offset + (uint64_t)e * a.env_adv + a.coff[k], &st);
+    hiprand_init(seed, (unsigned long long)(li - j * S), off + (uint64_t)e * a.env_adv + a.coff[k], &st);
     uint4 r = hiprand4(&st);
     for (int p = 0; p < j / 4; ++p) r = hiprand4(&st);
     const float x = torch_normal_component(r, j & 3);
@@ -4639,8 +4642,8 @@ __global__ void __launch_bounds__(256) ref_normals_kernel(RefNormalsArgs a) {
 }
 
 int tdmpc_reference_normals(const tdmpc_dims* d, float* noise, int32_t B, int64_t env_stride, int32_t H,
-                            int32_t I, int32_t eval_mode, uint64_t seed, uint64_t offset, int32_t grid_cap,
-                            uint64_t* offset_advance, void* stream) {
+                            int32_t I, int32_t eval_mode, uint64_t seed, uint64_t offset, const uint64_t* gen_state,
+                            int32_t grid_cap, uint64_t* offset_advance, void* stream) {
     if (!d || !noise || !offset_advance) return TDMPC_E_NULL;
     if (!check_dims(d)) return TDMPC_E_DIMS;
     const int64_t A = d->action_dim, N = d->num_samples, P = d->num_pi, T = N + P;
@@ -4678,7 +4681,7 @@ int tdmpc_reference_normals(const tdmpc_dims* d, float* noise, int32_t B, int64_
     a.blk[a.ndraw] = (int32_t)blk;
     a.noise = noise;
     a.env_stride = env_stride;
-    a.seed = seed, a.offset = offset, a.env_adv = coff;
+    a.seed = seed, a.offset = offset, a.env_adv = coff, a.gen_state = gen_state;
     *offset_advance = (uint64_t)B * coff;
     hipLaunchKernelGGL(ref_normals_kernel, dim3((unsigned)blk, (unsigned)B), dim3(256), 0, (hipStream_t)stream, a);
     HIPCHK(hipGetLastError());

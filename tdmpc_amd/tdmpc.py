@@ -99,7 +99,6 @@ class HipPlanner:
         # Env streams are packed with the CALL's per-env size (depends on H and I), so the flat buffers are
         # re-viewed per call (`noise_view`, `prev_mean_view`); sized for the maximum.
         self.noise_flat = torch.zeros(max_batch * sz.noise_floats_per_env, dtype=torch.float32, device=dev)
-        self.u = torch.zeros(max_batch, dtype=torch.float64, device=dev)
         self.prev_mean_flat = torch.zeros(max_batch * d.max_horizon * self.A, dtype=torch.float32, device=dev)
         self.action = torch.zeros(max_batch, self.A, dtype=torch.float32, device=dev)
         self.metrics = torch.zeros(max_batch, 2, dtype=torch.float32, device=dev)
@@ -109,20 +108,32 @@ class HipPlanner:
         self.warm_dev = torch.zeros(max_batch, dtype=torch.int32, device=dev)
         self._std_host = None
         self._warm_host = None
+        # per-call inputs, staged on the host and sent up as ONE copy: the observations, numpy's elite-choice
+        # uniforms (float64) and the torch generator's {seed, offset} that tdmpc_reference_normals reads when the
+        # graph replays; obs_buf / u / gen_state are views of one device block mirrored by one pinned host block
         if cfg.modality == "pixels":
-            self.obs_buf = torch.zeros(max_batch, *cfg.obs_shape, dtype=torch.uint8, device=dev)
+            obs_shape, obs_dt, np_dt = (max_batch, *cfg.obs_shape), torch.uint8, np.uint8
         else:
-            self.obs_buf = torch.zeros(max_batch, cfg.obs_shape[0], dtype=torch.float32, device=dev)
+            obs_shape, obs_dt, np_dt = (max_batch, cfg.obs_shape[0]), torch.float32, np.float32
+        ob = int(np.prod(obs_shape)) * (1 if obs_dt == torch.uint8 else 4)
+        self._u_off = -(-ob // 8) * 8
+        total = self._u_off + 8 * (max_batch + 2)
+        pin = dev.type == "cuda"
+        self._stage_d = torch.zeros(total, dtype=torch.uint8, device=dev)
+        self._stage_h = torch.zeros(total, dtype=torch.uint8, pin_memory=pin)
+        uo, ge = self._u_off, self._u_off + 8 * max_batch
+        self.obs_buf = self._stage_d[:ob].view(obs_dt).view(obs_shape)
+        self.u = self._stage_d[uo:ge].view(torch.float64)
+        self.gen_state = self._stage_d[ge:].view(torch.int64)
+        hs = self._stage_h.numpy()
+        self._h_obs = hs[:ob].view(np_dt).reshape(max_batch, -1)
+        self._h_u = hs[uo:ge].view(np.float64)
+        self._h_gen = hs[ge:].view(np.uint64)
         self._packed_key = None
         self._packed_model = None
         self._packed_params = []
         self._graphs = {}
-        # pinned host staging for the per-call traffic of the drop-in plan(): the observation and numpy's
-        # uniform go up, the metrics come down, each as one async copy (a pageable copy blocks the host and an
-        # intermediate device tensor costs a copy kernel)
-        pin = dev.type == "cuda"
-        self._pin_obs = torch.zeros(self.obs_buf.shape, dtype=self.obs_buf.dtype, pin_memory=pin)
-        self._pin_u = torch.zeros(max_batch, dtype=torch.float64, pin_memory=pin)
+        # the metrics come down through pinned memory too (a pageable copy blocks the host)
         self._pin_met = torch.zeros(max_batch, 2, dtype=torch.float32, pin_memory=pin)
         self._h2d_done = torch.cuda.Event() if pin else None
         # reference-order draws: "device" = one tdmpc_reference_normals launch per call, "torch" = the
@@ -131,6 +142,7 @@ class HipPlanner:
         if self.ref_draws not in ("device", "torch"):
             raise ValueError(f"TDMPC_REF_DRAWS must be device or torch, not {self.ref_draws!r}")
         self._grid_cap = None
+        self._ref_adv = {}
 
     # ------------------------------------------------------------------ weights
     def pack(self, model: TOLD):
@@ -174,24 +186,65 @@ class HipPlanner:
         if not eval_mode:
             buf[lay["act_off"]:lay["act_off"] + A].normal_()
 
-    def draw_reference_device(self, B: int, H: int, I: int, eval_mode: bool):
-        """The same values as B successive `draw_reference_torch` calls (env 0 first), recomputed by one kernel
-        (tdmpc_reference_normals) from the global generator's seed and Philox offset, which then advances
-        exactly as the B x 18 normal_ launches would have advanced it. Launched on the current stream, outside
-        any graph capture (the offset is read on the host)."""
+    def _gen(self):
         gen = torch.cuda.default_generators[self.device.index or 0]
         if self._grid_cap is None:
             prop = torch.cuda.get_device_properties(self.device)
             per_cu = getattr(prop, "max_threads_per_multi_processor", 2048) // 256
             self._grid_cap = prop.multi_processor_count * per_cu   # ATen calc_execution_policy's grid cap
+        return gen
+
+    def _reference_normals(self, B, H, I, eval_mode, seed, offset, gen_state):
         buf = self.noise_view(H, I, B)
-        off = gen.get_offset()
         adv = C.c_uint64(0)
         rc = self.L.tdmpc_reference_normals(C.byref(self.dims), C.c_void_p(buf.data_ptr()), B, buf.stride(0), H, I,
-                                            int(eval_mode), gen.initial_seed(), off, self._grid_cap, C.byref(adv),
+                                            int(eval_mode), seed, offset, gen_state, self._grid_cap, C.byref(adv),
                                             C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
         _lib.check(rc, "tdmpc_reference_normals")
-        gen.set_offset(off + adv.value)
+        key = (B, H, I, bool(eval_mode))
+        if self._ref_adv.setdefault(key, adv.value) != adv.value:
+            raise RuntimeError(f"reference draws: counter advance {adv.value} != staged {self._ref_adv[key]}")
+        return adv.value
+
+    def draw_reference_device(self, B: int, H: int, I: int, eval_mode: bool):
+        """The same values as B successive `draw_reference_torch` calls (env 0 first), recomputed by one kernel
+        (tdmpc_reference_normals) from the global generator's seed and Philox offset, which then advances
+        exactly as the B x 18 normal_ launches would have advanced it. Launched now on the current stream with
+        the generator state as arguments (not capturable: see launch_reference_draws)."""
+        gen = self._gen()
+        off = gen.get_offset()
+        gen.set_offset(off + self._reference_normals(B, H, I, eval_mode, gen.initial_seed(), off, None))
+
+    def launch_reference_draws(self, B: int, H: int, I: int, eval_mode: bool):
+        """Capturable form: the kernel reads {seed, offset} from `gen_state` when it runs; `stage_reference_state`
+        fills it (through the staging copy) before every launch or replay."""
+        self._gen()
+        self._reference_normals(B, H, I, eval_mode, 0, 0, C.c_void_p(self.gen_state.data_ptr()))
+
+    def stage_reference_state(self, B: int, H: int, I: int, eval_mode: bool):
+        """Host side of one call's reference-order draws: the generator's seed and offset into the staging block,
+        and the generator advanced past the B x 18 draws the kernel will make."""
+        gen = self._gen()
+        key = (B, H, I, bool(eval_mode))
+        adv = self._ref_adv.get(key)
+        if adv is None:
+            adv = self._ref_adv[key] = self.reference_advance(B, H, I, eval_mode)
+        off = gen.get_offset()
+        self._h_gen[0] = gen.initial_seed()
+        self._h_gen[1] = off
+        gen.set_offset(off + adv)
+
+    def reference_advance(self, B: int, H: int, I: int, eval_mode: bool) -> int:
+        """Philox counter advance of B envs' reference draws (ATen calc_execution_policy per normal_ call; the
+        same sum tdmpc_reference_normals returns)."""
+        self._gen()
+
+        def adv(n):
+            grid = min(self._grid_cap, -(-n // 256))
+            return ((n - 1) // (256 * grid * 4) + 1) * 4
+        P, N, A, T = self.P, self.N, self.A, self.T
+        per_env = (H * adv(P * A) if P > 0 else 0) + I * (adv(H * N * A) + adv(T * A)) + (0 if eval_mode else adv(A))
+        return B * per_env
 
     def load_noise(self, e: int, H: int, I: int, eps_pi, eps_cem, eps_term, eps_act):
         """Write an explicit noise stream for env e (parity tests feed the oracle's / the reference's draws)."""
@@ -471,51 +524,44 @@ class TDMPC:
             warm.append(w)
         pl.pack(self.model)
         host = not torch.is_tensor(obs) or obs.device.type == "cpu"
-        if host and pl._h2d_done is not None:
-            # host observations through the pinned staging buffer (the previous call's copy has drained first)
-            pl._h2d_done.synchronize()
-            pl._pin_obs[:B].view(B, -1).copy_(torch.as_tensor(obs).reshape(B, -1))
-            pl.obs_buf[:B].copy_(pl._pin_obs[:B], non_blocking=True)
+        if pl._h2d_done is not None:
+            pl._h2d_done.synchronize()   # the previous call's staging copy has drained
+        if host:
+            pl._h_obs[:B] = np.asarray(obs).reshape(B, -1)
         elif cfg.modality == "pixels":
-            src = torch.as_tensor(obs).to(self.device, torch.uint8)
-            pl.obs_buf[:B].copy_(src.view(B, *cfg.obs_shape))
+            pl.obs_buf[:B].copy_(obs.to(self.device, torch.uint8).view(B, *cfg.obs_shape))
         else:
-            src = torch.as_tensor(obs, dtype=torch.float32).to(self.device)
-            pl.obs_buf[:B].copy_(src.view(B, -1))
+            pl.obs_buf[:B].copy_(obs.to(self.device, torch.float32).view(B, -1))
         obs_u8 = cfg.modality == "pixels"
-        prm = pl.device_state_params(pl.params(H, I, B, warm[0], eval_mode, self.std))
         pl.set_call_state(self.std, warm)
         if noise is not None:
-            us = []
             for e, nb in enumerate(noise):
                 pl.load_noise(e, H, I, nb.eps_pi, nb.eps_cem, nb.eps_term, nb.eps_act)
-                us.append(float(nb.u))
-            pl.u[:B].copy_(torch.tensor(us, dtype=torch.float64))
+                pl._h_u[e] = float(nb.u)
         elif self.rng == "reference":
             # np.random.choice's uniform, drawn on the host from numpy's global generator (tdmpc.py:153)
-            us = [float(np.random.random_sample()) for _ in range(B)]
-            if pl._h2d_done is not None:
-                for e in range(B):
-                    pl._pin_u[e] = us[e]
-                pl.u[:B].copy_(pl._pin_u[:B], non_blocking=True)
-            else:
-                pl.u[:B].copy_(torch.tensor(us, dtype=torch.float64))
+            for e in range(B):
+                pl._h_u[e] = np.random.random_sample()
+        one_launch = noise is None and self.rng == "reference" and pl.ref_draws == "device"
+        if one_launch:
+            pl.stage_reference_state(B, H, I, eval_mode)
+        # one copy up: observations (host ones), uniforms, generator state
+        lo = 0 if host else pl._u_off
+        pl._stage_d[lo:].copy_(pl._stage_h[lo:], non_blocking=True)
         if pl._h2d_done is not None:
             pl._h2d_done.record()
 
-        one_launch = noise is None and self.rng == "reference" and pl.ref_draws == "device"
-        if one_launch:
-            pl.draw_reference_device(B, H, I, eval_mode)
-
         def device_work():
-            if noise is None and not one_launch:
-                if self.rng == "reference":
+            if noise is None:
+                if one_launch:
+                    pl.launch_reference_draws(B, H, I, eval_mode)
+                elif self.rng == "reference":
                     for e in range(B):
                         pl.draw_reference_torch(e, H, I, eval_mode)
                 else:
                     pl.noise_view(H, I, B).normal_()
                     pl.u[:B].uniform_()
-            pl.launch(prm, obs_u8, trace)
+            pl.launch(pl.device_state_params(pl.params(H, I, B, warm[0], eval_mode, self.std)), obs_u8, trace)
 
         if self.graph and noise is None and trace is None:
             key = (H, I, B, bool(eval_mode), self.rng, one_launch)   # self.std and the warm flags live on the device

@@ -89,12 +89,12 @@ def test_entry_points_reject_null_arguments():
     assert L.tdmpc_encode(C.byref(d), None, None, 0, 1, None, None, None) == E_NULL
     assert L.tdmpc_pack_weights(C.byref(d), None, 0, None, 0, None) == E_NULL
     adv = C.c_uint64(0)
-    assert L.tdmpc_reference_normals(C.byref(d), None, 1, 10**6, 5, 6, 0, 1, 0, 2048, C.byref(adv), None) == E_NULL
+    assert L.tdmpc_reference_normals(C.byref(d), None, 1, 10**6, 5, 6, 0, 1, 0, None, 2048, C.byref(adv), None) == E_NULL
     # shape checks before any launch: an env stride shorter than the stream, too many draws
     x = C.c_void_p(16)
     S = L.tdmpc_noise_floats(C.byref(d), 5, 6)
-    assert L.tdmpc_reference_normals(C.byref(d), x, 1, S - 1, 5, 6, 0, 1, 0, 2048, C.byref(adv), None) == -1
-    assert L.tdmpc_reference_normals(C.byref(d), x, 1, 10**9, 16, 60, 0, 1, 0, 2048, C.byref(adv), None) == -1
+    assert L.tdmpc_reference_normals(C.byref(d), x, 1, S - 1, 5, 6, 0, 1, 0, None, 2048, C.byref(adv), None) == -1
+    assert L.tdmpc_reference_normals(C.byref(d), x, 1, 10**9, 16, 60, 0, 1, 0, None, 2048, C.byref(adv), None) == -1
     assert b"draws" in L.tdmpc_last_error()
     # learner engine (include/tdmpc_learner.h)
     assert L.tdmpc_lg_gemm(None, 1, 1, None) == E_NULL

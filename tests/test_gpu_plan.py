@@ -200,22 +200,37 @@ def test_reference_normals_one_launch(task, ov, B, ev):
     assert bad.numel() == 0, f"{bad.shape[0]} of {got.numel()} differ, first at {bad[0].tolist()}"
 
 
-def test_plan_reference_draws_device_equals_torch(monkeypatch):
-    """plan() with the one-launch draws (default, outside the captured graph) equals plan() with the reference's
-    own normal_ launches captured in the graph, bitwise, over warm-started calls."""
+@pytest.mark.parametrize("graph,B", [(True, 1), (False, 1), (True, 3)])
+def test_plan_reference_draws_device_equals_torch(monkeypatch, graph, B):
+    """plan() / plan_batch with the one-launch draws (the default: in the captured graph, the generator state
+    staged through device memory) equals the same calls with the reference's own normal_ launches, bitwise, over
+    warm-started calls, eval-mode calls and a reseed between calls; the generator ends in the same state."""
     cfg = make_cfg("humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5)
-    obs = np.random.RandomState(4).standard_normal((3, cfg.obs_shape[0])).astype(np.float32)
+    obs = np.random.RandomState(4).standard_normal((4, B, cfg.obs_shape[0])).astype(np.float32)
     outs = []
     for mode in ("device", "torch"):
         monkeypatch.setenv("TDMPC_REF_DRAWS", mode)
-        agent = _agent(cfg, 2)
+        agent = TDMPC(cfg, max_batch=B, graph=graph)
+        agent.model.load_state_dict(synthetic_state_dict(cfg, 2))
+        agent.std = 0.05
         assert agent.planner.ref_draws == mode
         torch.manual_seed(11)
         np.random.seed(11)
-        outs.append([agent.plan(obs[k], step=10**6, t0=(k == 0))[0].clone() for k in range(3)])
-        outs[-1].append(torch.randn(4, device="cuda"))
+        res = []
+        for k in range(4):
+            if k == 2:
+                torch.manual_seed(5)   # a new seed between calls reaches the staged generator state
+            ev = k == 3
+            if B == 1:
+                a, m = agent.plan(obs[k, 0], eval_mode=ev, step=10**6, t0=(k == 0))
+                res += [a.clone(), torch.tensor([m["external_reward_mean"], m["current_std"]])]
+            else:
+                a, m = agent.plan_batch(obs[k], eval_mode=ev, step=10**6, t0=(k == 0), sync_metrics=False)
+                res += [a.clone(), m.clone()]
+        res.append(torch.randn(4, device="cuda"))
+        outs.append(res)
     for x, y in zip(*outs):
-        assert torch.equal(x, y)
+        assert torch.equal(x.cpu(), y.cpu())
 
 
 @pytest.mark.parametrize("path", PATHS)
