@@ -191,6 +191,7 @@ struct Work {
     float* rlast;    // [B*T] reward at t = H-1
     float* value;    // [B*T]
     float* qv;       // [2][xrows] Q-head outputs of the chain path
+    float* pimu;     // [xrows][Ap] tanh(pi(z_H)) per X row: the pi rows' terminal means, reused by CEM iterations >= 1
     float* zpart;    // [2][SPLIT_S][split_rows][max(Lr, Ar)] split-step partial z' / pi outputs, two parities
     float* rpart_s;  // [2][SPLIT_S][split_rows] split-step partial reward dots
     int split_rows;  // rows the split partial buffers hold (min(xrows, SPLIT_MAX_ROWS))
@@ -296,6 +297,7 @@ void make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k, int ex
     k->rlast = (float*)take(B * T * 4);
     k->value = (float*)take(B * T * 4);
     k->qv = (float*)take(2 * (size_t)k->xrows * 4);
+    k->pimu = (float*)take((size_t)k->xrows * w.Ap * 4);
     k->split_rows = std::min(k->xrows, SPLIT_MAX_ROWS);
     k->zpart = (float*)take((size_t)2 * SPLIT_S * k->split_rows * std::max(w.Lr, w.Ar) * 4);
     k->rpart_s = (float*)take((size_t)2 * SPLIT_S * k->split_rows * 4);
@@ -977,6 +979,7 @@ struct ChainArgs {
     float* G; float* rlast; float disc; int first, last;
     // CH_PI: TruncatedNormal noise
     const float* eps; int eps_G; long eps_env; long eps_off; float min_std, lo, hi; int A;
+    float* mu_out;                       // CH_PI, non-null: tanh(mu) of row x also to mu_out[x * nstore + col]
     // CH_Q: q_p of row x at q[p * q_ld + x]
     float* q; int q_ld;
 };
@@ -1710,12 +1713,15 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
             // TOLD.pi + TruncatedNormal.sample(clip=0.3) (tdmpc.py:39-45, helper.py:86-96); this thread's noise
             // was loaded at kernel start (pass (i - tid) / NTH < NIT: nstore/4 * 32 <= 512 items)
             const bool second = NIT > 1 && i >= tid + NTH;
+            float mu4[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 float x = 0.f;
+                mu4[k] = 0.f;
                 if (c + k < a.nvalid) {
                     const float muv = tanhf(o[k]);
                     x = muv;
+                    mu4[k] = muv;
                     if (a.min_std > 0.f) {
                         const float ee = tclamp(fmul(second ? eps4[NIT - 1][k] : eps4[0][k], a.min_std), -0.3f, 0.3f);
                         x = tclamp(fadd(muv, ee), a.lo, a.hi);
@@ -1723,6 +1729,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
                 }
                 o[k] = x;
             }
+            if (a.mu_out) *(float4*)(a.mu_out + (size_t)xr * a.nstore + c) = make_float4(mu4[0], mu4[1], mu4[2], mu4[3]);
         } else {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -2471,12 +2478,15 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
         float o[4] = {s.x + bb.x, s.y + bb.y, s.z + bb.z, s.w + bb.w};
         const int xr = map_row(a.amap, lm);
         if (MODE == CH_PI) {
+            float mu4[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 float x = 0.f;
+                mu4[k] = 0.f;
                 if (c + k < a.nvalid) {
                     const float muv = tanhf(o[k]);
                     x = muv;
+                    mu4[k] = muv;
                     if (a.min_std > 0.f) {
                         const float ee = tclamp(fmul(eps4[k], a.min_std), -0.3f, 0.3f);
                         x = tclamp(fadd(muv, ee), a.lo, a.hi);
@@ -2484,6 +2494,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
                 }
                 o[k] = x;
             }
+            if (a.mu_out) *(float4*)(a.mu_out + (size_t)xr * a.nstore + c) = make_float4(mu4[0], mu4[1], mu4[2], mu4[3]);
         } else {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -2750,6 +2761,42 @@ __global__ void __launch_bounds__(256) split_pi_finish_kernel(const SplitPiArgs 
             if (a.min_std > 0.f) {
                 const float ee = tclamp(fmul(ep[col], a.min_std), -0.3f, 0.3f);
                 x = tclamp(fadd(muv, ee), a.lo, a.hi);
+            }
+        }
+        o[cc] = x;
+    }
+    *(float4*)(a.Xo + (size_t)(xr >> 5) * a.x_ts + (size_t)q * 128 + (xr & 31) * 4) = make_float4(o[0], o[1], o[2], o[3]);
+}
+
+// The pi rows' terminal action in CEM iterations >= 1 (tdmpc.py:91, pi(z_H, min_std)): their z_H is the same in
+// every iteration (same z0, same pi actions), so mu = tanh(pi(z_H)) is the one the first iteration's pi launch
+// cached (ChainArgs::mu_out); only the TruncatedNormal sample is redrawn, with the chain epilogue's arithmetic.
+// One thread per (row, action quad).
+struct PiMuArgs {
+    int rows; RowMap amap; const float* mu; int Ap, A; float* Xo; long x_ts;
+    const float* eps; int eps_G; long eps_env; long eps_off; float min_std, lo, hi;
+};
+
+__global__ void __launch_bounds__(256) pi_from_mu_kernel(const PiMuArgs a) {
+    const int nq = a.Ap / 4;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int row = (int)(i / nq), q = (int)(i % nq);
+    if (row >= a.rows) return;
+    const int xr = map_row(a.amap, row);
+    const int e = row / a.eps_G, rr = row % a.eps_G;
+    const float* ep = a.eps + (size_t)e * a.eps_env + a.eps_off + (size_t)rr * a.A;
+    const float4 m = *(const float4*)(a.mu + (size_t)xr * a.Ap + 4 * q);
+    const float mv[4] = {m.x, m.y, m.z, m.w};
+    float o[4];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+        const int col = 4 * q + cc;
+        float x = 0.f;
+        if (col < a.A) {
+            x = mv[cc];
+            if (a.min_std > 0.f) {
+                const float ee = tclamp(fmul(ep[col], a.min_std), -0.3f, 0.3f);
+                x = tclamp(fadd(mv[cc], ee), a.lo, a.hi);
             }
         }
         o[cc] = x;
@@ -4195,7 +4242,7 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
 
 // pi(z_t) with TruncatedNormal noise for `rows` rows of X_t -> X_t action columns (tdmpc.py:39-45).
 int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps_env, int eps_G, long eps_off,
-           float min_std) {
+           float min_std, float* mu_out = nullptr) {
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
@@ -4208,6 +4255,7 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
         a.Xo = Xt(c, t); a.out_q0 = 0;
         a.eps = eps; a.eps_G = eps_G; a.eps_env = eps_env; a.eps_off = eps_off; a.A = w.A;
         a.min_std = min_std; a.lo = (float)(-1.0 + 1e-6); a.hi = (float)(1.0 - 1e-6);
+        a.mu_out = mu_out;
         return launch_chain(CH_PI, a, 1, c.s);
     }
     if (use_split_pi(c, rows)) {
@@ -4266,6 +4314,22 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
         a.lo = (float)(-1.0 + 1e-6); a.hi = (float)(1.0 - 1e-6);
         return launch_lin(a, 1, w.A, 0, PRO_PLAIN, c.s);
     }
+}
+
+// pi(z_H) of `rows` rows from the cached means k.pimu (pi_from_mu_kernel) -> X_H action columns.
+int policy_from_mu(const Ctx& c, int rows, RowMap map, const float* eps, long eps_env, int eps_G, long eps_off,
+                   float min_std) {
+    PiMuArgs f;
+    memset(&f, 0, sizeof f);
+    f.rows = rows; f.amap = map; f.mu = c.k.pimu; f.Ap = c.w.Ap; f.A = c.w.A;
+    f.Xo = Xt(c, c.H); f.x_ts = (long)c.Kx * 32;
+    f.eps = eps; f.eps_G = eps_G; f.eps_env = eps_env; f.eps_off = eps_off; f.min_std = min_std;
+    f.lo = (float)(-1.0 + 1e-6); f.hi = (float)(1.0 - 1e-6);
+    const long nth = (long)rows * (c.w.Ap / 4);
+    if (!nth) return 0;
+    hipLaunchKernelGGL(pi_from_mu_kernel, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, c.s, f);
+    HIPCHK(hipGetLastError());
+    return 0;
 }
 
 // Terminal value: Q(z_H, pi(z_H)) for all T rows of every env (tdmpc.py:91-92).
@@ -4855,15 +4919,28 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     }
     const size_t cem_lds = cem_lds_bytes(T, H, ca.K, c.A);
 
+    // The pi rows' terminal mean tanh(pi(z_H)) is the same in every iteration: the first iteration's pi launch over
+    // all T rows caches it (chain path), later ones run pi over the N sampled rows only and redraw the pi rows'
+    // TruncatedNormal sample from the cache (TDMPC_PI_CACHE=0: pi over all T rows every iteration).
+    static const int pi_cache_env = [] { const char* e = getenv("TDMPC_PI_CACHE"); return e ? atoi(e) : 1; }();
+    const bool pi_cache = pi_cache_env && P > 0 && use_chain(c, B * T, 1, CK_PI);
+    const RowMap pmH = {P, T, N};
     for (int i = 0; i < I; ++i) {
         if (i > 0 && (rc = prep(c, noise, i, nullptr))) return rc;
         if (i > 0 || P == 0)
             for (int t = 0; t < H; ++t)
                 if ((rc = step_next(c, t, B * N, rm, prm->discount_pow[t], t == 0, t == H - 1, 1)))
                     return rc;
-        if ((rc = policy(c, H, B * T, all, noise, c.eps_env, T, c.eps_cem_off + (long)i * c.eps_iter + c.eps_term_off,
-                         prm->min_std)))
+        const long toff = c.eps_cem_off + (long)i * c.eps_iter + c.eps_term_off;
+        if (pi_cache && i > 0) {
+            if ((rc = policy(c, H, B * N, rm, noise, c.eps_env, N, toff, prm->min_std))) return rc;
+            if ((rc = flush_split(c))) return rc;
+            if ((rc = policy_from_mu(c, B * P, pmH, noise, c.eps_env, P, toff + (long)N * c.A, prm->min_std)))
+                return rc;
+        } else if ((rc = policy(c, H, B * T, all, noise, c.eps_env, T, toff, prm->min_std,
+                                pi_cache ? c.k.pimu : nullptr))) {
             return rc;
+        }
         if ((rc = terminal_q(c, prm->discount_pow[H]))) return rc;
         ca.final_iter = i == I - 1;
         ca.iter = i;
