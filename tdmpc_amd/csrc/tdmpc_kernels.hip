@@ -225,7 +225,7 @@ constexpr unsigned P1_SPIN_MAX = 400000;   // ~0.3-0.5 s of polling before a wor
 
 // exchange region bytes (all offsets 256-aligned) for dims; 0 = not eligible
 struct P1Region {
-    unsigned o_sync, o_xb, o_h1, o_zp, o_rp, o_pp, o_qm, o_qp, o_val, o_rl, xb_t, xb_g, total;
+    unsigned o_sync, o_xb, o_h1, o_zp, o_rp, o_pp, o_qm, o_qp, o_val, o_rl, o_mu, xb_t, xb_g, total;
 };
 
 // the first layer's 32-k steps the kernel instantiation runs (4 or 6; steps past K meet zero activations)
@@ -251,6 +251,7 @@ inline P1Region p1_region(const tdmpc_dims* d, const Layout& w) {
     r.o_qp = take((size_t)P1_NG * 2 * 16 * P1_ROWS * 4);
     r.o_val = take(2 * T * 4);
     r.o_rl = take(T * 4);
+    r.o_mu = take((size_t)P1_NG * P1_ROWS * w.Ap * 4);   // the pi rows' cached terminal means
     r.total = (unsigned)o;
     return r;
 }
@@ -4316,6 +4317,12 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
     }
 }
 
+// TDMPC_PI_CACHE=0: the pi rows' terminal mean is recomputed in every CEM iteration (A/B switch; default on)
+int pi_cache_on() {
+    static const int v = [] { const char* e = getenv("TDMPC_PI_CACHE"); return e ? atoi(e) : 1; }();
+    return v;
+}
+
 // pi(z_H) of `rows` rows from the cached means k.pimu (pi_from_mu_kernel) -> X_H action columns.
 int policy_from_mu(const Ctx& c, int rows, RowMap map, const float* eps, long eps_env, int eps_G, long eps_off,
                    float min_std) {
@@ -4550,7 +4557,7 @@ int plan1_launch(const Ctx& c, const tdmpc_plan_params* prm, const float* noise,
     for (int t = 0; t <= c.H && t < 17; ++t) a.disc[t] = prm->discount_pow[t];
     a.base = c.k.p1; a.bytes = (unsigned)c.k.p1_bytes;
     a.o_sync = rg.o_sync; a.o_xb = rg.o_xb; a.o_h1 = rg.o_h1; a.o_zp = rg.o_zp; a.o_rp = rg.o_rp; a.o_pp = rg.o_pp;
-    a.o_qm = rg.o_qm; a.o_qp = rg.o_qp; a.o_val = rg.o_val; a.o_rl = rg.o_rl; a.xb_t = rg.xb_t; a.xb_g = rg.xb_g;
+    a.o_qm = rg.o_qm; a.o_qp = rg.o_qp; a.o_val = rg.o_val; a.o_rl = rg.o_rl; a.o_mu = rg.o_mu; a.pi_cache = pi_cache_on(); a.xb_t = rg.xb_t; a.xb_g = rg.xb_g;
     a.stamps = g_p1_stamps;
     HIPCHK(hipMemsetAsync(c.k.p1 + rg.o_sync, 0, P1_NG * 256 + 256, c.s));   // counters + error word
     const size_t lds = p1_lds_bytes(c.H, a.K, w.A, c.T);
@@ -4922,8 +4929,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     // The pi rows' terminal mean tanh(pi(z_H)) is the same in every iteration: the first iteration's pi launch over
     // all T rows caches it (chain path), later ones run pi over the N sampled rows only and redraw the pi rows'
     // TruncatedNormal sample from the cache (TDMPC_PI_CACHE=0: pi over all T rows every iteration).
-    static const int pi_cache_env = [] { const char* e = getenv("TDMPC_PI_CACHE"); return e ? atoi(e) : 1; }();
-    const bool pi_cache = pi_cache_env && P > 0 && use_chain(c, B * T, 1, CK_PI);
+    const bool pi_cache = pi_cache_on() && P > 0 && use_chain(c, B * T, 1, CK_PI);
     const RowMap pmH = {P, T, N};
     for (int i = 0; i < I; ++i) {
         if (i > 0 && (rc = prep(c, noise, i, nullptr))) return rc;
