@@ -59,7 +59,8 @@ def plan_flops(cfg, executed: bool) -> float:
     """Algorithmic FLOPs of one plan-step: 2*[P*H*(pi+d+R) + I*T*(H*(d+R) + pi + 2Q) + enc].
     executed=True counts what this build runs: the pi rows' H-step rollout is identical in every CEM
     iteration (same z0, same pi actions), so it is computed once per plan and only N rows are rolled out
-    per iteration."""
+    per iteration; the pi rows' terminal mean tanh(pi(z_H)) likewise, so the terminal pi runs over T rows in
+    iteration 0 and over the N sampled rows after it (only the TruncatedNormal sample is redrawn)."""
     L, A, M, E = cfg.latent_dim, cfg.action_dim, cfg.mlp_dim, cfg.enc_dim
     N = cfg.num_samples
     P = int(cfg.mixture_coef * N)
@@ -79,7 +80,7 @@ def plan_flops(cfg, executed: bool) -> float:
     else:
         enc = cfg.obs_shape[0] * E + E * L
     if executed:
-        macs = P * H * (pi + d + R) + I * (N * H * (d + R) + T * (pi + 2 * Q)) + enc
+        macs = P * H * (pi + d + R) + I * (N * H * (d + R) + T * 2 * Q) + (T + (I - 1) * N) * pi + enc
     else:
         macs = P * H * (pi + d + R) + I * T * (H * (d + R) + pi + 2 * Q) + enc
     return 2.0 * macs
