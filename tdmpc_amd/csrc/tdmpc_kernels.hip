@@ -191,6 +191,7 @@ struct Work {
     float* rlast;    // [B*T] reward at t = H-1
     float* value;    // [B*T]
     float* qv;       // [2][xrows] Q-head outputs of the chain path
+    float* z0c;      // [B][2][M] TOLD.next first layer's z0 share + bias per env (t = 0 steps of the chain kernel)
     float* pimu;     // [xrows][Ap] tanh(pi(z_H)) per X row: the pi rows' terminal means, reused by CEM iterations >= 1
     float* zpart;    // [2][SPLIT_S][split_rows][max(Lr, Ar)] split-step partial z' / pi outputs, two parities
     float* rpart_s;  // [2][SPLIT_S][split_rows] split-step partial reward dots
@@ -299,6 +300,7 @@ void make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k, int ex
     k->value = (float*)take(B * T * 4);
     k->qv = (float*)take(2 * (size_t)k->xrows * 4);
     k->pimu = (float*)take((size_t)k->xrows * w.Ap * 4);
+    k->z0c = (float*)take(B * 2 * M * 4);
     k->split_rows = std::min(k->xrows, SPLIT_MAX_ROWS);
     k->zpart = (float*)take((size_t)2 * SPLIT_S * k->split_rows * std::max(w.Lr, w.Ar) * 4);
     k->rpart_s = (float*)take((size_t)2 * SPLIT_S * k->split_rows * 4);
@@ -981,6 +983,9 @@ struct ChainArgs {
     // CH_PI: TruncatedNormal noise
     const float* eps; int eps_G; long eps_env; long eps_off; float min_std, lo, hi; int A;
     float* mu_out;                       // CH_PI, non-null: tanh(mu) of row x also to mu_out[x * nstore + col]
+    // CH_STEP at t = 0 (every row's latent is its env's z0): non-null, layer 1 runs over the first k1c columns only
+    // and its bias is z0c[env][head] = b1 + W1[:, k1c:] X_0[k1c:] (z0c_kernel), env = logical row / z0_G
+    const float* z0c; int z0_G, k1c;
     // CH_Q: q_p of row x at q[p * q_ld + x]
     float* q; int q_ld;
 };
@@ -1440,6 +1445,9 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     // x6: k groups of 16, blocks of 32 rows x K16 x 3 planes (bf16 elements)
     const int g1n = X6 ? (int)(rup(a.K1, 16) >> 4) : a.K1 >> 3, g2n = X6 ? M >> 4 : M >> 3;
     const long wb1 = (long)g1n * 1536, wb2 = (long)g2n * 1536;
+    // layer-1 k groups run here: all, or with z0c only the first k1c columns (the rest is in the per-env bias)
+    const bool zc = MODE == CH_STEP && a.z0c != nullptr;
+    const int g1e = zc ? (X6 ? a.k1c >> 4 : a.k1c >> 3) : g1n;
     const int cw0 = wave * TN;              // first 32-column block of this wave in the M-wide layers
     const bool head_dot = MODE == CH_Q || (MODE == CH_STEP && pb == 1);
 #ifdef TDMPC_STAMPS
@@ -1452,10 +1460,10 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     // consecutive lanes = 32 rows of one quad) and the parameter vectors
     float4 wr[X6 ? 1 : D][TN];
     uint4 wx[X6 ? D : 1][TN][3];
-    if constexpr (X6) ring6_fill<TN, D>(wx, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n);
-    else ring_fill<TN, D>(wr, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3);
+    if constexpr (X6) ring6_fill<TN, D>(wx, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1e);
+    else ring_fill<TN, D>(wr, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1e);
     // (x6: K1 rounded to 16 with zero quads)
-    const int q1n = X6 ? g1n * 4 : a.K1 >> 2;
+    const int q1n = zc ? a.k1c >> 2 : X6 ? g1n * 4 : a.K1 >> 2;
     for (int i = tid; i < q1n * 32; i += NTH) {
         const int row = i & 31, q = i >> 5;
         const int lm = m0 + row;
@@ -1484,8 +1492,9 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
             ((float4*)sH)[i] = x;
         }
     }
+    const float* b1src = zc ? a.z0c + ((size_t)(m0 / a.z0_G) * 2 + pb) * M : P.b1;
     for (int i = tid; i < M / 4; i += NTH) {
-        ((float4*)sb1)[i] = ((const float4*)P.b1)[i];
+        ((float4*)sb1)[i] = ((const float4*)b1src)[i];
         ((float4*)sb2)[i] = ((const float4*)P.b2)[i];
         if (head_dot) ((float4*)sw3)[i] = ((const float4*)P.w3v)[i];
         if (MODE == CH_Q) {
@@ -1528,10 +1537,10 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    if constexpr (X6 == 2) ring6p_run<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n, lane);
-    else if constexpr (X6 == 1 && NW == 4 && X6_PIPE) ring6_run_pipe<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n, r, h);
-    else if constexpr (X6 == 1) ring6_run<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n, r, h);
-    else ring_run<TN, D>(acc, wr, sH, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, a.K1 >> 3, r, h);
+    if constexpr (X6 == 2) ring6p_run<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1e, lane);
+    else if constexpr (X6 == 1 && NW == 4 && X6_PIPE) ring6_run_pipe<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1e, r, h);
+    else if constexpr (X6 == 1) ring6_run<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1e, r, h);
+    else ring_run<TN, D>(acc, wr, sH, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1e, r, h);
     // layer-2 weights in flight during the epilogue
     if constexpr (X6) ring6_fill<TN, D>(wx, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n);
     else ring_fill<TN, D>(wr, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3);
@@ -2769,6 +2778,25 @@ __global__ void __launch_bounds__(256) split_pi_finish_kernel(const SplitPiArgs 
     *(float4*)(a.Xo + (size_t)(xr >> 5) * a.x_ts + (size_t)q * 128 + (xr & 31) * 4) = make_float4(o[0], o[1], o[2], o[3]);
 }
 
+// TOLD.next's first layer at t = 0 splits as W1 [a | z0] = W1[:, :k1c] X_0[:k1c] + W1[:, k1c:] X_0[k1c:]: every
+// row of an env shares z0, so the second term (plus the bias) is computed once per env and head here and the chain
+// kernel's t = 0 steps run layer 1 over the first k1c columns (the actions, rounded up to a k group) only.
+// Grid (B, 2 heads, M / 256); one output column per thread, fp32 FMAs in k order; W1 is the fp32 panel.
+__global__ void __launch_bounds__(256) z0c_kernel(const float* W1, const float* b1, const float* z0, int Kx, int Ap,
+                                                   int Lp, int k1c, int M, float* out) {
+    const int e = blockIdx.x, p = blockIdx.y, n = blockIdx.z * 256 + threadIdx.x;
+    if (n >= M) return;
+    const int nn = p * M + n;
+    const float* wrow = W1 + (size_t)(nn >> 5) * Kx * 32 + (nn & 31) * 4;
+    float acc = 0.f;
+    for (int k = k1c; k < Kx; ++k) {
+        const int zi = k - Ap;
+        const float x = zi < Lp ? z0[(size_t)e * Lp + zi] : 0.f;
+        acc = fmaf(wrow[(k >> 2) * 128 + (k & 3)], x, acc);
+    }
+    out[((size_t)e * 2 + p) * M + n] = acc + b1[nn];
+}
+
 // The pi rows' terminal action in CEM iterations >= 1 (tdmpc.py:91, pi(z_H, min_std)): their z_H is the same in
 // every iteration (same z0, same pi actions), so mu = tanh(pi(z_H)) is the one the first iteration's pi launch
 // cached (ChainArgs::mu_out); only the TruncatedNormal sample is redrawn, with the chain epilogue's arithmetic.
@@ -3855,6 +3883,7 @@ int chain_xcd() {
 int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
     if (a0.rows <= 0) return 0;
     ChainArgs a = a0;
+    if (a.rb != 32) a.z0c = nullptr;   // (chain16 / chain64 run the full first layer)
     const int nw = a.rb == 16 ? 8 : a.nw;
     const size_t lds = ((size_t)a.hfl + (a.rb == 16 ? 256 : 64 * nw) + chain_param_floats(mode, a.M, a.n3)) * 4;
     const int nblk = (a.rows + a.rb - 1) / a.rb;
@@ -3948,6 +3977,7 @@ struct Ctx {
     mutable float split_disc = 0.f;
     mutable RowMap split_map = {1 << 30, 0, 0};
     mutable int split_rows = 0, split_t = 0;
+    int z0c_ready = 0;   // k.z0c holds this call's per-env first-layer z0 shares (tdmpc_plan)
 };
 
 float* Xt(const Ctx& c, int t) { return c.k.X + (size_t)t * c.k.x_stride; }
@@ -4139,6 +4169,19 @@ int flush_split(const Ctx& c) {
                         c.split_disc, c.split_first, 0);
 }
 
+// z0c split point: the action columns rounded up to a 16-k group (TDMPC_Z0C=0 disables the split)
+int z0c_k1c(const Ctx& c) { return (int)rup(c.w.Ap, 16); }
+bool z0c_eligible(const Ctx& c) {
+    static const int v = [] { const char* e = getenv("TDMPC_Z0C"); return e ? atoi(e) : 1; }();
+    return v && z0c_k1c(c) < (int)rup(c.Kx, 16);
+}
+int z0c_launch(const Ctx& c) {
+    hipLaunchKernelGGL(z0c_kernel, dim3(c.B, 2, (c.M + 255) / 256), dim3(256), 0, c.s, c.pw + c.w.w1x, c.pw + c.w.b1x,
+                       c.k.z0, c.Kx, c.w.Ap, c.w.Lp, z0c_k1c(c), c.M, c.k.z0c);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 // defer = 1 (a loop of consecutive steps over the same rows, nothing reading X_{t+1}'s latents in between): on the
 // split path the finish of this step is folded into the next step's launch.
 int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, int defer = 0) {
@@ -4163,6 +4206,7 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         }
         a.Xo = Xt(c, t + 1); a.out_q0 = w.Ap / 4;
         a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
+        if (t == 0 && c.z0c_ready && map.G % 32 == 0) { a.z0c = c.k.z0c; a.z0_G = map.G; a.k1c = z0c_k1c(c); }
         maybe_rb64(c, a, CH_STEP, 2);
         if (a.rb == 64) {
             const size_t rb1 = (size_t)(M / 32) * (rup(c.Kx, 16) / 16) * 1536;
@@ -4891,6 +4935,10 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     if (use_plan1(c))
         return plan1_launch(c, prm, noise, u, prev_mean, action, metrics, elite_out, score_out, value_out, mean_out, std_out);
     if ((rc = prep(c, noise, 0, c.k.z0))) return rc;
+    if (z0c_eligible(c)) {
+        if ((rc = z0c_launch(c))) return rc;
+        c.z0c_ready = 1;
+    }
 
     // pi pre-rollout (tdmpc.py:113-118) fused with CEM iteration 0: at each step t the policy rows get
     // pi(z_t) first, then ONE TOLD.next launch advances all T rows of every env (rollout rows with the
