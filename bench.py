@@ -60,7 +60,9 @@ def plan_flops(cfg, executed: bool) -> float:
     executed=True counts what this build runs: the pi rows' H-step rollout is identical in every CEM
     iteration (same z0, same pi actions), so it is computed once per plan and only N rows are rolled out
     per iteration; the pi rows' terminal mean tanh(pi(z_H)) likewise, so the terminal pi runs over T rows in
-    iteration 0 and over the N sampled rows after it (only the TruncatedNormal sample is redrawn)."""
+    iteration 0 and over the N sampled rows after it (only the TruncatedNormal sample is redrawn); and at t = 0
+    every row of an env starts from its z0, so TOLD.next's first layer runs over the action k group(s) only
+    (rup(A, 16) columns) with the latent share computed once per env and head (z0c_kernel)."""
     L, A, M, E = cfg.latent_dim, cfg.action_dim, cfg.mlp_dim, cfg.enc_dim
     N = cfg.num_samples
     P = int(cfg.mixture_coef * N)
@@ -81,6 +83,9 @@ def plan_flops(cfg, executed: bool) -> float:
         enc = cfg.obs_shape[0] * E + E * L
     if executed:
         macs = P * H * (pi + d + R) + I * (N * H * (d + R) + T * 2 * Q) + (T + (I - 1) * N) * pi + enc
+        k1c = -(-A // 16) * 16
+        macs -= (I * N + P) * 2 * M * max(0, L + A - k1c)   # t = 0 first layers: action columns only
+        macs += 2 * M * max(0, L + A - k1c)                  # z0c: once per env
     else:
         macs = P * H * (pi + d + R) + I * T * (H * (d + R) + pi + 2 * Q) + enc
     return 2.0 * macs
@@ -497,7 +502,8 @@ def main():
 
         rows = B * cfg.num_samples
         M, Lt, A = cfg.mlp_dim, cfg.latent_dim, cfg.action_dim
-        # dominant kernel: the CEM rollout step (TOLD.next, 5 of every iteration's launches, ~half the time).
+        # dominant kernel: the CEM rollout step (TOLD.next, 5 of every iteration's launches, ~half the time); the
+        # library times the t >= 1 launches only (t = 0 runs a reduced first layer, z0c_kernel).
         # Row-block chain kernel when the auto path picks it (>= 64 32-row blocks), else the layered hidden GEMM.
         n, ms, fl = timed(4, -1, 0, rows)
         peak = FP32_PEAK_TFLOPS
