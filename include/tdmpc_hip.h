@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define TDMPC_ABI_VERSION 5
+#define TDMPC_ABI_VERSION 6
 
 #define TDMPC_OK 0
 #define TDMPC_E_DIMS (-1)     /* unsupported or inconsistent dims / params */
@@ -73,15 +73,24 @@ typedef struct tdmpc_plan_params {
                               kernels wherever the shape allows (row block by launch size), 3 / 4 = chain
                               kernels on 32- / 16-row blocks only, 5 = TOLD.next on the column-split step kernel
                               (others layered), 6 = chain kernels with fp32 products from a three-way bf16
-                              split (TDMPC_PATH_CHAIN_X6), 7 = path 5 with those products, 8 = path 2 with
-                              TOLD.next / helper.q on 64-row x6 blocks (chain64), 9 = the persistent one-env plan
+                              split (TDMPC_PATH_CHAIN_X6), 7 = path 5 with those products, 8 = path 6 (the retired
+                              64-row blocks), 9 = the persistent one-env plan
                               (plan1: one launch after the encoder); results agree within the fp32 tolerance */
     /* ABI 5: per-call state read from device memory at run time, so one captured hipGraph serves every value */
     const int32_t* warm_flags; /* optional device int32 [batch]: per-env warm start (tdmpc.py:124-125, `not t0`
                                   for that env with a previous mean); NULL = warm_start for every env */
     const float* std_floor_dev;/* optional device float scalar: self.std (tdmpc.py:148), which update() moves
                                   every step during std_schedule (tdmpc.py:196); NULL = std_floor */
+    /* ABI 6 */
+    int32_t* status;           /* optional device int32, sticky: a plan that failed on the device ORs a nonzero
+                                  TDMPC_STATUS_* code into it (its action / metrics are NaN then). The caller zeroes
+                                  it once and checks it at its next host sync; the reference cannot fail this way,
+                                  so a nonzero status must be raised, never ignored. NULL = not reported. */
 } tdmpc_plan_params;
+
+/* tdmpc_plan_params.status bits */
+#define TDMPC_STATUS_P1_TIMEOUT 1   /* the persistent one-env plan (path 9 / auto at batch 1) gave up at a hand-off:
+                                       not every workgroup of its grid was resident (e.g. other work held CUs) */
 
 #define TDMPC_PATH_AUTO 0
 #define TDMPC_PATH_LAYERED 1
@@ -91,7 +100,7 @@ typedef struct tdmpc_plan_params {
 #define TDMPC_PATH_SPLIT 5
 #define TDMPC_PATH_CHAIN_X6 6   /* chain kernels, fp32 products from a three-way bf16 split (M = 512) */
 #define TDMPC_PATH_SPLIT_X6 7   /* the split path (5) with the x6 products (M = 512) */
-#define TDMPC_PATH_CHAIN64 8    /* chain kernels with TOLD.next / helper.q on 64-row x6 blocks at any width (M = 512) */
+#define TDMPC_PATH_CHAIN64 8    /* retired (64-row x6 blocks measured no faster): runs path 6 */
 #define TDMPC_PATH_PERSIST 9    /* one env: the whole plan after the encoder as ONE persistent launch (x6 products,
                                    weight-stationary; batch 1, M = 512, >= 256 CUs; the auto path's choice there);
                                    calls it does not apply to run the auto path */

@@ -11,7 +11,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDMPC_LIB_PATH") or os.path.join(HERE, "libtdmpc_hip.so")   # override: A/B of builds
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 PATHS = {"auto": 0, "layered": 1, "chain": 2, "chain32": 3, "chain16": 4, "split": 5, "chain_x6": 6, "split_x6": 7, "chain64": 8, "persist": 9}
 
 EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc_num_param_tensors",
@@ -40,7 +40,7 @@ class PlanParams(C.Structure):
                 ("min_std", C.c_float), ("temperature", C.c_float), ("momentum", C.c_float),
                 ("one_minus_momentum", C.c_float), ("std_floor", C.c_float),
                 ("discount_pow", C.c_float * 17), ("path", C.c_int32),
-                ("warm_flags", C.c_void_p), ("std_floor_dev", C.c_void_p)]
+                ("warm_flags", C.c_void_p), ("std_floor_dev", C.c_void_p), ("status", C.c_void_p)]
 
 
 class IcemParams(C.Structure):

@@ -635,7 +635,10 @@ __global__ void __launch_bounds__(256) lg_adam_kernel(float* p, const float* g, 
     float s = 0.f;
     for (int i = threadIdx.x; i < nblk; i += 256) s += normp[i];
     const float total = sqrtf(block_sum256(s, red));
-    const float coef = fminf(max_norm / (total + 1e-6f), 1.0f);
+    // torch.nn.utils.clip_grad_norm_: clamp(max_norm / (total + 1e-6), max=1), which keeps a NaN norm's NaN
+    // coefficient (and so NaN parameters, like the reference); fminf would drop it
+    const float c0 = max_norm / (total + 1e-6f);
+    const float coef = c0 != c0 ? c0 : fminf(c0, 1.0f);
     if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = total;
     const int t = step[0];
     const double bc1 = 1.0 - pow((double)b1, (double)t), bc2 = 1.0 - pow((double)b2, (double)t);

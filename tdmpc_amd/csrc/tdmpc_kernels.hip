@@ -1058,12 +1058,6 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 #ifndef X6_D3
 #define X6_D3 2   // weight-ring depth of the x6 chain kernel's last layer (k groups of 16)
 #endif
-#ifndef X6_PIPE
-// 1: 4-wave x6 chain workgroups split group g + 1 under group g's MFMAs (ring6_run_pipe). Off: measured 3 % slower
-// (6.56 vs 6.35 ms per B = 32 plan, 2.31 vs 2.22 at B = 8, round-1 run) -- the other wave on the SIMD already
-// fills the split's VALU slots, and the extra live operands cost more than the overlap gains
-#define X6_PIPE 0
-#endif
 DEVI bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 
 // Weights (pack time, pack_x6_kernel): x = hi + mid + lo exactly, each part round-to-nearest (the smallest dropped
@@ -1079,30 +1073,44 @@ DEVI void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
     lo = (__bf16)__fsub_rn(r1, (float)mid);
 }
 
-// Activations (in the hot loop, once per MFMA k group): hi = the truncated top half of x (one AND; finite for every
-// finite x, beyond bf16's largest value included), then mid / lo round-to-nearest: x = hi + mid + lo exactly for
-// finite x (the residual keeps <= 16 significant bits). The dropped terms (w_mid x_lo + w_lo x_mid + w_lo x_lo) are
-// <= 1.5 * 2^-23 of |w x|, the size of an fp32 product rounding. Same VALU cost as a round-to-nearest hi (the AND
-// replaces the bf16 -> fp32 unpack). A NaN stays NaN; an infinite activation gives NaN products (inf - inf in the
-// residual) where fp32 gives +-inf -- the reference's next mixed-sign layer or LayerNorm turns those into NaN too,
-// so G after nan_to_num (tdmpc.py:92) agrees (tests/test_gpu_configs.py::test_estimate_value_nonfinite).
-DEVI void split3_act(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
+// Activations (in the hot loop, once per MFMA k group). Finite x: hi = the truncated top half of x (one AND; finite for
+// every finite x, beyond bf16's largest value included), then mid / lo round-to-nearest: x = hi + mid + lo exactly (the
+// residual keeps <= 16 significant bits). The dropped terms (w_mid x_lo + w_lo x_mid + w_lo x_lo) are <= 1.5 * 2^-23
+// of |w x|, the size of an fp32 product rounding.
+// Non-finite x (+-inf, NaN): only the w_hi.x_hi term sees it (`h`: x's own top half -- arithmetic NaNs keep their
+// payload there); the w_mid.x_hi and w_lo.x_hi terms take `s` = 0 and mid = lo = 0, so the x6 product is w_hi * x:
+// +-inf or NaN exactly where fp32's w * x is (w_hi is 0 only for w = 0, or |w| under bf16's smallest subnormal).
+// With one hi operand for all three weight planes, an infinite activation met 0 * inf = NaN in every weight whose mid
+// or lo part is zero, and a +inf hidden unit that fp32 carries to G = +FLT_MAX came out as G = 0
+// (tests/test_gpu_configs.py::test_estimate_value_nonfinite, cases inf_hidden*). A non-finite WEIGHT is not handled
+// (its w_hi.x_mid / w_hi.x_lo terms meet zero activation parts): planning weights are finite.
+struct X6B {
+    bf16x8_t h;   // hi of x (w_hi term)
+    bf16x8_t s;   // hi of x, 0 where x is not finite (w_mid / w_lo terms)
+    bf16x8_t m, l;
+};
+DEVI void split3_act(float x, __bf16& hi, __bf16& hs, __bf16& mid, __bf16& lo) {
     const uint32_t u = __float_as_uint(x);
-    const float h = __uint_as_float(u & 0xffff0000u);
+    const float xs = __builtin_isfinite(x) ? x : 0.f;
+    const uint32_t us = __float_as_uint(xs);
+    const float h = __uint_as_float(us & 0xffff0000u);
     hi = __builtin_bit_cast(__bf16, (unsigned short)(u >> 16));
-    const float r1 = __fsub_rn(x, h);
+    hs = __builtin_bit_cast(__bf16, (unsigned short)(us >> 16));
+    const float r1 = __fsub_rn(xs, h);
     mid = (__bf16)r1;
     lo = (__bf16)__fsub_rn(r1, (float)mid);
 }
 
-DEVI void split8(const float4& a0, const float4& a1, bf16x8_t& bh, bf16x8_t& bm, bf16x8_t& bl) {
+DEVI X6B split8(const float4& a0, const float4& a1) {
     const float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    X6B b;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-        __bf16 h, m, l;
-        split3_act(x[e], h, m, l);
-        bh[e] = h; bm[e] = m; bl[e] = l;
+        __bf16 h, hs, m, l;
+        split3_act(x[e], h, hs, m, l);
+        b.h[e] = h; b.s[e] = hs; b.m[e] = m; b.l[e] = l;
     }
+    return b;
 }
 
 // Weight ring of the x6 form: D k groups (16 k each) x TN blocks x 3 planes of 1 KiB wave loads. Wp is the wave's
@@ -1121,21 +1129,20 @@ DEVI void ring6_fill(uint4 (&wr)[D][TN][3], const unsigned short* Wp, long wbs, 
 
 template <int TN>
 DEVI void x6_group(floatx16 (&acc)[TN], const uint4 (&w)[TN][3], const float4& a0, const float4& a1) {
-    bf16x8_t bh, bm, bl;
-    split8(a0, a1, bh, bm, bl);
+    const X6B b = split8(a0, a1);
     // small terms first, the hi.hi term last
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][1]), bm, acc[j], 0, 0, 0);
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][1]), b.m, acc[j], 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][2]), bh, acc[j], 0, 0, 0);
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][2]), b.s, acc[j], 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), bl, acc[j], 0, 0, 0);
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), b.l, acc[j], 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][1]), bh, acc[j], 0, 0, 0);
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][1]), b.s, acc[j], 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), bm, acc[j], 0, 0, 0);
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), b.m, acc[j], 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), bh, acc[j], 0, 0, 0);
+    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), b.h, acc[j], 0, 0, 0);
 }
 
 // acc[j] += W(block j) . A over k groups [g0, g1); A from the fp32 LDS block [K/4][32][4] (quads 4g + h and
@@ -1179,151 +1186,6 @@ DEVI void ring6_run(floatx16 (&acc)[TN], uint4 (&wr)[D][TN][3], const float* sA,
             x6_group<TN>(acc, wr[d], a0, a1);
         }
     }
-}
-
-// Software-pipelined form of ring6_run (4-wave workgroups, which have the VGPRs): group g + 1's operand split is
-// issued in the same scheduling region as group g's MFMAs, so the VALU work fills the MFMA gaps of its own wave.
-template <int TN>
-DEVI void x6_mfma6(floatx16 (&acc)[TN], const uint4 (&w)[TN][3], const bf16x8_t& bh, const bf16x8_t& bm,
-                   const bf16x8_t& bl) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][1]), bm, acc[j], 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][2]), bh, acc[j], 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), bl, acc[j], 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][1]), bh, acc[j], 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), bm, acc[j], 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][0]), bh, acc[j], 0, 0, 0);
-}
-
-template <int TN, int D>
-DEVI void ring6_run_pipe(floatx16 (&acc)[TN], uint4 (&wr)[D][TN][3], const float* sA, const unsigned short* Wp,
-                         long wbs, int g0, int g1, int r, int h) {
-    const int gl = g1 - 1;
-    const float* ap = sA + (h * 32 + r) * 4;
-    bf16x8_t bh, bm, bl;
-    {
-        const float4 a0 = *(const float4*)(ap + (size_t)g0 * 512), a1 = *(const float4*)(ap + (size_t)g0 * 512 + 256);
-        split8(a0, a1, bh, bm, bl);
-    }
-    const size_t g1o = (size_t)min(g0 + 1, gl) * 512;
-    float4 n0 = *(const float4*)(ap + g1o), n1 = *(const float4*)(ap + g1o + 256);
-    int gb = g0;
-    for (; gb + D <= g1; gb += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const int g = gb + d;
-            const bf16x8_t ch = bh, cm = bm, cl = bl;
-            split8(n0, n1, bh, bm, bl);                       // group g + 1 (the last one again past the end)
-            const size_t gn = (size_t)min(g + 2, gl) * 512;
-            n0 = *(const float4*)(ap + gn);
-            n1 = *(const float4*)(ap + gn + 256);
-            x6_mfma6<TN>(acc, wr[d], ch, cm, cl);
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    wr[d][j][p] = *(const uint4*)(Wp + j * wbs + ((size_t)min(g + D, gl) * 3 + p) * 512);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-#pragma unroll
-    for (int d = 0; d < D - 1; ++d) {
-        if (gb + d < g1) {
-            const bf16x8_t ch = bh, cm = bm, cl = bl;
-            split8(n0, n1, bh, bm, bl);
-            const size_t gn = (size_t)min(gb + d + 2, gl) * 512;
-            n0 = *(const float4*)(ap + gn);
-            n1 = *(const float4*)(ap + gn + 256);
-            x6_mfma6<TN>(acc, wr[d], ch, cm, cl);
-        }
-    }
-}
-
-// Planes form of the x6 activations (X6 = 2): the LDS block holds the split activations, group g (16 k) as
-// [3 planes][64 lanes][8 bf16] in the weights' k order, written once by the producing epilogue (or the input
-// staging) instead of being split again by every wave at every read.
-DEVI uint4 as_u4(const bf16x8_t& v) { return __builtin_bit_cast(uint4, v); }
-
-template <int TN, int D>
-DEVI void ring6p_run(floatx16 (&acc)[TN], uint4 (&wr)[D][TN][3], const float* sA, const unsigned short* Wp, long wbs,
-                     int g0, int g1, int lane) {
-    const int gl = g1 - 1;
-    const uint4* ap = (const uint4*)sA + lane;   // group g plane p at ap[(3g + p) * 64]
-    uint4 n[3];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) n[p] = ap[(size_t)(3 * g0 + p) * 64];
-    int gb = g0;
-    for (; gb + D <= g1; gb += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const int g = gb + d;
-            const bf16x8_t bh = as_bf16x8(n[0]), bm = as_bf16x8(n[1]), bl = as_bf16x8(n[2]);
-            const int gn = min(g + 1, gl);
-#pragma unroll
-            for (int p = 0; p < 3; ++p) n[p] = ap[(size_t)(3 * gn + p) * 64];
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), bm, acc[j], 0, 0, 0);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][2]), bh, acc[j], 0, 0, 0);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bl, acc[j], 0, 0, 0);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), bh, acc[j], 0, 0, 0);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bm, acc[j], 0, 0, 0);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bh, acc[j], 0, 0, 0);
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    wr[d][j][p] = *(const uint4*)(Wp + j * wbs + ((size_t)min(g + D, gl) * 3 + p) * 512);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-#pragma unroll
-    for (int d = 0; d < D - 1; ++d) {
-        if (gb + d < g1) {
-            const bf16x8_t bh = as_bf16x8(n[0]), bm = as_bf16x8(n[1]), bl = as_bf16x8(n[2]);
-            const int gn = min(gb + d + 1, gl);
-#pragma unroll
-            for (int p = 0; p < 3; ++p) n[p] = ap[(size_t)(3 * gn + p) * 64];
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), bm, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][2]), bh, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bl, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), bh, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bm, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bh, acc[j], 0, 0, 0);
-            }
-        }
-    }
-}
-
-// a layer's register tile into the planes block: tile j's registers 8s..8s+7 are exactly group 2(cw0 + j) + s of
-// the lane's row in the x6 k order (the accumulator-as-operand map), so each is one split and 3 b128 stores
-template <int TN>
-DEVI void chain_store_planes(float* sH, const float (&v)[TN * 16], int cw0, int lane) {
-    uint4* dst = (uint4*)sH + lane;
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-            const float* x = v + j * 16 + 8 * s2;
-            bf16x8_t bh, bm, bl;
-            split8(make_float4(x[0], x[1], x[2], x[3]), make_float4(x[4], x[5], x[6], x[7]), bh, bm, bl);
-            const size_t g = 2 * (cw0 + j) + s2;
-            dst[(3 * g + 0) * 64] = as_u4(bh);
-            dst[(3 * g + 1) * 64] = as_u4(bm);
-            dst[(3 * g + 2) * 64] = as_u4(bl);
-        }
 }
 
 // Workgroup barrier for the chain kernels' LDS hand-offs: waits for this wave's LDS traffic only. HIP's
@@ -1414,8 +1276,8 @@ DEVI void chain_store_lds(float* sH, const float (&v)[TN * 16], int cw0, int r, 
 }
 
 // NW = 8 or 16 waves per workgroup (16: 4 waves per SIMD on one 32-row block, TN = M / 512).
-// X6: 0 = f32 MFMA; 1 = x6 with the activations kept fp32 in LDS and split as read; 2 = x6 with the activations as
-// split planes in LDS (one workgroup per CU: 96 KB at M = 512).
+// X6: 0 = f32 MFMA; 1 = x6 with the activations kept fp32 in LDS and split as read (a split-planes form in LDS
+// measured 2-3 % slower and was retired in round 3).
 template <int MODE, int TN, int NW = 8, int D = 4, int D3 = 8, int X6 = 0>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6 == 1 && NW == 8 ? 4 : X6 == 1 && NW == 4 ? 2 : 1))) chain_kernel(const ChainArgs a) {
     constexpr int NTH = 64 * NW;
@@ -1471,26 +1333,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
         const float4 x = q < (a.K1 >> 2)
             ? *(const float4*)(a.X + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.q1 + q) * 128 + (xr & 31) * 4)
             : make_float4(0.f, 0.f, 0.f, 0.f);
-        if constexpr (X6 == 2) {
-            // quad q = 4g + qq: lane half qq & 1, elements 4 (qq >> 1) .. + 3 of the group's slot
-            const int g = q >> 2, qq = q & 3, ln = (qq & 1) * 32 + row, j0 = 4 * (qq >> 1);
-            const float xs[4] = {x.x, x.y, x.z, x.w};
-            unsigned short hb[4], mb[4], lb[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                __bf16 hh, mm, ll;
-                split3_act(xs[e], hh, mm, ll);
-                hb[e] = __builtin_bit_cast(unsigned short, hh);
-                mb[e] = __builtin_bit_cast(unsigned short, mm);
-                lb[e] = __builtin_bit_cast(unsigned short, ll);
-            }
-            unsigned short* d16 = (unsigned short*)sH;
-            *(uint2*)(d16 + ((size_t)(3 * g + 0) * 64 + ln) * 8 + j0) = make_uint2(hb[0] | (hb[1] << 16), hb[2] | (hb[3] << 16));
-            *(uint2*)(d16 + ((size_t)(3 * g + 1) * 64 + ln) * 8 + j0) = make_uint2(mb[0] | (mb[1] << 16), mb[2] | (mb[3] << 16));
-            *(uint2*)(d16 + ((size_t)(3 * g + 2) * 64 + ln) * 8 + j0) = make_uint2(lb[0] | (lb[1] << 16), lb[2] | (lb[3] << 16));
-        } else {
-            ((float4*)sH)[i] = x;
-        }
+        ((float4*)sH)[i] = x;
     }
     const float* b1src = zc ? a.z0c + ((size_t)(m0 / a.z0_G) * 2 + pb) * M : P.b1;
     for (int i = tid; i < M / 4; i += NTH) {
@@ -1537,9 +1380,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    if constexpr (X6 == 2) ring6p_run<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1e, lane);
-    else if constexpr (X6 == 1 && NW == 4 && X6_PIPE) ring6_run_pipe<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1e, r, h);
-    else if constexpr (X6 == 1) ring6_run<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1e, r, h);
+    if constexpr (X6 == 1) ring6_run<TN, D>(acc, wx, sH, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1e, r, h);
     else ring_run<TN, D>(acc, wr, sH, P.W1 + (size_t)cw0 * a.K1 * 32 + lo, (long)a.K1 * 32, 0, g1e, r, h);
     // layer-2 weights in flight during the epilogue
     if constexpr (X6) ring6_fill<TN, D>(wx, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n);
@@ -1561,7 +1402,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
 #pragma unroll
             for (int i = 0; i < TN * 16; ++i) v[i] = elu_f(v[i]);
         }
-        if constexpr (X6 == 2) chain_store_planes<TN>(sH, v, cw0, lane); else chain_store_lds<TN>(sH, v, cw0, r, h);
+        chain_store_lds<TN>(sH, v, cw0, r, h);
     }
     lds_barrier();
 #ifdef TDMPC_STAMPS
@@ -1573,9 +1414,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    if constexpr (X6 == 2) ring6p_run<TN, D>(acc, wx, sH, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n, lane);
-    else if constexpr (X6 == 1 && NW == 4 && X6_PIPE) ring6_run_pipe<TN, D>(acc, wx, sH, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n, r, h);
-    else if constexpr (X6 == 1) ring6_run<TN, D>(acc, wx, sH, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n, r, h);
+    if constexpr (X6 == 1) ring6_run<TN, D>(acc, wx, sH, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n, r, h);
     else ring_run<TN, D>(acc, wr, sH, P.W2 + (size_t)cw0 * M * 32 + lo, (long)M * 32, 0, M >> 3, r, h);
 #ifdef TDMPC_STAMPS
     STAMP(3);
@@ -1645,7 +1484,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
 #pragma unroll
     for (int i = 0; i < TN * 16; ++i) v[i] = elu_f(v[i]);
     lds_barrier();
-    if constexpr (X6 == 2) chain_store_planes<TN>(sH, v, cw0, lane); else chain_store_lds<TN>(sH, v, cw0, r, h);
+    chain_store_lds<TN>(sH, v, cw0, r, h);
     lds_barrier();
 
     // ---- layer 3: [32 x M] . W3^T -> [32 x n3]; partial tiles meet in the activation block after the reads
@@ -1654,9 +1493,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     for (int e = 0; e < 16; ++e) { a3a[0][e] = 0.f; a3b[0][e] = 0.f; }
     if (wave < items) {
         const int blk = wave / ks, kp = wave % ks;
-        if constexpr (X6 == 2)
-            ring6p_run<1, D3>(a3a, w3x, sH, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, lane);
-        else if constexpr (X6 == 1)
+        if constexpr (X6 == 1)
             ring6_run<1, D3>(a3a, w3x, sH, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, r, h);
         else
             ring_run<1, D3>(a3a, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
@@ -1665,10 +1502,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
         const int blk = (wave + NW) / ks, kp = (wave + NW) % ks;
         if constexpr (X6) {
             ring6_fill<1, D3>(w3x, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper);
-            if constexpr (X6 == 2)
-                ring6p_run<1, D3>(a3b, w3x, sH, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, lane);
-            else
-                ring6_run<1, D3>(a3b, w3x, sH, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, r, h);
+            ring6_run<1, D3>(a3b, w3x, sH, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, r, h);
         } else {
             ring_fill<1, D3>(w3r, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper);
             ring_run<1, D3>(a3b, w3r, sH, a.W3 + (size_t)blk * M * 32 + lo, (long)M * 32, kp * gper, (kp + 1) * gper, r, h);
@@ -1753,320 +1587,6 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     STAMP(4);
     STAMP_RECORD();
 #endif
-}
-
-#ifndef CHAIN64_DIAG
-#define CHAIN64_DIAG 0   // diagnostic builds only (tools/gpu/chain64_diag.sh): 1 = hi.hi term only, 2 = no weight refill
-#endif
-// ------------------------------------------------------------------------------------------------ chain64
-// 64-row blocks for the wide x6 launches (TOLD.next and helper.q at >= one workgroup per CU): one 8-wave workgroup
-// per CU carries TWO 32-row tiles through the head, and every 1 KiB weight fragment it streams from L2 feeds both
-// tiles' MFMAs. Why: the x6 products run the bf16 MFMA at 16x the f32 rate, so a 32-row block needs
-// 6 B x 32 cols per 16-deep k group per MFMA pass -- at full MFMA rate 64 B/cycle of weights per CU, the whole L2
-// share of a CU (34.5 TB/s / 256 CUs ~ 62 B/cycle); the 32-row chain kernel sat at ~0.5 MFMA busy behind it.
-// Two tiles per fragment halve that to 32 B/cycle. Wave w owns output columns [64w, 64w + 64) (TN = 2) of the
-// M = 512 layers for both tiles (4 accumulators); the activation block is [2][K/4][32][4] fp32 (128 KB at M = 512),
-// so one workgroup per CU with two waves per SIMD. The math per row is the 32-row x6 kernel's (same k order, same
-// split, same epilogues), so results equal chain_kernel<..., X6 = 1> bitwise row for row.
-template <int TN, int D>
-DEVI void ring6x2_run(floatx16 (&acc)[TN][2], uint4 (&wr)[D][TN][3], const float* sA, long tile_fl,
-                      const unsigned short* Wp, long wbs, int g0, int g1, int r, int h) {
-    const int gl = g1 - 1;
-    const float* ap = sA + (h * 32 + r) * 4;
-    const float* bp = ap + tile_fl;
-    float4 n0 = *(const float4*)(ap + (size_t)g0 * 512), n1 = *(const float4*)(ap + (size_t)g0 * 512 + 256);
-    float4 m0 = *(const float4*)(bp + (size_t)g0 * 512), m1 = *(const float4*)(bp + (size_t)g0 * 512 + 256);
-    int gb = g0;
-    for (; gb < g1; gb += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const int g = gb + d;
-            if (g >= g1) break;
-            const float4 a0 = n0, a1 = n1, b0 = m0, b1 = m1;
-            const size_t gn = (size_t)min(g + 1, gl) * 512;
-            n0 = *(const float4*)(ap + gn);
-            n1 = *(const float4*)(ap + gn + 256);
-            m0 = *(const float4*)(bp + gn);
-            m1 = *(const float4*)(bp + gn + 256);
-            __builtin_amdgcn_sched_barrier(0);
-            bf16x8_t ah, am, al, bh, bm, bl;
-            split8(a0, a1, ah, am, al);
-            split8(b0, b1, bh, bm, bl);
-#if CHAIN64_DIAG == 1
-            // diagnostic: the hi.hi term only (1 MFMA per product instead of 6; results inexact)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), ah, acc[j][0], 0, 0, 0);
-                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bh, acc[j][1], 0, 0, 0);
-            }
-            if (0)
-#endif
-            {
-            // small terms first, the hi.hi term last (x6_group's order), both tiles per weight fragment
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), am, acc[j][0], 0, 0, 0);
-                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), bm, acc[j][1], 0, 0, 0);
-            }
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][2]), ah, acc[j][0], 0, 0, 0);
-                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][2]), bh, acc[j][1], 0, 0, 0);
-            }
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), al, acc[j][0], 0, 0, 0);
-                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bl, acc[j][1], 0, 0, 0);
-            }
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), ah, acc[j][0], 0, 0, 0);
-                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][1]), bh, acc[j][1], 0, 0, 0);
-            }
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), am, acc[j][0], 0, 0, 0);
-                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bm, acc[j][1], 0, 0, 0);
-            }
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), ah, acc[j][0], 0, 0, 0);
-                acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wr[d][j][0]), bh, acc[j][1], 0, 0, 0);
-            }
-            }
-            // refill this slot D groups ahead (past the end: the last group again, never used)
-#if CHAIN64_DIAG != 2   // diagnostic 2: no refill (the first D groups' weights reused; results inexact)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    wr[d][j][p] = *(const uint4*)(Wp + j * wbs + ((size_t)min(g + D, gl) * 3 + p) * 512);
-#endif
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-}
-
-template <int TN>
-DEVI void zero_acc2(floatx16 (&acc)[TN][2]) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[j][t][e] = 0.f;
-}
-
-// per-tile copies of the chain helpers' register tile
-template <int TN>
-DEVI void take_tile(floatx16 (&dst)[TN], const floatx16 (&acc)[TN][2], int t) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) dst[j] = acc[j][t];
-}
-
-template <int MODE, int D = 2, int D3 = 2>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) chain64_kernel(const ChainArgs a) {
-    constexpr int NW = 8, NTH = 512, TN = 2;
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-    const int pb = blockIdx.y;
-    const ChainProb& P = a.p[pb];
-    const int M = a.M;
-    const int m0 = blockIdx.x * 64;
-    float* sH = smem;                       // activation block [2 tiles][max(K1, M)/4][32][4]
-    const long tfl = a.hfl / 2;             // floats per tile
-    float* red0 = smem + a.hfl;             // [NW][64]
-    float* red1 = red0 + 64 * NW;           // [NW][64]
-    float* sp = red1 + 64 * NW;             // parameter vectors (chain_param_floats)
-    float* sb1 = sp;
-    float* sb2 = sp + M;
-    float* sw3 = sp + 2 * M;
-    float* sb3 = sp + 3 * M;
-    float* sg1 = sp + 3 * M;
-    float* sbe1 = sp + 4 * M;
-    float* sg2 = sp + 5 * M;
-    float* sbe2 = sp + 6 * M;
-    const int g1n = (int)(rup(a.K1, 16) >> 4), g2n = M >> 4;
-    const long wb1 = (long)g1n * 1536, wb2 = (long)g2n * 1536;
-    const int cw0 = wave * TN;
-    const bool head_dot = MODE == CH_Q || (MODE == CH_STEP && pb == 1);
-
-    uint4 wx[D][TN][3];
-    ring6_fill<TN, D>(wx, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n);
-    // input rows: both tiles, K1 rounded to 16 with zero quads (64 consecutive threads = 32 rows of a quad x 2 tiles)
-    const int q1n = g1n * 4;
-    for (int i = tid; i < q1n * 64; i += NTH) {
-        const int rr = i & 31, t = (i >> 5) & 1, q = i >> 6;
-        const int lm = m0 + t * 32 + rr;
-        const int xr = map_row(a.amap, lm < a.rows ? lm : 0);
-        const float4 x = q < (a.K1 >> 2)
-            ? *(const float4*)(a.X + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.q1 + q) * 128 + (xr & 31) * 4)
-            : make_float4(0.f, 0.f, 0.f, 0.f);
-        *(float4*)(sH + t * tfl + (q * 32 + rr) * 4) = x;
-    }
-    for (int i = tid; i < M / 4; i += NTH) {
-        ((float4*)sb1)[i] = ((const float4*)P.b1)[i];
-        ((float4*)sb2)[i] = ((const float4*)P.b2)[i];
-        if (head_dot) ((float4*)sw3)[i] = ((const float4*)P.w3v)[i];
-        if (MODE == CH_Q) {
-            ((float4*)sg1)[i] = ((const float4*)P.g1)[i];
-            ((float4*)sbe1)[i] = ((const float4*)P.be1)[i];
-            ((float4*)sg2)[i] = ((const float4*)P.g2)[i];
-            ((float4*)sbe2)[i] = ((const float4*)P.be2)[i];
-        }
-    }
-    if (!head_dot)
-        for (int i = tid; i < a.n3 / 4; i += NTH) ((float4*)sb3)[i] = ((const float4*)a.b3)[i];
-    float g_old = 0.f;   // the running return of this thread's row (reward workgroups, tid < 64)
-    if (MODE == CH_STEP && pb == 1 && tid < 64 && !a.first && m0 + tid < a.rows)
-        g_old = a.G[map_row(a.amap, m0 + tid)];
-    lds_barrier();
-
-    // ---- layer 1
-    floatx16 acc[TN][2];
-    zero_acc2<TN>(acc);
-    ring6x2_run<TN, D>(acc, wx, sH, tfl, P.X1 + (size_t)cw0 * wb1 + lane * 8, wb1, 0, g1n, r, h);
-    ring6_fill<TN, D>(wx, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n);
-    lds_barrier();   // every wave is done with the input tiles: sH becomes h1
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        floatx16 at[TN];
-        take_tile<TN>(at, acc, t);
-        float v[TN * 16];
-        chain_bias<TN>(v, at, sb1, cw0, h);
-        if (MODE == CH_Q) {
-            float mean, rs;
-            chain_row_moments<TN, NW>(v, red0 + t * 32 * NW, red1 + t * 32 * NW, wave, r, h, M, mean, rs);
-            chain_ln<TN>(v, rs, -rs * mean, sg1, sbe1, cw0, h);
-#pragma unroll
-            for (int i = 0; i < TN * 16; ++i) v[i] = tanh_f(v[i]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < TN * 16; ++i) v[i] = elu_f(v[i]);
-        }
-        chain_store_lds<TN>(sH + t * tfl, v, cw0, r, h);
-    }
-    lds_barrier();
-
-    // ---- layer 2
-    zero_acc2<TN>(acc);
-    ring6x2_run<TN, D>(acc, wx, sH, tfl, P.X2 + (size_t)cw0 * wb2 + lane * 8, wb2, 0, g2n, r, h);
-    const int nb3 = a.n3 >> 5;
-    const int ks = nb3 >= NW ? 1 : NW / nb3;
-    const int items = nb3 * ks;
-    const int gper = g2n / ks;
-    uint4 w3x[D3][1][3];
-    if (!head_dot && wave < items)
-        ring6_fill<1, D3>(w3x, a.X3 + (size_t)(wave / ks) * wb2 + lane * 8, wb2, (wave % ks) * gper, (wave % ks + 1) * gper);
-    if (head_dot) {
-        float s[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            floatx16 at[TN];
-            take_tile<TN>(at, acc, t);
-            float v[TN * 16];
-            chain_bias<TN>(v, at, sb2, cw0, h);
-            if (MODE == CH_Q) {
-                float mean, rs;
-                chain_row_moments<TN, NW>(v, red0 + t * 32 * NW, red1 + t * 32 * NW, wave, r, h, M, mean, rs);
-                chain_ln<TN>(v, rs, -rs * mean, sg2, sbe2, cw0, h);
-            }
-            float d = 0.f;
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 w4 = *(const float4*)(sw3 + (cw0 + j) * 32 + 8 * q + 4 * h);
-                    const float* x = v + j * 16 + 4 * q;
-                    d += (elu_f(x[0]) * w4.x + elu_f(x[1]) * w4.y) + (elu_f(x[2]) * w4.z + elu_f(x[3]) * w4.w);
-                }
-            s[t] = d + __shfl_xor(d, 32);
-        }
-        lds_barrier();   // red0 is free again (the LayerNorm moments are read)
-        if (h == 0) {
-            red0[wave * 64 + r] = s[0];
-            red0[wave * 64 + 32 + r] = s[1];
-        }
-        lds_barrier();
-        if (tid < 64) {
-            const int lm = m0 + tid;
-            if (lm < a.rows) {
-                const int xr = map_row(a.amap, lm);
-                float tot = 0.f;
-#pragma unroll
-                for (int w = 0; w < NW; ++w) tot += red0[w * 64 + tid];
-                const float o = tot + P.b3v[0];
-                if (MODE == CH_Q) {
-                    a.q[(size_t)pb * a.q_ld + xr] = o;
-                } else {
-                    const float dr = fmul(a.disc, o);
-                    a.G[xr] = a.first ? dr : fadd(g_old, dr);
-                    if (a.last) a.rlast[xr] = o;
-                }
-            }
-        }
-        return;
-    }
-    // dynamics: h2 = ELU(y2) into the activation block once every wave is done reading h1
-    {
-        float v0[TN * 16], v1[TN * 16];
-        floatx16 at[TN];
-        take_tile<TN>(at, acc, 0);
-        chain_bias<TN>(v0, at, sb2, cw0, h);
-        take_tile<TN>(at, acc, 1);
-        chain_bias<TN>(v1, at, sb2, cw0, h);
-#pragma unroll
-        for (int i = 0; i < TN * 16; ++i) { v0[i] = elu_f(v0[i]); v1[i] = elu_f(v1[i]); }
-        lds_barrier();
-        chain_store_lds<TN>(sH, v0, cw0, r, h);
-        chain_store_lds<TN>(sH + tfl, v1, cw0, r, h);
-    }
-    lds_barrier();
-
-    // ---- layer 3: [64 x M] . W3^T -> [64 x n3]; items = (32-column block, K part), both tiles each
-    floatx16 p3[2][1][2];
-    int nit = 0;
-    for (int it = wave; it < items && nit < 2; it += NW, ++nit) {
-        const int blk = it / ks, kp = it % ks;
-        if (nit > 0)
-            ring6_fill<1, D3>(w3x, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper);
-        floatx16 a3[1][2];
-        zero_acc2<1>(a3);
-        ring6x2_run<1, D3>(a3, w3x, sH, tfl, a.X3 + (size_t)blk * wb2 + lane * 8, wb2, kp * gper, (kp + 1) * gper, r, h);
-        p3[nit][0][0] = a3[0][0];
-        p3[nit][0][1] = a3[0][1];
-    }
-    lds_barrier();   // partial tiles overwrite h2: item it, tile t at sH + (it * 2 + t) * 1024
-    for (int k = 0; k < nit; ++k) {
-        const int it = wave + k * NW;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                *(float4*)(sH + (size_t)(it * 2 + t) * 1024 + ((2 * q + h) * 32 + r) * 4) =
-                    make_float4(p3[k][0][t][4 * q], p3[k][0][t][4 * q + 1], p3[k][0][t][4 * q + 2], p3[k][0][t][4 * q + 3]);
-    }
-    lds_barrier();
-    for (int i = tid; i < (a.nstore >> 2) * 64; i += NTH) {
-        const int rr = i & 31, t = (i >> 5) & 1, cq = i >> 6;
-        const int lm = m0 + t * 32 + rr;
-        if (lm >= a.rows) continue;
-        const int blk = cq >> 3, qi = cq & 7;
-        float4 sv = *(const float4*)(sH + (size_t)(blk * ks * 2 + t) * 1024 + (qi * 32 + rr) * 4);
-        for (int kp = 1; kp < ks; ++kp) {
-            const float4 u = *(const float4*)(sH + (size_t)((blk * ks + kp) * 2 + t) * 1024 + (qi * 32 + rr) * 4);
-            sv.x += u.x; sv.y += u.y; sv.z += u.z; sv.w += u.w;
-        }
-        const int c = 4 * cq;
-        const float4 bb = *(const float4*)(sb3 + c);
-        float o[4] = {sv.x + bb.x, sv.y + bb.y, sv.z + bb.z, sv.w + bb.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (c + k >= a.nvalid) o[k] = 0.f;
-        const int xr = map_row(a.amap, lm);
-        *(float4*)(a.Xo + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.out_q0 + cq) * 128 + (xr & 31) * 4) =
-            make_float4(o[0], o[1], o[2], o[3]);
-    }
 }
 
 // ------------------------------------------------------------------------------------------------ chain16
@@ -2164,20 +1684,19 @@ DEVI void ring16x6_fill(uint4 (&wr)[D][NT][3], const unsigned short* Wb, int nf0
 
 template <int NT>
 DEVI void x6_group16(floatx4 (&acc)[NT], const uint4 (&w)[NT][3], const float4& a0, const float4& a1) {
-    bf16x8_t bh, bm, bl;
-    split8(a0, a1, bh, bm, bl);
+    const X6B b = split8(a0, a1);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][1]), bm, acc[j], 0, 0, 0);
+    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][1]), b.m, acc[j], 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][2]), bh, acc[j], 0, 0, 0);
+    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][2]), b.s, acc[j], 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][0]), bl, acc[j], 0, 0, 0);
+    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][0]), b.l, acc[j], 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][1]), bh, acc[j], 0, 0, 0);
+    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][1]), b.s, acc[j], 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][0]), bm, acc[j], 0, 0, 0);
+    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][0]), b.m, acc[j], 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][0]), bh, acc[j], 0, 0, 0);
+    for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][0]), b.h, acc[j], 0, 0, 0);
 }
 
 // acc[j] += W(tile j) . A over 32-k groups [g0, g1); A = the fp32 16-row LDS block (group G at sA + G * 512)
@@ -3597,13 +3116,10 @@ int init_attrs() {
     CHAIN_ATTR(CH_Q, 1) CHAIN_ATTR(CH_Q, 2) CHAIN_ATTR(CH_Q, 4)
 #undef CHAIN_ATTR
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 2, 8, 2, X6_D3, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 2, 8, 4, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 4, 4, 2, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 2, 8, 2, X6_D3, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 2, 8, 4, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 4, 4, 2, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 2, 8, 2, X6_D3, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 2, 8, 4, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_Q, 4, 4, 2, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_STEP, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain_kernel<CH_PI, 1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -3616,12 +3132,6 @@ int init_attrs() {
     HIPCHK(hipFuncSetAttribute((const void*)chain16_kernel<CH_PI, 4, 4, 4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)chain16_kernel<CH_Q, 4, 4, 4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 #undef CHAIN16_ATTR
-#define C64_ATTR(MODE, D, D3) \
-    HIPCHK(hipFuncSetAttribute((const void*)chain64_kernel<MODE, D, D3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-#define C64_ATTRS(MODE) C64_ATTR(MODE, 2, 2)
-    C64_ATTRS(CH_STEP) C64_ATTRS(CH_Q)
-#undef C64_ATTRS
-#undef C64_ATTR
     if (rc) return TDMPC_E_HIP;
     done = 1;
     return 0;
@@ -3889,7 +3399,7 @@ int chain_xcd() {
 int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
     if (a0.rows <= 0) return 0;
     ChainArgs a = a0;
-    if (a.rb != 32) a.z0c = nullptr;   // (chain16 / chain64 run the full first layer)
+    if (a.rb != 32) a.z0c = nullptr;   // (chain16 runs the full first layer)
     const int nw = a.rb == 16 ? 8 : a.nw;
     const size_t lds = ((size_t)a.hfl + (a.rb == 16 ? 256 : 64 * nw) + chain_param_floats(mode, a.M, a.n3)) * 4;
     const int nblk = (a.rows + a.rb - 1) / a.rb;
@@ -3908,22 +3418,6 @@ int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
     const bool prof = pf.armed && pf.cfg == 4 + mode && pf.n + 2 <= pf.cap && (pf.rows == 0 || a.rows == pf.rows) &&
                       a.z0c == nullptr;
     if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], s));
-    if (a.rb == 64) {
-        const size_t lds64 = ((size_t)a.hfl + 2 * 64 * 8 + chain_param_floats(mode, a.M, a.n3)) * 4;
-        const dim3 g64((a.rows + 63) / 64, nprob);
-        a.il = 0;
-        // (weight-ring depths D / D3 of 3-4 / 6 measured 1-3 % slower than 2 / 2 on MI355X)
-        if (mode == CH_STEP) hipLaunchKernelGGL((chain64_kernel<CH_STEP, 2, 2>), g64, dim3(512), lds64, s, a);
-        else if (mode == CH_Q) hipLaunchKernelGGL((chain64_kernel<CH_Q, 2, 2>), g64, dim3(512), lds64, s, a);
-        else { snprintf(g_err, sizeof g_err, "chain64: unsupported mode %d", mode); return TDMPC_E_DIMS; }
-        HIPCHK(hipGetLastError());
-        if (prof) {
-            HIPCHK(hipEventRecord(pf.ev[pf.n + 1], s));
-            pf.n += 2;
-            pf.flops += 2.0 * a.rows * chain_macs_per_row(mode, a, nprob);
-        }
-        return 0;
-    }
     if (a.rb == 16) {
         const int nt = a.M / 128;
 #define CHAIN16_LAUNCH(MODE, NT) \
@@ -3947,7 +3441,6 @@ int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
 #define CHAIN_LAUNCH(MODE, TN) \
     if (mode == MODE && tn == TN) { \
         if (a.x6 == 3 && TN == 4 && nw == 4) hipLaunchKernelGGL((chain_kernel<MODE, 4, 4, 2, 2, 1>), grid, block, lds, s, a); \
-        else if (a.x6 == 2 && TN == 2) hipLaunchKernelGGL((chain_kernel<MODE, 2, 8, 4, 4, 2>), grid, block, lds, s, a); \
         else if (a.x6 && TN == 2) hipLaunchKernelGGL((chain_kernel<MODE, 2, 8, 2, X6_D3, 1>), grid, block, lds, s, a); \
         else if (nw == 16 && TN == 1) hipLaunchKernelGGL((chain_kernel<MODE, 1, 16>), grid, block, lds, s, a); \
         else hipLaunchKernelGGL((chain_kernel<MODE, TN>), grid, block, lds, s, a); \
@@ -4040,8 +3533,8 @@ int chain_nw() {
 // forced by TDMPC_PATH_CHAIN_X6, the default of the auto / chain paths (TDMPC_X6=0 turns it off there); the
 // chain32 / chain16 paths keep the exact f32 MFMA. M = 512 only (the one instantiated width). Measured on MI355X
 // (humanoid-run, round-1 run): 8.89 -> 6.52 ms per B = 32 plan, 3.03 -> 2.19 ms at B = 8.
-// Returns the x6 mode of a chain launch (0 = f32 MFMA; 1 = 8-wave workgroups, activations split as read; 2 = split
-// planes in LDS; 3 = mode 1 on 4-wave workgroups of 128 columns per wave, the default: the per-wave split serves
+// Returns the x6 mode of a chain launch (0 = f32 MFMA; 1 = 8-wave workgroups, activations split as read; 3 = mode 1
+// on 4-wave workgroups of 128 columns per wave, the default: the per-wave split serves
 // twice the MFMAs -- measured 6.37 vs 6.60 ms per B = 32 plan, 2.23 vs 2.28 at B = 8, round-1 run). TDMPC_X6
 // picks the mode, 0 turns x6 off on the auto / chain paths.
 int use_x6(const Ctx& c) {
@@ -4051,7 +3544,8 @@ int use_x6(const Ctx& c) {
         const char* e = getenv("TDMPC_X6");
         en = e ? atoi(e) : 3;
     }
-    if (c.path == TDMPC_PATH_CHAIN_X6) return en >= 1 && en <= 3 ? en : 3;
+    if (en == 2) en = 3;   // (mode 2, the split planes in LDS, retired)
+    if (c.path == TDMPC_PATH_CHAIN_X6) return en == 1 || en == 3 ? en : 3;
     if (c.path == TDMPC_PATH_SPLIT_X6) return 1;
     return (c.path == TDMPC_PATH_AUTO || c.path == TDMPC_PATH_CHAIN) ? en : 0;
 }
@@ -4073,29 +3567,6 @@ int chain_rb(const Ctx& c, int rows, int nprob) {
     return (rows + 31) / 32 * nprob > num_cus() / 2 ? 32 : 16;
 }
 
-// 64-row x6 blocks (chain64_kernel) for TOLD.next / helper.q launches wide enough to give every CU a workgroup:
-// TDMPC_CHAIN64=1 on the auto / chain paths, every such launch on TDMPC_PATH_CHAIN64 (parity tests). Off by default:
-// measured on MI355X (humanoid-run B = 32, rocprofv3): step 137.1 vs 136.9 us, Q 181.8 vs 180.2 us for the 32-row x6
-// kernel. In the M x M loop alone the 64-row form is faster (0.66-0.70 vs 0.55-0.60 MFMA busy,
-// tools/mb/x6_stream.hip: the CUs' vector-memory path carries the weight stream), but its 128 KB activation block
-// allows one workgroup per CU, and the staging / layer-1 / layer-3 / epilogue phases it can no longer overlap with a
-// co-resident workgroup eat the gain.
-void maybe_rb64(const Ctx& c, ChainArgs& a, int mode, int nprob) {
-    static int en = -1;
-    if (en < 0) {
-        const char* e = getenv("TDMPC_CHAIN64");
-        en = e ? atoi(e) : 0;
-    }
-    if (c.w.M != 512 || (mode != CH_STEP && mode != CH_Q)) return;
-    const bool forced = c.path == TDMPC_PATH_CHAIN64;
-    if (!forced && (!en || !a.x6 || a.rb != 32 || (c.path != TDMPC_PATH_AUTO && c.path != TDMPC_PATH_CHAIN) ||
-                    (a.rows + 63) / 64 * nprob < num_cus()))
-        return;
-    const int hfl = std::max((int)rup(c.Kx, 32), c.M) * 64;
-    if (((size_t)hfl + 2 * 64 * 8 + chain_param_floats(mode, c.M, a.n3)) * 4 > 160 * 1024) return;
-    a.rb = 64; a.nw = 8; a.x6 = 1; a.hfl = hfl;
-}
-
 ChainArgs chain0(const Ctx& c, int rows, RowMap map, int t, int K1, int q1, int nprob) {
     ChainArgs a;
     memset(&a, 0, sizeof a);
@@ -4108,8 +3579,8 @@ ChainArgs chain0(const Ctx& c, int rows, RowMap map, int t, int K1, int q1, int 
     // (at most four per wave) Lr, Ar <= 512; otherwise mode 1
     if (a.x6 == 3 && (c.w.Ap / 4 * 32 > 512 || std::max(c.w.Lr, c.w.Ar) > 4 * 4 * 32)) a.x6 = 1;
     a.nw = a.x6 == 3 ? 4 : a.rb == 32 && !a.x6 && chain_nw() == 16 && chain_nw16_ok(c.w) ? 16 : 8;
-    // activation block: fp32 [K/4][rb][4], or for x6 mode 2 the split planes (6 bytes per value)
-    a.hfl = std::max((int)rup(c.Kx, 32), c.M) * (a.x6 == 2 ? 48 : a.rb);
+    // activation block: fp32 [K/4][rb][4]
+    a.hfl = std::max((int)rup(c.Kx, 32), c.M) * a.rb;
     a.X = Xt(c, t); a.x_ts = (long)c.Kx * 32;
     return a;
 }
@@ -4216,12 +3687,6 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         a.Xo = Xt(c, t + 1); a.out_q0 = w.Ap / 4;
         a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
         if (t == 0 && c.z0c_ready && map.G % 32 == 0) { a.z0c = c.k.z0c; a.z0_G = map.G; a.k1c = z0c_k1c(c); }
-        maybe_rb64(c, a, CH_STEP, 2);
-        if (a.rb == 64) {
-            const size_t rb1 = (size_t)(M / 32) * (rup(c.Kx, 16) / 16) * 1536;
-            d.X1 = x6p(c, X6_W1X); r.X1 = x6p(c, X6_W1X) + rb1;
-            d.X2 = x6p(c, X6_W2D); r.X2 = x6p(c, X6_W2R); a.X3 = x6p(c, X6_W3D);
-        }
         return launch_chain(CH_STEP, a, 2, c.s);
     }
     if (use_split(c, rows)) {
@@ -4432,12 +3897,6 @@ int q_chain(const Ctx& c, int rows, RowMap map) {
         }
     }
     a.q = c.k.qv; a.q_ld = c.k.xrows;
-    maybe_rb64(c, a, CH_Q, 2);
-    if (a.rb == 64)
-        for (int q = 0; q < 2; ++q) {
-            a.p[q].X1 = x6p(c, X6_WQ1X) + (size_t)q * (M / 32) * (rup(c.Kx, 16) / 16) * 1536;
-            a.p[q].X2 = x6p(c, X6_WQ2) + (size_t)q * (M / 32) * (M / 16) * 1536;
-        }
     return launch_chain(CH_Q, a, 2, c.s);
 }
 
@@ -4574,6 +4033,23 @@ unsigned long long* g_p1_stamps = nullptr;   // tdmpc_debug_plan1_stamps (diagno
 // TDMPC_PATH_PERSIST, when the shape fits, batch 1, >= 256 CUs (every workgroup of its 256-block grid must be
 // resident). Measured on MI355X (humanoid-run, one env, same box, alternating): 1.083-1.087 vs 1.142-1.144 ms per
 // plan_batch call, 1.185-1.198 vs 1.237-1.251 ms per literal plan() -- see DESIGN.md §4 for its per-phase timeline.
+// Can every workgroup of plan1's 256-block grid be resident at once (one per CU: its LDS and registers)? Its hand-offs
+// assume so; the occupancy query is checked once per LDS size, and a grid that does not fit takes the launch chain.
+bool plan1_resident(const Ctx& c) {
+    static size_t ok_lds[2] = {0, 0}, bad_lds[2] = {0, 0};
+    const int ks = p1_ks(c.w) == 4 ? 0 : 1;
+    const size_t lds = p1_lds_bytes(c.H, c.d->num_elites, c.w.A, c.T);
+    if (ok_lds[ks] == lds) return true;
+    if (bad_lds[ks] == lds) return false;
+    int per_cu = 0;
+    const hipError_t e = ks == 0
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, plan1_kernel<4>, P1_NT, lds)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, plan1_kernel<6>, P1_NT, lds);
+    const bool ok = e == hipSuccess && (long)per_cu * num_cus() >= P1_NG * P1_WPG;
+    (ok ? ok_lds : bad_lds)[ks] = lds;
+    return ok;
+}
+
 bool use_plan1(const Ctx& c) {
     static int en = -1;
     if (en < 0) {
@@ -4581,7 +4057,7 @@ bool use_plan1(const Ctx& c) {
         en = e ? atoi(e) : 1;
     }
     if (c.path != TDMPC_PATH_PERSIST && (c.path != TDMPC_PATH_AUTO || !en)) return false;
-    return c.B == 1 && c.k.p1 && num_cus() >= P1_NG * P1_WPG && c.H <= 16;
+    return c.B == 1 && c.k.p1 && num_cus() >= P1_NG * P1_WPG && c.H <= 16 && plan1_resident(c);
 }
 
 // encode_kernel has written z0 and the initial mean / std; one memset node (the hand-off counters) + one launch.
@@ -4612,6 +4088,11 @@ int plan1_launch(const Ctx& c, const tdmpc_plan_params* prm, const float* noise,
     a.o_sync = rg.o_sync; a.o_xb = rg.o_xb; a.o_h1 = rg.o_h1; a.o_zp = rg.o_zp; a.o_rp = rg.o_rp; a.o_pp = rg.o_pp;
     a.o_qm = rg.o_qm; a.o_qp = rg.o_qp; a.o_val = rg.o_val; a.o_rl = rg.o_rl; a.o_mu = rg.o_mu; a.pi_cache = pi_cache_on(); a.xb_t = rg.xb_t; a.xb_g = rg.xb_g;
     a.stamps = g_p1_stamps;
+    a.status = prm->status;
+    {
+        const char* e = getenv("TDMPC_P1_DEBUG_SKIP");   // test knob, read per launch (captured with the graph)
+        a.debug_skip = e && atoi(e) ? 1 : 0;
+    }
     HIPCHK(hipMemsetAsync(c.k.p1 + rg.o_sync, 0, P1_NG * 256 + 256, c.s));   // counters + error word
     const size_t lds = p1_lds_bytes(c.H, a.K, w.A, c.T);
     if (p1_ks(w) == 4) hipLaunchKernelGGL(plan1_kernel<4>, dim3(P1_NG * P1_WPG), dim3(P1_NT), lds, c.s, a);
@@ -4935,7 +4416,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     const int H = prm->horizon, I = prm->iterations, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream))) return rc;
     if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
-    c.path = prm->path;
+    c.path = prm->path == TDMPC_PATH_CHAIN64 ? TDMPC_PATH_CHAIN_X6 : prm->path;   // (64-row blocks retired: path 6)
     const int N = c.N, P = c.P, T = c.T;
     // TDMPC_PATH_PERSIST: the persistent plan where it applies (one env, supported shape), the auto path elsewhere
     if (c.path == TDMPC_PATH_PERSIST && !use_plan1(c)) c.path = TDMPC_PATH_AUTO;
@@ -5038,7 +4519,8 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
     if (I <= 0 || I > 16) { snprintf(g_err, sizeof g_err, "iCEM: 1..16 iterations"); return TDMPC_E_DIMS; }
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream, K))) return rc;
     if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
-    c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path;   // (persist: whole plans only)
+    c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path == TDMPC_PATH_CHAIN64 ? TDMPC_PATH_CHAIN_X6
+           : prm->path;   // (persist: whole plans only; the retired 64-row path is path 6)
     const int N = d->num_samples, Pmax = d->num_pi, Tw = N + K + Pmax, pi_base = N + K, P0 = prm->n_pi0;
     c.T = Tw;
     if (P0 <= 0 || P0 > Pmax || prm->n_samples[0] != N) { snprintf(g_err, sizeof g_err, "iCEM: bad counts"); return TDMPC_E_DIMS; }
@@ -5136,7 +4618,8 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
     if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
-    c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path;   // (persist: whole plans only)
+    c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path == TDMPC_PATH_CHAIN64 ? TDMPC_PATH_CHAIN_X6
+           : prm->path;   // (persist: whole plans only; the retired 64-row path is path 6)
     if (rows != c.T) { snprintf(g_err, sizeof g_err, "rows must equal N+P"); return TDMPC_E_DIMS; }
     const int T = c.T, L = c.w.L;
     HIPCHK(hipMemsetAsync(c.k.z0, 0, (size_t)B * c.w.Lp * 4, c.s));
@@ -5181,7 +4664,8 @@ int tdmpc_pi_rollout(const tdmpc_dims* d, const tdmpc_plan_params* prm, const vo
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
     if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
-    c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path;   // (persist: whole plans only)
+    c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path == TDMPC_PATH_CHAIN64 ? TDMPC_PATH_CHAIN_X6
+           : prm->path;   // (persist: whole plans only; the retired 64-row path is path 6)
     const int N = c.N, P = c.P, T = c.T;
     const long A = c.A;
     if (P <= 0) { snprintf(g_err, sizeof g_err, "num_pi is 0"); return TDMPC_E_DIMS; }
@@ -5210,7 +4694,8 @@ int tdmpc_cem_iter(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
     if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
-    c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path;   // (persist: whole plans only)
+    c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path == TDMPC_PATH_CHAIN64 ? TDMPC_PATH_CHAIN_X6
+           : prm->path;   // (persist: whole plans only; the retired 64-row path is path 6)
     const int N = c.N, P = c.P, T = c.T, A = c.A, HA = H * A;
     if (P > 0 && !pi_actions) return TDMPC_E_NULL;
     // the caller's mean/std [B][H][A] -> the workspace's [B][Hmax][A]

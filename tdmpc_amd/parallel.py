@@ -70,16 +70,32 @@ class EnvShardedPlanner:
         self._local[:, :self.A].copy_(a)
         self._local[:, self.A:].copy_(m)
         if self.world > 1:
-            dist.all_gather_into_tensor(self._all, self._local, group=self.group)
+            self._all_gather()
             res = self._all
         else:
             res = self._local
         return res[:, :self.A], res[:, self.A:]
+
+    def _all_gather(self):
+        """RCCL ("nccl") gathers the device tensors directly over xGMI. The gloo transport (ranks sharing one GPU, or
+        a host without peer access: the world-2 tests) moves host copies; the gathered values are the same bytes."""
+        if self._local.is_cuda and dist.get_backend(self.group) == "gloo":
+            host_all = torch.empty(self._all.shape, dtype=self._all.dtype)
+            dist.all_gather_into_tensor(host_all, self._local.cpu(), group=self.group)
+            self._all.copy_(host_all)
+        else:
+            dist.all_gather_into_tensor(self._all, self._local, group=self.group)
 
     @torch.no_grad()
     def broadcast_weights(self, model: torch.nn.Module, src: int = 0):
         """Make every rank's TOLD replica equal to rank `src`'s (after a checkpoint load or an update)."""
         if self.world == 1:
             return
+        gloo = dist.get_backend(self.group) == "gloo"
         for p in model.state_dict().values():
-            dist.broadcast(p, src=src, group=self.group)
+            if gloo and p.is_cuda:
+                h = p.cpu()
+                dist.broadcast(h, src=src, group=self.group)
+                p.copy_(h)
+            else:
+                dist.broadcast(p, src=src, group=self.group)

@@ -16,6 +16,7 @@ numpy's. Pass `u=` to `sample` to supply it (parity tests).
 from __future__ import annotations
 
 import ctypes as C
+import warnings
 from copy import deepcopy
 
 import torch
@@ -132,6 +133,7 @@ class ReplayBuffer:
             C.c_void_p(self._n_used.data_ptr()), C.c_void_p(self._ws.data_ptr()), self._ws.numel(),
             self._stream()), "tdmpc_replay_sample")
         self._u_keep = u   # the kernels read it asynchronously
+        self._n_u_last = u.numel()
         self.last_probs = probs
         return (self._out_obs, self._out_next, self._out_action, self._out_reward.unsqueeze(2), self._out_idx,
                 self._out_w)
@@ -144,6 +146,14 @@ class ReplayBuffer:
 
     def check_sample(self):
         """Raise like the reference's np.random.choice(replace=False) when the last sample could not find
-        batch_size distinct non-zero-probability transitions (device flag; synchronises)."""
-        if self.uniforms_used == -2:
+        batch_size distinct non-zero-probability transitions (device flag; synchronises). Warn when numpy's
+        rounds needed more uniforms than were supplied: the kernel then continued on its own hash stream, so
+        the draw is still a valid without-replacement sample but no longer numpy's for the supplied stream."""
+        used = self.uniforms_used
+        if used == -2:
             raise ValueError("Fewer non-zero entries in p than size")
+        n_u = getattr(self, "_n_u_last", None)
+        if n_u is not None and used > n_u:
+            warnings.warn(f"replay sample consumed {used} uniforms, {n_u} supplied: the rounds past the supplied "
+                          "stream used the kernel's hash stream (not numpy's draw for this stream)", RuntimeWarning)
+        return used

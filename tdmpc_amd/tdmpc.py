@@ -106,6 +106,8 @@ class HipPlanner:
         # of self.std over std_schedule and every per-env t0 pattern
         self.std_dev = torch.zeros(1, dtype=torch.float32, device=dev)
         self.warm_dev = torch.zeros(max_batch, dtype=torch.int32, device=dev)
+        # sticky device status word (tdmpc_plan_params.status): nonzero after a plan that failed on the device
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self._std_host = None
         self._warm_host = None
         # per-call inputs, staged on the host and sent up as ONE copy: the observations, numpy's elite-choice
@@ -135,6 +137,7 @@ class HipPlanner:
         self._graphs = {}
         # the metrics come down through pinned memory too (a pageable copy blocks the host)
         self._pin_met = torch.zeros(max_batch, 2, dtype=torch.float32, pin_memory=pin)
+        self._pin_status = torch.zeros(1, dtype=torch.int32, pin_memory=pin)
         self._h2d_done = torch.cuda.Event() if pin else None
         # reference-order draws: "device" = one tdmpc_reference_normals launch per call, "torch" = the
         # reference's own normal_ launches (18 per env at humanoid sizes); equal bitwise
@@ -293,7 +296,20 @@ class HipPlanner:
         """Point prm at the device-resident std floor and warm flags (set_call_state)."""
         prm.std_floor_dev = self.std_dev.data_ptr()
         prm.warm_flags = self.warm_dev.data_ptr()
+        prm.status = self.status.data_ptr()
         return prm
+
+    def raise_status(self, st: int):
+        """Raise for a nonzero device status (and clear it): the plan's outputs are NaN, never return them."""
+        if st:
+            self.status.zero_()
+            raise RuntimeError(f"tdmpc_plan failed on the device (status {st}: the persistent one-env plan timed out "
+                               "at a hand-off -- not every workgroup of its grid was resident). Its action is NaN; "
+                               "set TDMPC_PERSIST=0 to plan on the launch chain instead.")
+
+    def check_status(self):
+        """Synchronising check of the sticky status word (for callers that plan with sync_metrics=False)."""
+        self.raise_status(int(self.status.item()))
 
     def launch(self, prm, obs_is_u8: bool, trace: dict | None = None):
         L = self.L
@@ -460,7 +476,10 @@ class TDMPC:
 
     def update_pi(self, zs):
         """tdmpc.py:165-182."""
-        return float(self.learner().update_pi(zs))
+        loss = float(self.learner().update_pi(zs))
+        # the engine writes the policy weights in place (no tensor version bump): repack before the next plan
+        self.planner._packed_key = None
+        return loss
 
     def _td_target(self, next_obs, reward):
         """tdmpc.py:184-190."""
@@ -583,8 +602,12 @@ class TDMPC:
             return actions, pl.metrics[:B]
         if pl._h2d_done is not None:
             pl._pin_met[:B].copy_(pl.metrics[:B], non_blocking=True)
+            pl._pin_status.copy_(pl.status, non_blocking=True)
             torch.cuda.current_stream(self.device).synchronize()
             m = pl._pin_met[:B].tolist()
+            st = int(pl._pin_status[0])
         else:
             m = pl.metrics[:B].double().cpu().tolist()
+            st = int(pl.status[0])
+        pl.raise_status(st)
         return actions, [{"external_reward_mean": float(r), "current_std": float(s)} for r, s in m]

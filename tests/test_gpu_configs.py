@@ -32,7 +32,7 @@ CONFIGS = {
     "quadruped-run-pixels": ("quadruped", dict(FULL, modality="pixels")),
     "dog-run": ("dog", dict(FULL)),
 }
-PATHS = ["layered", "chain16", "chain32", "split", "chain_x6", "split_x6", "chain", "chain64", "persist"]
+PATHS = ["layered", "chain16", "chain32", "split", "chain_x6", "split_x6", "chain", "persist"]
 
 
 def _agent(cfg, wseed, B=1, path="auto", **kw):
@@ -171,10 +171,30 @@ def _nf_case(case, sd, z0):
         sd["_Q2.6.bias"][:] = float("-inf")       # +inf + -inf = NaN -> 0
     elif case == "large_finite":
         sd["_reward.4.weight"].mul_(3e37)         # |G| ~ 1e37, finite
+    elif case == "inf_hidden":
+        # an infinite HIDDEN activation: reward unit 5's layer-1 bias is +inf, so h1[5] = ELU(+inf) = +inf
+        # on every row; with W2[:, 5] > 0 every layer-2 unit is +inf and with w3 > 0 the reward is +inf: fp32 gives
+        # G = +inf -> +FLT_MAX (tdmpc.py:92). The x6 products must keep w * inf = +inf (no 0 * inf from a weight's
+        # zero mid / lo part, no inf - inf from a negative mid part)
+        sd["_reward.0.bias"][5] = float("inf")
+        sd["_reward.2.weight"][:, 5] = sd["_reward.2.weight"][:, 5].abs() + 1e-3
+        sd["_reward.4.weight"][:] = sd["_reward.4.weight"].abs() + 1e-3
+    elif case == "inf_hidden_rows":
+        # the same through overflow, on SOME rows only: reward unit 5 sees 3e38 * (a_0 + a_1), which overflows to +inf
+        # where a_0 + a_1 > ~1.13 (then G = +FLT_MAX) and stays finite (or ELU -> -1) elsewhere; W2[:, 5] ~ 1e-31 > 0
+        # keeps the finite rows' rewards ~1e8
+        L = sd["_reward.0.weight"].shape[1] - sd["_pi.4.weight"].shape[0]   # cat[z, a]: a starts at column L
+        sd["_reward.0.weight"][5, L] = 3e38
+        sd["_reward.0.weight"][5, L + 1] = 3e38
+        sd["_reward.2.weight"][:, 5] = (sd["_reward.2.weight"][:, 5].abs() + 1e-3) * 1e-30
+        sd["_reward.4.weight"][:] = sd["_reward.4.weight"].abs() + 1e-3
 
 
-@pytest.mark.parametrize("case", ["beyond_bf16", "inf_latent", "nan_latent", "reward_pos_overflow",
-                                  "reward_neg_overflow", "inf_minus_inf", "large_finite"])
+NF_CASES = ["beyond_bf16", "inf_latent", "nan_latent", "reward_pos_overflow", "reward_neg_overflow", "inf_minus_inf",
+            "large_finite", "inf_hidden", "inf_hidden_rows"]
+
+
+@pytest.mark.parametrize("case", NF_CASES)
 @pytest.mark.parametrize("path", PATHS)
 def test_estimate_value_nonfinite(case, path):
     cfg = make_cfg("humanoid", num_samples=512, num_elites=64)
@@ -201,10 +221,43 @@ def test_estimate_value_nonfinite(case, path):
     # follows the terms' scale, not |G|: absolute tolerance 1e-5 of the largest |G| there
     atol = 1e-5 * float(np.abs(rv).max()) if case in ("large_finite", "beyond_bf16") else 1e-5
     assert close(gv[~special], rv[~special], atol=atol).all(), np.abs(gv - rv)[~special].max()
-    if case in ("reward_pos_overflow", "reward_neg_overflow", "inf_minus_inf", "nan_latent", "inf_latent"):
+    if case in ("reward_pos_overflow", "reward_neg_overflow", "inf_minus_inf", "nan_latent", "inf_latent", "inf_hidden"):
         assert special.all()   # the case does hit the guard's branches
+    if case == "inf_hidden":
+        assert (rv == FMAX).all()   # +inf -> +FLT_MAX on every row (not NaN -> 0)
+    if case == "inf_hidden_rows":
+        assert (rv == FMAX).any() and not special.all()   # a mix of overflowed and finite rows
     if case in ("beyond_bf16", "large_finite"):
         assert not special.any()
+
+
+@pytest.mark.parametrize("case", ["inf_hidden", "inf_hidden_rows"])
+@pytest.mark.parametrize("path", ["persist", "auto", "chain_x6"])
+def test_plan_nonfinite_hidden(case, path):
+    """A whole plan() (one env: the persistent kernel on path persist / auto) with an infinite hidden activation:
+    the first CEM iteration's values equal the oracle's -- +FLT_MAX on the overflowed rows, the rest within the
+    tolerance. (Later iterations pick elites among +FLT_MAX ties, whose order torch.topk leaves open.)"""
+    cfg = make_cfg("humanoid", **FULL)
+    sd = synthetic_state_dict(cfg, 7)
+    _nf_case(case, sd, torch.zeros(1, cfg.latent_dim))
+    agent = TDMPC(cfg, path=path)
+    agent.model.load_state_dict(sd)
+    agent.std = 0.05
+    told = tdmpc_ref.RefTOLD(sd, cfg)
+    obs = np.random.RandomState(1).standard_normal(cfg.obs_shape).astype(np.float32)
+    torch.manual_seed(2)
+    np.random.seed(2)
+    nb = tdmpc_ref.draw_noise(cfg, 10**6, False)
+    tr, rtr = {}, {}
+    agent._plan_envs(obs[None], False, 10**6, [True], trace=tr, noise=[nb])
+    tdmpc_ref.plan(told, cfg, tdmpc_ref.PlanState(0.05), obs, nb, eval_mode=False, step=10**6, t0=True, trace=rtr)
+    gv = tr["value"][0, 0].cpu().numpy()
+    rv = rtr["value"][0][:, 0].numpy()
+    assert np.isfinite(gv).all()
+    special = (np.abs(rv) == FMAX) | (rv == 0)
+    np.testing.assert_array_equal(gv[special], rv[special])
+    assert close(gv[~special], rv[~special]).all(), np.abs(gv - rv)[~special].max()
+    assert (rv == FMAX).any()
 
 
 def test_default_plan_graph_equals_eager():

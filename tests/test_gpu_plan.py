@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 from parity_util import ATOL, RTOL, compare_iterations as _compare_iterations, close as _close, \
     elites as _elites, near_tie as _near_tie, record
 
-PATHS = ["layered", "chain16", "chain32", "split", "chain_x6", "split_x6", "chain", "chain64", "persist"]
+PATHS = ["layered", "chain16", "chain32", "split", "chain_x6", "split_x6", "chain", "persist"]
 
 
 def _agent(cfg, wseed, B=1, path="auto"):
@@ -313,6 +313,51 @@ def test_bench_batch_vs_oracle():
     assert compared >= B // 2, "too many near-tie elite swaps to compare actions"
 
 
+def test_bench_shape_b32_vs_oracle():
+    """The bench line's exact workload: humanoid-run (N=512, H=5, 6 iterations) at 32 envs in one plan_batch call
+    (auto path: 512 x6 chain workgroups per head, two co-resident per CU, the z0c first layer at t = 0, the cached
+    pi-row terminal means), a cold call then a warm-started one, every env against the oracle on its own noise.
+    At least B - 2 envs must run every comparison to the end on each call (near-tie escapes are counted too)."""
+    cfg = make_cfg("humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5)
+    B = 32
+    agent = _agent(cfg, 13, B=B)
+    told = tdmpc_ref.RefTOLD(synthetic_state_dict(cfg, 13), cfg)
+    states = [tdmpc_ref.PlanState(0.05) for _ in range(B)]
+    rs = np.random.RandomState(31)
+    torch.manual_seed(32)
+    np.random.seed(32)
+    live = list(range(B))                       # envs whose every comparison so far ran to the end
+    for call, t0 in enumerate([True, False]):
+        obs = rs.standard_normal((B, cfg.obs_shape[0])).astype(np.float32)
+        noises = [tdmpc_ref.draw_noise(cfg, 10**6, False) for _ in range(B)]
+        tr = {}
+        a, m = agent._plan_envs(obs, False, 10**6, [t0] * B, trace=tr, noise=noises)
+        a = a.cpu().numpy()
+        pm = agent.planner.prev_mean_view(5, B).cpu().numpy()
+        full = []
+        for e in range(B):
+            rtr = {}
+            ra, rm = tdmpc_ref.plan(told, cfg, states[e], obs[e], noises[e], eval_mode=False, step=10**6, t0=t0,
+                                    trace=rtr)
+            if e not in live:
+                continue
+            ref_vals = torch.stack(rtr["value"]).squeeze(-1).numpy()
+            same = _compare_iterations(tr["value"][e].cpu().numpy(), ref_vals, cfg.num_elites)
+            record(same, f"bench_b32/call{call}/env{e}")
+            if not same:
+                continue
+            np.testing.assert_allclose(a[e], ra.numpy(), atol=2e-5, rtol=0, err_msg=f"call {call} env {e}")
+            np.testing.assert_allclose(tr["mean"][e, -1].cpu().numpy(), rtr["mean"][-1].numpy(), atol=2e-5, rtol=0)
+            np.testing.assert_allclose(tr["std"][e, -1].cpu().numpy(), rtr["std"][-1].numpy(), atol=2e-5, rtol=0)
+            np.testing.assert_allclose([m[e]["external_reward_mean"], m[e]["current_std"]],
+                                       [rm["external_reward_mean"], rm["current_std"]], atol=2e-5, rtol=1e-4)
+            np.testing.assert_allclose(pm[e], states[e].prev_mean.numpy(), atol=2e-5, rtol=0)
+            full.append(e)
+        need = len(live) - 2
+        assert len(full) >= need, f"call {call}: {len(full)} of {len(live)} envs compared to the end"
+        live = full
+
+
 def test_graph_replay_equals_eager_batched():
     """B=8 humanoid through a captured HIP graph (the bench's mode: chain kernels on two streams, the side
     stream joining the capture through events) equals the same calls issued eagerly, bitwise."""
@@ -448,3 +493,24 @@ def test_x6_accuracy_matches_f32_mfma():
     ex6 = np.abs(outs["chain_x6"] - G64).max()
     print(f"max |G - G_fp64|: f32 MFMA {e32:.3e}, x6 {ex6:.3e}")
     assert ex6 <= 2 * e32 + 1e-6, (e32, ex6)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_persist_timeout_raises(monkeypatch, graph):
+    """The persistent one-env plan assumes its whole 256-workgroup grid is resident. With a debug knob one workgroup
+    never arrives at the first hand-off, so every other one times out (bounded spin): the kernel ORs
+    TDMPC_STATUS_P1_TIMEOUT into the caller's status word and plan() raises instead of returning the NaN action.
+    The status is sticky until raised; the next healthy call plans normally."""
+    cfg = make_cfg("humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5)
+    agent = TDMPC(cfg, path="persist", graph=graph)
+    agent.model.load_state_dict(synthetic_state_dict(cfg, 9))
+    agent.std = 0.05
+    obs = np.random.RandomState(0).standard_normal(cfg.obs_shape).astype(np.float32)
+    monkeypatch.setenv("TDMPC_P1_DEBUG_SKIP", "1")
+    with pytest.raises(RuntimeError, match="timed out"):
+        agent.plan(obs, step=10**6, t0=True)
+    assert int(agent.planner.status.item()) == 0   # cleared when raised
+    monkeypatch.delenv("TDMPC_P1_DEBUG_SKIP")
+    agent.planner._graphs.clear()                  # (a captured graph keeps the knob's launch arguments)
+    a, m = agent.plan(obs, step=10**6, t0=True)
+    assert torch.isfinite(a).all() and np.isfinite(m["current_std"])

@@ -1,0 +1,62 @@
+"""The product env-sharding path with more than one rank (SURVEY.md §8e, configs[3]: 64 vectorised dog-run envs):
+two processes, each the real HIP `TDMPC` under `EnvShardedPlanner`'s default plan_fn (plan_batch of its 32-env
+shard, HIP graph, reference-order device draws), one all-gather of [envs, A+2] per call. Both ranks share the one
+GPU of the test box, so the collective runs on the gloo transport (RCCL refuses two ranks on one device); the
+planning path is the one `bench.py --gpus N` runs per GPU. Every env's gathered action and metrics must equal,
+bitwise, a single-process plan_batch over all 64 envs: envs are independent and N, T are multiples of the 32-row
+block, so an env's arithmetic does not depend on its slot or on the batch size (every launch of both batch sizes
+picks the same kernels at >= 17 envs per call)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import shard_worker as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_sharded_dog64_world2_equals_single_process(tmp_path):
+    world, port = 2, _free_port()
+    env = dict(os.environ, WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    here = os.path.dirname(os.path.abspath(__file__))
+    procs = [subprocess.Popen([sys.executable, os.path.join(here, "shard_worker.py"), str(tmp_path)],
+                              env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out)
+        assert p.returncode == 0, out[-3000:]
+    got = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(world)]
+    # single process, all 64 envs, same weights and generator states
+    c = W.cfg()
+    agent = W.TDMPC(c, max_batch=W.N_ENVS)
+    agent.model.load_state_dict(W.synthetic_state_dict(c, W.WSEED))
+    agent.std = 0.05
+    H, I = agent.horizon(10**6), c.iterations
+    for k, obs in enumerate(W.observations(c)):
+        W.position_rngs(agent, 0, k, H, I)
+        a, m = agent.plan_batch(obs, step=10**6, t0=(k == 0), sync_metrics=False)
+        a, m = a.cpu().numpy(), m.cpu().numpy()
+        assert np.isfinite(a).all()
+        for r in range(world):   # every rank holds the whole gathered batch
+            np.testing.assert_array_equal(got[r][f"a{k}"], a, err_msg=f"call {k} rank {r} actions")
+            np.testing.assert_array_equal(got[r][f"m{k}"], m, err_msg=f"call {k} rank {r} metrics")

@@ -70,3 +70,30 @@ def test_train_loop_plans_with_updated_weights():
     v_gpu, v_ref = _oracle_first_values(agent, cfg, obs, step)
     err = (v_gpu - v_ref).abs().max().item()
     assert err < 1e-4 * (1 + v_ref.abs().max().item()), f"plan after graph-replayed updates: max|dG| {err}"
+
+
+@pytest.mark.gpu
+def test_update_pi_then_plan_repacks():
+    """TDMPC.update_pi (tdmpc.py:165-182) on the learner engine writes the policy weights in place (no tensor version
+    bump); the next plan() must plan with them: its first-iteration values equal the oracle's on the agent's
+    current weights (the planner kept the stale packed policy)."""
+    from tdmpc_amd.tdmpc import TDMPC
+    cfg = learner_cfg()
+    agent = TDMPC(cfg)
+    agent.model.load_state_dict(synthetic_state_dict(cfg, 43))
+    agent.model_target.load_state_dict(synthetic_state_dict(cfg, 44))
+    rs = np.random.RandomState(5)
+    obs = rs.standard_normal(cfg.obs_shape).astype(np.float32)
+    torch.manual_seed(1)
+    np.random.seed(1)
+    step = 10**6
+    agent.plan(obs, step=step, t0=True)            # packs the initial weights
+    pi0 = [p.detach().clone() for p in agent.model._pi.parameters()]
+    g = torch.Generator(device="cuda").manual_seed(7)
+    zs = [torch.randn(cfg.batch_size, cfg.latent_dim, device="cuda", generator=g) for _ in range(cfg.horizon + 1)]
+    for _ in range(3):
+        agent.update_pi(zs)
+    assert any(not torch.equal(p, q) for p, q in zip(agent.model._pi.parameters(), pi0)), "update_pi changed nothing"
+    v_gpu, v_ref = _oracle_first_values(agent, cfg, obs, step)
+    err = (v_gpu - v_ref).abs().max().item()
+    assert err < 1e-4 * (1 + v_ref.abs().max().item()), f"plan after update_pi: max|dG| {err}"
