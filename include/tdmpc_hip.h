@@ -75,7 +75,8 @@ typedef struct tdmpc_plan_params {
                               (others layered), 6 = chain kernels with fp32 products from a three-way bf16
                               split (TDMPC_PATH_CHAIN_X6), 7 = path 5 with those products, 8 = path 6 (the retired
                               64-row blocks), 9 = the persistent one-env plan
-                              (plan1: one launch after the encoder); results agree within the fp32 tolerance */
+                              (plan1: one launch after the encoder), 10 = the wide step kernel (TDMPC_PATH_WIDE);
+                              results agree within the fp32 tolerance */
     /* ABI 5: per-call state read from device memory at run time, so one captured hipGraph serves every value */
     const int32_t* warm_flags; /* optional device int32 [batch]: per-env warm start (tdmpc.py:124-125, `not t0`
                                   for that env with a previous mean); NULL = warm_start for every env */
@@ -104,6 +105,9 @@ typedef struct tdmpc_plan_params {
 #define TDMPC_PATH_PERSIST 9    /* one env: the whole plan after the encoder as ONE persistent launch (x6 products,
                                    weight-stationary; batch 1, M = 512, >= 256 CUs; the auto path's choice there);
                                    calls it does not apply to run the auto path */
+#define TDMPC_PATH_WIDE 10      /* TOLD.next on the 128-row wide step kernel (x6, weights streamed once per workgroup
+                                   through an LDS ring) at every width it supports, x6 chain kernels elsewhere;
+                                   the auto path picks it for launches with >= one 128-row block per CU and head */
 
 /* Byte sizes the caller must allocate (all 256-byte aligned). */
 typedef struct tdmpc_sizes {

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDMPC_LIB_PATH") or os.path.join(HERE, "libtdmpc_hip.so")   # override: A/B of builds
 
 ABI_VERSION = 6
-PATHS = {"auto": 0, "layered": 1, "chain": 2, "chain32": 3, "chain16": 4, "split": 5, "chain_x6": 6, "split_x6": 7, "chain64": 8, "persist": 9}
+PATHS = {"auto": 0, "layered": 1, "chain": 2, "chain32": 3, "chain16": 4, "split": 5, "chain_x6": 6, "split_x6": 7, "chain64": 8, "persist": 9, "wide": 10}
 
 EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc_num_param_tensors",
             "tdmpc_pack_weights", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_pi_rollout",

@@ -3081,6 +3081,7 @@ int set_lds_attr() {
 }
 
 #include "plan1.inc"
+#include "wide_step.inc"
 
 #define FOR_EACH_LINEAR(X)                                                                          \
     X(1, 1, 1, 1, 0, 32, false) X(1, 1, 1, 1, 0, 64, false) X(1, 1, 1, 1, 0, 128, false)              \
@@ -3100,6 +3101,10 @@ int init_attrs() {
     HIPCHK(hipFuncSetAttribute((const void*)cem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)plan1_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)plan1_kernel<6>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+#define WIDE_ATTR(G1, NB3) \
+    HIPCHK(hipFuncSetAttribute((const void*)wide_step_kernel<G1, NB3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    WIDE_FOR_EACH(WIDE_ATTR)
+#undef WIDE_ATTR
     HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -3545,7 +3550,7 @@ int use_x6(const Ctx& c) {
         en = e ? atoi(e) : 3;
     }
     if (en == 2) en = 3;   // (mode 2, the split planes in LDS, retired)
-    if (c.path == TDMPC_PATH_CHAIN_X6) return en == 1 || en == 3 ? en : 3;
+    if (c.path == TDMPC_PATH_CHAIN_X6 || c.path == TDMPC_PATH_WIDE) return en == 1 || en == 3 ? en : 3;
     if (c.path == TDMPC_PATH_SPLIT_X6) return 1;
     return (c.path == TDMPC_PATH_AUTO || c.path == TDMPC_PATH_CHAIN) ? en : 0;
 }
@@ -3556,7 +3561,9 @@ int use_x6(const Ctx& c) {
 // blocks, which double the workgroups of a narrow launch (B = 4 step: 36.7 us vs 56 us on 128 32-row
 // workgroups). TDMPC_CHAIN_RB forces 16 or 32 for experiments.
 int chain_rb(const Ctx& c, int rows, int nprob) {
-    if (!chain16_shape_ok(c.w) || c.path == TDMPC_PATH_CHAIN32 || c.path == TDMPC_PATH_CHAIN_X6) return 32;
+    if (!chain16_shape_ok(c.w) || c.path == TDMPC_PATH_CHAIN32 || c.path == TDMPC_PATH_CHAIN_X6 ||
+        c.path == TDMPC_PATH_WIDE)
+        return 32;
     if (c.path == TDMPC_PATH_CHAIN16) return 16;
     static int forced = -1;
     if (forced < 0) {
@@ -3662,6 +3669,66 @@ int z0c_launch(const Ctx& c) {
     return 0;
 }
 
+// ---- the wide step kernel (wide_step.inc) for TOLD.next launches with >= one 128-row block per CU and head (B >= 32
+// envs at N = 512; TDMPC_WIDE=0 turns it off, TDMPC_PATH_WIDE forces it at every width it supports)
+int wide_g1(const Ctx& c, bool z0c) {   // first-layer 16-k groups the kernel runs, padded to even
+    const int g = (z0c ? z0c_k1c(c) : (int)rup(c.Kx, 16)) / 16;
+    return (g + 1) & ~1;
+}
+bool use_wide(const Ctx& c, int rows, const RowMap& map, bool z0c) {
+    static const int en = [] { const char* e = getenv("TDMPC_WIDE"); return e ? atoi(e) : 1; }();
+    if (c.w.M != 512 || !use_x6(c) || !num_cus()) return false;
+    if (c.path != TDMPC_PATH_AUTO && c.path != TDMPC_PATH_CHAIN && c.path != TDMPC_PATH_WIDE) return false;
+    if (c.path != TDMPC_PATH_WIDE && !en) return false;
+    if (rows % 32 || map.G % 32 || map.S % 32 || map.O % 32) return false;   // a wave's 32 rows = one X panel block
+    const int g1 = wide_g1(c, z0c), nb3 = c.w.Lr / 32;
+    if (g1 > 10 || (nb3 != 1 && nb3 != 2 && nb3 != 4)) return false;
+    return c.path == TDMPC_PATH_WIDE || (rows + 127) / 128 * 2 >= num_cus();
+}
+int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, bool z0c) {
+    const Layout& w = c.w;
+    const int M = c.M;
+    WideArgs a;
+    memset(&a, 0, sizeof a);
+    const size_t rb1 = (size_t)(M / 32) * (rup(c.Kx, 16) / 16) * 1536;   // bf16 per M rows of x6 W1
+    a.p[0].X1 = x6p(c, X6_W1X); a.p[1].X1 = x6p(c, X6_W1X) + rb1;
+    a.p[0].X2 = x6p(c, X6_W2D); a.p[1].X2 = x6p(c, X6_W2R);
+    a.p[0].b1 = c.pw + w.b1x; a.p[1].b1 = c.pw + w.b1x + M;
+    a.p[0].b2 = c.pw + w.b2d; a.p[1].b2 = c.pw + w.b2r;
+    a.p[1].w3v = c.pw + w.w3r; a.p[1].b3v = c.pw + w.b3r;
+    a.X3 = x6p(c, X6_W3D); a.b3 = c.pw + w.b3d; a.nvalid = w.L; a.nstore = w.Lp;
+    a.rows = rows; a.nrb = (rows + 127) / 128; a.amap = map;
+    a.X = Xt(c, t); a.x_ts = (long)c.Kx * 32;
+    a.kq = (z0c ? z0c_k1c(c) : c.Kx) / 4; a.g1s = (int)(rup(c.Kx, 16) / 16);
+    a.Xo = Xt(c, t + 1); a.out_q0 = w.Ap / 4;
+    a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
+    if (z0c) { a.z0c = c.k.z0c; a.z0_G = map.G; }
+    const int g1 = wide_g1(c, z0c), nb3 = w.Lr / 32;
+    const dim3 grid((unsigned)rup(a.nrb, 4) * 2), block(64 * WS_NW);
+    // diagnostic timer (tdmpc_profile_begin cfg 4: the step kernel); t = 0 launches with the z0c first layer are not
+    // timed (less than the algorithmic work), as in launch_chain
+    Profiler& pf = g_prof;
+    const bool prof = pf.armed && pf.cfg == 4 + CH_STEP && pf.n + 2 <= pf.cap && (pf.rows == 0 || rows == pf.rows) && !z0c;
+    if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], c.s));
+    bool done = false;
+#define WIDE_LAUNCH(G1, NB3) \
+    if (!done && g1 == G1 && nb3 == NB3) { \
+        hipLaunchKernelGGL((wide_step_kernel<G1, NB3>), grid, block, WS_LDS, c.s, a); \
+        done = true; \
+    }
+    WIDE_FOR_EACH(WIDE_LAUNCH)
+#undef WIDE_LAUNCH
+    if (!done) { snprintf(g_err, sizeof g_err, "wide step: no instance for G1 %d NB3 %d", g1, nb3); return TDMPC_E_DIMS; }
+    HIPCHK(hipGetLastError());
+    if (prof) {
+        HIPCHK(hipEventRecord(pf.ev[pf.n + 1], c.s));
+        pf.n += 2;
+        const double K1 = w.L + w.A;
+        pf.flops += 2.0 * rows * (2 * (K1 * M + (double)M * M) + (double)M * w.L + M);
+    }
+    return 0;
+}
+
 // defer = 1 (a loop of consecutive steps over the same rows, nothing reading X_{t+1}'s latents in between): on the
 // split path the finish of this step is folded into the next step's launch.
 int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, int defer = 0) {
@@ -3671,6 +3738,13 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
     if (c.split_pend && (!use_split(c, rows) || rows != c.split_rows || t != c.split_t + 1 ||
                          memcmp(&map, &c.split_map, sizeof map)))
         if ((rc = flush_split(c))) return rc;
+    {
+        const bool z0c = t == 0 && c.z0c_ready && map.G % 32 == 0;
+        if (use_wide(c, rows, map, z0c)) {
+            if ((rc = flush_split(c))) return rc;
+            return launch_wide(c, t, rows, map, disc, first, last, z0c);
+        }
+    }
     if (use_chain(c, rows, 2, CK_STEP)) {
         ChainArgs a = chain0(c, rows, map, t, c.Kx, 0, 2);
         ChainProb& d = a.p[0];
@@ -4415,7 +4489,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     int rc;
     const int H = prm->horizon, I = prm->iterations, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > TDMPC_PATH_WIDE) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path == TDMPC_PATH_CHAIN64 ? TDMPC_PATH_CHAIN_X6 : prm->path;   // (64-row blocks retired: path 6)
     const int N = c.N, P = c.P, T = c.T;
     // TDMPC_PATH_PERSIST: the persistent plan where it applies (one env, supported shape), the auto path elsewhere
@@ -4518,7 +4592,7 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
     const int H = prm->horizon, I = prm->iterations, B = prm->batch, K = d->num_elites;
     if (I <= 0 || I > 16) { snprintf(g_err, sizeof g_err, "iCEM: 1..16 iterations"); return TDMPC_E_DIMS; }
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, I, (hipStream_t)stream, K))) return rc;
-    if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > TDMPC_PATH_WIDE) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path == TDMPC_PATH_CHAIN64 ? TDMPC_PATH_CHAIN_X6
            : prm->path;   // (persist: whole plans only; the retired 64-row path is path 6)
     const int N = d->num_samples, Pmax = d->num_pi, Tw = N + K + Pmax, pi_base = N + K, P0 = prm->n_pi0;
@@ -4617,7 +4691,7 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > TDMPC_PATH_WIDE) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path == TDMPC_PATH_CHAIN64 ? TDMPC_PATH_CHAIN_X6
            : prm->path;   // (persist: whole plans only; the retired 64-row path is path 6)
     if (rows != c.T) { snprintf(g_err, sizeof g_err, "rows must equal N+P"); return TDMPC_E_DIMS; }
@@ -4663,7 +4737,7 @@ int tdmpc_pi_rollout(const tdmpc_dims* d, const tdmpc_plan_params* prm, const vo
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > TDMPC_PATH_WIDE) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path == TDMPC_PATH_CHAIN64 ? TDMPC_PATH_CHAIN_X6
            : prm->path;   // (persist: whole plans only; the retired 64-row path is path 6)
     const int N = c.N, P = c.P, T = c.T;
@@ -4693,7 +4767,7 @@ int tdmpc_cem_iter(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void
     int rc;
     const int H = prm->horizon, B = prm->batch;
     if ((rc = setup_ctx(c, d, packed, workspace, ws_bytes, B, H, 1, (hipStream_t)stream))) return rc;
-    if (prm->path < 0 || prm->path > TDMPC_PATH_PERSIST) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
+    if (prm->path < 0 || prm->path > TDMPC_PATH_WIDE) { snprintf(g_err, sizeof g_err, "bad path"); return TDMPC_E_DIMS; }
     c.path = prm->path == TDMPC_PATH_PERSIST ? TDMPC_PATH_AUTO : prm->path == TDMPC_PATH_CHAIN64 ? TDMPC_PATH_CHAIN_X6
            : prm->path;   // (persist: whole plans only; the retired 64-row path is path 6)
     const int N = c.N, P = c.P, T = c.T, A = c.A, HA = H * A;

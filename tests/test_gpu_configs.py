@@ -32,7 +32,7 @@ CONFIGS = {
     "quadruped-run-pixels": ("quadruped", dict(FULL, modality="pixels")),
     "dog-run": ("dog", dict(FULL)),
 }
-PATHS = ["layered", "chain16", "chain32", "split", "chain_x6", "split_x6", "chain", "persist"]
+PATHS = ["layered", "chain16", "chain32", "split", "chain_x6", "split_x6", "chain", "persist", "wide"]
 
 
 def _agent(cfg, wseed, B=1, path="auto", **kw):

@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 from parity_util import ATOL, RTOL, compare_iterations as _compare_iterations, close as _close, \
     elites as _elites, near_tie as _near_tie, record
 
-PATHS = ["layered", "chain16", "chain32", "split", "chain_x6", "split_x6", "chain", "persist"]
+PATHS = ["layered", "chain16", "chain32", "split", "chain_x6", "split_x6", "chain", "persist", "wide"]
 
 
 def _agent(cfg, wseed, B=1, path="auto"):
