@@ -3682,7 +3682,7 @@ bool use_wide(const Ctx& c, int rows, const RowMap& map, bool z0c) {
     if (c.path != TDMPC_PATH_WIDE && !en) return false;
     if (rows % 32 || map.G % 32 || map.S % 32 || map.O % 32) return false;   // a wave's 32 rows = one X panel block
     const int g1 = wide_g1(c, z0c), nb3 = c.w.Lr / 32;
-    if (g1 > 10 || (nb3 != 1 && nb3 != 2 && nb3 != 4)) return false;
+    if (g1 > 10 || (nb3 != 2 && nb3 != 4)) return false;
     return c.path == TDMPC_PATH_WIDE || (rows + 127) / 128 * 2 >= num_cus();
 }
 int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, bool z0c) {
@@ -3713,7 +3713,7 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
     bool done = false;
 #define WIDE_LAUNCH(G1, NB3) \
     if (!done && g1 == G1 && nb3 == NB3) { \
-        hipLaunchKernelGGL((wide_step_kernel<G1, NB3>), grid, block, WS_LDS, c.s, a); \
+        hipLaunchKernelGGL((wide_step_kernel<G1, NB3>), grid, block, ws_lds<G1>(), c.s, a); \
         done = true; \
     }
     WIDE_FOR_EACH(WIDE_LAUNCH)
