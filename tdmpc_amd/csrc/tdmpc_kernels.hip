@@ -3669,14 +3669,17 @@ int z0c_launch(const Ctx& c) {
     return 0;
 }
 
+unsigned long long* g_p1_stamps = nullptr;   // tdmpc_debug_plan1_stamps (diagnostic; also the wide kernel's stamps)
+
 // ---- the wide step kernel (wide_step.inc) for TOLD.next launches with >= one 128-row block per CU and head (B >= 32
-// envs at N = 512; TDMPC_WIDE=0 turns it off, TDMPC_PATH_WIDE forces it at every width it supports)
+// envs at N = 512). Opt-in (TDMPC_WIDE=1) until it beats the chain step kernel; TDMPC_PATH_WIDE forces it at every
+// width it supports)
 int wide_g1(const Ctx& c, bool z0c) {   // first-layer 16-k groups the kernel runs, padded to even
     const int g = (z0c ? z0c_k1c(c) : (int)rup(c.Kx, 16)) / 16;
     return (g + 1) & ~1;
 }
 bool use_wide(const Ctx& c, int rows, const RowMap& map, bool z0c) {
-    static const int en = [] { const char* e = getenv("TDMPC_WIDE"); return e ? atoi(e) : 1; }();
+    static const int en = [] { const char* e = getenv("TDMPC_WIDE"); return e ? atoi(e) : 0; }();
     if (c.w.M != 512 || !use_x6(c) || !num_cus()) return false;
     if (c.path != TDMPC_PATH_AUTO && c.path != TDMPC_PATH_CHAIN && c.path != TDMPC_PATH_WIDE) return false;
     if (c.path != TDMPC_PATH_WIDE && !en) return false;
@@ -3703,6 +3706,7 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
     a.Xo = Xt(c, t + 1); a.out_q0 = w.Ap / 4;
     a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
     if (z0c) { a.z0c = c.k.z0c; a.z0_G = map.G; }
+    a.stamps = g_p1_stamps;   // (read only by a -DWS_STAMPS diagnostic build)
     const int g1 = wide_g1(c, z0c), nb3 = w.Lr / 32;
     const dim3 grid((unsigned)rup(a.nrb, 4) * 2), block(64 * WS_NW);
     // diagnostic timer (tdmpc_profile_begin cfg 4: the step kernel); t = 0 launches with the z0c first layer are not
@@ -4101,7 +4105,6 @@ int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, const float*
     return 0;
 }
 
-unsigned long long* g_p1_stamps = nullptr;   // tdmpc_debug_plan1_stamps (diagnostic)
 
 // The persistent one-env plan (plan1.inc) for this call? The auto path's choice (TDMPC_PERSIST=0 turns it off) and
 // TDMPC_PATH_PERSIST, when the shape fits, batch 1, >= 256 CUs (every workgroup of its 256-block grid must be

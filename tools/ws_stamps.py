@@ -1,0 +1,48 @@
+"""Per-step timeline of the wide step kernel (diagnostic; needs the -DWS_STAMPS build, TDMPC_LIB_PATH pointing at it).
+
+    python tools/ws_stamps.py [B]
+Runs humanoid-run plan_batch(B) a few times, then one call with stamps on, and prints for workgroups 0 (dynamics) and 4
+(reward) per wave: total cycles, cycles waiting at the per-step vmcnt + barrier, and the per-phase split."""
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from tdmpc_amd import _lib
+from tdmpc_amd.config import bench_cfg
+from tdmpc_amd.tdmpc import TDMPC
+from tdmpc_amd.told import synthetic_state_dict
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+cfg = bench_cfg("humanoid-run")
+agent = TDMPC(cfg, max_batch=B, rng="fused", graph=False)
+agent.model.load_state_dict(synthetic_state_dict(cfg, 0))
+agent.std = 0.05
+obs = np.random.RandomState(0).standard_normal((B,) + tuple(cfg.obs_shape)).astype(np.float32)
+for i in range(3):
+    agent.plan_batch(obs, step=10**6, t0=(i == 0), sync_metrics=False)
+torch.cuda.synchronize()
+buf = torch.zeros(8192, dtype=torch.int64, device="cuda")
+L = _lib.lib()
+L.tdmpc_debug_plan1_stamps(C.c_void_p(buf.data_ptr()))
+agent.plan_batch(obs, step=10**6, t0=False, sync_metrics=False)   # the last wide launch's stamps remain
+torch.cuda.synchronize()
+L.tdmpc_debug_plan1_stamps(None)
+st = buf.cpu().numpy().view(np.uint64).astype(np.int64)
+for name, base in (("dynamics wg0", 0), ("reward wg4", 4096)):
+    for w in range(4):
+        s = st[base + w * 1024: base + w * 1024 + 1024].reshape(512, 2)
+        n = int((s[:, 0] > 0).sum())
+        s = s[:n]
+        wait = s[:, 1] - s[:, 0]
+        comp = s[1:, 0] - s[:-1, 1]
+        tot = s[-1, 1] - s[0, 0]
+        print(f"{name} wave {w}: steps {n} total {tot} cyc, wait {wait.sum()} ({wait.sum() / tot:.2f}), compute "
+              f"{comp.sum()} median step compute {np.median(comp):.0f} wait {np.median(wait):.0f}")
+        if w == 0:
+            print("   first steps wait:", wait[:12].tolist())
+            print("   first steps comp:", comp[:12].tolist())
+            print("   L2 steps comp:", comp[4:20].tolist())
