@@ -511,7 +511,18 @@ def main():
             rb = 32 if (rows + 31) // 32 * 2 > torch.cuda.get_device_properties(dev).multi_processor_count // 2 else 16
             rb = int(os.environ.get("TDMPC_CHAIN_RB", rb))
             x6 = rb == 32 and M == 512 and os.environ.get("TDMPC_X6", "3") != "0"
-            if x6:
+            cus = torch.cuda.get_device_properties(dev).multi_processor_count
+            # the library's use_wide(): M = 512, x6, 16-row map, <= 5 first-layer 32-k groups, L in (48, 64] / (96, 112]
+            wide = (x6 and os.environ.get("TDMPC_WIDE", "1") != "0" and (rows + 127) // 128 * 2 >= cus
+                    and (A + 7) // 8 * 8 + (Lt + 7) // 8 * 8 <= 160 and (Lt + 15) // 16 in (4, 7))
+            if wide:
+                peak = X6_PEAK_TFLOPS
+                kernel = (f"wide_step_kernel<G1=4, NB3=7> (TOLD.next: dynamics + reward heads on 128-row workgroups, "
+                          f"8 waves x 16 rows x all {M} hidden columns in registers, layer 1 streamed into layer 2 by "
+                          f"64-column chunks, x6 weight fragments LDS-DMA'd once per workgroup into an LDS ring; "
+                          f"{rows} rows x 2 heads per launch), fp32 products from a three-way bf16 split of both "
+                          f"operands: 6 v_mfma_f32_16x16x32_bf16 per product, fp32 accumulation (peak = dense BF16 / 6)")
+            elif x6:
                 peak = X6_PEAK_TFLOPS
                 kernel = (f"chain_kernel<CH_STEP, TN=4, NW=4, X6> (TOLD.next: dynamics + reward heads, 32-row blocks "
                           f"of 4 waves x 128 columns, hidden "
@@ -524,7 +535,7 @@ def main():
                           f"fp32 {'v_mfma_f32_32x32x2_f32' if rb == 32 else 'v_mfma_f32_16x16x4_f32'}")
             kx = A + Lt
             alg_bytes = 4.0 * (rows * (kx + Lt + 2) + 2 * M * kx + 2 * M * M + M * Lt + M)
-            pmc_key = f"{args.config}/B{B}/chain_step" + ("_x6" if x6 else "")
+            pmc_key = f"{args.config}/B{B}/" + ("wide_step" if wide else "chain_step" + ("_x6" if x6 else ""))
         else:
             n, ms, fl = timed(0, 0, M, rows)
             kernel = (f"linear_lds_kernel (128x128 LDS-staged tile): CEM rollout layer 2 (dynamics + reward "

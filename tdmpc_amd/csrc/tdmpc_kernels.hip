@@ -97,6 +97,8 @@ struct Layout {
     size_t wq3, bq3;                                 // [2][M], [2]
     // the chain kernels' weight panels again as three bf16 planes (x6 layout, X6_* below, pack_x6_kernel)
     size_t x6[9];
+    // the wide step kernel's copies of X6_W1X .. X6_W3D in the x6q layout (16-row x 32-k blocks, pack_x6q_kernel)
+    size_t x6q[4];
     size_t total;
 };
 
@@ -169,6 +171,11 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
         int r, k;
         x6_shape(*w, i, &r, &k);
         w->x6[i] = take(rup(r, 32) * rup(k, 16) * 3 / 2);   // bf16 elements / 2 = floats
+    }
+    for (int i = 0; i < 4; ++i) {
+        int r, k;
+        x6_shape(*w, i, &r, &k);
+        w->x6q[i] = take(rup(r, 16) * rup(k, 32) * 3 / 2);
     }
     w->total = o;
     return true;
@@ -3030,6 +3037,29 @@ __global__ void pack_x6_kernel(const float* src, int rows, int K, unsigned short
     }
 }
 
+// The x6q layout (wide_step_kernel): block (nb, g) of 16 rows x 32 k is [3 planes][64 lanes][8 bf16]: lane l
+// (m = l & 15, q = l >> 4) element j holds row 16 nb + m, k = 32 g + 16 (j >> 2) + 4 q + (j & 3) -- the
+// v_mfma_f32_16x16x32_bf16 A fragment, in the k order in which a 16x16 accumulator tile pair (a lane holding
+// features 16t + 4q + i of its row) is the next layer's B fragment.
+__global__ void pack_x6q_kernel(const float* src, int rows, int K, unsigned short* dst) {
+    const int G = (K + 31) / 32;
+    const size_t total = (size_t)((rows + 15) / 16) * G * 512;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int j = i & 7, lane = (i >> 3) & 63;
+        const size_t blk = i >> 9;
+        const int g = (int)(blk % G), nb = (int)(blk / G);
+        const int r = 16 * nb + (lane & 15), q = lane >> 4;
+        const int k = 32 * g + 16 * (j >> 2) + 4 * q + (j & 3);
+        const float x = k < K && r < rows ? src[(size_t)(r >> 5) * K * 32 + (size_t)(k >> 2) * 128 + (r & 31) * 4 + (k & 3)]
+                                          : 0.f;
+        __bf16 hi, mid, lo;
+        split3(x, hi, mid, lo);
+        dst[(blk * 3 + 0) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, hi);
+        dst[(blk * 3 + 1) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, mid);
+        dst[(blk * 3 + 2) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, lo);
+    }
+}
+
 // candidate actions act [B][H][Ts][A] -> the action columns of rows e * Td + r0 + r of X_t (t < H)
 __global__ void scatter_actions_kernel(const float* act, float* X, size_t x_stride, int H, int Ts, int A, int Ap,
                                        int Kx, int B, int Td, int r0) {
@@ -3672,20 +3702,19 @@ int z0c_launch(const Ctx& c) {
 unsigned long long* g_p1_stamps = nullptr;   // tdmpc_debug_plan1_stamps (diagnostic; also the wide kernel's stamps)
 
 // ---- the wide step kernel (wide_step.inc) for TOLD.next launches with >= one 128-row block per CU and head (B >= 32
-// envs at N = 512). Opt-in (TDMPC_WIDE=1) until it beats the chain step kernel; TDMPC_PATH_WIDE forces it at every
-// width it supports)
-int wide_g1(const Ctx& c, bool z0c) {   // first-layer 16-k groups the kernel runs, padded to even
-    const int g = (z0c ? z0c_k1c(c) : (int)rup(c.Kx, 16)) / 16;
-    return (g + 1) & ~1;
+// envs at N = 512; TDMPC_WIDE=0 turns it off, TDMPC_PATH_WIDE forces it at every width it supports)
+int wide_g1(const Ctx& c, bool z0c) {   // first-layer 32-k groups the kernel runs
+    return (int)rup(z0c ? z0c_k1c(c) : c.Kx, 32) / 32;
 }
 bool use_wide(const Ctx& c, int rows, const RowMap& map, bool z0c) {
-    static const int en = [] { const char* e = getenv("TDMPC_WIDE"); return e ? atoi(e) : 0; }();
+    static const int en = [] { const char* e = getenv("TDMPC_WIDE"); return e ? atoi(e) : 1; }();
     if (c.w.M != 512 || !use_x6(c) || !num_cus()) return false;
     if (c.path != TDMPC_PATH_AUTO && c.path != TDMPC_PATH_CHAIN && c.path != TDMPC_PATH_WIDE) return false;
     if (c.path != TDMPC_PATH_WIDE && !en) return false;
-    if (rows % 32 || map.G % 32 || map.S % 32 || map.O % 32) return false;   // a wave's 32 rows = one X panel block
-    const int g1 = wide_g1(c, z0c), nb3 = c.w.Lr / 32;
-    if (g1 > 10 || (nb3 != 2 && nb3 != 4)) return false;
+    if (rows % 16 || map.G % 16 || map.S % 16 || map.O % 16) return false;   // a wave's 16 rows in one X panel block
+    if (z0c && map.G % 128) return false;   // the per-env first-layer bias is per workgroup
+    const int g1 = wide_g1(c, z0c), nb3 = (int)rup(c.w.L, 16) / 16;
+    if (g1 > 5 || (nb3 != 4 && nb3 != 7)) return false;
     return c.path == TDMPC_PATH_WIDE || (rows + 127) / 128 * 2 >= num_cus();
 }
 int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, bool z0c) {
@@ -3693,21 +3722,23 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
     const int M = c.M;
     WideArgs a;
     memset(&a, 0, sizeof a);
-    const size_t rb1 = (size_t)(M / 32) * (rup(c.Kx, 16) / 16) * 1536;   // bf16 per M rows of x6 W1
-    a.p[0].X1 = x6p(c, X6_W1X); a.p[1].X1 = x6p(c, X6_W1X) + rb1;
-    a.p[0].X2 = x6p(c, X6_W2D); a.p[1].X2 = x6p(c, X6_W2R);
+    auto q6 = [&](int i) { return (const unsigned short*)(c.pw + w.x6q[i]); };
+    a.g1s = (int)(rup(c.Kx, 32) / 32);
+    const size_t rb1 = (size_t)(M / 16) * a.g1s * 1536;   // bf16 per M rows of x6q W1
+    a.p[0].X1 = q6(X6_W1X); a.p[1].X1 = q6(X6_W1X) + rb1;
+    a.p[0].X2 = q6(X6_W2D); a.p[1].X2 = q6(X6_W2R);
     a.p[0].b1 = c.pw + w.b1x; a.p[1].b1 = c.pw + w.b1x + M;
     a.p[0].b2 = c.pw + w.b2d; a.p[1].b2 = c.pw + w.b2r;
     a.p[1].w3v = c.pw + w.w3r; a.p[1].b3v = c.pw + w.b3r;
-    a.X3 = x6p(c, X6_W3D); a.b3 = c.pw + w.b3d; a.nvalid = w.L; a.nstore = w.Lp;
+    a.X3 = q6(X6_W3D); a.b3 = c.pw + w.b3d; a.nvalid = w.L; a.nstore = w.Lp;
     a.rows = rows; a.nrb = (rows + 127) / 128; a.amap = map;
     a.X = Xt(c, t); a.x_ts = (long)c.Kx * 32;
-    a.kq = (z0c ? z0c_k1c(c) : c.Kx) / 4; a.g1s = (int)(rup(c.Kx, 16) / 16);
+    a.kq = (z0c ? z0c_k1c(c) : c.Kx) / 4;
     a.Xo = Xt(c, t + 1); a.out_q0 = w.Ap / 4;
     a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
     if (z0c) { a.z0c = c.k.z0c; a.z0_G = map.G; }
     a.stamps = g_p1_stamps;   // (read only by a -DWS_STAMPS diagnostic build)
-    const int g1 = wide_g1(c, z0c), nb3 = w.Lr / 32;
+    const int g1 = wide_g1(c, z0c), nb3 = (int)rup(w.L, 16) / 16;
     const dim3 grid((unsigned)rup(a.nrb, 4) * 2), block(64 * WS_NW);
     // diagnostic timer (tdmpc_profile_begin cfg 4: the step kernel); t = 0 launches with the z0c first layer are not
     // timed (less than the algorithmic work), as in launch_chain
@@ -4464,6 +4495,14 @@ int tdmpc_pack_weights(const tdmpc_dims* d, const float* const* t, int32_t n, vo
         const size_t n = (size_t)rup(rows, 32) * rup(k, 16) * 3;
         hipLaunchKernelGGL(pack_x6_kernel, dim3((unsigned)std::min<size_t>(2048, (n / 3 + 255) / 256)), dim3(256), 0, s,
                            pw + x6_src(w, x), rows, k, (unsigned short*)(pw + w.x6[x]));
+        HIPCHK(hipGetLastError());
+    }
+    for (int x = 0; x < 4; ++x) {
+        int rows, k;
+        x6_shape(w, x, &rows, &k);
+        const size_t n = (size_t)rup(rows, 16) * rup(k, 32);
+        hipLaunchKernelGGL(pack_x6q_kernel, dim3((unsigned)std::min<size_t>(2048, (n + 255) / 256)), dim3(256), 0, s,
+                           pw + x6_src(w, x), rows, k, (unsigned short*)(pw + w.x6q[x]));
         HIPCHK(hipGetLastError());
     }
     return 0;

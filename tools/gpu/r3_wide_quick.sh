@@ -14,10 +14,10 @@ for i in 1 2; do
   done
 done
 export TMPDIR=/tmp
-timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python -u tools/quick_time.py humanoid-run 32 > $O/prof.log 2>&1 || exit 1
+TDMPC_WIDE=1 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python -u tools/quick_time.py humanoid-run 32 > $O/prof.log 2>&1 || exit 1
 python tools/rocpd_summary.py $O/prof/run_results.db 8 --grid > $O/prof_summary.txt 2>&1
 grep -v amdgpu.ids $O/ab.txt
 cut -c1-140 $O/prof_summary.txt
 if [ -f tdmpc_amd/libtdmpc_hip_ws.so ]; then
-  TDMPC_LIB_PATH=$PWD/tdmpc_amd/libtdmpc_hip_ws.so timeout -k 10 200 python -u tools/ws_stamps.py 32 > $O/stamps.txt 2>&1 && grep -v amdgpu.ids $O/stamps.txt
+  TDMPC_WIDE=1 TDMPC_LIB_PATH=$PWD/tdmpc_amd/libtdmpc_hip_ws.so timeout -k 10 200 python -u tools/ws_stamps.py 32 > $O/stamps.txt 2>&1 && grep -v amdgpu.ids $O/stamps.txt
 fi
