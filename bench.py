@@ -98,17 +98,58 @@ def synthetic_obs(cfg, B, seed=0):
     return rs.standard_normal((B,) + tuple(cfg.obs_shape)).astype(np.float32)
 
 
+def _core_id(c: int) -> str:
+    try:
+        with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+            return f.read().strip()
+    except OSError:
+        return str(c)
+
+
 def physical_cores() -> int:
     """Physical cores this process may run on: the affinity mask's CPUs, counting SMT siblings once."""
     cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
-    seen = set()
-    for c in cpus:
-        try:
-            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
-                seen.add(f.read().strip())
-        except OSError:
-            seen.add(str(c))
-    return max(1, len(seen))
+    return max(1, len({_core_id(c) for c in cpus}))
+
+
+def cpu_quota():
+    """CPUs' worth of time the cgroup grants this process (cpu.max / cfs quota), None when unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def numa_cores():
+    """{node: [one CPU per physical core]} over the CPUs this process may use (node order, SMT siblings once)."""
+    allowed = set(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else set(range(os.cpu_count() or 1))
+    nodes = {}
+    base = "/sys/devices/system/node"
+    try:
+        names = sorted((d for d in os.listdir(base) if d.startswith("node") and d[4:].isdigit()), key=lambda d: int(d[4:]))
+    except OSError:
+        names = []
+    for d in names:
+        cpus = []
+        for part in open(f"{base}/{d}/cpulist").read().strip().split(","):
+            if part:
+                lo, _, hi = part.partition("-")
+                cpus += range(int(lo), int(hi or lo) + 1)
+        seen, pick = set(), []
+        for c in cpus:
+            if c in allowed and _core_id(c) not in seen:
+                seen.add(_core_id(c))
+                pick.append(c)
+        if pick:
+            nodes[int(d[4:])] = pick
+    return nodes or {0: sorted(allowed)}
 
 
 def cpu_baseline(cfg, budget_s: float, threads: int):
@@ -149,15 +190,36 @@ def cpu_baseline(cfg, budget_s: float, threads: int):
 
 
 def cpu_baselines(cfg, budget_s: float):
-    """The oracle at 1 thread, at the box's 16-CPU share and at every physical core this process may use
-    (the reference's CPU path on the host cores of the same box). The headline cpu_baseline is
-    the fastest of them (the CPU's best showing); all are reported."""
-    phys = physical_cores()
-    counts = sorted({1, min(16, phys), phys})
-    runs = {str(n): cpu_baseline(cfg, budget_s if n > 1 else 2 * budget_s, n) for n in counts}
+    """The oracle at 1 thread and on one NUMA node (the reference's CPU path on the host cores of the
+    same box). The node leg pins the process to one physical core per thread of NUMA node 0 (no SMT sibling, no
+    cross-socket traffic) with as many threads as the cgroup's CPU quota allows. The headline cpu_baseline is the
+    fastest leg (the CPU's best showing); all are reported.
+
+    Why not every core: the GPU box's cgroup grants this process ~16 CPUs of time (cpu.max) while its affinity mask
+    spans both sockets' 128 cores. Round 2 ran 128 unpinned threads and got 1.18 plan-steps/s against 10.1 at 16:
+    torch's intra-op threads were time-sliced by the quota (each parallel region waits for its slowest, throttled
+    thread) and spread over two sockets. Threads beyond the quota buy nothing."""
+    quota = cpu_quota()
+    nodes = numa_cores()
+    node0 = nodes[min(nodes)]
+    n_node = len(node0) if quota is None else max(1, min(len(node0), int(quota)))
+    keep = os.sched_getaffinity(0) if hasattr(os, "sched_setaffinity") else None
+    runs = {}
+    try:
+        for n in sorted({1, n_node}):
+            if keep is not None:
+                os.sched_setaffinity(0, node0[:n])
+            r = cpu_baseline(cfg, budget_s if n > 1 else 2 * budget_s, n)
+            r["sample"] += f"; pinned to {n} physical core(s) of NUMA node {min(nodes)}"
+            runs[str(n)] = r
+    finally:
+        if keep is not None:
+            os.sched_setaffinity(0, keep)
     best = max(runs.values(), key=lambda r: r["value"])
     out = dict(best)
-    out["physical_cores"] = phys
+    out["physical_cores"] = physical_cores()
+    out["numa_nodes"] = {str(k): len(v) for k, v in nodes.items()}
+    out["cgroup_cpu_quota"] = quota
     out["by_threads"] = {k: {"value": v["value"], "sample": v["sample"]} for k, v in runs.items()}
     return out
 
@@ -312,6 +374,67 @@ def learner_bench(cfg, dev, cpu=True, reps=30):
                                "cores": torch.get_num_threads(),
                                "sample": f"{n} oracle update() calls (reference math on torch CPU)"}
         out["speedup_vs_cpu"] = round(cdt / out["graph"]["ms_per_update"] * 1e3, 1)
+    return out
+
+
+def train_loop_bench(cfg, dev, reps=40):
+    """The training loop's per-env-step GPU work (src/train.py:94-108 after the seed steps): one agent.plan(obs,
+    step, t0) exactly as train.py calls it (TDMPC(cfg) defaults, host numpy obs, metrics synced to the host), then
+    one agent.update(buffer, step) (batch 512 from a 50k-transition device replay buffer, HIP-graph replay; the
+    update repacks the planner's weights from the learner's flat buffer inside that graph). Also each half alone,
+    in the same process: the loop's overhead over plan + update is what the hand-over between them costs."""
+    from types import SimpleNamespace
+    from tdmpc_amd.replay import ReplayBuffer
+    lcfg = bench_cfg(args_config_for_learner(cfg), batch_size=512)
+    lcfg.device = str(dev)
+    L = 500
+    rc = SimpleNamespace(**{**vars(lcfg), "train_steps": 50_000, "max_buffer_size": 10**6, "episode_length": L,
+                            "env_horizon": lcfg.horizon})
+    rs = np.random.RandomState(0)
+    O, A = lcfg.obs_shape[0], lcfg.action_dim
+    ep = SimpleNamespace(obs=torch.from_numpy(rs.standard_normal((L + 1, O)).astype(np.float32)),
+                         action=torch.from_numpy(rs.uniform(-1, 1, (L, A)).astype(np.float32)),
+                         reward=torch.from_numpy(rs.standard_normal(L).astype(np.float32)))
+    agent = TDMPC(lcfg)
+    agent.model.load_state_dict(synthetic_state_dict(lcfg, 0))
+    agent.model_target.load_state_dict(synthetic_state_dict(lcfg, 1))
+    agent.std = 0.05
+    buf = ReplayBuffer(rc, latent_plan=True)
+    for _ in range(50_000 // L - 1):
+        buf.add(ep)
+    obs = synthetic_obs(lcfg, 1, seed=0)[0]
+    step = 10**6
+
+    def plan(i):
+        agent.plan(obs, step=step + i, t0=(i == 0))
+
+    def update(i):
+        agent.update(buf, step + i)
+
+    def loop(i):
+        plan(i)
+        update(i)
+
+    out = {"config": f"{lcfg.task}: plan N={lcfg.num_samples} H={lcfg.horizon} iters={lcfg.iterations} (1 env, "
+                     f"train.py's call) + update batch {lcfg.batch_size} (replay 50k transitions)"}
+    for i in range(8):   # warm-up: both graphs captured, the planner packed from the learner's buffer
+        loop(i)
+    torch.cuda.synchronize()
+    res = {}
+    for name, fn in (("loop", loop), ("plan", plan), ("update", update), ("loop_again", loop)):
+        t = time.perf_counter()
+        for i in range(reps):
+            fn(100 + i)
+        torch.cuda.synchronize()
+        res[name] = (time.perf_counter() - t) / reps * 1e3
+    loop_ms = min(res["loop"], res["loop_again"])
+    out["ms_per_env_step"] = round(loop_ms, 4)
+    out["value"] = round(1e3 / loop_ms, 2)
+    out["unit"] = "env-steps/s"
+    out["plan_ms"] = round(res["plan"], 4)
+    out["update_ms"] = round(res["update"], 4)
+    out["overhead_us"] = round((loop_ms - res["plan"] - res["update"]) * 1e3, 1)
+    out["live_repack"] = bool(getattr(agent._learner, "_live_pack", False)) if hasattr(agent, "_learner") else None
     return out
 
 
@@ -644,6 +767,10 @@ def main():
     if not args.no_learner and world == 1 and cfg.modality == "state":
         learner = learner_bench(cfg, dev, cpu=not args.no_cpu)
 
+    loop = None
+    if not args.no_learner and world == 1 and cfg.modality == "state":
+        loop = train_loop_bench(cfg, dev)
+
     icem = None
     if not args.no_icem and world == 1 and cfg.modality == "state":
         icem = icem_bench(cfg, dev, cpu=not args.no_cpu)
@@ -698,6 +825,7 @@ def main():
             "configs": others,
             "replay_sampler": replay,
             "learner": learner,
+            "train_loop": loop,
             "icem": icem,
             "cpu_baseline": cpu,
         }

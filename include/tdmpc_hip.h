@@ -151,10 +151,19 @@ int tdmpc_reference_normals(const tdmpc_dims* dims, float* noise, int32_t batch,
 int tdmpc_num_param_tensors(const tdmpc_dims* dims);
 
 /* Pack the TOLD parameters (device pointers, reference state_dict order, fp32, contiguous nn.Linear
- * [out,in] / Conv2d [out,in,kh,kw] layout) into `packed` (replaces TDMPC.model for planning). Enqueued on
- * `stream`; re-run whenever the parameters change (after TDMPC.update). */
+ * [out,in] / Conv2d [out,in,kh,kw] layout) into `packed` (replaces TDMPC.model for planning). ONE kernel
+ * launch enqueued on `stream` (its job table is uploaded on the first call with a given set of pointers, so
+ * that call must not be inside a stream capture; later ones may be); re-run whenever the parameters change
+ * (after TDMPC.update -- the learner does so from its flat parameter buffer inside its update graph).
+ * `packed` must be zero-filled once when allocated: every tensor's region is rewritten whole, padding
+ * included, but the alignment gaps between regions are not, and padded vector reads may touch them. */
 int tdmpc_pack_weights(const tdmpc_dims* dims, const float* const* tensors, int32_t n_tensors,
                        void* packed, size_t packed_bytes, void* stream);
+
+/* Diagnostic, host only (no HIP call): bounds-checks tdmpc_pack_weights' job table for these dims, given the
+ * element count of each of the n reference tensors (state_dict order). Returns the number of jobs, or
+ * TDMPC_E_SIZE naming the first job that would write outside the layout or read outside its tensor. */
+int tdmpc_debug_pack_check(const tdmpc_dims* d, const int64_t* numel, int32_t n);
 
 /* TOLD.h for `batch` observations (tdmpc.py:115,121 / helper.enc). obs: state fp32 [batch, obs_dim]; pixels
  * uint8 [batch, C, S, S] if obs_is_u8 else fp32 of the same shape (raw 0..255 values, /255 inside).

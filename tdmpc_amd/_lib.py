@@ -17,6 +17,7 @@ PATHS = {"auto": 0, "layered": 1, "chain": 2, "chain32": 3, "chain16": 4, "split
 EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc_num_param_tensors",
             "tdmpc_pack_weights", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_pi_rollout",
             "tdmpc_cem_iter", "tdmpc_reference_normals", "tdmpc_last_error", "tdmpc_debug_plan1_stamps",
+            "tdmpc_debug_pack_check",
             "tdmpc_profile_begin", "tdmpc_profile_end", "tdmpc_icem_sizes_for", "tdmpc_plan_icem",
             # include/tdmpc_replay.h
             "tdmpc_replay_workspace_bytes", "tdmpc_replay_add_priorities", "tdmpc_replay_update_priorities",
@@ -126,6 +127,8 @@ def lib():
     L.tdmpc_reference_normals.argtypes = [C.POINTER(Dims), vp, i32, C.c_int64, i32, i32, i32, C.c_uint64,
                                           C.c_uint64, vp, i32, C.POINTER(C.c_uint64), vp]
     L.tdmpc_pack_weights.argtypes = [C.POINTER(Dims), C.POINTER(vp), i32, vp, sz, vp]
+    if hasattr(L, "tdmpc_debug_pack_check"):   # (diagnostic; absent from older builds used in A/B runs)
+        L.tdmpc_debug_pack_check.argtypes = [C.POINTER(Dims), C.POINTER(C.c_int64), i32]
     L.tdmpc_encode.argtypes = [C.POINTER(Dims), vp, vp, i32, i32, vp, vp, vp]
     L.tdmpc_plan.argtypes = [C.POINTER(Dims), C.POINTER(PlanParams), vp, vp, i32, vp, vp, vp, vp, vp,
                              vp, vp, vp, vp, vp, vp, sz, vp]
@@ -159,7 +162,7 @@ def lib():
     L.tdmpc_lg_lerp.argtypes = [vp, vp, C.c_int64, C.c_float, vp]
     L.tdmpc_lg_act.argtypes = [vp, vp, C.c_int64, i32, vp]
     for name in EXPORTED:
-        if not hasattr(L, name):
+        if not hasattr(L, name) and not (name.startswith("tdmpc_debug_") and os.environ.get("TDMPC_LIB_PATH")):
             raise RuntimeError(f"{LIB_PATH} does not export {name}")
     if L.tdmpc_abi_version() != ABI_VERSION:
         raise RuntimeError("libtdmpc_hip ABI version mismatch")

@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <vector>
 
 #include "../../include/tdmpc_hip.h"
 
@@ -95,9 +96,12 @@ struct Layout {
     size_t wq1x, bq1x, g1, be1;                      // panel [2M][Kx]; LN1 gamma/beta [2M]
     size_t wq2, bq2, g2, be2;                        // 2 panels [M][M]; LN2 [2M]
     size_t wq3, bq3;                                 // [2][M], [2]
-    // the chain kernels' weight panels again as three bf16 planes (x6 layout, X6_* below, pack_x6_kernel)
+    // the chain kernels' weight panels again as three bf16 planes (x6 layout, X6_* below, pack_fused_kernel)
     size_t x6[9];
-    // the wide step kernel's copies of X6_W1X .. X6_W3D in the x6q layout (16-row x 32-k blocks, pack_x6q_kernel)
+    // the wide step kernel's copies of X6_W1X .. X6_W3D in the x6q layout: block (nb, g) of 16 rows x 32 k is
+    // [3 planes][64 lanes][8 bf16]: lane l (m = l & 15, q = l >> 4) element j holds row 16 nb + m,
+    // k = 32 g + 16 (j >> 2) + 4 q + (j & 3) -- the v_mfma_f32_16x16x32_bf16 A fragment, in the k order in which a
+    // 16x16 accumulator tile pair (a lane holding features 16t + 4q + i of its row) is the next layer's B fragment
     size_t x6q[4];
     size_t total;
 };
@@ -1059,7 +1063,7 @@ DEVI void ring_run(floatx16 (&acc)[TN], float4 (&wr)[D][TN], const float* sA, co
 // operand x = hi + mid + lo (bf16 each, the residuals exact in fp32); a product keeps the six terms down to
 // 2^-16 relative (hi.hi, hi.mid, mid.hi, hi.lo, lo.hi, mid.mid), dropping mid.lo, lo.mid, lo.lo (<= 2^-24
 // relative, the size of one fp32 rounding), and accumulates in fp32: the accuracy of an fp32 GEMM, at 6/16 of
-// the f32 MFMA cycles. Weights come pre-split (Layout::x6, pack_x6_kernel); the activations stay fp32 in LDS
+// the f32 MFMA cycles. Weights come pre-split (Layout::x6, pack_fused_kernel); the activations stay fp32 in LDS
 // and are split as they are read.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 #ifndef X6_D3
@@ -1067,7 +1071,7 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 #endif
 DEVI bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 
-// Weights (pack time, pack_x6_kernel): x = hi + mid + lo exactly, each part round-to-nearest (the smallest dropped
+// Weights (pack time, pack_fused_kernel): x = hi + mid + lo exactly, each part round-to-nearest (the smallest dropped
 // terms). A finite weight beyond bf16's largest value (whose rounding would be inf) takes its truncated top half as hi,
 // and a non-finite one passes through whole in hi (mid = lo = 0).
 DEVI void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
@@ -2997,69 +3001,6 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(const void* in, int in_u
     }
 }
 
-// ------------------------------------------------------------------------------------------------ packing
-// dst panel (total `dcols` columns): element (r, dc0 + c) = src[r * sld + sc0 + c], r < rows, c < cols
-__global__ void pack_panel_kernel(const float* src, int sld, int sc0, int rows, int cols, float* dst, int dcols,
-                                  int dc0) {
-    const size_t total = (size_t)rows * cols;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = i / cols, c = i % cols;
-        dst[pidx(r, dc0 + c, dcols)] = src[r * sld + sc0 + c];
-    }
-}
-
-// dst[c * rows + r] = src[r * cols + c]
-__global__ void pack_transpose_kernel(const float* src, int rows, int cols, float* dst) {
-    const size_t total = (size_t)rows * cols;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = i / cols, c = i % cols;
-        dst[c * rows + r] = src[i];
-    }
-}
-
-// Candidate actions [B][H][T][A] -> X_t panels' action columns (zero pad to Ap) (estimate_value entry).
-// fp32 weight panel [rows/32][K/4][32][4] -> the x6 planes (Layout::x6): block (nb, g) [3][64][8] bf16
-__global__ void pack_x6_kernel(const float* src, int rows, int K, unsigned short* dst) {
-    const int G = (K + 15) / 16;
-    const size_t total = (size_t)((rows + 31) / 32) * G * 512;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const int j = i & 7, lane = (i >> 3) & 63;
-        const size_t blk = i >> 9;
-        const int g = (int)(blk % G), nb = (int)(blk / G);
-        const int r = lane & 31, h = lane >> 5;
-        const int k = 16 * g + 8 * (j >> 2) + 4 * h + (j & 3);
-        const float x = k < K ? src[(size_t)nb * K * 32 + (size_t)(k >> 2) * 128 + r * 4 + (k & 3)] : 0.f;
-        __bf16 hi, mid, lo;
-        split3(x, hi, mid, lo);
-        dst[(blk * 3 + 0) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, hi);
-        dst[(blk * 3 + 1) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, mid);
-        dst[(blk * 3 + 2) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, lo);
-    }
-}
-
-// The x6q layout (wide_step_kernel): block (nb, g) of 16 rows x 32 k is [3 planes][64 lanes][8 bf16]: lane l
-// (m = l & 15, q = l >> 4) element j holds row 16 nb + m, k = 32 g + 16 (j >> 2) + 4 q + (j & 3) -- the
-// v_mfma_f32_16x16x32_bf16 A fragment, in the k order in which a 16x16 accumulator tile pair (a lane holding
-// features 16t + 4q + i of its row) is the next layer's B fragment.
-__global__ void pack_x6q_kernel(const float* src, int rows, int K, unsigned short* dst) {
-    const int G = (K + 31) / 32;
-    const size_t total = (size_t)((rows + 15) / 16) * G * 512;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const int j = i & 7, lane = (i >> 3) & 63;
-        const size_t blk = i >> 9;
-        const int g = (int)(blk % G), nb = (int)(blk / G);
-        const int r = 16 * nb + (lane & 15), q = lane >> 4;
-        const int k = 32 * g + 16 * (j >> 2) + 4 * q + (j & 3);
-        const float x = k < K && r < rows ? src[(size_t)(r >> 5) * K * 32 + (size_t)(k >> 2) * 128 + (r & 31) * 4 + (k & 3)]
-                                          : 0.f;
-        __bf16 hi, mid, lo;
-        split3(x, hi, mid, lo);
-        dst[(blk * 3 + 0) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, hi);
-        dst[(blk * 3 + 1) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, mid);
-        dst[(blk * 3 + 2) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, lo);
-    }
-}
-
 // candidate actions act [B][H][Ts][A] -> the action columns of rows e * Td + r0 + r of X_t (t < H)
 __global__ void scatter_actions_kernel(const float* act, float* X, size_t x_stride, int H, int Ts, int A, int Ap,
                                        int Kx, int B, int Td, int r0) {
@@ -4169,6 +4110,11 @@ bool use_plan1(const Ctx& c) {
 }
 
 // encode_kernel has written z0 and the initial mean / std; one memset node (the hand-off counters) + one launch.
+// zero fill as a kernel of our own (the graph-captured paths avoid hipMemsetAsync nodes: see plan1_launch)
+__global__ void zero_words_kernel(unsigned* p, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0u;
+}
+
 int plan1_launch(const Ctx& c, const tdmpc_plan_params* prm, const float* noise, const double* u, float* prev_mean,
                  float* action, float* metrics, float* elite_out, float* score_out, float* value_out, float* mean_out,
                  float* std_out) {
@@ -4201,7 +4147,12 @@ int plan1_launch(const Ctx& c, const tdmpc_plan_params* prm, const float* noise,
         const char* e = getenv("TDMPC_P1_DEBUG_SKIP");   // test knob, read per launch (captured with the graph)
         a.debug_skip = e && atoi(e) ? 1 : 0;
     }
-    HIPCHK(hipMemsetAsync(c.k.p1 + rg.o_sync, 0, P1_NG * 256 + 256, c.s));   // counters + error word
+    // counters + error word zeroed by a kernel of our own, not hipMemsetAsync: in a replayed HIP graph the memset
+    // node was seen writing a stale 16-byte pattern instead of zeros (the kernel then exits on a garbage error word
+    // with the NaN-poisoned outputs; tests/test_gpu_plan.py::test_plan_reference_draws_device_equals_torch)
+    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(P1_NG * 64 + 64), 0, c.s, (unsigned*)(c.k.p1 + rg.o_sync),
+                       P1_NG * 64 + 64);
+    HIPCHK(hipGetLastError());
     const size_t lds = p1_lds_bytes(c.H, a.K, w.A, c.T);
     if (p1_ks(w) == 4) hipLaunchKernelGGL(plan1_kernel<4>, dim3(P1_NG * P1_WPG), dim3(P1_NT), lds, c.s, a);
     else hipLaunchKernelGGL(plan1_kernel<6>, dim3(P1_NG * P1_WPG), dim3(P1_NT), lds, c.s, a);
@@ -4234,17 +4185,234 @@ int setup_ctx(Ctx& c, const tdmpc_dims* d, const void* packed, void* ws, size_t 
     return init_attrs();
 }
 
-int launch_pack_panel(const float* src, int sld, int sc0, int rows, int cols, float* dst, int dcols, int dc0,
-                      hipStream_t s) {
-    hipLaunchKernelGGL(pack_panel_kernel, dim3(std::min(1024, (rows * cols + 255) / 256)), dim3(256), 0, s, src, sld,
-                       sc0, rows, cols, dst, dcols, dc0);
-    HIPCHK(hipGetLastError());
-    return 0;
+// ---- the fused weight pack (tdmpc_pack_weights): ONE launch writes every region of the packed buffer -- fp32
+// copies, transposes, weight panels, their x6 and x6q bf16 planes -- straight from the reference's tensors (the
+// learner passes views of its flat parameter buffer, so a post-update repack is one kernel, capturable into the
+// update's HIP graph). Each job's padded region is written whole (zeros where the layout pads), so no memset.
+// The x6 / x6q planes are split from the source tensors directly (the same values as from the fp32 panel).
+struct PackSrc {                 // a weight panel's source: rows [0, r0) of p0, then [r0, r0 + r1) of p1
+    const float* p0; const float* p1;
+    int r0, r1, sld, ncols;      // source row length; plain map: panel column k < ncols <- source column k
+    int first;                   // first-layer map: panel [a | 0 | z | 0] <- source [z | a] (L = ncols, A below)
+    int L, A, Ap;
+};
+__host__ __device__ inline float pack_val(const PackSrc& m, int r, int k) {
+    const float* row;
+    if (r < m.r0) row = m.p0 + (size_t)r * m.sld;
+    else if (r < m.r0 + m.r1) row = m.p1 + (size_t)(r - m.r0) * m.sld;
+    else return 0.f;
+    int col;
+    if (m.first) col = k < m.A ? m.L + k : (k >= m.Ap && k < m.Ap + m.L ? k - m.Ap : -1);
+    else col = k < m.ncols ? k : -1;
+    return col < 0 ? 0.f : row[col];
+}
+enum { PJ_COPY, PJ_TRANS, PJ_PANEL, PJ_X6, PJ_X6Q };
+struct PackJob {
+    int kind;
+    int blk0;                    // first workgroup of this job in the launch
+    size_t dst;                  // float offset into the packed buffer
+    long work;                   // work items
+    const float* src; int n, rows, cols;   // COPY: n values then zeros to `work`; TRANS: [rows][cols] -> [cols][rows]
+    PackSrc m; int prow, pk;     // PANEL: [prow][pk] panel; X6 / X6Q: prow rows x pk k of the source map
+};
+constexpr int PACK_WG = 256, PACK_PER = 8;   // threads per workgroup, items per thread
+
+__global__ void __launch_bounds__(PACK_WG) pack_fused_kernel(const PackJob* jobs, int nj, float* pw) {
+    // the workgroup's job: last job whose blk0 <= blockIdx.x (binary search over the job table)
+    int lo = 0, hi = nj - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (jobs[mid].blk0 <= (int)blockIdx.x) lo = mid;
+        else hi = mid - 1;
+    }
+    const PackJob& J = jobs[lo];
+    const long base = (long)(blockIdx.x - J.blk0) * PACK_WG * PACK_PER;
+    for (int u = 0; u < PACK_PER; ++u) {
+        const long i = base + (long)u * PACK_WG + threadIdx.x;
+        if (i >= J.work) break;
+        switch (J.kind) {
+            case PJ_COPY: pw[J.dst + i] = i < J.n ? J.src[i] : 0.f; break;
+            case PJ_TRANS: {
+                const long r = i % J.rows, c = i / J.rows;   // dst[c * rows + r] = src[r * cols + c]
+                pw[J.dst + i] = J.src[r * J.cols + c];
+                break;
+            }
+            case PJ_PANEL: {   // dst index i = pidx(r, k, pk): [r / 32][k / 4][r % 32][k % 4]
+                const int e = i & 3, rr = (i >> 2) & 31;
+                const long q = i >> 7;
+                const int kq = (int)(q % (J.pk / 4));
+                const int r = (int)(q / (J.pk / 4)) * 32 + rr, k = kq * 4 + e;
+                pw[J.dst + i] = pack_val(J.m, r, k);
+                break;
+            }
+            case PJ_X6: case PJ_X6Q: {
+                const int j = i & 7, lane = (i >> 3) & 63;
+                const long blk = i >> 9;
+                int r, k;
+                if (J.kind == PJ_X6) {   // the x6 layout (Layout::x6): 32-row x 16-k blocks
+                    const int G = (J.pk + 15) / 16;
+                    const int g = (int)(blk % G), nb = (int)(blk / G);
+                    r = 32 * nb + (lane & 31);
+                    k = 16 * g + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
+                } else {                 // the x6q layout (Layout::x6q): 16-row x 32-k blocks
+                    const int G = (J.pk + 31) / 32;
+                    const int g = (int)(blk % G), nb = (int)(blk / G);
+                    r = 16 * nb + (lane & 15);
+                    k = 32 * g + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
+                }
+                const float x = k < J.pk && r < J.prow ? pack_val(J.m, r, k) : 0.f;
+                __bf16 h, m, l;
+                split3(x, h, m, l);
+                unsigned short* d = (unsigned short*)(pw + J.dst);
+                d[(blk * 3 + 0) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, h);
+                d[(blk * 3 + 1) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, m);
+                d[(blk * 3 + 2) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, l);
+                break;
+            }
+        }
+    }
 }
 
-int launch_transpose(const float* src, int rows, int cols, float* dst, hipStream_t s) {
-    hipLaunchKernelGGL(pack_transpose_kernel, dim3(std::min(1024, (rows * cols + 255) / 256)), dim3(256), 0, s, src,
-                       rows, cols, dst);
+// The job list of a layout and the reference tensors t (state_dict order, tdmpc_num_param_tensors of them)
+void pack_jobs(const Layout& w, const float* const* t, std::vector<PackJob>& jobs) {
+    const int M = w.M, L = w.L, A = w.A;
+    auto job = [&](int kind, size_t dst, long work) -> PackJob& {
+        PackJob j;
+        memset(&j, 0, sizeof j);
+        j.kind = kind; j.dst = dst; j.work = work;
+        jobs.push_back(j);
+        return jobs.back();
+    };
+    auto cp = [&](size_t dst, const float* src, int n) {   // zero tail to the 64-float slot take() reserved
+        PackJob& j = job(PJ_COPY, dst, (long)rup(n, 64));
+        j.src = src; j.n = n;
+    };
+    auto tr = [&](size_t dst, const float* src, int rows, int cols) {
+        PackJob& j = job(PJ_TRANS, dst, (long)rows * cols);
+        j.src = src; j.rows = rows; j.cols = cols;
+    };
+    auto msrc = [&](const float* p0, const float* p1, int r0, int r1, int sld, int ncols, int first) {
+        PackSrc m;
+        memset(&m, 0, sizeof m);
+        m.p0 = p0; m.p1 = p1 ? p1 : p0; m.r0 = r0; m.r1 = r1; m.sld = sld; m.ncols = ncols; m.first = first;
+        m.L = L; m.A = A; m.Ap = w.Ap;
+        return m;
+    };
+    auto panel = [&](size_t dst, const PackSrc& m, int prow, int pk) {
+        PackJob& j = job(PJ_PANEL, dst, (long)rup(prow, 32) * pk);
+        j.m = m; j.prow = prow; j.pk = pk;
+    };
+    int i = 0;
+    if (w.modality == 0) {
+        tr(w.enc_w1t, t[i++], w.E, w.obs_dim);
+        cp(w.enc_b1, t[i++], w.E);
+        if (w.enc_norm) { cp(w.enc_lng, t[i++], w.E); cp(w.enc_lnb, t[i++], w.E); }
+        tr(w.enc_w2t, t[i++], L, w.E);
+        cp(w.enc_b2, t[i++], L);
+    } else {
+        static const int ks[4] = {7, 5, 3, 3};
+        int cin = w.img_c;
+        for (int c = 0; c < 4; ++c) {
+            const float* cw = t[i++];
+            cp(w.cw[c], cw, w.nch * cin * ks[c] * ks[c]);
+            tr(w.cwt[c], cw, w.nch, cin * ks[c] * ks[c]);
+            cp(w.cb[c], t[i++], w.nch);
+            cin = w.nch;
+        }
+        tr(w.pl_wt, t[i++], L, w.flat);
+        cp(w.pl_b, t[i++], L);
+    }
+    const int KI = L + A;
+    const float* const* dyn = t + i;        // 0.w 0.b 2.w 2.b 4.w 4.b
+    const float* const* rew = dyn + 6;
+    const float* const* pi = rew + 6;
+    const float* const* q1 = pi + 6;        // 0.w 0.b 1.w 1.b 3.w 3.b 4.w 4.b 6.w 6.b
+    const float* const* q2 = q1 + 10;
+    const PackSrc sW1X = msrc(dyn[0], rew[0], M, M, KI, L, 1), sW2D = msrc(dyn[2], nullptr, M, 0, M, M, 0),
+                  sW2R = msrc(rew[2], nullptr, M, 0, M, M, 0), sW3D = msrc(dyn[4], nullptr, L, 0, M, M, 0),
+                  sWP1 = msrc(pi[0], nullptr, M, 0, L, L, 0), sWP2 = msrc(pi[2], nullptr, M, 0, M, M, 0),
+                  sWP3 = msrc(pi[4], nullptr, A, 0, M, M, 0), sWQ1X = msrc(q1[0], q2[0], M, M, KI, L, 1),
+                  sWQ2 = msrc(q1[4], q2[4], M, M, M, M, 0);
+    panel(w.w1x, sW1X, 2 * M, w.Kx);
+    cp(w.b1x, dyn[1], M); cp(w.b1x + M, rew[1], M);
+    panel(w.w2d, sW2D, M, M); cp(w.b2d, dyn[3], M);
+    panel(w.w3d, sW3D, w.Lr, M); cp(w.b3d, dyn[5], L);
+    panel(w.w2r, sW2R, M, M); cp(w.b2r, rew[3], M);
+    cp(w.w3r, rew[4], M); cp(w.b3r, rew[5], 1);
+    panel(w.wp1, sWP1, M, w.Lp); cp(w.bp1, pi[1], M);
+    panel(w.wp2, sWP2, M, M); cp(w.bp2, pi[3], M);
+    panel(w.wp3, sWP3, w.Ar, M); cp(w.bp3, pi[5], A);
+    panel(w.wq1x, sWQ1X, 2 * M, w.Kx);
+    panel(w.wq2, sWQ2, 2 * M, M);
+    const float* const* qs[2] = {q1, q2};
+    for (int q = 0; q < 2; ++q) {
+        const float* const* Q = qs[q];
+        // (the 2M-float LN / bias slots hold both heads: each copy's zero tail stops at the next head's start)
+        PackJob* jb;
+        cp(w.bq1x + q * M, Q[1], M); cp(w.g1 + q * M, Q[2], M); cp(w.be1 + q * M, Q[3], M);
+        cp(w.bq2 + q * M, Q[5], M); cp(w.g2 + q * M, Q[6], M); cp(w.be2 + q * M, Q[7], M);
+        cp(w.wq3 + q * M, Q[8], M);
+        jb = &job(PJ_COPY, w.bq3 + q, 1);
+        jb->src = Q[9]; jb->n = 1;
+    }
+    const PackSrc* xs[X6_N] = {&sW1X, &sW2D, &sW2R, &sW3D, &sWP1, &sWP2, &sWP3, &sWQ1X, &sWQ2};
+    for (int x = 0; x < X6_N; ++x) {
+        int rows, k;
+        x6_shape(w, x, &rows, &k);
+        PackJob& j = job(PJ_X6, w.x6[x], (long)((rows + 31) / 32) * ((k + 15) / 16) * 512);
+        j.m = *xs[x]; j.prow = rows; j.pk = k;
+    }
+    for (int x = 0; x < 4; ++x) {
+        int rows, k;
+        x6_shape(w, x, &rows, &k);
+        PackJob& j = job(PJ_X6Q, w.x6q[x], (long)((rows + 15) / 16) * ((k + 31) / 32) * 512);
+        j.m = *xs[x]; j.prow = rows; j.pk = k;
+    }
+}
+
+// Job tables live in device memory, one immutable copy per distinct table (a HIP graph that captured a pack keeps
+// pointing at its table, whatever other planners pack later), uploaded on first use by a synchronous copy -- not
+// while the stream is being captured: the learner packs once before it captures its update.
+struct PackTable { std::vector<PackJob> host; PackJob* dev; };
+std::vector<PackTable> g_pack_tables;
+
+int launch_pack(std::vector<PackJob>& jobs, float* pw, hipStream_t s) {
+    int blk = 0;
+    for (PackJob& j : jobs) {
+        j.blk0 = blk;
+        blk += (int)((j.work + PACK_WG * PACK_PER - 1) / (PACK_WG * PACK_PER));
+    }
+    const size_t nb = jobs.size() * sizeof(PackJob);
+    const PackJob* dev = nullptr;
+    for (const PackTable& t : g_pack_tables)
+        if (t.host.size() == jobs.size() && !memcmp(t.host.data(), jobs.data(), nb)) { dev = t.dev; break; }
+    if (!dev) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIPCHK(hipStreamIsCapturing(s, &cs));
+        if (cs != hipStreamCaptureStatusNone) {
+            snprintf(g_err, sizeof g_err, "tdmpc_pack_weights: new tensors while capturing (pack once before capture)");
+            return TDMPC_E_DIMS;
+        }
+        // tables are carved from 256 KiB device chunks and written by a copy on the caller's stream, drained
+        // before returning (the host vector then dies)
+        static char* chunk = nullptr;
+        static size_t used = 0;
+        const size_t need = rup(nb, 256), CH = 256 * 1024;
+        if (need > CH) { snprintf(g_err, sizeof g_err, "tdmpc_pack_weights: job table too large"); return TDMPC_E_SIZE; }
+        if (!chunk || used + need > CH) {
+            HIPCHK(hipMalloc(&chunk, CH));
+            used = 0;
+        }
+        PackTable t;
+        t.host = jobs;
+        t.dev = (PackJob*)(chunk + used);
+        used += need;
+        HIPCHK(hipMemcpyAsync(t.dev, jobs.data(), nb, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+        g_pack_tables.push_back(t);
+        dev = t.dev;
+    }
+    hipLaunchKernelGGL(pack_fused_kernel, dim3((unsigned)blk), dim3(PACK_WG), 0, s, dev, (int)jobs.size(), pw);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -4417,95 +4585,49 @@ int tdmpc_pack_weights(const tdmpc_dims* d, const float* const* t, int32_t n, vo
     if (init_attrs()) return TDMPC_E_HIP;
     for (int i = 0; i < n; ++i)
         if (!t[i]) return TDMPC_E_NULL;
-    hipStream_t s = (hipStream_t)stream;
-    float* pw = (float*)packed;
-    const int M = w.M, L = w.L, A = w.A, F = 4;
-    int rc;
-    HIPCHK(hipMemsetAsync(packed, 0, w.total * 4, s));
-    auto cp = [&](size_t dst, const float* src, size_t nfl) {
-        return hipMemcpyAsync(pw + dst, src, nfl * F, hipMemcpyDeviceToDevice, s);
+    std::vector<PackJob> jobs;
+    pack_jobs(w, t, jobs);
+    return launch_pack(jobs, (float*)packed, (hipStream_t)stream);
+}
+
+int tdmpc_debug_pack_check(const tdmpc_dims* d, const int64_t* numel, int32_t n) {
+    // Host-only bounds check of the fused pack's job table (no HIP call): every write inside the layout, every
+    // read inside its source tensor. Tensor i is given the fake base address (i + 1) << 40.
+    if (!d || !numel) return TDMPC_E_NULL;
+    if (!check_dims(d)) return TDMPC_E_DIMS;
+    Layout w;
+    make_layout(d, &w);
+    if (n != tdmpc_num_param_tensors(d)) return TDMPC_E_DIMS;
+    std::vector<const float*> t(n);
+    for (int i = 0; i < n; ++i) t[i] = (const float*)((uintptr_t)(i + 1) << 40);
+    std::vector<PackJob> jobs;
+    pack_jobs(w, t.data(), jobs);
+    auto in_tensor = [&](const float* p, long last) -> bool {   // reads p[0 .. last]
+        const uintptr_t u = (uintptr_t)p;
+        const long i = (long)(u >> 40) - 1;
+        if (i < 0 || i >= n) return false;
+        const long off = (long)((u & (((uintptr_t)1 << 40) - 1)) / 4);
+        return off + last < numel[i];
     };
-    int i = 0;
-    if (w.modality == 0) {
-        if ((rc = launch_transpose(t[i++], w.E, w.obs_dim, pw + w.enc_w1t, s))) return rc;
-        HIPCHK(cp(w.enc_b1, t[i++], w.E));
-        if (w.enc_norm) {
-            HIPCHK(cp(w.enc_lng, t[i++], w.E));
-            HIPCHK(cp(w.enc_lnb, t[i++], w.E));
+    auto src_ok = [&](const PackSrc& m, int maxk) -> bool {
+        const int maxcol = m.first ? m.L + m.A - 1 : std::min(maxk, m.ncols - 1);
+        if (m.r0 > 0 && !in_tensor(m.p0, (long)(m.r0 - 1) * m.sld + maxcol)) return false;
+        if (m.r1 > 0 && !in_tensor(m.p1, (long)(m.r1 - 1) * m.sld + maxcol)) return false;
+        return true;
+    };
+    for (size_t j = 0; j < jobs.size(); ++j) {
+        const PackJob& J = jobs[j];
+        const double end = J.kind == PJ_X6 || J.kind == PJ_X6Q ? (double)J.dst + 1.5 * J.work : (double)(J.dst + J.work);
+        bool ok = end <= (double)w.total;
+        if (J.kind == PJ_COPY) ok = ok && J.n <= J.work && in_tensor(J.src, J.n - 1);
+        else if (J.kind == PJ_TRANS) ok = ok && in_tensor(J.src, (long)J.rows * J.cols - 1);
+        else ok = ok && src_ok(J.m, J.pk - 1);
+        if (!ok) {
+            snprintf(g_err, sizeof g_err, "pack job %d (kind %d, dst %zu) out of bounds", (int)j, J.kind, J.dst);
+            return TDMPC_E_SIZE;
         }
-        if ((rc = launch_transpose(t[i++], L, w.E, pw + w.enc_w2t, s))) return rc;
-        HIPCHK(cp(w.enc_b2, t[i++], L));
-    } else {
-        static const int ks[4] = {7, 5, 3, 3};
-        int cin = w.img_c;
-        for (int c = 0; c < 4; ++c) {
-            HIPCHK(cp(w.cw[c], t[i++], (size_t)w.nch * cin * ks[c] * ks[c]));
-            if ((rc = launch_transpose(t[i - 1], w.nch, cin * ks[c] * ks[c], pw + w.cwt[c], s))) return rc;
-            HIPCHK(cp(w.cb[c], t[i++], w.nch));
-            cin = w.nch;
-        }
-        if ((rc = launch_transpose(t[i++], L, w.flat, pw + w.pl_wt, s))) return rc;
-        HIPCHK(cp(w.pl_b, t[i++], L));
     }
-    const int KI = L + A;  // reference input width of cat[z, a]
-    // first layers: panel [rows][Kx] columns [a | 0 | z | 0] <- reference [z | a]
-    auto first = [&](size_t dst, int row0, int rows, const float* src) -> int {
-        int r;
-        if ((r = launch_pack_panel(src, KI, L, rows, A, pw + dst + (size_t)row0 * w.Kx, w.Kx, 0, s))) return r;
-        return launch_pack_panel(src, KI, 0, rows, L, pw + dst + (size_t)row0 * w.Kx, w.Kx, w.Ap, s);
-    };
-    auto panel = [&](size_t dst, const float* src, int rows, int cols, int dcols) {
-        return launch_pack_panel(src, cols, 0, rows, cols, pw + dst, dcols, 0, s);
-    };
-    // dynamics: 0.w 0.b 2.w 2.b 4.w 4.b
-    if ((rc = first(w.w1x, 0, M, t[i++]))) return rc;
-    HIPCHK(cp(w.b1x, t[i++], M));
-    if ((rc = panel(w.w2d, t[i++], M, M, M))) return rc;
-    HIPCHK(cp(w.b2d, t[i++], M));
-    if ((rc = panel(w.w3d, t[i++], L, M, M))) return rc;
-    HIPCHK(cp(w.b3d, t[i++], L));
-    // reward
-    if ((rc = first(w.w1x, M, M, t[i++]))) return rc;
-    HIPCHK(cp(w.b1x + M, t[i++], M));
-    if ((rc = panel(w.w2r, t[i++], M, M, M))) return rc;
-    HIPCHK(cp(w.b2r, t[i++], M));
-    HIPCHK(cp(w.w3r, t[i++], M));
-    HIPCHK(cp(w.b3r, t[i++], 1));
-    // pi
-    if ((rc = panel(w.wp1, t[i++], M, L, w.Lp))) return rc;
-    HIPCHK(cp(w.bp1, t[i++], M));
-    if ((rc = panel(w.wp2, t[i++], M, M, M))) return rc;
-    HIPCHK(cp(w.bp2, t[i++], M));
-    if ((rc = panel(w.wp3, t[i++], A, M, M))) return rc;
-    HIPCHK(cp(w.bp3, t[i++], A));
-    // Q1, Q2: 0.w 0.b 1.w 1.b 3.w 3.b 4.w 4.b 6.w 6.b
-    for (int q = 0; q < 2; ++q) {
-        if ((rc = first(w.wq1x, q * M, M, t[i++]))) return rc;
-        HIPCHK(cp(w.bq1x + q * M, t[i++], M));
-        HIPCHK(cp(w.g1 + q * M, t[i++], M)); HIPCHK(cp(w.be1 + q * M, t[i++], M));
-        if ((rc = panel(w.wq2 + (size_t)q * M * M, t[i++], M, M, M))) return rc;
-        HIPCHK(cp(w.bq2 + q * M, t[i++], M));
-        HIPCHK(cp(w.g2 + q * M, t[i++], M)); HIPCHK(cp(w.be2 + q * M, t[i++], M));
-        HIPCHK(cp(w.wq3 + q * M, t[i++], M)); HIPCHK(cp(w.bq3 + q, t[i++], 1));
-    }
-    // the x6 copies of the chain kernels' panels (stream-ordered after the panels above)
-    for (int x = 0; x < X6_N; ++x) {
-        int rows, k;
-        x6_shape(w, x, &rows, &k);
-        const size_t n = (size_t)rup(rows, 32) * rup(k, 16) * 3;
-        hipLaunchKernelGGL(pack_x6_kernel, dim3((unsigned)std::min<size_t>(2048, (n / 3 + 255) / 256)), dim3(256), 0, s,
-                           pw + x6_src(w, x), rows, k, (unsigned short*)(pw + w.x6[x]));
-        HIPCHK(hipGetLastError());
-    }
-    for (int x = 0; x < 4; ++x) {
-        int rows, k;
-        x6_shape(w, x, &rows, &k);
-        const size_t n = (size_t)rup(rows, 16) * rup(k, 32);
-        hipLaunchKernelGGL(pack_x6q_kernel, dim3((unsigned)std::min<size_t>(2048, (n + 255) / 256)), dim3(256), 0, s,
-                           pw + x6_src(w, x), rows, k, (unsigned short*)(pw + w.x6q[x]));
-        HIPCHK(hipGetLastError());
-    }
-    return 0;
+    return (int)jobs.size();
 }
 
 int tdmpc_encode(const tdmpc_dims* d, const void* packed, const void* obs, int32_t obs_is_u8, int32_t batch,
@@ -4738,7 +4860,8 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
            : prm->path;   // (persist: whole plans only; the retired 64-row path is path 6)
     if (rows != c.T) { snprintf(g_err, sizeof g_err, "rows must equal N+P"); return TDMPC_E_DIMS; }
     const int T = c.T, L = c.w.L;
-    HIPCHK(hipMemsetAsync(c.k.z0, 0, (size_t)B * c.w.Lp * 4, c.s));
+    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(256), 0, c.s, (unsigned*)c.k.z0, (int)((size_t)B * c.w.Lp));
+    HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy2DAsync(c.k.z0, c.w.Lp * 4, z0, L * 4, L * 4, B, hipMemcpyDeviceToDevice, c.s));
     hipLaunchKernelGGL(scatter_actions_kernel, dim3(512), dim3(256), 0, c.s, actions, c.k.X, c.k.x_stride, H, T, c.A,
                        c.w.Ap, c.Kx, B, T, 0);
@@ -4767,7 +4890,8 @@ int tdmpc_estimate_value(const tdmpc_dims* d, const tdmpc_plan_params* prm, cons
 // z0 [B][L] -> the workspace's padded z0 [B][Lp] and the latent columns of X_0 for all T rows of every env
 static int load_z0(const Ctx& c, const float* z0) {
     const int L = c.w.L;
-    HIPCHK(hipMemsetAsync(c.k.z0, 0, (size_t)c.B * c.w.Lp * 4, c.s));
+    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(256), 0, c.s, (unsigned*)c.k.z0, (int)((size_t)c.B * c.w.Lp));
+    HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy2DAsync(c.k.z0, c.w.Lp * 4, z0, L * 4, L * 4, c.B, hipMemcpyDeviceToDevice, c.s));
     return prep(c, nullptr, 0, c.k.z0);
 }

@@ -75,7 +75,7 @@ class TdICEM:
         sz = _lib.Sizes()
         _lib.check(self.L.tdmpc_icem_sizes_for(C.byref(d), C.byref(sz)), "tdmpc_icem_sizes_for")
         dev = self.device
-        self.packed = torch.empty(sz.packed_weight_bytes // 4, dtype=torch.float32, device=dev)
+        self.packed = torch.zeros(sz.packed_weight_bytes // 4, dtype=torch.float32, device=dev)   # (gaps stay 0)
         self.workspace = torch.empty(sz.workspace_bytes // 4, dtype=torch.float32, device=dev)
         self.E_max = int(cfg.fraction_elites_reused * K)
         T_max = N + self.E_max + self.P_max

@@ -144,6 +144,7 @@ class Learner:
             agent.pi_optim = torch.optim.Adam(self.pi_params, lr=self.cfg.lr, capturable=graph, fused=True)
         self.calls = 0
         self._graphs = {}
+        self._live_pack = False   # the last update repacked the planner's weights itself (repack_live)
         H = self.cfg.horizon
         # rho^t, t = 0..H, as float32 like the reference's Python-float scalar multiplies (tdmpc.py:212, 179)
         self._rho = torch.tensor([self.cfg.rho ** t for t in range(H + 1)], dtype=torch.float32,
@@ -179,7 +180,12 @@ class Learner:
         """One TDMPC.update without the EMA (tdmpc.py:192-241) -> metrics tensor [7] (METRICS order).
         noise: optional list of 2H+1 [B, A] TruncatedNormal draws (H for the TD targets, H+1 for update_pi)."""
         if self.engine is not None:
-            return self.engine.update(buffer, noise)
+            m = self.engine.update(buffer, noise)
+            from .tdmpc import repack_live
+            # the planner's packed weights straight from the engine's flat buffer (one fused launch, inside the
+            # captured graph when this step is captured); without a live pack the next plan() repacks
+            self._live_pack = repack_live(self.agent.planner, self.agent.model)
+            return m
         a, cfg = self.agent, self.cfg
         m = a.model
         H = cfg.horizon
@@ -265,6 +271,10 @@ class Learner:
             if g is None:
                 if len(self._graphs) >= 2:   # the buffer grew: drop the stale captures
                     self._graphs.clear()
+                if self.engine is not None:
+                    # the captured update repacks the planner from the engine's buffer (repack_live): pack once now
+                    # so the planner holds the live tensors and the pack's job table exists before the capture
+                    self.agent.planner.pack(self.agent.model)
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
                     out = self.step(buffer)
@@ -276,6 +286,8 @@ class Learner:
         if step % self.cfg.update_freq == 0:
             self.ema()
         self.agent.model.eval()
-        # parameters changed in place (a graph replay does not bump tensor versions): repack for planning
-        self.agent.planner._packed_key = None
+        # parameters changed in place (a graph replay does not bump tensor versions): repack for planning, unless
+        # the update itself repacked from the engine's buffer (repack_live)
+        if not self._live_pack:
+            self.agent.planner._packed_key = None
         return m

@@ -73,6 +73,24 @@ def pack_told(pl, model):
                                         pl.packed.numel() * 4, C.c_void_p(stream)), "tdmpc_pack_weights")
     pl._keep = params  # keep source tensors alive until the stream has consumed them
     pl._packed_key = key
+    # the pointer array stays valid for repack_live() while the packed tensors ARE the model's (no dtype / device
+    # / layout copy was made)
+    live = all(q.data_ptr() == p.data_ptr() for q, p in zip(params, pl._packed_params))
+    pl._ptr_arr = (arr, n) if live else None
+
+
+def repack_live(pl, model) -> bool:
+    """Repack after an in-place update of the tensors the last pack_told() read (the learner's flat-buffer views,
+    written by its HIP optimizer): one tdmpc_pack_weights launch over the cached pointer array -- no state_dict()
+    walk, capturable into the learner's update graph. False (nothing launched) when the planner has not packed
+    this model's live tensors yet: the next plan() then packs from the state_dict."""
+    if pl._packed_model is not model or getattr(pl, "_ptr_arr", None) is None:
+        return False
+    arr, n = pl._ptr_arr
+    stream = torch.cuda.current_stream(pl.device).cuda_stream
+    _lib.check(pl.L.tdmpc_pack_weights(C.byref(pl.dims), arr, n, C.c_void_p(pl.packed.data_ptr()),
+                                        pl.packed.numel() * 4, C.c_void_p(stream)), "tdmpc_pack_weights")
+    return True
 
 
 class HipPlanner:
@@ -90,7 +108,9 @@ class HipPlanner:
         _lib.check(self.L.tdmpc_sizes_for(C.byref(self.dims), C.byref(sz)), "tdmpc_sizes_for")
         self.sizes = sz
         dev = self.device
-        self.packed = torch.empty(sz.packed_weight_bytes // 4, dtype=torch.float32, device=dev)
+        # zeroed once: tdmpc_pack_weights writes every tensor's region (padding included) but not the alignment gaps
+        # between them, which padded vector reads may touch
+        self.packed = torch.zeros(sz.packed_weight_bytes // 4, dtype=torch.float32, device=dev)
         self.workspace = torch.empty(sz.workspace_bytes // 4, dtype=torch.float32, device=dev)
         d = self.dims
         self.N, self.P, self.A = d.num_samples, d.num_pi, d.action_dim
@@ -134,6 +154,7 @@ class HipPlanner:
         self._packed_key = None
         self._packed_model = None
         self._packed_params = []
+        self._ptr_arr = None
         self._graphs = {}
         # the metrics come down through pinned memory too (a pageable copy blocks the host)
         self._pin_met = torch.zeros(max_batch, 2, dtype=torch.float32, pin_memory=pin)

@@ -229,8 +229,8 @@ def test_plan_reference_draws_device_equals_torch(monkeypatch, graph, B):
                 res += [a.clone(), m.clone()]
         res.append(torch.randn(4, device="cuda"))
         outs.append(res)
-    for x, y in zip(*outs):
-        assert torch.equal(x.cpu(), y.cpu())
+    for i, (x, y) in enumerate(zip(*outs)):
+        assert torch.equal(x.cpu(), y.cpu()), f"output {i}: device {x[:3].tolist()} vs torch {y[:3].tolist()}"
 
 
 @pytest.mark.parametrize("path", PATHS)

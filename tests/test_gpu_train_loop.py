@@ -97,3 +97,43 @@ def test_update_pi_then_plan_repacks():
     v_gpu, v_ref = _oracle_first_values(agent, cfg, obs, step)
     err = (v_gpu - v_ref).abs().max().item()
     assert err < 1e-4 * (1 + v_ref.abs().max().item()), f"plan after update_pi: max|dG| {err}"
+
+
+@pytest.mark.gpu
+def test_live_repack_equals_full_pack():
+    """The learner's captured update repacks the planner's weights from its flat parameter buffer (one fused
+    tdmpc_pack_weights launch inside the graph, no state_dict walk): after graph-replayed updates the packed
+    buffer is bitwise what a full pack of the agent's current state_dict writes."""
+    from tdmpc_amd.replay import ReplayBuffer
+    from tdmpc_amd.tdmpc import TDMPC, pack_told
+    cfg = learner_cfg()
+    rc = SimpleNamespace(**{**vars(cfg), "device": "cuda", "train_steps": 2000, "max_buffer_size": 10**6,
+                            "episode_length": 200, "env_horizon": cfg.horizon})
+    rs = np.random.RandomState(9)
+    agent = TDMPC(cfg)
+    agent.model.load_state_dict(synthetic_state_dict(cfg, 51))
+    agent.model_target.load_state_dict(synthetic_state_dict(cfg, 52))
+    lrn = agent.learner(graph=True, warmup=2)
+    if lrn.engine is None:
+        pytest.skip("learner engine not used for this config")
+    buf = ReplayBuffer(rc, latent_plan=True)
+    for _ in range(3):
+        buf.add(SimpleNamespace(obs=torch.from_numpy(rs.standard_normal((201, 5)).astype(np.float32)),
+                                action=torch.from_numpy(rs.uniform(-1, 1, (200, 1)).astype(np.float32)),
+                                reward=torch.from_numpy(rs.standard_normal(200).astype(np.float32))))
+    obs = rs.standard_normal(cfg.obs_shape).astype(np.float32)
+    step = 10**6
+    for k in range(6):
+        agent.plan(obs, step=step, t0=(k == 0))
+        agent.update(buf, k + 1)
+    assert lrn._graphs and lrn._live_pack, "the captured update did not repack the planner itself"
+    pl = agent.planner
+    packed0 = pl.packed.clone()
+    agent.update(buf, 7)                      # one more graph replay: its live repack changes the packed weights
+    torch.cuda.synchronize()
+    live = pl.packed.clone()
+    assert not torch.equal(live, packed0)
+    pl._packed_key = None                     # a full pack of the same (current) weights from the state_dict
+    pack_told(pl, agent.model)
+    torch.cuda.synchronize()
+    assert torch.equal(pl.packed.view(torch.int32), live.view(torch.int32))
