@@ -3718,6 +3718,19 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         const bool z0c = t == 0 && c.z0c_ready && map.G % 32 == 0;
         if (use_wide(c, rows, map, z0c)) {
             if ((rc = flush_split(c))) return rc;
+            // A launch of 1.5 rounds of workgroups (iteration 0's N + P rows: 384 blocks on 256 CUs) runs its whole
+            // rounds on the wide kernel and the rest on the path that fits it (the chain kernel's many small
+            // workgroups), instead of a half-empty second round. Identity row maps only (physical row = logical row
+            // + offset), t >= 1 (the z0c bias is indexed by the logical row); TDMPC_WIDE_SPLIT=0 turns it off.
+            static const int split = [] { const char* e = getenv("TDMPC_WIDE_SPLIT"); return e ? atoi(e) : 1; }();
+            const int round = 128 * std::max(1, num_cus() / 2);
+            if (split && !z0c && map.G == map.S && map.O == 0 && rows > round && rows % round) {
+                const int r1 = rows / round * round;
+                if ((rc = launch_wide(c, t, r1, map, disc, first, last, false))) return rc;
+                RowMap rest = map;
+                rest.O = r1;
+                return step_next(c, t, rows - r1, rest, disc, first, last);
+            }
             return launch_wide(c, t, rows, map, disc, first, last, z0c);
         }
     }
