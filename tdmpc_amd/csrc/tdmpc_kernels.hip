@@ -237,7 +237,7 @@ constexpr unsigned P1_SPIN_MAX = 400000;   // ~0.3-0.5 s of polling before a wor
 
 // exchange region bytes (all offsets 256-aligned) for dims; 0 = not eligible
 struct P1Region {
-    unsigned o_sync, o_xb, o_h1, o_zp, o_rp, o_pp, o_qm, o_qp, o_val, o_rl, o_mu, xb_t, xb_g, total;
+    unsigned o_sync, o_xb, o_h1, o_zp, o_rp, o_pp, o_qm, o_qp, o_val, o_rl, o_mu, o_y2, xb_t, xb_g, total;
 };
 
 // the first layer's 32-k steps the kernel instantiation runs (4 or 6; steps past K meet zero activations)
@@ -264,15 +264,17 @@ inline P1Region p1_region(const tdmpc_dims* d, const Layout& w) {
     r.o_val = take(2 * T * 4);
     r.o_rl = take(T * 4);
     r.o_mu = take((size_t)P1_NG * P1_ROWS * w.Ap * 4);   // the pi rows' cached terminal means
+    r.o_y2 = take((size_t)P1_NG * 2 * P1_ROWS * P1_H1LD * 4);   // the Q heads' raw second-layer rows
     r.total = (unsigned)o;
     return r;
 }
 
 // LDS of plan1_kernel: the hidden-layer weight slice (96 KB), a layer's 32-column slice of the group's rows (+ per-row
 // LayerNorm scalars), the CEM step's top-k keys and elite actions, mean / std / scores / bias slices
-__host__ __device__ inline size_t p1_cem_floats(int H, int K, int A, int T) {   // top-k keys + elites | K-half partials
+__host__ __device__ inline size_t p1_cem_floats(int H, int K, int A, int T) {
+    // CEM step: top-k keys + elites | phases: K-half partials (8 KB) + every wave's dynamics W3 fragment (8 x 3 KB)
     const size_t c = (size_t)(T + 63) / 64 * 64 * 2 + rup((size_t)H * K * A, 4);
-    return c > 4 * 2 * 64 * 4 ? c : 4 * 2 * 64 * 4;
+    return c > 8192 ? c : 8192;
 }
 inline size_t p1_lds_bytes(int H, int K, int A, int T) {
     const size_t HA = (size_t)H * A;
@@ -3707,7 +3709,8 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
 
 // defer = 1 (a loop of consecutive steps over the same rows, nothing reading X_{t+1}'s latents in between): on the
 // split path the finish of this step is folded into the next step's launch.
-int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, int defer = 0) {
+int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, int defer = 0,
+              bool nowide = false) {
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
@@ -3716,20 +3719,23 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         if ((rc = flush_split(c))) return rc;
     {
         const bool z0c = t == 0 && c.z0c_ready && map.G % 32 == 0;
-        if (use_wide(c, rows, map, z0c)) {
+        if (!nowide && use_wide(c, rows, map, z0c)) {
             if ((rc = flush_split(c))) return rc;
-            // A launch of 1.5 rounds of workgroups (iteration 0's N + P rows: 384 blocks on 256 CUs) runs its whole
-            // rounds on the wide kernel and the rest on the path that fits it (the chain kernel's many small
-            // workgroups), instead of a half-empty second round. Identity row maps only (physical row = logical row
-            // + offset), t >= 1 (the z0c bias is indexed by the logical row); TDMPC_WIDE_SPLIT=0 turns it off.
+            // Iteration 0's fused launch over all T = N + P rows of every env is 1.5 rounds of workgroups at B = 32
+            // (384 blocks on 256 CUs): the sampled rows of every env run on the wide kernel (one whole round) and the
+            // policy rows on the chain kernel's many small workgroups, instead of a half-empty second round. The
+            // split is by a row's role, never by the launch's size or a row's position in it, so a row's kernel (and
+            // its rounding) does not depend on the batch size (tests/test_gpu_sharded.py: two 32-env shards equal
+            // the 64-env batch bitwise). At t = 0 both parts keep the z0c first layer (the per-env bias is indexed by
+            // logical row / G, and G is the per-env row count of each part's map). TDMPC_WIDE_SPLIT=0 turns it off.
             static const int split = [] { const char* e = getenv("TDMPC_WIDE_SPLIT"); return e ? atoi(e) : 1; }();
-            const int round = 128 * std::max(1, num_cus() / 2);
-            if (split && !z0c && map.G == map.S && map.O == 0 && rows > round && rows % round) {
-                const int r1 = rows / round * round;
-                if ((rc = launch_wide(c, t, r1, map, disc, first, last, false))) return rc;
-                RowMap rest = map;
-                rest.O = r1;
-                return step_next(c, t, rows - r1, rest, disc, first, last);
+            const RowMap rm = {c.N, map.S, 0}, pm = {c.P, map.S, c.N};
+            const int envs = rows / std::max(1, map.G);
+            const bool z0c_rm = t == 0 && c.z0c_ready;   // (rm.G = N: use_wide checks N % 128 for the z0c bias)
+            if (split && c.P > 0 && c.N + c.P == c.T && map.G == c.T && map.S == c.T && map.O == 0 && rows == envs * c.T &&
+                use_wide(c, envs * c.N, rm, z0c_rm)) {
+                if ((rc = launch_wide(c, t, envs * c.N, rm, disc, first, last, z0c_rm))) return rc;
+                return step_next(c, t, envs * c.P, pm, disc, first, last, 0, true);
             }
             return launch_wide(c, t, rows, map, disc, first, last, z0c);
         }
@@ -4153,7 +4159,7 @@ int plan1_launch(const Ctx& c, const tdmpc_plan_params* prm, const float* noise,
     for (int t = 0; t <= c.H && t < 17; ++t) a.disc[t] = prm->discount_pow[t];
     a.base = c.k.p1; a.bytes = (unsigned)c.k.p1_bytes;
     a.o_sync = rg.o_sync; a.o_xb = rg.o_xb; a.o_h1 = rg.o_h1; a.o_zp = rg.o_zp; a.o_rp = rg.o_rp; a.o_pp = rg.o_pp;
-    a.o_qm = rg.o_qm; a.o_qp = rg.o_qp; a.o_val = rg.o_val; a.o_rl = rg.o_rl; a.o_mu = rg.o_mu; a.pi_cache = pi_cache_on(); a.xb_t = rg.xb_t; a.xb_g = rg.xb_g;
+    a.o_qm = rg.o_qm; a.o_qp = rg.o_qp; a.o_val = rg.o_val; a.o_rl = rg.o_rl; a.o_mu = rg.o_mu; a.o_y2 = rg.o_y2; a.pi_cache = pi_cache_on(); a.xb_t = rg.xb_t; a.xb_g = rg.xb_g;
     a.stamps = g_p1_stamps;
     a.status = prm->status;
     {

@@ -3,9 +3,10 @@ two processes, each the real HIP `TDMPC` under `EnvShardedPlanner`'s default pla
 shard, HIP graph, reference-order device draws), one all-gather of [envs, A+2] per call. Both ranks share the one
 GPU of the test box, so the collective runs on the gloo transport (RCCL refuses two ranks on one device); the
 planning path is the one `bench.py --gpus N` runs per GPU. Every env's gathered action and metrics must equal,
-bitwise, a single-process plan_batch over all 64 envs: envs are independent and N, T are multiples of the 32-row
-block, so an env's arithmetic does not depend on its slot or on the batch size (every launch of both batch sizes
-picks the same kernels at >= 17 envs per call)."""
+bitwise, a single-process plan_batch over all 64 envs: envs are independent and N, T are multiples of the 128-row
+block, so an env's arithmetic does not depend on its slot or on the batch size (every row of both batch sizes runs on
+the same kernel at >= 32 envs per call: the wide step kernel for the sampled rows, the chain kernel for iteration 0's
+policy rows -- the split is by a row's role, tdmpc_kernels.hip step_next)."""
 import os
 import socket
 import subprocess
