@@ -121,13 +121,16 @@ class HipPlanner:
         self.noise_flat = torch.zeros(max_batch * sz.noise_floats_per_env, dtype=torch.float32, device=dev)
         self.prev_mean_flat = torch.zeros(max_batch * d.max_horizon * self.A, dtype=torch.float32, device=dev)
         self.action = torch.zeros(max_batch, self.A, dtype=torch.float32, device=dev)
-        self.metrics = torch.zeros(max_batch, 2, dtype=torch.float32, device=dev)
+        # one device block [status word | 3 pad words | metrics [max_batch, 2]] so a call's status and metrics come
+        # down as ONE copy; status: the sticky device status word (tdmpc_plan_params.status), nonzero after a plan
+        # that failed on the device
+        self._ms_dev = torch.zeros(4 + 2 * max_batch, dtype=torch.float32, device=dev)
+        self.status = self._ms_dev[:1].view(torch.int32)
+        self.metrics = self._ms_dev[4:].view(max_batch, 2)
         # per-call state the kernels read from device memory (ABI 5), so one captured graph serves every value
         # of self.std over std_schedule and every per-env t0 pattern
         self.std_dev = torch.zeros(1, dtype=torch.float32, device=dev)
         self.warm_dev = torch.zeros(max_batch, dtype=torch.int32, device=dev)
-        # sticky device status word (tdmpc_plan_params.status): nonzero after a plan that failed on the device
-        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self._std_host = None
         self._warm_host = None
         # per-call inputs, staged on the host and sent up as ONE copy: the observations, numpy's elite-choice
@@ -157,8 +160,7 @@ class HipPlanner:
         self._ptr_arr = None
         self._graphs = {}
         # the metrics come down through pinned memory too (a pageable copy blocks the host)
-        self._pin_met = torch.zeros(max_batch, 2, dtype=torch.float32, pin_memory=pin)
-        self._pin_status = torch.zeros(1, dtype=torch.int32, pin_memory=pin)
+        self._pin_ms = torch.zeros(4 + 2 * max_batch, dtype=torch.float32, pin_memory=pin)
         self._h2d_done = torch.cuda.Event() if pin else None
         # reference-order draws: "device" = one tdmpc_reference_normals launch per call, "torch" = the
         # reference's own normal_ launches (18 per env at humanoid sizes); equal bitwise
@@ -520,9 +522,9 @@ class TDMPC:
         if step < cfg.seed_steps and not eval_mode:
             return (torch.empty(cfg.action_dim, dtype=torch.float32, device=self.device).uniform_(-1, 1),
                     plan_metrics)
-        a, m = self._plan_envs(np.asarray(obs)[None], eval_mode, step, [t0])
+        a, m = self._plan_envs(np.asarray(obs)[None], eval_mode, step, [t0], clone=True)
         plan_metrics.update(m[0])
-        return a[0].clone(), plan_metrics
+        return a[0], plan_metrics
 
     @torch.no_grad()
     def plan_batch(self, obs, eval_mode=False, step=None, t0=True, sync_metrics=True):
@@ -546,9 +548,10 @@ class TDMPC:
     def horizon(self, step):
         return int(min(self.cfg.horizon, linear_schedule(self.cfg.horizon_schedule, step)))
 
-    def _plan_envs(self, obs, eval_mode, step, t0s, sync_metrics=True, trace=None, noise=None):
+    def _plan_envs(self, obs, eval_mode, step, t0s, sync_metrics=True, trace=None, noise=None, clone=False):
         """noise: optional list (one per env) of objects with eps_pi / eps_cem / eps_term / u / eps_act
-        (e.g. oracle NoiseBundles) used instead of drawing."""
+        (e.g. oracle NoiseBundles) used instead of drawing. clone: return a copy of the actions (enqueued right
+        after the plan, before the metrics sync, so its launch is off the host's critical path)."""
         cfg, pl = self.cfg, self.planner
         B = obs.shape[0]
         if B > pl.max_batch:
@@ -585,13 +588,20 @@ class TDMPC:
         one_launch = noise is None and self.rng == "reference" and pl.ref_draws == "device"
         if one_launch:
             pl.stage_reference_state(B, H, I, eval_mode)
-        # one copy up: observations (host ones), uniforms, generator state
+        # one copy up: observations (host ones), uniforms, generator state. A synchronising call (the drop-in
+        # plan()) replays it as the captured graph's first node (a memcpy node from the pinned staging block: one
+        # launch fewer on the host's critical path); otherwise it goes ahead of the replay, and an event marks the
+        # staging block reusable as soon as the copy is done, so the host stages the next call under this plan
         lo = 0 if host else pl._u_off
-        pl._stage_d[lo:].copy_(pl._stage_h[lo:], non_blocking=True)
-        if pl._h2d_done is not None:
-            pl._h2d_done.record()
+        copy_in_graph = self.graph and sync_metrics and noise is None and trace is None
+        if not copy_in_graph:
+            pl._stage_d[lo:].copy_(pl._stage_h[lo:], non_blocking=True)
+            if pl._h2d_done is not None:
+                pl._h2d_done.record()
 
         def device_work():
+            if copy_in_graph:
+                pl._stage_d[lo:].copy_(pl._stage_h[lo:], non_blocking=True)
             if noise is None:
                 if one_launch:
                     pl.launch_reference_draws(B, H, I, eval_mode)
@@ -604,7 +614,8 @@ class TDMPC:
             pl.launch(pl.device_state_params(pl.params(H, I, B, warm[0], eval_mode, self.std)), obs_u8, trace)
 
         if self.graph and noise is None and trace is None:
-            key = (H, I, B, bool(eval_mode), self.rng, one_launch)   # self.std and the warm flags live on the device
+            # (self.std and the warm flags live on the device)
+            key = (H, I, B, bool(eval_mode), self.rng, one_launch, copy_in_graph, lo)
             g = pl._graphs.get(key)
             if g is None:
                 # No eager warm-up: the library has no lazy initialisation left after pack(), and an eager
@@ -614,19 +625,20 @@ class TDMPC:
                     device_work()
                 pl._graphs[key] = g
             g.replay()
+            if copy_in_graph and pl._h2d_done is not None:
+                pl._h2d_done.record()
         else:
             device_work()
         self._has_prev[:B] = True
         self._prev_H[:B] = H
-        actions = pl.action[:B]
+        actions = pl.action[:B].clone() if clone else pl.action[:B]
         if not sync_metrics:
             return actions, pl.metrics[:B]
         if pl._h2d_done is not None:
-            pl._pin_met[:B].copy_(pl.metrics[:B], non_blocking=True)
-            pl._pin_status.copy_(pl.status, non_blocking=True)
+            pl._pin_ms[:4 + 2 * B].copy_(pl._ms_dev[:4 + 2 * B], non_blocking=True)   # status + metrics: one copy
             torch.cuda.current_stream(self.device).synchronize()
-            m = pl._pin_met[:B].tolist()
-            st = int(pl._pin_status[0])
+            m = pl._pin_ms[4:4 + 2 * B].view(B, 2).tolist()
+            st = int(pl._pin_ms[:1].view(torch.int32)[0])
         else:
             m = pl.metrics[:B].double().cpu().tolist()
             st = int(pl.status[0])

@@ -31,8 +31,8 @@ for i in range(I):
         if i == 0:
             labels += [f"i0 t{t} pi.l1", f"i0 t{t} pi.l3", f"i0 t{t} pi.fin"]
         labels += [f"i{i} t{t} st.l1", f"i{i} t{t} st.l3", f"i{i} t{t} st.red"]
-    labels += [f"i{i} pi.l1", f"i{i} pi.l3", f"i{i} pi.fin", f"i{i} q.m1", f"i{i} q.a1", f"i{i} q.m2", f"i{i} q.qp",
-               f"i{i} GRID"]
+    labels += [f"i{i} pi.l1", f"i{i} pi.l3", f"i{i} pi.fin", f"i{i} q.m1", f"i{i} q.a1", f"i{i} q.m2",
+               f"i{i} q.own+GRID"]
     if i < I - 1:
         labels += [f"i{i} cem.x0"]
 for w, base in (("wg0", 0), ("wg255", 1024)):
@@ -48,7 +48,7 @@ for w, base in (("wg0", 0), ("wg255", 1024)):
         tot_work += work
         tot_wait += wait
         rows.append((labels[k - 1], work, wait))
-    for lab, wk, wt in rows[:60]:
+    for lab, wk, wt in rows[:62]:
         print(f"{lab:18s} work {wk:7.2f} us  wait {wt:7.2f} us")
     print(f"total work {tot_work:.1f} us, wait {tot_wait:.1f} us")
 mk, ck = s[900:906], s[920:926]

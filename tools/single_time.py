@@ -4,7 +4,8 @@ import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from tdmpc_amd.config import bench_cfg
-from tdmpc_amd.tdmpc import TDMPC
+import importlib
+TDMPC = importlib.import_module(os.environ.get("SINGLE_MOD", "tdmpc_amd.tdmpc")).TDMPC   # (A/B of host-side variants)
 from tdmpc_amd.told import synthetic_state_dict
 
 cfg = bench_cfg(sys.argv[1] if len(sys.argv) > 1 else "humanoid-run")
