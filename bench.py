@@ -382,7 +382,8 @@ def train_loop_bench(cfg, dev, reps=40):
     step, t0) exactly as train.py calls it (TDMPC(cfg) defaults, host numpy obs, metrics synced to the host), then
     one agent.update(buffer, step) (batch 512 from a 50k-transition device replay buffer, HIP-graph replay; the
     update repacks the planner's weights from the learner's flat buffer inside that graph). Also each half alone,
-    in the same process: the loop's overhead over plan + update is what the hand-over between them costs."""
+    in the same process, in 4 interleaved rounds (medians): the loop's overhead over plan + update is what the
+    hand-over between them costs."""
     from types import SimpleNamespace
     from tdmpc_amd.replay import ReplayBuffer
     lcfg = bench_cfg(args_config_for_learner(cfg), batch_size=512)
@@ -420,14 +421,18 @@ def train_loop_bench(cfg, dev, reps=40):
     for i in range(8):   # warm-up: both graphs captured, the planner packed from the learner's buffer
         loop(i)
     torch.cuda.synchronize()
-    res = {}
-    for name, fn in (("loop", loop), ("plan", plan), ("update", update), ("loop_again", loop)):
-        t = time.perf_counter()
-        for i in range(reps):
-            fn(100 + i)
-        torch.cuda.synchronize()
-        res[name] = (time.perf_counter() - t) / reps * 1e3
-    loop_ms = min(res["loop"], res["loop_again"])
+    # interleaved rounds (loop, plan alone, update alone), the median of each: a box's drift over the measurement
+    # lands on all three alike
+    samples = {"loop": [], "plan": [], "update": []}
+    for r in range(4):
+        for name, fn in (("loop", loop), ("plan", plan), ("update", update)):
+            t = time.perf_counter()
+            for i in range(reps // 4):
+                fn(100 + 10 * reps * r + i)
+            torch.cuda.synchronize()
+            samples[name].append((time.perf_counter() - t) / (reps // 4) * 1e3)
+    res = {k: float(np.median(v)) for k, v in samples.items()}
+    loop_ms = res["loop"]
     out["ms_per_env_step"] = round(loop_ms, 4)
     out["value"] = round(1e3 / loop_ms, 2)
     out["unit"] = "env-steps/s"

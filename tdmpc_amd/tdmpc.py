@@ -492,7 +492,15 @@ class TDMPC:
         m = self.learner().update(replay_buffer, step, noise=noise)
         if not sync_metrics:
             return m
-        out = {k: float(v) for k, v in zip(METRICS, m.double().cpu().tolist())}
+        if m.is_cuda:   # one non-blocking copy into pinned memory + a stream sync (no cast kernel, no pageable copy)
+            if getattr(self, "_pin_upd", None) is None:
+                self._pin_upd = torch.zeros(len(METRICS), dtype=torch.float32, pin_memory=True)
+            self._pin_upd.copy_(m, non_blocking=True)
+            torch.cuda.current_stream(m.device).synchronize()
+            vals = self._pin_upd.tolist()
+        else:
+            vals = m.tolist()
+        out = {k: float(v) for k, v in zip(METRICS, vals)}
         if getattr(replay_buffer, "_full", False) and hasattr(replay_buffer, "check_sample"):
             replay_buffer.check_sample()   # numpy's choice(replace=False) error, raised at this existing sync
         return out
