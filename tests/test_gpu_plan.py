@@ -514,3 +514,24 @@ def test_persist_timeout_raises(monkeypatch, graph):
     agent.planner._graphs.clear()                  # (a captured graph keeps the knob's launch arguments)
     a, m = agent.plan(obs, step=10**6, t0=True)
     assert torch.isfinite(a).all() and np.isfinite(m["current_std"])
+
+
+def test_plan_returns_its_own_action():
+    """plan() returns a tensor of its own (the reference returns a fresh `a`, tdmpc.py:160-163): the next call, which
+    overwrites the planner's action buffer, leaves an earlier returned action untouched. The copy is enqueued right
+    after the captured plan and before the metrics sync, so its value is the plan's action, bitwise."""
+    cfg = make_cfg("humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5)
+    agent = TDMPC(cfg)
+    agent.model.load_state_dict(synthetic_state_dict(cfg, 4))
+    agent.std = 0.05
+    rs = np.random.RandomState(2)
+    a0, m0 = agent.plan(rs.standard_normal(cfg.obs_shape).astype(np.float32), step=10**6, t0=True)
+    kept = a0.clone()
+    assert torch.equal(a0, agent.planner.action[0])
+    assert a0.data_ptr() != agent.planner.action.data_ptr()
+    a1, m1 = agent.plan(rs.standard_normal(cfg.obs_shape).astype(np.float32), step=10**6, t0=False)
+    torch.cuda.synchronize()
+    assert torch.equal(a0, kept) and not torch.equal(a0, a1)
+    assert torch.equal(a1, agent.planner.action[0])
+    assert a0.shape == (cfg.action_dim,) and a0.is_contiguous()
+    assert np.isfinite([m0["current_std"], m0["external_reward_mean"], m1["current_std"]]).all()
