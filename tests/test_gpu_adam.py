@@ -1,0 +1,69 @@
+"""tdmpc_lg_adam (include/tdmpc_learner.h) against torch's own clip_grad_norm_ + Adam.step, the pair the reference's
+update() runs (/root/reference/src/algorithm/tdmpc.py:236-238: clip_grad_norm_(..., cfg.grad_clip_norm,
+error_if_nonfinite=False) then optim.step()). Finite gradients above the clip norm agree to fp32 rounding (rtol
+1e-5: torch reduces the norm in another order); a NaN gradient entry makes the clip coefficient NaN and with it EVERY
+parameter (torch's clamp keeps NaN), an inf entry makes it 0 (inf * 0 = NaN in that entry, 0 elsewhere) -- both
+bitwise in their non-finite pattern."""
+import ctypes as C
+
+import pytest
+import torch
+
+from tdmpc_amd import _lib
+
+LR, B1, B2, EPS, MAX_NORM = 1e-3, 0.9, 0.999, 1e-8, 10.0
+
+
+def _torch_steps(p0, grads):
+    p = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.Adam([p], lr=LR, betas=(B1, B2), eps=EPS, foreach=False)
+    for g in grads:
+        p.grad = g.clone()
+        torch.nn.utils.clip_grad_norm_([p], MAX_NORM, error_if_nonfinite=False)
+        opt.step()
+    return p.detach()
+
+
+def _hip_steps(p0, grads):
+    L = _lib.lib()
+    dev = torch.device("cuda:0")
+    p = p0.to(dev).clone()
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    step = torch.zeros(1, dtype=torch.int32, device=dev)
+    norm_out = torch.zeros(1, device=dev)
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for g in grads:
+        gd = g.to(dev).contiguous()
+        normp = (gd.double() ** 2).sum().float().reshape(1)   # one block's squared norm (lg_finalize's output)
+        step += 1                                             # lg_finalize advances the step before lg_adam
+        rc = L.tdmpc_lg_adam(C.c_void_p(p.data_ptr()), C.c_void_p(gd.data_ptr()), C.c_void_p(m.data_ptr()),
+                             C.c_void_p(v.data_ptr()), p.numel(), C.c_void_p(normp.data_ptr()), 1,
+                             C.c_void_p(step.data_ptr()), LR, B1, B2, EPS, MAX_NORM, C.c_void_p(norm_out.data_ptr()),
+                             st)
+        _lib.check(rc, "tdmpc_lg_adam")
+    torch.cuda.synchronize()
+    return p.cpu()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["finite_clipped", "finite_unclipped", "nan_entry", "inf_entry"])
+def test_lg_adam_matches_torch_clip_and_adam(case):
+    gen = torch.Generator().manual_seed(7)
+    n = 70_000   # > 256 x 256: several grid-stride rounds of the kernel
+    p0 = torch.randn(n, generator=gen)
+    scale = 1.0 if case != "finite_unclipped" else 1e-3
+    grads = [torch.randn(n, generator=gen) * scale for _ in range(2)]
+    if case == "nan_entry":
+        grads[1][12_345] = float("nan")
+    elif case == "inf_entry":
+        grads[1][54_321] = float("inf")
+    ref = _torch_steps(p0, grads)
+    got = _hip_steps(p0, grads)
+    assert torch.equal(torch.isnan(got), torch.isnan(ref))
+    if case == "nan_entry":
+        assert bool(torch.isnan(got).all())   # the NaN norm poisons every parameter, as torch's clip does
+        return
+    fin = torch.isfinite(ref)
+    if case == "inf_entry":
+        assert int((~fin).sum()) == 1
+    torch.testing.assert_close(got[fin], ref[fin], rtol=1e-5, atol=1e-7)

@@ -8,6 +8,7 @@ relative); indices then still agree unless a uniform falls within that rounding 
 golden cases do not hit.
 """
 import os
+import warnings
 
 import numpy as np
 import pytest
@@ -197,7 +198,13 @@ def test_gpu_norepl_concentrated_priorities():
     *_, idxs, _ = buf.sample(u=u[:512])
     got = idxs.cpu().numpy()
     assert len(set(got.tolist())) == 512 and (probs[got] > 0).all() and buf.uniforms_used > 512
-    buf.check_sample()
+    with pytest.warns(RuntimeWarning, match="uniforms"):   # past the supplied stream: no longer numpy's draw
+        buf.check_sample()
+    # enough uniforms supplied: no warning
+    buf.sample(u=u)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert buf.check_sample() == used
 
 
 @pytest.mark.gpu
