@@ -1,4 +1,4 @@
-"""Multi-process coverage of the env-sharded path on CPU (gloo, world_size 2).
+"""Multi-process coverage of the env-sharded path on CPU (gloo, world_size 2 and 4).
 
 Each rank plans its shard of a vectorised batch with the oracle's restatement of the reference plan() (CPU)
 and all-gathers the results; the gathered batch must equal a single-process run over all envs with the same
@@ -88,14 +88,16 @@ def test_shard_bounds():
     assert [shard_bounds(5, r, 2) for r in range(2)] == [(0, 3), (3, 5)]
 
 
-def test_sharded_plan_gloo_world2():
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_plan_gloo(world):
+    """world 4 rehearses more ranks than the 2 the GPU tests run (one env per rank here)."""
     cfg = _cfg()
     rs = np.random.RandomState(0)
     obs = torch.from_numpy(rs.standard_normal((N_ENVS,) + tuple(cfg.obs_shape)).astype(np.float32))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, obs, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, obs, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
