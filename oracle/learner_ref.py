@@ -74,6 +74,20 @@ def pi(p, z, std):
     return mu
 
 
+
+def _clip_grad_norm_19(params, max_norm):
+    """torch 1.9's clip_grad_norm_ (the reference pins pytorch=1.9, environment.yaml:6; called at tdmpc.py:178, 228):
+    total = ||stack(||g||)||, clip_coef = max_norm / (total + 1e-6), grads scaled only `if clip_coef < 1` (a NaN norm
+    scales nothing). The norm is reduced as the installed torch's clip_grad_norm_ reduces it (_foreach_norm per tensor,
+    then the norm of their stack), so finite norms stay bitwise equal to the reference-generated fixtures."""
+    grads = [p.grad for p in params if p.grad is not None]
+    total = torch.linalg.vector_norm(torch.stack(torch._foreach_norm([g.detach() for g in grads], 2.0)), 2.0)
+    clip_coef = max_norm / (total + 1e-6)
+    if clip_coef < 1:
+        for g in grads:
+            g.detach().mul_(clip_coef)
+    return total
+
 class RefLearner:
     """model / target parameters as leaf tensors in state_dict order; Adam like the reference (tdmpc.py:62-63)."""
 
@@ -104,7 +118,7 @@ class RefLearner:
             q = torch.min(*Q(self.p, cfg, z, a))
             pi_loss += -q.mean() * (cfg.rho ** t)
         pi_loss.backward()
-        torch.nn.utils.clip_grad_norm_(self.pi_params, cfg.grad_clip_norm, error_if_nonfinite=False)
+        _clip_grad_norm_19(self.pi_params, cfg.grad_clip_norm)
         self.pi_optim.step()
         for v in self.q_params:
             v.requires_grad_(True)
@@ -137,7 +151,7 @@ class RefLearner:
         weighted_loss = (total_loss * weights).mean()
         weighted_loss.register_hook(lambda grad: grad * (1 / cfg.horizon))
         weighted_loss.backward()
-        grad_norm = torch.nn.utils.clip_grad_norm_(self.params, cfg.grad_clip_norm, error_if_nonfinite=False)
+        grad_norm = _clip_grad_norm_19(self.params, cfg.grad_clip_norm)
         self.optim.step()
         new_prio = priority_loss.clamp(max=1e4).detach()
         pi_loss = self.update_pi(zs)

@@ -635,10 +635,11 @@ __global__ void __launch_bounds__(256) lg_adam_kernel(float* p, const float* g, 
     float s = 0.f;
     for (int i = threadIdx.x; i < nblk; i += 256) s += normp[i];
     const float total = sqrtf(block_sum256(s, red));
-    // torch.nn.utils.clip_grad_norm_: clamp(max_norm / (total + 1e-6), max=1), which keeps a NaN norm's NaN
-    // coefficient (and so NaN parameters, like the reference); fminf would drop it
-    const float c0 = max_norm / (total + 1e-6f);
-    const float coef = c0 != c0 ? c0 : fminf(c0, 1.0f);
+    // torch.nn.utils.clip_grad_norm_ as the reference's pinned torch 1.9 runs it (/root/reference/environment.yaml:6):
+    // `if clip_coef < 1: grad.mul_(clip_coef)`. A NaN norm fails the test, so the gradients go unscaled and only the
+    // entries whose gradient is NaN turn NaN (torch >= 1.13 clamps instead and poisons every parameter); an inf norm
+    // scales by 0. fminf(NaN, 1) = 1 is exactly that test.
+    const float coef = fminf(max_norm / (total + 1e-6f), 1.0f);
     if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = total;
     const int t = step[0];
     const double bc1 = 1.0 - pow((double)b1, (double)t), bc2 = 1.0 - pow((double)b2, (double)t);

@@ -30,6 +30,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
 #include <vector>
 
@@ -4389,11 +4390,17 @@ void pack_jobs(const Layout& w, const float* const* t, std::vector<PackJob>& job
     }
 }
 
-// Job tables live in device memory, one immutable copy per distinct table (a HIP graph that captured a pack keeps
-// pointing at its table, whatever other planners pack later), uploaded on first use by a synchronous copy -- not
-// while the stream is being captured: the learner packs once before it captures its update.
-struct PackTable { std::vector<PackJob> host; PackJob* dev; };
+// Job tables live in device memory, one immutable copy per distinct table and device (a HIP graph that captured a
+// pack keeps pointing at its table, whatever other planners pack later), uploaded on first use by a synchronous copy
+// -- not while the stream is being captured: the learner packs once before it captures its update. A table is keyed
+// by its content, i.e. by the source tensors' pointers: the host keeps those stable (tdmpc_amd.tdmpc.pack_told copies
+// non-live sources into per-planner staging tensors), so the set stays one table per planner and packed buffer.
+// Tables are never freed (a captured graph may still read one); past PACK_TABLES_WARN distinct tables the library
+// reports the growth once on stderr. Guarded by one mutex (planners on several host threads).
+struct PackTable { std::vector<PackJob> host; PackJob* dev; int device; };
 std::vector<PackTable> g_pack_tables;
+std::mutex g_pack_mu;
+constexpr size_t PACK_TABLES_WARN = 256;
 
 int launch_pack(std::vector<PackJob>& jobs, float* pw, hipStream_t s) {
     int blk = 0;
@@ -4402,9 +4409,15 @@ int launch_pack(std::vector<PackJob>& jobs, float* pw, hipStream_t s) {
         blk += (int)((j.work + PACK_WG * PACK_PER - 1) / (PACK_WG * PACK_PER));
     }
     const size_t nb = jobs.size() * sizeof(PackJob);
+    int device = 0;
+    HIPCHK(hipGetDevice(&device));
     const PackJob* dev = nullptr;
+    std::lock_guard<std::mutex> lock(g_pack_mu);
     for (const PackTable& t : g_pack_tables)
-        if (t.host.size() == jobs.size() && !memcmp(t.host.data(), jobs.data(), nb)) { dev = t.dev; break; }
+        if (t.device == device && t.host.size() == jobs.size() && !memcmp(t.host.data(), jobs.data(), nb)) {
+            dev = t.dev;
+            break;
+        }
     if (!dev) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         HIPCHK(hipStreamIsCapturing(s, &cs));
@@ -4412,23 +4425,29 @@ int launch_pack(std::vector<PackJob>& jobs, float* pw, hipStream_t s) {
             snprintf(g_err, sizeof g_err, "tdmpc_pack_weights: new tensors while capturing (pack once before capture)");
             return TDMPC_E_DIMS;
         }
-        // tables are carved from 256 KiB device chunks and written by a copy on the caller's stream, drained
-        // before returning (the host vector then dies)
-        static char* chunk = nullptr;
-        static size_t used = 0;
+        // tables are carved from 256 KiB device chunks (one current chunk per device) and written by a copy on the
+        // caller's stream, drained before returning (the host vector then dies)
+        struct Chunk { char* base; size_t used; };
+        static std::vector<Chunk> chunks;   // indexed by device
+        if ((int)chunks.size() <= device) chunks.resize(device + 1, Chunk{nullptr, 0});
+        Chunk& ch = chunks[device];
         const size_t need = rup(nb, 256), CH = 256 * 1024;
         if (need > CH) { snprintf(g_err, sizeof g_err, "tdmpc_pack_weights: job table too large"); return TDMPC_E_SIZE; }
-        if (!chunk || used + need > CH) {
-            HIPCHK(hipMalloc(&chunk, CH));
-            used = 0;
+        if (!ch.base || ch.used + need > CH) {
+            HIPCHK(hipMalloc(&ch.base, CH));
+            ch.used = 0;
         }
         PackTable t;
         t.host = jobs;
-        t.dev = (PackJob*)(chunk + used);
-        used += need;
+        t.dev = (PackJob*)(ch.base + ch.used);
+        t.device = device;
+        ch.used += need;
         HIPCHK(hipMemcpyAsync(t.dev, jobs.data(), nb, hipMemcpyHostToDevice, s));
         HIPCHK(hipStreamSynchronize(s));
         g_pack_tables.push_back(t);
+        if (g_pack_tables.size() == PACK_TABLES_WARN)
+            fprintf(stderr, "tdmpc_pack_weights: %zu distinct job tables (source tensors re-allocated per pack?)\n",
+                    g_pack_tables.size());
         dev = t.dev;
     }
     hipLaunchKernelGGL(pack_fused_kernel, dim3((unsigned)blk), dim3(PACK_WG), 0, s, dev, (int)jobs.size(), pw);

@@ -384,7 +384,8 @@ class TdICEM:
         _lib.check(rc, "tdmpc_plan_icem")
         if trace is not None:
             trace.update(value=[value_out[0, i, :n + e + pp] for i, (n, pp, e) in enumerate(cts)],
-                         mean=mean_out[0], std=std_out[0])
+                         mean=mean_out[0], std=std_out[0], counts=cts,
+                         value_all=value_out, mean_all=mean_out, std_all=std_out)   # (every env: [B, I, ...])
         self._has_prev = True
         self._has_elites = True
         self._elite_H = H

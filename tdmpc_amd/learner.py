@@ -32,6 +32,19 @@ import torch.nn.functional as F
 METRICS = ("consistency_loss", "reward_loss", "value_loss", "pi_loss", "total_loss", "weighted_loss", "grad_norm")
 
 
+
+def clip_grad_norm_19(params, max_norm):
+    """clip_grad_norm_(params, max_norm, error_if_nonfinite=False) as the reference's pinned torch 1.9 runs it
+    (/root/reference/environment.yaml:6; tdmpc.py:178, 228): `if clip_coef < 1: grad.mul_(clip_coef)`, so a NaN norm
+    scales nothing (torch >= 1.13 clamps and poisons every gradient). Written without a host sync (capturable): the
+    coefficient is where(coef < 1, coef, 1), and multiplying by exactly 1 leaves a gradient bitwise unchanged."""
+    grads = [p.grad for p in params if p.grad is not None]
+    total = torch.linalg.vector_norm(torch.stack(torch._foreach_norm(grads, 2.0)), 2.0)
+    coef = max_norm / (total + 1e-6)
+    coef = torch.where(coef < 1, coef, torch.ones_like(coef))
+    torch._foreach_mul_(grads, coef)
+    return total
+
 class RandomShiftsAug(torch.nn.Module):
     """helper.py:250-283: random-shift augmentation of pixel observations (identity for state). The shifts are
     drawn exactly as the reference draws them (one torch.randint of [n, 1, 1, 2] on the input's device, so the
@@ -171,7 +184,7 @@ class Learner:
         q = torch.min(*a.model.Q(Z, act)).view(n, -1)
         pi_loss = (-q.mean(dim=1) * self._rho[:n].view(n)).sum()
         pi_loss.backward()
-        torch.nn.utils.clip_grad_norm_(self.pi_params, cfg.grad_clip_norm, error_if_nonfinite=False, foreach=True)
+        clip_grad_norm_19(self.pi_params, cfg.grad_clip_norm)
         a.pi_optim.step()
         a.model.track_q_grad(True)
         return pi_loss.detach()
@@ -234,8 +247,7 @@ class Learner:
         zs = [zz.detach() for zz in zs]
         weighted_loss.register_hook(lambda grad: grad * (1 / H))
         weighted_loss.backward()
-        grad_norm = torch.nn.utils.clip_grad_norm_(self.params, cfg.grad_clip_norm, error_if_nonfinite=False,
-                                                   foreach=True)
+        grad_norm = clip_grad_norm_19(self.params, cfg.grad_clip_norm)
         a.optim.step()
         buffer.update_priorities(idxs, prio)
         pi_loss = self.update_pi(zs, eps=None if noise is None else noise[H:])

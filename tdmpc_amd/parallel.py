@@ -51,8 +51,17 @@ class EnvShardedPlanner:
         self.device = torch.device(device) if device is not None else (
             agent.device if agent is not None else torch.device("cpu"))
         b = self.hi - self.lo
-        self._local = torch.empty(b, action_dim + 2, device=self.device)
-        self._all = torch.empty(self.world * b, action_dim + 2, device=self.device)
+        # per env: action | reward mean, std | the planning rank's device status word (as float; 0 = healthy)
+        self._local = torch.zeros(b, action_dim + 3, device=self.device)
+        self._all = torch.zeros(self.world * b, action_dim + 3, device=self.device)
+        # RCCL path: the gathered status column goes down behind an event and is checked two calls later (the copy
+        # is queued ahead of the next call, so the wait leaves no bubble); gloo moves host copies anyway and checks
+        # at once. Every rank sees the same gathered block, so every rank raises at the same call.
+        pin = self.device.type == "cuda"
+        self._st_pin = torch.zeros(2, self.world * b, dtype=torch.float32, pin_memory=pin)
+        self._st_ev = [None, None]
+        self._st_pending = [False, False]
+        self._st_k = 0
 
     def local_obs(self, global_obs):
         return global_obs[self.lo:self.hi]
@@ -66,15 +75,65 @@ class EnvShardedPlanner:
             if len(t0) != self.n_envs:
                 raise ValueError(f"per-env t0 has {len(t0)} entries for {self.n_envs} envs")
             t0 = t0[self.lo:self.hi]   # this rank's envs' flags
+        self._deferred_status()
         a, m = self.plan_fn(self.local_obs(global_obs), step, t0)
         self._local[:, :self.A].copy_(a)
-        self._local[:, self.A:].copy_(m)
+        self._local[:, self.A:self.A + 2].copy_(m)
+        pl = getattr(self.agent, "planner", None)
+        if pl is not None and hasattr(pl, "status"):
+            self._local[:, self.A + 2].copy_(pl.status.float().expand(self._local.shape[0]))
         if self.world > 1:
-            self._all_gather()
+            host = self._all_gather()
             res = self._all
         else:
-            res = self._local
-        return res[:, :self.A], res[:, self.A:]
+            host, res = None, self._local
+        if host is not None:
+            self._raise_if_failed(host[:, self.A + 2])
+        else:
+            self._post_status(res[:, self.A + 2])
+        return res[:, :self.A], res[:, self.A:self.A + 2]
+
+    def check_status(self):
+        """Synchronising check of every rank's status as last gathered (raises like the deferred check)."""
+        self._st_pending = [False, False]
+        self._raise_if_failed(self._all[:, self.A + 2].cpu() if self.world > 1 else self._local[:, self.A + 2].cpu())
+
+    def _post_status(self, col):
+        if not self._st_pin.is_pinned():
+            self._raise_if_failed(col.cpu())
+            return
+        s = self._st_k % 2
+        if self._st_ev[s] is None:
+            self._st_ev[s] = torch.cuda.Event()
+        self._st_pin[s].copy_(col, non_blocking=True)
+        self._st_ev[s].record()
+        self._st_pending[s] = True
+        self._st_k += 1
+
+    def _deferred_status(self):
+        s = self._st_k % 2
+        if self._st_pending[s]:
+            self._st_ev[s].synchronize()
+            self._st_pending[s] = False
+            self._raise_if_failed(self._st_pin[s])
+
+    def _raise_if_failed(self, col):
+        """Raise on any nonzero gathered status (the device status word of the rank that planned that env: its
+        actions are NaN, tdmpc_hip.h ABI 6); the failing rank's sticky word is cleared, so the next call plans."""
+        bad = torch.nonzero(col != 0).flatten().tolist()
+        if not bad:
+            return
+        self._st_pending = [False, False]
+        b = self.hi - self.lo
+        ranks = sorted({e // b for e in bad})
+        st = int(col[bad[0]])
+        pl = getattr(self.agent, "planner", None)
+        if pl is not None and hasattr(pl, "status"):
+            pl.status.zero_()
+            pl._st_pending = [False, False]
+        raise RuntimeError(f"tdmpc_plan failed on the device of rank(s) {ranks} (status {st}): those envs' actions "
+                           "are NaN. Status 1 = the persistent one-env plan timed out at a hand-off; set "
+                           "TDMPC_PERSIST=0 to plan on the launch chain instead.")
 
     def _all_gather(self):
         """RCCL ("nccl") gathers the device tensors directly over xGMI. The gloo transport (ranks sharing one GPU, or
@@ -83,8 +142,9 @@ class EnvShardedPlanner:
             host_all = torch.empty(self._all.shape, dtype=self._all.dtype)
             dist.all_gather_into_tensor(host_all, self._local.cpu(), group=self.group)
             self._all.copy_(host_all)
-        else:
-            dist.all_gather_into_tensor(self._all, self._local, group=self.group)
+            return host_all
+        dist.all_gather_into_tensor(self._all, self._local, group=self.group)
+        return self._all if not self._all.is_cuda else None
 
     @torch.no_grad()
     def broadcast_weights(self, model: torch.nn.Module, src: int = 0):

@@ -121,8 +121,10 @@ class ReplayBuffer:
             raise RuntimeError("sample() on an empty buffer")
         if u is None:
             u = self._ubuf.uniform_()
+            self._n_u_last = None   # own draws: no caller stream whose numpy draw could be departed from
         else:
             u = torch.as_tensor(u, dtype=torch.float64).to(self.device).contiguous()
+            self._n_u_last = u.numel()
         probs = torch.empty(total, dtype=torch.float32, device=self.device) if keep_probs else None
         _lib.check(self._L.tdmpc_replay_sample(
             C.byref(self._dims), C.byref(self._store), total, int(self._full), C.c_float(cfg.per_alpha),
@@ -133,7 +135,6 @@ class ReplayBuffer:
             C.c_void_p(self._n_used.data_ptr()), C.c_void_p(self._ws.data_ptr()), self._ws.numel(),
             self._stream()), "tdmpc_replay_sample")
         self._u_keep = u   # the kernels read it asynchronously
-        self._n_u_last = u.numel()
         self.last_probs = probs
         return (self._out_obs, self._out_next, self._out_action, self._out_reward.unsqueeze(2), self._out_idx,
                 self._out_w)

@@ -64,6 +64,17 @@ def pack_told(pl, model):
     pl._packed_model, pl._packed_params = model, params
     key = tuple((p.data_ptr(), p._version) for p in params)
     params = [p.detach().to(pl.device, torch.float32).contiguous() for p in params]
+    # a source that is not the model's own device fp32 tensor is copied into a staging tensor kept per planner, so the
+    # pointer set -- the key of the library's device job-table cache -- stays the same from one repack to the next
+    stage = getattr(pl, "_pack_stage", None)
+    if stage is None or len(stage) != len(params):
+        stage = pl._pack_stage = [None] * len(params)
+    for i, (q, p) in enumerate(zip(params, pl._packed_params)):
+        if q.data_ptr() != p.data_ptr():
+            if stage[i] is None or stage[i].shape != q.shape:
+                stage[i] = torch.empty_like(q)
+            stage[i].copy_(q)
+            params[i] = stage[i]
     n = pl.L.tdmpc_num_param_tensors(C.byref(pl.dims))
     if n != len(params):
         raise ValueError(f"TOLD has {len(params)} tensors, the packer expects {n}")
@@ -169,6 +180,13 @@ class HipPlanner:
             raise ValueError(f"TDMPC_REF_DRAWS must be device or torch, not {self.ref_draws!r}")
         self._grid_cap = None
         self._ref_adv = {}
+        # deferred status check of the non-synchronising calls (sync_metrics=False): after each call the sticky status
+        # word is copied into pinned slot k % 2 behind an event; call k + 2 waits for that event (queued ahead of call
+        # k + 1, so the wait leaves no bubble in the stream) and raises on a nonzero word. check_status() drains both.
+        self._st_pin = torch.zeros(2, dtype=torch.int32, pin_memory=pin)
+        self._st_ev = [None, None]
+        self._st_pending = [False, False]
+        self._st_k = 0
 
     # ------------------------------------------------------------------ weights
     def pack(self, model: TOLD):
@@ -332,7 +350,34 @@ class HipPlanner:
 
     def check_status(self):
         """Synchronising check of the sticky status word (for callers that plan with sync_metrics=False)."""
+        self._st_pending = [False, False]
         self.raise_status(int(self.status.item()))
+
+    def post_status(self):
+        """After a non-synchronising call: enqueue the status word's copy into the pinned slot of this call."""
+        if not self._st_pin.is_pinned():
+            return
+        s = self._st_k % 2
+        if self._st_ev[s] is None:
+            self._st_ev[s] = torch.cuda.Event()
+        self._st_pin[s:s + 1].copy_(self.status, non_blocking=True)
+        self._st_ev[s].record()
+        self._st_pending[s] = True
+        self._st_k += 1
+
+    def deferred_status(self):
+        """Before a call: raise if the status copied two non-synchronising calls ago is nonzero (the word is sticky,
+        so that covers every earlier call too). That copy sits ahead of the previous call in the stream, so waiting
+        for it does not drain the queue."""
+        s = self._st_k % 2
+        if not self._st_pending[s]:
+            return
+        self._st_ev[s].synchronize()
+        self._st_pending[s] = False
+        st = int(self._st_pin[s])
+        if st:
+            self._st_pending = [False, False]
+            self.raise_status(st)
 
     def launch(self, prm, obs_is_u8: bool, trace: dict | None = None):
         L = self.L
@@ -564,6 +609,7 @@ class TDMPC:
         B = obs.shape[0]
         if B > pl.max_batch:
             raise ValueError(f"batch {B} > max_batch {pl.max_batch}")
+        pl.deferred_status()
         H = self.horizon(step)
         I = int(cfg.iterations)
         warm = []
@@ -641,7 +687,9 @@ class TDMPC:
         self._prev_H[:B] = H
         actions = pl.action[:B].clone() if clone else pl.action[:B]
         if not sync_metrics:
+            pl.post_status()   # raised by the call after next (deferred_status) or by check_status()
             return actions, pl.metrics[:B]
+        pl._st_pending = [False, False]   # (the synchronous read below covers every earlier call: the word is sticky)
         if pl._h2d_done is not None:
             pl._pin_ms[:4 + 2 * B].copy_(pl._ms_dev[:4 + 2 * B], non_blocking=True)   # status + metrics: one copy
             torch.cuda.current_stream(self.device).synchronize()

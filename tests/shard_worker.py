@@ -40,10 +40,43 @@ def position_rngs(agent, first_env, call, H, I):
     np.random.random_sample(call * N_ENVS + first_env)
 
 
+def status_main(out):
+    """One env per rank (the persistent one-env plan's regime); rank 1's plan1 never completes a hand-off
+    (TDMPC_P1_DEBUG_SKIP), so its actions are NaN and its status word is set. Every rank must raise from
+    EnvShardedPlanner.plan at the same call -- the failing rank's status travels in the gathered block -- and the
+    call after the raise plans normally on every rank."""
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    c = cfg()
+    agent = TDMPC(c, max_batch=1, path="persist" if rank == 1 else "chain")
+    agent.model.load_state_dict(synthetic_state_dict(c, WSEED))
+    agent.std = 0.05
+    planner = EnvShardedPlanner(world, c.action_dim, agent=agent)
+    obs = torch.from_numpy(np.random.RandomState(SEED).standard_normal((world, c.obs_shape[0])).astype(np.float32))
+    if rank == 1:
+        os.environ["TDMPC_P1_DEBUG_SKIP"] = "1"
+    raised = None
+    try:
+        planner.plan(obs, 10**6, t0=True)
+    except RuntimeError as e:
+        raised = str(e)
+    if rank == 1:
+        del os.environ["TDMPC_P1_DEBUG_SKIP"]
+        agent.planner._graphs.clear()   # (the captured graph keeps the knob's launch arguments)
+    a, m = planner.plan(obs, 10**6, t0=True)
+    with open(os.path.join(out, f"status{rank}.txt"), "w") as f:
+        f.write(f"{raised}\n{bool(torch.isfinite(a).all())}\n{int(agent.planner.status.item())}\n")
+
+
 def main(out):
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if len(sys.argv) > 2 and sys.argv[2] == "status":
+        try:
+            status_main(out)
+        finally:
+            dist.destroy_process_group()
+        return
     try:
         c = cfg()
         b = N_ENVS // world

@@ -516,6 +516,34 @@ def test_persist_timeout_raises(monkeypatch, graph):
     assert torch.isfinite(a).all() and np.isfinite(m["current_std"])
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_persist_timeout_raises_without_sync(monkeypatch, graph):
+    """The non-synchronising path (plan_batch(sync_metrics=False): the bench, EnvShardedPlanner's plan_fn) surfaces
+    the sticky device status too: each call queues the word's copy behind an event and the call after next waits for
+    it (no stream bubble) and raises; check_status() raises at once. Neither path hands on the NaN actions silently."""
+    cfg = make_cfg("humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5)
+    agent = TDMPC(cfg, path="persist", graph=graph)
+    agent.model.load_state_dict(synthetic_state_dict(cfg, 9))
+    agent.std = 0.05
+    obs = np.random.RandomState(0).standard_normal((1, *cfg.obs_shape)).astype(np.float32)
+    monkeypatch.setenv("TDMPC_P1_DEBUG_SKIP", "1")
+    a, m = agent.plan_batch(obs, step=10**6, t0=True, sync_metrics=False)   # failed on the device; no sync yet
+    agent.plan_batch(obs, step=10**6, t0=True, sync_metrics=False)
+    with pytest.raises(RuntimeError, match="timed out"):
+        agent.plan_batch(obs, step=10**6, t0=True, sync_metrics=False)      # call 0's status, two calls later
+    assert int(agent.planner.status.item()) == 0
+    assert not torch.isfinite(a).all()
+    agent.plan_batch(obs, step=10**6, t0=True, sync_metrics=False)
+    with pytest.raises(RuntimeError, match="timed out"):
+        agent.planner.check_status()                                        # the synchronising check
+    monkeypatch.delenv("TDMPC_P1_DEBUG_SKIP")
+    agent.planner._graphs.clear()
+    for _ in range(3):
+        a, m = agent.plan_batch(obs, step=10**6, t0=True, sync_metrics=False)
+    agent.planner.check_status()
+    assert torch.isfinite(a).all() and torch.isfinite(m).all()
+
+
 def test_plan_returns_its_own_action():
     """plan() returns a tensor of its own (the reference returns a fresh `a`, tdmpc.py:160-163): the next call, which
     overwrites the planner's action buffer, leaves an earlier returned action untouched. The copy is enqueued right

@@ -29,14 +29,14 @@ def _free_port():
     return p
 
 
-def test_sharded_dog64_world2_equals_single_process(tmp_path):
-    world, port = 2, _free_port()
+def _run_world(tmp_path, world, *mode):
+    port = _free_port()
     env = dict(os.environ, WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    env.pop("TDMPC_P1_DEBUG_SKIP", None)
     here = os.path.dirname(os.path.abspath(__file__))
-    procs = [subprocess.Popen([sys.executable, os.path.join(here, "shard_worker.py"), str(tmp_path)],
+    procs = [subprocess.Popen([sys.executable, os.path.join(here, "shard_worker.py"), str(tmp_path), *mode],
                               env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True) for r in range(world)]
-    outs = []
     for p in procs:
         try:
             out, _ = p.communicate(timeout=240)
@@ -44,8 +44,24 @@ def test_sharded_dog64_world2_equals_single_process(tmp_path):
             for q in procs:
                 q.kill()
             raise
-        outs.append(out)
         assert p.returncode == 0, out[-3000:]
+
+
+def test_sharded_status_raises_on_every_rank(tmp_path):
+    """ABI 6 through the sharded path (sync_metrics=False under the hood): rank 1's one-env persistent plan fails
+    on the device (debug knob), its status word rides in the gathered block, and BOTH ranks raise from
+    EnvShardedPlanner.plan at that call instead of handing on rank 1's NaN actions; the next call is healthy."""
+    world = 2
+    _run_world(tmp_path, world, "status")
+    for r in range(world):
+        raised, finite, st = open(os.path.join(tmp_path, f"status{r}.txt")).read().split("\n")[:3]
+        assert "rank(s) [1]" in raised and "status 1" in raised, (r, raised)
+        assert finite == "True" and st == "0", (r, finite, st)
+
+
+def test_sharded_dog64_world2_equals_single_process(tmp_path):
+    world = 2
+    _run_world(tmp_path, world)
     got = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(world)]
     # single process, all 64 envs, same weights and generator states
     c = W.cfg()

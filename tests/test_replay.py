@@ -205,6 +205,12 @@ def test_gpu_norepl_concentrated_priorities():
     with warnings.catch_warnings():
         warnings.simplefilter("error")
         assert buf.check_sample() == used
+    # the buffer's own draws (u=None, as TDMPC.update samples): no caller stream, so no warning however many
+    # uniforms the rounds took
+    buf.sample()
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert buf.check_sample() > 0
 
 
 @pytest.mark.gpu
