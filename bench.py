@@ -224,6 +224,60 @@ def cpu_baselines(cfg, budget_s: float):
     return out
 
 
+def cpu_node_leg(cfg, budget_s: float):
+    """The oracle for one config on NUMA node 0's physical cores, as many threads as the cgroup quota grants (the
+    faster of cpu_baselines' two legs at every config measured so far)."""
+    quota = cpu_quota()
+    nodes = numa_cores()
+    node0 = nodes[min(nodes)]
+    n = len(node0) if quota is None else max(1, min(len(node0), int(quota)))
+    keep = os.sched_getaffinity(0) if hasattr(os, "sched_setaffinity") else None
+    try:
+        if keep is not None:
+            os.sched_setaffinity(0, node0[:n])
+        r = cpu_baseline(cfg, budget_s, n)
+    finally:
+        if keep is not None:
+            os.sched_setaffinity(0, keep)
+    r["sample"] += f"; pinned to {n} physical core(s) of NUMA node {min(nodes)}"
+    return r
+
+
+def config_leg(name, B, args, dev, graph, cpu):
+    """One more BASELINE.json config timed in the same run: B envs per plan_batch call on this GPU (graph replay,
+    device RNG), the dominant step kernel's roofline and helper.q's rate from HIP events, and the oracle on this
+    host's cores as its own cpu_baseline."""
+    oc = bench_cfg(name)
+    oc.device = str(dev)
+    ao = make_agent(oc, B, args.rng, graph, 3)
+    oo = torch.from_numpy(synthetic_obs(oc, B, seed=0)).to(dev)
+    step = 10**6
+    ko = max(20, args.steps // 2)
+
+    def fn(i):
+        return ao.plan_batch(oo, step=step, t0=(i % 100 == 0), sync_metrics=False)
+
+    elo = time_steps(fn, 3, ko, None)
+    ao.planner.check_status()
+    fo = min(plan_flops(oc, False), plan_flops(oc, True))
+    value = B * ko / elo
+    out = {"value": round(value, 3), "unit": "plan-steps/s", "ms_per_step": round(elo / ko * 1e3, 4),
+           "envs_per_gpu": B, "steps": ko,
+           "workload": f"{name}: TDMPC.plan N={oc.num_samples} H={oc.horizon} iters={oc.iterations} "
+                       f"K={oc.num_elites} L={oc.latent_dim} A={oc.action_dim} modality={oc.modality}, {B} envs per call",
+           "frac_of_fp32_peak": round(value * fo / 1e12 / FP32_PEAK_TFLOPS, 4),
+           "frac_of_x6_peak": round(value * fo / 1e12 / X6_PEAK_TFLOPS, 4)}
+    if not args.no_roofline:
+        out["roofline"] = step_roofline(oc, B, ao, fn, 3, dev, f"{name}/B{B}")
+        out["roofline"]["q_head"] = q_roofline(oc, B, ao, fn, 3)
+    del ao
+    if cpu:
+        c = cpu_node_leg(oc, args.cpu_budget_config)
+        out["cpu_baseline"] = c
+        out["speedup_vs_cpu"] = round(value / c["value"], 2)
+    return out
+
+
 def sampleable(rs, total, n, L=500, H=5):
     """n random storage indices outside the masked last H steps of each episode (helper.py:468-470): the
     positions a learner's priority write-back can touch, so every sampled window stays inside its episode."""
@@ -525,6 +579,117 @@ def make_agent(cfg, B, rng, graph, seed, path="auto"):
     return agent
 
 
+def step_roofline(cfg, B, agent, one_step, n_r, dev, pmc_prefix):
+    """Roofline of the dominant kernel (the CEM rollout step, TOLD.next: 5 of every iteration's launches): HIP events
+    around each t >= 1 step launch (t = 0 runs a reduced first layer, z0c_kernel, and is not timed) on the stream it
+    is launched on, over an eager replay of `n_r` plan calls; FLOPs counted by the library per launch. PMC traffic /
+    MFMA busy from profiles/pmc_*.json when a pass of the same kernel and shape was committed."""
+    L = _lib.lib()
+    graph = agent.graph
+    agent.graph = False
+    one_step(0)
+    torch.cuda.synchronize()
+
+    def timed(cfg_id, pro, kdim, rows):
+        _lib.check(L.tdmpc_profile_begin(cfg_id, pro, kdim, rows, 8192), "profile_begin")
+        for i in range(n_r):
+            one_step(1 + i)
+        n, ms, fl = C.c_int32(), C.c_double(), C.c_double()
+        _lib.check(L.tdmpc_profile_end(C.byref(n), C.byref(ms), C.byref(fl)), "profile_end")
+        return n.value, ms.value, fl.value
+
+    rows = B * cfg.num_samples
+    M, Lt, A = cfg.mlp_dim, cfg.latent_dim, cfg.action_dim
+    n, ms, fl = timed(4, -1, 0, rows)
+    peak = FP32_PEAK_TFLOPS
+    if n > 0:
+        name = L.tdmpc_profile_kernel().decode()   # the library names the kernel it launched
+        wide = name.startswith("wide_step_kernel")
+        x6 = wide or name.endswith(", x6>")
+        rb = 16 if name.startswith("chain16") else 32
+        if wide:
+            peak = X6_PEAK_TFLOPS
+            kernel = (f"{name} (TOLD.next: dynamics + reward heads on 128-row "
+                      f"workgroups, 8 waves x 16 rows x all {M} hidden columns in registers, layer 1 streamed into "
+                      f"layer 2 by 64-column chunks, x6 weight fragments LDS-DMA'd once per workgroup into an LDS ring; "
+                      f"{rows} rows x 2 heads per launch), fp32 products from a three-way bf16 split of both "
+                      f"operands: 6 v_mfma_f32_16x16x32_bf16 per product, fp32 accumulation (peak = dense BF16 / 6)")
+        elif x6:
+            peak = X6_PEAK_TFLOPS
+            kernel = (f"{name} (TOLD.next: dynamics + reward heads, {rb}-row blocks, hidden activations in LDS, weights streamed from L2; {rows} rows x 2 "
+                      f"heads per launch), fp32 products from a three-way bf16 split of both operands: 6 "
+                      f"{'v_mfma_f32_32x32x16_bf16' if rb == 32 else 'v_mfma_f32_16x16x32_bf16'} per product, fp32 "
+                      f"accumulation (peak = dense BF16 / 6)")
+        else:
+            kernel = (f"{name} (TOLD.next: dynamics + reward heads, "
+                      f"{rb}-row blocks, hidden activations in LDS, weights streamed from L2; {rows} rows x 2 heads per "
+                      f"launch), fp32 {'v_mfma_f32_32x32x2_f32' if rb == 32 else 'v_mfma_f32_16x16x4_f32'}")
+        kx = A + Lt
+        alg_bytes = 4.0 * (rows * (kx + Lt + 2) + 2 * M * kx + 2 * M * M + M * Lt + M)
+        pmc_key = f"{pmc_prefix}/" + ("wide_step" if wide else "chain_step" + ("_x6" if x6 else ""))
+    else:
+        n, ms, fl = timed(0, 0, M, rows)
+        kernel = (f"linear_lds_kernel (128x128 LDS-staged tile): CEM rollout layer 2 (dynamics + reward "
+                  f"hidden {M}x{M} Linear + ELU, {rows} rows x 2 problems), fp32 v_mfma_f32_32x32x2_f32")
+        alg_bytes = 4.0 * (rows * 2 * M + 2 * M * M + rows * M)
+        pmc_key = pmc_prefix
+    agent.graph = graph
+    avg_s = ms / max(n, 1) * 1e-3
+    per_launch = fl / max(n, 1)
+    achieved = per_launch / avg_s / 1e12
+    roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "frac_of_fp32_mfma_peak": round(achieved / FP32_PEAK_TFLOPS, 4),
+            "traffic": None, "kernel": kernel,
+            "launches": n, "avg_launch_us": round(avg_s * 1e6, 3), "flops_per_launch": per_launch,
+            "algorithmic_bytes_per_launch": alg_bytes,
+            "hbm_gbs_algorithmic": round(alg_bytes / avg_s / 1e9, 1)}
+    mf = os.path.join(REPO, "profiles", "pmc_mfma.json")
+    if os.path.exists(mf):
+        try:
+            t = json.load(open(mf)).get(pmc_key)
+            if t:   # rocprofv3 PMC pass of the same kernel and shape (tools/gpu/suite.sh pmc, tools/pmc_mfma.py)
+                roof["mfma_util_pmc"] = t.get("mfma_util")
+                roof["clock_ghz_pmc"] = t.get("clock_ghz")
+        except (OSError, ValueError):
+            pass
+    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            t = json.load(open(pmc)).get(pmc_key)
+            if t:
+                roof["traffic"] = t.get("hbm_bytes_per_launch")
+                roof["traffic_source"] = t.get("source")
+        except (OSError, ValueError):
+            pass
+    # the HBM roofline the north star asks for, next to the binding MFMA one: algorithmic and PMC bytes per launch
+    # over the measured launch time, as fractions of the 8 TB/s peak
+    roof["hbm_frac_algorithmic"] = round(roof["hbm_gbs_algorithmic"] / HBM_PEAK_GBS, 4)
+    if roof["traffic"]:
+        roof["hbm_gbs_pmc"] = round(roof["traffic"] / avg_s / 1e9, 1)
+        roof["hbm_frac_pmc"] = round(roof["hbm_gbs_pmc"] / HBM_PEAK_GBS, 4)
+    return roof
+
+
+def q_roofline(cfg, B, agent, one_step, n_r):
+    """helper.q (both Q heads, tdmpc.py:47-50) at every iteration's terminal value: HIP events around its launches
+    (library profile cfg 4 + CH_Q over the N + P rows of every env), FLOPs counted by the library."""
+    L = _lib.lib()
+    graph = agent.graph
+    agent.graph = False
+    _lib.check(L.tdmpc_profile_begin(6, -1, 0, 0, 8192), "profile_begin")
+    for i in range(n_r):
+        one_step(1 + i)
+    n, ms, fl = C.c_int32(), C.c_double(), C.c_double()
+    _lib.check(L.tdmpc_profile_end(C.byref(n), C.byref(ms), C.byref(fl)), "profile_end")
+    agent.graph = graph
+    if n.value == 0:
+        return None
+    avg_s = ms.value / n.value * 1e-3
+    per = fl.value / n.value
+    return {"launches": n.value, "avg_launch_us": round(avg_s * 1e6, 3), "flops_per_launch": per,
+            "achieved": round(per / avg_s / 1e12, 3), "frac_of_x6_peak": round(per / avg_s / 1e12 / X6_PEAK_TFLOPS, 4)}
+
+
 def _sync():
     if torch.cuda.is_available():
         torch.cuda.synchronize()
@@ -570,8 +735,12 @@ def main():
     ap.add_argument("--rng", default="fused", choices=["fused", "reference"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU work per thread count timed")
-    ap.add_argument("--also", default="humanoid-run-l512",
-                    help="comma-separated other configs timed at N=1 in the same run (reported under 'configs')")
+    ap.add_argument("--also", default="cheetah-run,dog-run@8,quadruped-run-pixels,humanoid-run-l512",
+                    help="comma-separated other configs (name[@envs per call], default --envs-per-gpu) timed at N=1 "
+                         "in the same run, each with its own roofline and cpu_baseline (reported under 'configs')")
+    ap.add_argument("--cpu-budget-config", type=float, default=5.0,
+                    help="seconds of CPU work for each --also config's cpu_baseline")
+    ap.add_argument("--single-calls", type=int, default=200, help="literal plan() calls timed one by one (median)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-single", action="store_true")
@@ -614,96 +783,8 @@ def main():
     # steps on the same stream (graph replays cannot carry the events)
     roof = None
     if not args.no_roofline:
-        L = _lib.lib()
-        agent.graph = False
-        one_step(0)
-        torch.cuda.synchronize()
-        n_r = max(3, min(args.steps, 10))
-
-        def timed(cfg_id, pro, kdim, rows):
-            _lib.check(L.tdmpc_profile_begin(cfg_id, pro, kdim, rows, 8192), "profile_begin")
-            for i in range(n_r):
-                one_step(1 + i)
-            n, ms, fl = C.c_int32(), C.c_double(), C.c_double()
-            _lib.check(L.tdmpc_profile_end(C.byref(n), C.byref(ms), C.byref(fl)), "profile_end")
-            return n.value, ms.value, fl.value
-
-        rows = B * cfg.num_samples
-        M, Lt, A = cfg.mlp_dim, cfg.latent_dim, cfg.action_dim
-        # dominant kernel: the CEM rollout step (TOLD.next, 5 of every iteration's launches, ~half the time); the
-        # library times the t >= 1 launches only (t = 0 runs a reduced first layer, z0c_kernel).
-        # Row-block chain kernel when the auto path picks it (>= 64 32-row blocks), else the layered hidden GEMM.
-        n, ms, fl = timed(4, -1, 0, rows)
-        peak = FP32_PEAK_TFLOPS
-        if n > 0:
-            rb = 32 if (rows + 31) // 32 * 2 > torch.cuda.get_device_properties(dev).multi_processor_count // 2 else 16
-            rb = int(os.environ.get("TDMPC_CHAIN_RB", rb))
-            x6 = rb == 32 and M == 512 and os.environ.get("TDMPC_X6", "3") != "0"
-            cus = torch.cuda.get_device_properties(dev).multi_processor_count
-            # the library's use_wide(): M = 512, x6, 16-row map, <= 5 first-layer 32-k groups, L in (48, 64] / (96, 112]
-            wide = (x6 and os.environ.get("TDMPC_WIDE", "1") != "0" and (rows + 127) // 128 * 2 >= cus
-                    and (A + 7) // 8 * 8 + (Lt + 7) // 8 * 8 <= 160 and (Lt + 15) // 16 in (4, 7))
-            if wide:
-                peak = X6_PEAK_TFLOPS
-                kernel = (f"wide_step_kernel<G1=4, NB3=7> (TOLD.next: dynamics + reward heads on 128-row workgroups, "
-                          f"8 waves x 16 rows x all {M} hidden columns in registers, layer 1 streamed into layer 2 by "
-                          f"64-column chunks, x6 weight fragments LDS-DMA'd once per workgroup into an LDS ring; "
-                          f"{rows} rows x 2 heads per launch), fp32 products from a three-way bf16 split of both "
-                          f"operands: 6 v_mfma_f32_16x16x32_bf16 per product, fp32 accumulation (peak = dense BF16 / 6)")
-            elif x6:
-                peak = X6_PEAK_TFLOPS
-                kernel = (f"chain_kernel<CH_STEP, TN=4, NW=4, X6> (TOLD.next: dynamics + reward heads, 32-row blocks "
-                          f"of 4 waves x 128 columns, hidden "
-                          f"activations in LDS, weights streamed from L2; {rows} rows x 2 heads per launch), fp32 "
-                          f"products from a three-way bf16 split of both operands: 6 v_mfma_f32_32x32x16_bf16 per "
-                          f"product, fp32 accumulation (peak = dense BF16 / 6)")
-            else:
-                kernel = (f"{'chain_kernel' if rb == 32 else 'chain16_kernel'}<CH_STEP> (TOLD.next: dynamics + reward heads, {rb}-row blocks, hidden "
-                          f"activations in LDS, weights streamed from L2; {rows} rows x 2 heads per launch), "
-                          f"fp32 {'v_mfma_f32_32x32x2_f32' if rb == 32 else 'v_mfma_f32_16x16x4_f32'}")
-            kx = A + Lt
-            alg_bytes = 4.0 * (rows * (kx + Lt + 2) + 2 * M * kx + 2 * M * M + M * Lt + M)
-            pmc_key = f"{args.config}/B{B}/" + ("wide_step" if wide else "chain_step" + ("_x6" if x6 else ""))
-        else:
-            n, ms, fl = timed(0, 0, M, rows)
-            kernel = (f"linear_lds_kernel (128x128 LDS-staged tile): CEM rollout layer 2 (dynamics + reward "
-                      f"hidden {M}x{M} Linear + ELU, {rows} rows x 2 problems), fp32 v_mfma_f32_32x32x2_f32")
-            alg_bytes = 4.0 * (rows * 2 * M + 2 * M * M + rows * M)
-            pmc_key = f"{args.config}/B{B}"
-        agent.graph = graph
-        avg_s = ms / max(n, 1) * 1e-3
-        per_launch = fl / max(n, 1)
-        achieved = per_launch / avg_s / 1e12
-        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "frac_of_fp32_mfma_peak": round(achieved / FP32_PEAK_TFLOPS, 4),
-                "traffic": None, "kernel": kernel,
-                "launches": n, "avg_launch_us": round(avg_s * 1e6, 3), "flops_per_launch": per_launch,
-                "algorithmic_bytes_per_launch": alg_bytes,
-                "hbm_gbs_algorithmic": round(alg_bytes / avg_s / 1e9, 1)}
-        mf = os.path.join(REPO, "profiles", "pmc_mfma.json")
-        if os.path.exists(mf):
-            try:
-                t = json.load(open(mf)).get(pmc_key)
-                if t:   # rocprofv3 PMC pass of the same kernel and shape (tools/gpu41.sh, tools/pmc_mfma.py)
-                    roof["mfma_util_pmc"] = t.get("mfma_util")
-                    roof["clock_ghz_pmc"] = t.get("clock_ghz")
-            except (OSError, ValueError):
-                pass
-        pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            try:
-                t = json.load(open(pmc)).get(pmc_key)
-                if t:
-                    roof["traffic"] = t.get("hbm_bytes_per_launch")
-                    roof["traffic_source"] = t.get("source")
-            except (OSError, ValueError):
-                pass
-        # the HBM roofline the north star asks for, next to the binding MFMA one: algorithmic and PMC bytes per
-        # launch over the measured launch time, as fractions of the 8 TB/s peak
-        roof["hbm_frac_algorithmic"] = round(roof["hbm_gbs_algorithmic"] / HBM_PEAK_GBS, 4)
-        if roof["traffic"]:
-            roof["hbm_gbs_pmc"] = round(roof["traffic"] / avg_s / 1e9, 1)
-            roof["hbm_frac_pmc"] = round(roof["hbm_gbs_pmc"] / HBM_PEAK_GBS, 4)
+        roof = step_roofline(cfg, B, agent, one_step, max(3, min(args.steps, 10)), dev, f"{args.config}/B{B}")
+        roof["q_head"] = q_roofline(cfg, B, agent, one_step, max(3, min(args.steps, 10)))
 
     fl_alg = plan_flops(cfg, executed=False)
     fl_exec = plan_flops(cfg, executed=True)
@@ -732,13 +813,25 @@ def main():
         a1.model.load_state_dict(synthetic_state_dict(cfg, 0))
         a1.std = 0.05
         o1 = synthetic_obs(cfg, 1, seed=0)[0]
-        ks = max(10, args.steps // 2)
-        el1 = time_steps(lambda i: a1.plan(o1, step=step, t0=(i % 100 == 0)), 3, ks, None)
-        single = {"value": round(ks / el1, 3), "unit": "plan-steps/s", "ms_per_step": round(el1 / ks * 1e3, 4),
-                  "note": "agent.plan(obs, step, t0) exactly as src/train.py:95 calls it: TDMPC(cfg) defaults "
-                          "(reference-order RNG on torch's / numpy's global generators -- the torch draws as one "
-                          "tdmpc_reference_normals launch, bitwise torch's -- HIP graph replay), numpy obs "
-                          "copied to the device, metrics synced to the host; same GPU, same run"}
+        # every call synchronises (metrics to the host), so each is timed on its own: the median of
+        # --single-calls calls after a warm-up (a few slow calls -- host preemption -- do not move it)
+        for i in range(10):
+            a1.plan(o1, step=step, t0=(i == 0))
+        per = []
+        for i in range(args.single_calls):
+            t1 = time.perf_counter()
+            a1.plan(o1, step=step, t0=False)
+            per.append(time.perf_counter() - t1)
+        med = float(np.median(per))
+        single = {"value": round(1.0 / med, 3), "unit": "plan-steps/s", "ms_per_step": round(med * 1e3, 4),
+                  "calls": len(per), "ms_mean": round(float(np.mean(per)) * 1e3, 4),
+                  "ms_p10_p90": [round(float(np.percentile(per, 10)) * 1e3, 4),
+                                 round(float(np.percentile(per, 90)) * 1e3, 4)],
+                  "note": "median over the timed calls of agent.plan(obs, step, t0) exactly as src/train.py:95 calls "
+                          "it: TDMPC(cfg) defaults (reference-order RNG on torch's / numpy's global generators -- the "
+                          "torch draws as one tdmpc_reference_normals launch, bitwise torch's -- HIP graph replay), "
+                          "numpy obs copied to the device, metrics synced to the host; same GPU, same run"}
+        ks = max(20, args.steps // 2)
         # the same env through the batch API with device RNG and graph replay (no host sync)
         ab1 = make_agent(cfg, 1, args.rng, graph, 7)
         ob1 = obs[:1].clone()
@@ -782,23 +875,15 @@ def main():
 
     others = None
     if world == 1 and args.also:
-        # other BASELINE.json configs timed by the same driver run (fewer steps): the same 32-env workload
+        # the other BASELINE.json configs, timed by the same driver run
         others = {}
-        for name in [x for x in args.also.split(",") if x.strip() and x != args.config]:
-            oc = bench_cfg(name)
-            oc.device = str(dev)
-            ao = make_agent(oc, B, args.rng, graph, 3)
-            oo = torch.from_numpy(synthetic_obs(oc, B, seed=0)).to(dev)
-            ko = max(10, args.steps // 2)
-            elo = time_steps(lambda i: ao.plan_batch(oo, step=step, t0=(i % 100 == 0), sync_metrics=False),
-                             3, ko, None)
-            fo = min(plan_flops(oc, False), plan_flops(oc, True))
-            others[name] = {"value": round(B * ko / elo, 3), "unit": "plan-steps/s",
-                            "ms_per_step": round(elo / ko * 1e3, 4), "envs_per_gpu": B,
-                            "workload": f"{name}: TDMPC.plan N={oc.num_samples} H={oc.horizon} iters={oc.iterations} "
-                                        f"K={oc.num_elites} L={oc.latent_dim} A={oc.action_dim}",
-                            "frac_of_fp32_peak": round(B * ko / elo * fo / 1e12 / FP32_PEAK_TFLOPS, 4)}
-            del ao
+        for spec in [x.strip() for x in args.also.split(",") if x.strip()]:
+            name, _, eb = spec.partition("@")
+            eb = int(eb) if eb else B
+            if name == args.config and eb == B:
+                continue
+            key = name if eb == B else f"{name}@{eb}"
+            others[key] = config_leg(name, eb, args, dev, graph, cpu=not args.no_cpu)
 
     cpu = None
     if rank == 0 and not args.no_cpu and world == 1:

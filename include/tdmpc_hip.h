@@ -280,6 +280,8 @@ int tdmpc_cem_iter(const tdmpc_dims* dims, const tdmpc_plan_params* params, cons
  * head's MACs per row at the real, unpadded widths). Eager use only (events are not graph-capturable). */
 int tdmpc_profile_begin(int32_t cfg, int32_t pro, int32_t kdim, int32_t rows, int32_t max_launches);
 int tdmpc_profile_end(int32_t* launches, double* total_ms, double* flops);
+/* Name of the kernel (and its template arguments) of the last launch the armed profiler timed, "" if none. */
+const char* tdmpc_profile_kernel(void);
 
 /* Diagnostic: persistent one-env plans (TDMPC_PATH_PERSIST) launched after this call record, for workgroups 0 and
  * 255, the 100 MHz realtime clock at every hand-off's arrival and release into `dev` (device, 2048 uint64:

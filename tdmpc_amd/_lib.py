@@ -18,7 +18,7 @@ EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc
             "tdmpc_pack_weights", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_pi_rollout",
             "tdmpc_cem_iter", "tdmpc_reference_normals", "tdmpc_last_error", "tdmpc_debug_plan1_stamps",
             "tdmpc_debug_pack_check",
-            "tdmpc_profile_begin", "tdmpc_profile_end", "tdmpc_icem_sizes_for", "tdmpc_plan_icem",
+            "tdmpc_profile_begin", "tdmpc_profile_end", "tdmpc_profile_kernel", "tdmpc_icem_sizes_for", "tdmpc_plan_icem",
             # include/tdmpc_replay.h
             "tdmpc_replay_workspace_bytes", "tdmpc_replay_add_priorities", "tdmpc_replay_update_priorities",
             "tdmpc_replay_sample",
@@ -138,6 +138,7 @@ def lib():
     L.tdmpc_cem_iter.argtypes = [C.POINTER(Dims), C.POINTER(PlanParams), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                  vp, vp, sz, vp]
     L.tdmpc_last_error.restype = C.c_char_p
+    L.tdmpc_profile_kernel.restype = C.c_char_p
     L.tdmpc_profile_begin.argtypes = [i32, i32, i32, i32, i32]
     L.tdmpc_profile_end.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.tdmpc_icem_sizes_for.argtypes = [C.POINTER(Dims), C.POINTER(Sizes)]

@@ -3124,6 +3124,7 @@ struct Profiler {
     int armed = 0, cfg = 0, pro = -1, n = 0, cap = 0, kdim = 0, rows = 0;
     hipEvent_t* ev = nullptr;
     double flops = 0.0;
+    char kernel[128] = "";   // the last timed launch's kernel (tdmpc_profile_kernel)
 };
 thread_local Profiler g_prof;
 
@@ -3396,7 +3397,12 @@ int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
     // achieved rate is not flattered by them)
     const bool prof = pf.armed && pf.cfg == 4 + mode && pf.n + 2 <= pf.cap && (pf.rows == 0 || a.rows == pf.rows) &&
                       a.z0c == nullptr;
-    if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], s));
+    if (prof) {
+        static const char* mname[3] = {"CH_STEP", "CH_PI", "CH_Q"};
+        snprintf(pf.kernel, sizeof pf.kernel, "%s<%s%s>", a.rb == 16 ? "chain16_kernel" : "chain_kernel", mname[mode],
+                 a.x6 ? ", x6" : ", f32");
+        HIPCHK(hipEventRecord(pf.ev[pf.n], s));
+    }
     if (a.rb == 16) {
         const int nt = a.M / 128;
 #define CHAIN16_LAUNCH(MODE, NT) \
@@ -3688,7 +3694,10 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
     // timed (less than the algorithmic work), as in launch_chain
     Profiler& pf = g_prof;
     const bool prof = pf.armed && pf.cfg == 4 + CH_STEP && pf.n + 2 <= pf.cap && (pf.rows == 0 || rows == pf.rows) && !z0c;
-    if (prof) HIPCHK(hipEventRecord(pf.ev[pf.n], c.s));
+    if (prof) {
+        snprintf(pf.kernel, sizeof pf.kernel, "wide_step_kernel<%d, %d>", g1, nb3);
+        HIPCHK(hipEventRecord(pf.ev[pf.n], c.s));
+    }
     bool done = false;
 #define WIDE_LAUNCH(G1, NB3) \
     if (!done && g1 == G1 && nb3 == NB3) { \
@@ -5041,5 +5050,7 @@ int tdmpc_profile_end(int32_t* launches, double* total_ms, double* flops) {
     if (flops) *flops = pf.flops;
     return 0;
 }
+
+const char* tdmpc_profile_kernel(void) { return g_prof.kernel; }
 
 }  // extern "C"

@@ -46,7 +46,7 @@ def status_main(out):
     EnvShardedPlanner.plan at the same call -- the failing rank's status travels in the gathered block -- and the
     call after the raise plans normally on every rank."""
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    c = cfg()
+    c = make_cfg("humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5)   # (a plan1 shape)
     agent = TDMPC(c, max_batch=1, path="persist" if rank == 1 else "chain")
     agent.model.load_state_dict(synthetic_state_dict(c, WSEED))
     agent.std = 0.05
