@@ -24,20 +24,37 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    deps = SRCS + [os.path.join(HERE, "csrc", "plan1.inc"), os.path.join(HERE, "csrc", "wide_step.inc")] + [os.path.join(REPO, "include", h) for h in ("tdmpc_hip.h", "tdmpc_replay.h", "tdmpc_learner.h")]
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
-        return OUT
-    tmp = OUT + ".tmp"
+def build(force: bool = False, verbose: bool = True, variant: str = "", defines=()) -> str:
+    """The library (every source compiled in parallel, then linked); a variant (-DNAME defines, diagnostics or an A/B
+    of a kernel knob) goes to libtdmpc_hip_<variant>.so, loaded with TDMPC_LIB_PATH."""
+    deps = SRCS + [os.path.join(HERE, "csrc", f) for f in ("plan1.inc", "wide_step.inc", "wide2.inc")] + \
+        [os.path.join(REPO, "include", h) for h in ("tdmpc_hip.h", "tdmpc_replay.h", "tdmpc_learner.h")]
+    out = OUT if not variant else os.path.join(HERE, f"libtdmpc_hip_{variant}.so")
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+        return out
     # -fno-slp-vectorize: no packed v_pk_add/mul_f32 from pairs of scalar f32 ops -- beside MFMAs a packed f32 VALU
     # instruction costs ~+22-26 cycles where two scalar ones are free (MI355X_MICROARCH.md, filler prices)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-slp-vectorize",
-           "-I", os.path.join(REPO, "include"), "-o", tmp] + SRCS
+    base = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vectorize",
+            "-I", os.path.join(REPO, "include")] + [f"-D{d}" for d in defines]
+    objs, procs = [], []
+    for src in SRCS:
+        obj = os.path.join(HERE, "csrc", os.path.basename(src) + (f".{variant}" if variant else "") + ".o")
+        cmd = base + ["-c", "-o", obj, src]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    if any(p.wait() != 0 for p in procs):
+        raise subprocess.CalledProcessError(1, "hipcc")
+    tmp = out + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    for o in objs:
+        os.remove(o)
+    os.replace(tmp, out)
+    return out
 
 
 EXAMPLE_SRC = os.path.join(REPO, "examples", "plan_c.cpp")
@@ -60,5 +77,10 @@ def build_example(force: bool = False, verbose: bool = True) -> str:
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
-    build_example(force="--force" in sys.argv)
+    # python -m tdmpc_amd.build [--force] [--variant NAME -DDEFINE ...]
+    args = sys.argv[1:]
+    var = args[args.index("--variant") + 1] if "--variant" in args else ""
+    defs = [a[2:] for a in args if a.startswith("-D")]
+    build(force="--force" in args or bool(var), variant=var, defines=defs)
+    if not var:
+        build_example(force="--force" in args)

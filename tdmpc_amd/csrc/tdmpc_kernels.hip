@@ -3056,6 +3056,7 @@ int set_lds_attr() {
 
 #include "plan1.inc"
 #include "wide_step.inc"
+#include "wide2.inc"
 
 #define FOR_EACH_LINEAR(X)                                                                          \
     X(1, 1, 1, 1, 0, 32, false) X(1, 1, 1, 1, 0, 64, false) X(1, 1, 1, 1, 0, 128, false)              \
@@ -3076,7 +3077,8 @@ int init_attrs() {
     HIPCHK(hipFuncSetAttribute((const void*)plan1_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)plan1_kernel<6>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 #define WIDE_ATTR(G1, NB3) \
-    HIPCHK(hipFuncSetAttribute((const void*)wide_step_kernel<G1, NB3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)wide_step_kernel<G1, NB3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)); \
+    HIPCHK(hipFuncSetAttribute((const void*)wide2_step_kernel<G1, NB3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     WIDE_FOR_EACH(WIDE_ATTR)
 #undef WIDE_ATTR
     HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -3653,6 +3655,12 @@ unsigned long long* g_p1_stamps = nullptr;   // tdmpc_debug_plan1_stamps (diagno
 
 // ---- the wide step kernel (wide_step.inc) for TOLD.next launches with >= one 128-row block per CU and head (B >= 32
 // envs at N = 512; TDMPC_WIDE=0 turns it off, TDMPC_PATH_WIDE forces it at every width it supports)
+// TDMPC_WIDE2=1: wide2_step_kernel (4 phases of 8 first-layer tiles, pipelined operand splits, wide2.inc) instead of
+// the round-3 wide_step_kernel (8 chunks of 4); an A/B switch while wide2 is measured, the default stays wide_step
+int wide_v2() {
+    static const int v = [] { const char* e = getenv("TDMPC_WIDE2"); return e ? atoi(e) : 0; }();
+    return v;
+}
 int wide_g1(const Ctx& c, bool z0c) {   // first-layer 32-k groups the kernel runs
     return (int)rup(z0c ? z0c_k1c(c) : c.Kx, 32) / 32;
 }
@@ -3695,13 +3703,14 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
     Profiler& pf = g_prof;
     const bool prof = pf.armed && pf.cfg == 4 + CH_STEP && pf.n + 2 <= pf.cap && (pf.rows == 0 || rows == pf.rows) && !z0c;
     if (prof) {
-        snprintf(pf.kernel, sizeof pf.kernel, "wide_step_kernel<%d, %d>", g1, nb3);
+        snprintf(pf.kernel, sizeof pf.kernel, "%s<%d, %d>", wide_v2() ? "wide2_step_kernel" : "wide_step_kernel", g1, nb3);
         HIPCHK(hipEventRecord(pf.ev[pf.n], c.s));
     }
     bool done = false;
 #define WIDE_LAUNCH(G1, NB3) \
     if (!done && g1 == G1 && nb3 == NB3) { \
-        hipLaunchKernelGGL((wide_step_kernel<G1, NB3>), grid, block, ws_lds<G1>(), c.s, a); \
+        if (wide_v2()) hipLaunchKernelGGL((wide2_step_kernel<G1, NB3>), grid, block, ws_lds<G1>(), c.s, a); \
+        else hipLaunchKernelGGL((wide_step_kernel<G1, NB3>), grid, block, ws_lds<G1>(), c.s, a); \
         done = true; \
     }
     WIDE_FOR_EACH(WIDE_LAUNCH)

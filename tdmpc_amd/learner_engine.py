@@ -104,6 +104,10 @@ class Engine:
         # lg_gemm's products: fp32-accurate x6 (default) or the exact f32 MFMA (TDMPC_LG_X6=0, or set before the
         # first update: the captured graph keeps the choice)
         self.x6 = os.environ.get("TDMPC_LG_X6", "1") != "0"
+        # every product on the hand-written lg_gemm (grouped launches, fused ELU / ELU' epilogues); TDMPC_LG_BLAS=1
+        # puts the plain M x M products back on hipBLASLt (torch.mm / addmm) for an A/B
+        self.blas = os.environ.get("TDMPC_LG_BLAS", "0") == "1"
+        self._aux = {}
 
     def _alias(self, model, flat):
         """Make every parameter of `model` a view into `flat` (values kept)."""
@@ -126,10 +130,9 @@ class Engine:
         return (self.PT if target else self.P)[o:o + n].view(shape)
 
     def mm(self, x, k, out, bias=None, target=False, transpose=False, cols=None, acc=False):
-        """out = x @ W^T (+ bias) -- or x @ W with transpose=True (the backward's dX) -- for the products of a
-        pass with no epilogue to fuse, on hipBLASLt (20-30 % faster than lg_gemm at the learner's 2560-3072-row
-        shapes, tools/mm_calibrate.py vs tools/lg_gemm_bench.py). cols: W's input columns [c0, c1) only (a
-        layer whose input is split over two tensors); acc: out += x @ W^T."""
+        """out = x @ W^T (+ bias) -- or x @ W with transpose=True (the backward's dX) -- on hipBLASLt; kept only for
+        the TDMPC_LG_BLAS=1 A/B of the products `job` puts on lg_gemm. cols: W's input columns [c0, c1) only;
+        acc: out += x @ W^T."""
         w = self.wv(k, target)
         if cols is not None:
             w = w[:, cols[0]:cols[1]]
@@ -140,6 +143,51 @@ class Engine:
             torch.mm(x, w, out=out)
         else:
             torch.addmm(self.wv(bias, target), x, w, out=out)
+
+    def job(self, parts, k, out, bias=None, target=False, transpose=False, epi=EPI_NONE, aux=None):
+        """One lg_gemm job: out = sum over parts (x, c0, c1) of x @ W[:, c0:c1]^T (+ bias, + epilogue) -- or
+        x @ W (transpose=True, the backward's dX; parts = [(dY, 0, 0)]). x / out may be row-strided views.
+        epi EPI_ELU fuses the ELU, EPI_ELU_BWD multiplies by ELU'(aux) (aux: the ELU output)."""
+        w = self.wv(k, target)
+        N, K = w.shape
+        segs = []
+        for x, c0, c1 in parts:
+            if transpose:
+                segs.append(_seg(_p(x), x.stride(0), _p(w), K, N, bmode=1))
+            else:
+                segs.append(_seg(_p(x), x.stride(0), _p(w, c0), K, c1 - c0))
+        j = dict(segs=segs, m=out.shape[0], n=K if transpose else N, c=_p(out), ldc=out.stride(0), epi=epi)
+        if bias is not None:
+            j["bias"] = self.w(bias, target)
+        if aux is not None:
+            j["aux"], j["ldaux"] = _p(aux), aux.stride(0)
+        return j
+
+    def mms(self, jobs, blas):
+        """Run a group of `job` products: ONE lg_gemm launch (default), or -- TDMPC_LG_BLAS=1, the A/B -- each on
+        hipBLASLt through `mm` plus a tdmpc_lg_act launch for a fused epilogue. blas: the mm() arguments per job."""
+        if not self.blas:
+            self.gemm(jobs)
+            return
+        for j, (parts, k, out, bias, target, transpose) in zip(jobs, blas):
+            for i, (x, c0, c1) in enumerate(parts):
+                self.mm(x, k, out, bias=bias if i == 0 else None, target=target, transpose=transpose,
+                        cols=None if transpose or (c0 == 0 and c1 == self.wv(k, target).shape[1]) else (c0, c1),
+                        acc=i > 0)
+            if j["epi"] == EPI_ELU:
+                self.act(out)
+            elif j["epi"] == EPI_ELU_BWD:
+                self.act(out, self._aux[j["aux"]])
+
+    def prod(self, specs):
+        """specs: (parts, k, out, bias, target, transpose, epi, aux) per product -> one grouped launch."""
+        jobs, blas = [], []
+        for parts, k, out, bias, target, transpose, epi, aux in specs:
+            jobs.append(self.job(parts, k, out, bias, target, transpose, epi, aux))
+            blas.append((parts, k, out, bias, target, transpose))
+            if aux is not None:
+                self._aux[_p(aux)] = aux
+        self.mms(jobs, blas)
 
     def act(self, x, y=None):
         """x <- ELU(x) (y None) or x <- x * ELU'(y) in place (tdmpc_lg_act)."""
@@ -243,32 +291,30 @@ class Engine:
                         ldc=L, bias=wt("_encoder.2.bias")),
                    dict(segs=[_seg(_p(b["Yo1"]), E, w("_encoder.2.weight"), E, E)], m=R, n=L, c=_p(b["Xtd"]),
                         ldc=LA, bias=w("_encoder.2.bias"))])
-        self.mm(b["Xtd"][:, :L], "_pi.0.weight", b["T1"], bias="_pi.0.bias")
-        self.act(b["T1"])
-        self.mm(b["T1"], "_pi.2.weight", b["T2"], bias="_pi.2.bias")
-        self.act(b["T2"])
+        self.prod([([(b["Xtd"][:, :L], 0, L)], "_pi.0.weight", b["T1"], "_pi.0.bias", False, False, EPI_ELU, None)])
+        self.prod([([(b["T1"], 0, M)], "_pi.2.weight", b["T2"], "_pi.2.bias", False, False, EPI_ELU, None)])
         self.gemm([dict(segs=[_seg(_p(b["T2"]), M, w("_pi.4.weight"), M, M)], m=R, n=A, c=_p(b["Xtd"], L),
                         ldc=LA, bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MUtd"]), ldc2=A,
                         std=float(self.cfg.min_std))])
         PA, PB = b["PAt"], b["PBt"]
-        for h in range(2):
-            self.mm(b["Xtd"], f"_Q{h + 1}.0.weight", PA[h, :R], bias=f"_Q{h + 1}.0.bias", target=True)
+        self.prod([([(b["Xtd"], 0, LA)], f"_Q{h + 1}.0.weight", PA[h, :R], f"_Q{h + 1}.0.bias", True, False,
+                    EPI_NONE, None) for h in range(2)])
         self.rows([dict(x=_p(PA[h]), y=_p(PB[h]), ln=1, g=wt(f"_Q{h + 1}.1.weight"), beta=wt(f"_Q{h + 1}.1.bias"),
                         act=TANH) for h in range(2)], R)
-        for h in range(2):
-            self.mm(PB[h, :R], f"_Q{h + 1}.3.weight", PA[h, :R], bias=f"_Q{h + 1}.3.bias", target=True)
+        self.prod([([(PB[h, :R], 0, M)], f"_Q{h + 1}.3.weight", PA[h, :R], f"_Q{h + 1}.3.bias", True, False,
+                    EPI_NONE, None) for h in range(2)])
         self.rows([dict(x=_p(PA[h]), ln=1, g=wt(f"_Q{h + 1}.4.weight"), beta=wt(f"_Q{h + 1}.4.bias"), act=ELU,
                         tail=1, w3=wt(f"_Q{h + 1}.6.weight"), b3=wt(f"_Q{h + 1}.6.bias"), out=_p(b["TQ"][h]))
                    for h in range(2)], R, reward=rew, td=_p(b["TD"]), gamma=float(self.cfg.discount))
 
-    def q_forward(self, b, n, parts):
+    def q_forward(self, b, n, parts, extra=()):
         """helper.q layer 1 + LayerNorm + Tanh for both Q heads over n rows; the input is the concatenation of
-        parts [(tensor [n, c1 - c0], c0, c1)] along the feature axis."""
+        parts [(tensor [n, c1 - c0], c0, c1)] along the feature axis. extra: more prod() specs run in the same
+        grouped launch as the two first layers (the reward head's, which reads the same input)."""
         w = self.w
         PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = (b[k] for k in ("PA", "PB", "Y1", "Y2", "XH1", "XH2", "RS1", "RS2"))
-        for h in range(2):
-            for i, (x, c0, c1) in enumerate(parts):
-                self.mm(x, f"_Q{h + 1}.0.weight", PA[h, :n], bias=f"_Q{h + 1}.0.bias", cols=(c0, c1), acc=i > 0)
+        self.prod([(parts, f"_Q{h + 1}.0.weight", PA[h, :n], f"_Q{h + 1}.0.bias", False, False, EPI_NONE, None)
+                   for h in range(2)] + list(extra))
         self.rows([dict(x=_p(PA[h]), y=_p(Y1[h]), xhat=_p(XH1[h]), rstd=_p(RS1[h]), ln=1,
                         g=w(f"_Q{h + 1}.1.weight"), beta=w(f"_Q{h + 1}.1.bias"), act=TANH) for h in range(2)], n)
         return PA, PB, Y1, Y2, XH1, XH2, RS1, RS2
@@ -314,13 +360,15 @@ class Engine:
             self.gemm([dict(segs=[_seg(_p(b["Yd2"], t * B * M), M, w("_dynamics.4.weight"), M, M)], m=B, n=L,
                             c=_p(X0, (t + 1) * B * LA), ldc=LA, bias=w("_dynamics.4.bias"),
                             c2=_p(b["ZP"], t * B * L), ldc2=L)])
-        PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(b, R, [(X0[:R], 0, LA)])
-        # reward head layer 1 (ELU) rides in its own slot 2 of PA / Y2 buffers
-        self.mm(X0[:R], "_reward.0.weight", PA[2, :R], bias="_reward.0.bias")
-        self.act(PA[2, :R])
-        for h in range(2):
-            self.mm(Y1[h, :R], f"_Q{h + 1}.3.weight", PB[h, :R], bias=f"_Q{h + 1}.3.bias")
-        self.mm(PA[2, :R], "_reward.2.weight", PB[2, :R], bias="_reward.2.bias")
+        # reward head layer 1 (ELU) rides in its own slot 2 of PA / Y2 buffers, in the Q heads' first-layer launch
+        PA = b["PA"]
+        PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(
+            b, R, [(X0[:R], 0, LA)], extra=[([(X0[:R], 0, LA)], "_reward.0.weight", PA[2, :R], "_reward.0.bias",
+                                              False, False, EPI_ELU, None)])
+        self.prod([([(Y1[h, :R], 0, M)], f"_Q{h + 1}.3.weight", PB[h, :R], f"_Q{h + 1}.3.bias", False, False,
+                    EPI_NONE, None) for h in range(2)] +
+                  [([(PA[2, :R], 0, M)], "_reward.2.weight", PB[2, :R], "_reward.2.bias", False, False, EPI_NONE,
+                    None)])
         Q = b["Q"]
         heads = [dict(x=_p(PB[h]), y=_p(Y2[h]), xhat=_p(XH2[h]), rstd=_p(RS2[h]), ln=1, g=w(f"_Q{h + 1}.4.weight"),
                       beta=w(f"_Q{h + 1}.4.bias"), act=ELU, tail=1, w3=w(f"_Q{h + 1}.6.weight"),
@@ -353,10 +401,9 @@ class Engine:
         heads.append(dict(y=_p(dP2[2]), yact=_p(Y2[2]), act=ELU, tail=1, w3=w("_reward.4.weight"), dq=_p(dq[2]),
                           part=_p(partr)))
         self.rows(heads, R, bwd=True)
-        for h in range(2):
-            self.mm(dP2[h, :R], f"_Q{h + 1}.3.weight", dA[h, :R], transpose=True)
-        self.gemm([dict(segs=[_seg(_p(dP2[2]), M, w("_reward.2.weight"), M, M, bmode=1)], m=R, n=M,
-                        c=_p(dP1[2]), ldc=M, epi=EPI_ELU_BWD, aux=_p(PA[2]), ldaux=M)])
+        self.prod([([(dP2[h, :R], 0, 0)], f"_Q{h + 1}.3.weight", dA[h, :R], None, False, True, EPI_NONE, None)
+                   for h in range(2)] +
+                  [([(dP2[2, :R], 0, 0)], "_reward.2.weight", dP1[2, :R], None, False, True, EPI_ELU_BWD, PA[2, :R])])
         self.rows([dict(x=_p(dA[h]), y=_p(dP1[h]), yact=_p(Y1[h]), xhat=_p(XH1[h]), rstd=_p(RS1[h]), ln=1,
                         g=w(f"_Q{h + 1}.1.weight"), act=TANH, part=_p(part1[h])) for h in range(2)], R, bwd=True)
         # gradient of z_t from the three heads (+ the consistency term on z_t): S = sum_h dP1_h W1_h[:, :L] + dZP
@@ -465,16 +512,14 @@ class Engine:
         n = nt * B
         w = self.w
         z, ldz = _p(zt), zt.stride(0)
-        self.mm(zt, "_pi.0.weight", b["Yp1"][:n], bias="_pi.0.bias")
-        self.act(b["Yp1"][:n])
-        self.mm(b["Yp1"][:n], "_pi.2.weight", b["Yp2"][:n], bias="_pi.2.bias")
-        self.act(b["Yp2"][:n])
+        self.prod([([(zt, 0, L)], "_pi.0.weight", b["Yp1"][:n], "_pi.0.bias", False, False, EPI_ELU, None)])
+        self.prod([([(b["Yp1"][:n], 0, M)], "_pi.2.weight", b["Yp2"][:n], "_pi.2.bias", False, False, EPI_ELU, None)])
         self.gemm([dict(segs=[_seg(_p(b["Yp2"]), M, w("_pi.4.weight"), M, M)], m=n, n=A, c=_p(b["ACT"]), ldc=A,
                         bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MU"]), ldc2=A,
                         std=float(self.cfg.min_std))])
         PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(b, n, [(zt, 0, L), (b["ACT"][:n], L, LA)])
-        for h in range(2):
-            self.mm(Y1[h, :n], f"_Q{h + 1}.3.weight", PB[h, :n], bias=f"_Q{h + 1}.3.bias")
+        self.prod([([(Y1[h, :n], 0, M)], f"_Q{h + 1}.3.weight", PB[h, :n], f"_Q{h + 1}.3.bias", False, False,
+                    EPI_NONE, None) for h in range(2)])
         Q = b["Q"]
         self.rows([dict(x=_p(PB[h]), y=_p(Y2[h]), xhat=_p(XH2[h]), rstd=_p(RS2[h]), ln=1, g=w(f"_Q{h + 1}.4.weight"),
                         beta=w(f"_Q{h + 1}.4.bias"), act=ELU, tail=1, w3=w(f"_Q{h + 1}.6.weight"),
@@ -487,8 +532,8 @@ class Engine:
         self.rows([dict(y=_p(dP2[h]), yact=_p(Y2[h]), xhat=_p(XH2[h]), rstd=_p(RS2[h]), ln=1,
                         g=w(f"_Q{h + 1}.4.weight"), act=ELU, tail=1, w3=w(f"_Q{h + 1}.6.weight"))
                    for h in range(2)], n, bwd=True, q1=_p(Q[0]), q2=_p(Q[1]), rho=_p(self.rho), bsz=B)
-        for h in range(2):
-            self.mm(dP2[h, :n], f"_Q{h + 1}.3.weight", dA[h, :n], transpose=True)
+        self.prod([([(dP2[h, :n], 0, 0)], f"_Q{h + 1}.3.weight", dA[h, :n], None, False, True, EPI_NONE, None)
+                   for h in range(2)])
         self.rows([dict(x=_p(dA[h]), y=_p(dP1[h]), yact=_p(Y1[h]), xhat=_p(XH1[h]), rstd=_p(RS1[h]), ln=1,
                         g=w(f"_Q{h + 1}.1.weight"), act=TANH) for h in range(2)], n, bwd=True)
         self.gemm([dict(segs=[_seg(_p(dP1[h]), M, w(f"_Q{h + 1}.0.weight") + 4 * L, LA, M, bmode=1)
@@ -496,8 +541,8 @@ class Engine:
                         m=n, n=A, c=_p(b["dACT"]), ldc=A, epi=EPI_PI_BWD, aux=_p(b["MU"]), ldaux=A)])
         self.gemm([dict(segs=[_seg(_p(b["dACT"]), A, w("_pi.4.weight"), M, A, bmode=1)], m=n, n=M,
                         c=_p(b["dPp2"]), ldc=M, epi=EPI_ELU_BWD, aux=_p(b["Yp2"]), ldaux=M)])
-        self.mm(b["dPp2"][:n], "_pi.2.weight", b["dPp1"][:n], transpose=True)
-        self.act(b["dPp1"][:n], b["Yp1"][:n])
+        self.prod([([(b["dPp2"][:n], 0, 0)], "_pi.2.weight", b["dPp1"][:n], None, False, True, EPI_ELU_BWD,
+                    b["Yp1"][:n])])
         sp = 4 if n >= 1024 else 1
         dw = [("_pi.4", A, M, [_seg(_p(b["dACT"]), A, _p(b["Yp2"]), M, n, 1, 1, M)], sp),
               ("_pi.2", M, M, [_seg(_p(b["dPp2"]), M, _p(b["Yp1"]), M, n, 1, 1, M)], sp),

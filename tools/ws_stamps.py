@@ -32,7 +32,10 @@ agent.plan_batch(obs, step=10**6, t0=False, sync_metrics=False)   # the last wid
 torch.cuda.synchronize()
 L.tdmpc_debug_plan1_stamps(None)
 st = buf.cpu().numpy().view(np.uint64).astype(np.int64)
+V2 = os.environ.get("TDMPC_WIDE2", "0") != "0"
 S1 = 2   # humanoid: 4 first-layer 32-k groups -> 2 steps per chunk, then 8 layer-2 steps
+if V2:
+    S1 = 4   # wide2: 4 phases of (4 layer-1 steps, 16 layer-2 steps)
 for name, base in (("dynamics wg0", 0), ("reward wg4", 4096)):
     for w in range(8):
         s = st[base + w * 512: base + w * 512 + 512].reshape(256, 2)
@@ -43,12 +46,17 @@ for name, base in (("dynamics wg0", 0), ("reward wg4", 4096)):
         tot = s[-1, 1] - s[0, 0]
         ph = {"L1": [], "L2": [], "L3": []}
         for k in range(n - 1):
-            c, r = divmod(k, S1 + 8)
-            key = "L3" if c >= 8 else ("L1" if r < S1 else "L2")
+            if V2:
+                c, r = divmod(k, S1 + 16)
+                key = "L3" if c >= 4 else ("L1" if r < S1 else "L2")
+            else:
+                c, r = divmod(k, S1 + 8)
+                key = "L3" if c >= 8 else ("L1" if r < S1 else "L2")
             ph[key].append(comp[k] + wait[k + 1])
         print(f"{name} wave {w}: steps {n} total {tot} cyc, wait {wait.sum()} ({wait.sum() / tot:.2f}); per-step "
               "(compute + next wait) median: " + ", ".join(f"{k} {np.median(v):.0f} x{len(v)}" for k, v in ph.items() if v))
         if w == 0:
             print("   first steps wait:", wait[:12].tolist())
             print("   first steps comp:", comp[:12].tolist())
-            print("   L2 steps comp:", comp[2:10].tolist(), "L3:", comp[80:90].tolist())
+            print("   steps comp:", comp[:24].tolist())
+            print("   steps wait:", wait[:24].tolist())
