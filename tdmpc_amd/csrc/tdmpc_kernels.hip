@@ -103,7 +103,7 @@ struct Layout {
     // [3 planes][64 lanes][8 bf16]: lane l (m = l & 15, q = l >> 4) element j holds row 16 nb + m,
     // k = 32 g + 16 (j >> 2) + 4 q + (j & 3) -- the v_mfma_f32_16x16x32_bf16 A fragment, in the k order in which a
     // 16x16 accumulator tile pair (a lane holding features 16t + 4q + i of its row) is the next layer's B fragment
-    size_t x6q[4];
+    size_t x6q[9];   // (X6_N: every x6 matrix; the wide kernels read W1X .. W3D and WQ1X, WQ2)
     size_t total;
 };
 
@@ -177,7 +177,7 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
         x6_shape(*w, i, &r, &k);
         w->x6[i] = take(rup(r, 32) * rup(k, 16) * 3 / 2);   // bf16 elements / 2 = floats
     }
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < X6_N; ++i) {
         int r, k;
         x6_shape(*w, i, &r, &k);
         w->x6q[i] = take(rup(r, 16) * rup(k, 32) * 3 / 2);
@@ -3057,6 +3057,7 @@ int set_lds_attr() {
 #include "plan1.inc"
 #include "wide_step.inc"
 #include "wide2.inc"
+#include "wide_q.inc"
 
 #define FOR_EACH_LINEAR(X)                                                                          \
     X(1, 1, 1, 1, 0, 32, false) X(1, 1, 1, 1, 0, 64, false) X(1, 1, 1, 1, 0, 128, false)              \
@@ -3081,6 +3082,10 @@ int init_attrs() {
     HIPCHK(hipFuncSetAttribute((const void*)wide2_step_kernel<G1, NB3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     WIDE_FOR_EACH(WIDE_ATTR)
 #undef WIDE_ATTR
+#define WIDE_Q_ATTR(G1) \
+    HIPCHK(hipFuncSetAttribute((const void*)wide_q_kernel<G1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    WIDE_Q_FOR_EACH(WIDE_Q_ATTR)
+#undef WIDE_Q_ATTR
     HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -3988,6 +3993,65 @@ int q_chain(const Ctx& c, int rows, RowMap map) {
     return launch_chain(CH_Q, a, 2, c.s);
 }
 
+// helper.q for both heads on the wide kernel (wide_q.inc) over `rows` rows of X_H mapped by `map` -> k.qv. Used for
+// the N sampled rows of every env when their 128-row blocks cover the CUs (B >= 32 envs at N = 512); the policy rows
+// stay on the chain kernel -- a row's kernel follows its role, never the launch size, as in step_next.
+// TDMPC_WIDE_Q=1 turns it on (off by default until measured).
+int wide_q_g1(const Ctx& c) { return (int)rup(c.Kx, 32) / 32; }
+bool use_wide_q(const Ctx& c, int rows, const RowMap& map) {
+    static const int en = [] { const char* e = getenv("TDMPC_WIDE_Q"); return e ? atoi(e) : 0; }();
+    if (!en || c.w.M != 512 || !use_x6(c) || !num_cus()) return false;
+    if (c.path != TDMPC_PATH_AUTO && c.path != TDMPC_PATH_CHAIN && c.path != TDMPC_PATH_WIDE) return false;
+    if (rows % 16 || map.G % 16 || map.S % 16 || map.O % 16) return false;
+    const int g1 = wide_q_g1(c);
+    if (g1 < 2 || g1 > 5) return false;
+    return c.path == TDMPC_PATH_WIDE || (rows + 127) / 128 * 2 >= num_cus();
+}
+int launch_wide_q(const Ctx& c, int rows, RowMap map) {
+    const Layout& w = c.w;
+    const int M = c.M;
+    WideQArgs a;
+    memset(&a, 0, sizeof a);
+    a.g1s = (int)(rup(c.Kx, 32) / 32);
+    const unsigned short* x1 = (const unsigned short*)(c.pw + w.x6q[X6_WQ1X]);
+    const unsigned short* x2 = (const unsigned short*)(c.pw + w.x6q[X6_WQ2]);
+    for (int h = 0; h < 2; ++h) {
+        a.X1[h] = x1 + (size_t)h * (M / 16) * a.g1s * 1536;
+        a.X2[h] = x2 + (size_t)h * (M / 16) * (M / 32) * 1536;
+        a.b1[h] = c.pw + w.bq1x + h * M; a.g1[h] = c.pw + w.g1 + h * M; a.be1[h] = c.pw + w.be1 + h * M;
+        a.b2[h] = c.pw + w.bq2 + h * M; a.g2[h] = c.pw + w.g2 + h * M; a.be2[h] = c.pw + w.be2 + h * M;
+        a.w3[h] = c.pw + w.wq3 + h * M; a.b3[h] = c.pw + w.bq3 + h;
+    }
+    a.rows = rows; a.nrb = (rows + 127) / 128; a.amap = map;
+    a.X = Xt(c, c.H); a.x_ts = (long)c.Kx * 32; a.kq = c.Kx / 4;
+    a.q = c.k.qv; a.q_ld = c.k.xrows;
+    const int g1 = wide_q_g1(c);
+    const dim3 grid((unsigned)rup(a.nrb, 4) * 2), block(64 * WS_NW);
+    // diagnostic timer (tdmpc_profile_begin cfg 7: the wide helper.q launches)
+    Profiler& pf = g_prof;
+    const bool prof = pf.armed && pf.cfg == 7 && pf.n + 2 <= pf.cap && (pf.rows == 0 || rows == pf.rows);
+    if (prof) {
+        snprintf(pf.kernel, sizeof pf.kernel, "wide_q_kernel<%d>", g1);
+        HIPCHK(hipEventRecord(pf.ev[pf.n], c.s));
+    }
+    bool done = false;
+#define WIDE_Q_LAUNCH(G1) \
+    if (!done && g1 == G1) { \
+        hipLaunchKernelGGL((wide_q_kernel<G1>), grid, block, ws_lds<G1>(), c.s, a); \
+        done = true; \
+    }
+    WIDE_Q_FOR_EACH(WIDE_Q_LAUNCH)
+#undef WIDE_Q_LAUNCH
+    if (!done) { snprintf(g_err, sizeof g_err, "wide q: no instance for G1 %d", g1); return TDMPC_E_DIMS; }
+    HIPCHK(hipGetLastError());
+    if (prof) {
+        HIPCHK(hipEventRecord(pf.ev[pf.n + 1], c.s));
+        pf.n += 2;
+        pf.flops += 2.0 * rows * 2 * ((double)(w.L + w.A) * M + (double)M * M + M);   // algorithmic (one layer 1)
+    }
+    return 0;
+}
+
 // Terminal value of `rows` rows of X_H mapped by `map`: the chain path leaves q1, q2 per row in k.qv (consumed
 // by cem_kernel / qvalue_kernel); the layered path gathers the rows into H1, runs the Q heads and writes
 // value = nan_to_num(G + gamma^H min(Q1, Q2)) back to the mapped rows (value_kernel).
@@ -4036,7 +4100,14 @@ int terminal_q_rows(const Ctx& c, int rows, RowMap map, float discH, bool chain)
 
 int terminal_q(const Ctx& c, float discH) {
     const int rows = c.B * c.T;
-    return terminal_q_rows(c, rows, RowMap{1 << 30, 0, 0}, discH, use_chain(c, rows, 2, CK_Q));
+    const bool chain = use_chain(c, rows, 2, CK_Q);
+    const RowMap rm = {c.N, c.T, 0}, pm = {c.P, c.T, c.N};
+    if (chain && use_wide_q(c, c.B * c.N, rm)) {   // sampled rows wide, policy rows chain (by role)
+        int rc;
+        if ((rc = launch_wide_q(c, c.B * c.N, rm))) return rc;
+        return c.P > 0 ? q_chain(c, c.B * c.P, pm) : 0;
+    }
+    return terminal_q_rows(c, rows, RowMap{1 << 30, 0, 0}, discH, chain);
 }
 
 // TOLD.h for `batch` observations -> z0 [B][Lp]; optionally initialises the CEM mean/std.
@@ -4400,7 +4471,7 @@ void pack_jobs(const Layout& w, const float* const* t, std::vector<PackJob>& job
         PackJob& j = job(PJ_X6, w.x6[x], (long)((rows + 31) / 32) * ((k + 15) / 16) * 512);
         j.m = *xs[x]; j.prow = rows; j.pk = k;
     }
-    for (int x = 0; x < 4; ++x) {
+    for (int x = 0; x < X6_N; ++x) {
         int rows, k;
         x6_shape(w, x, &rows, &k);
         PackJob& j = job(PJ_X6Q, w.x6q[x], (long)((rows + 15) / 16) * ((k + 31) / 32) * 512);
