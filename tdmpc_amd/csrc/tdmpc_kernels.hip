@@ -4027,9 +4027,9 @@ int launch_wide_q(const Ctx& c, int rows, RowMap map) {
     a.q = c.k.qv; a.q_ld = c.k.xrows;
     const int g1 = wide_q_g1(c);
     const dim3 grid((unsigned)rup(a.nrb, 4) * 2), block(64 * WS_NW);
-    // diagnostic timer (tdmpc_profile_begin cfg 7: the wide helper.q launches)
+    // diagnostic timer (tdmpc_profile_begin cfg 4 + CH_Q, as the chain helper.q launches)
     Profiler& pf = g_prof;
-    const bool prof = pf.armed && pf.cfg == 7 && pf.n + 2 <= pf.cap && (pf.rows == 0 || rows == pf.rows);
+    const bool prof = pf.armed && pf.cfg == 4 + CH_Q && pf.n + 2 <= pf.cap && (pf.rows == 0 || rows == pf.rows);
     if (prof) {
         snprintf(pf.kernel, sizeof pf.kernel, "wide_q_kernel<%d>", g1);
         HIPCHK(hipEventRecord(pf.ev[pf.n], c.s));

@@ -101,9 +101,10 @@ class Engine:
         # the learner's HIP graph as parallel branches): the TD target beside the encoder + latent rollout, the
         # heads' weight gradients beside the rollout's backward. Both pairs touch disjoint buffers.
         self.side = torch.cuda.Stream(self.dev)
-        # lg_gemm's products: fp32-accurate x6 (default) or the exact f32 MFMA (TDMPC_LG_X6=0, or set before the
-        # first update: the captured graph keeps the choice)
-        self.x6 = os.environ.get("TDMPC_LG_X6", "1") != "0"
+        # lg_gemm's products: the exact f32 MFMA (default: as fast as x6 on the learner's shapes, which are launch-
+        # and latency-bound rather than MFMA-bound) or the x6 form (TDMPC_LG_X6=1; set before the first update: the
+        # captured graph keeps the choice)
+        self.x6 = os.environ.get("TDMPC_LG_X6", "0") == "1"
         # every product on the hand-written lg_gemm (grouped launches, fused ELU / ELU' epilogues); TDMPC_LG_BLAS=1
         # puts the plain M x M products back on hipBLASLt (torch.mm / addmm) for an A/B
         self.blas = os.environ.get("TDMPC_LG_BLAS", "0") == "1"
