@@ -1127,6 +1127,72 @@ DEVI X6B split8(const float4& a0, const float4& a1) {
     return b;
 }
 
+// The x6 B operand as dwords (two bf16 per dword, the fragment's k order), THREE planes: x = h + m + l for finite x
+// (h its upper 16 bits, m = bf16(x - h), l = bf16(x - h - m)), and h = m = 0, l = x (inf, or a quiet bf16 NaN) for
+// non-finite x, so that of the six products only w_hi l = w_hi x carries it -- the fp32 product's inf / NaN, and
+// nothing from the w_mid / w_lo terms (split3_act's separate finite-zeroed hi plane does the same with a fourth
+// plane). Finite operands give the products of ws_x6 bit for bit. Built a PAIR of elements at a time and packed at
+// once (an element-wise bf16 build keeps every half in a register of its own until the vector is assembled).
+struct X6U { uint4 h, m, l; };
+typedef float w2f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 w2b2 __attribute__((ext_vector_type(2)));
+DEVI unsigned w2_pk(float a, float b) {   // round-to-nearest-even bf16 pair {a, b}
+    return __builtin_bit_cast(unsigned, __builtin_convertvector((w2f2){a, b}, w2b2));
+}
+DEVI void w2_split_pair(X6U& b, int d, float x0, float x1) {
+    const bool f0 = __builtin_isfinite(x0), f1 = __builtin_isfinite(x1);
+    const unsigned us0 = f0 ? __float_as_uint(x0) : 0u, us1 = f1 ? __float_as_uint(x1) : 0u;
+    const unsigned h = __builtin_amdgcn_perm(us1, us0, 0x07060302u);
+    const float r0 = __fsub_rn(__uint_as_float(us0), __uint_as_float(us0 & 0xffff0000u));
+    const float r1 = __fsub_rn(__uint_as_float(us1), __uint_as_float(us1 & 0xffff0000u));
+    const unsigned m = w2_pk(r0, r1);
+    unsigned l = w2_pk(__fsub_rn(r0, __uint_as_float(m << 16)), __fsub_rn(r1, __uint_as_float(m & 0xffff0000u)));
+    if (!f0) l = (l & 0xffff0000u) | (x0 != x0 ? 0x7fc0u : __float_as_uint(x0) >> 16);
+    if (!f1) l = (l & 0x0000ffffu) | (x1 != x1 ? 0x7fc00000u : __float_as_uint(x1) & 0xffff0000u);
+    if (d == 0) { b.h.x = h; b.m.x = m; b.l.x = l; }
+    else if (d == 1) { b.h.y = h; b.m.y = m; b.l.y = l; }
+    else if (d == 2) { b.h.z = h; b.m.z = m; b.l.z = l; }
+    else { b.h.w = h; b.m.w = m; b.l.w = l; }
+}
+DEVI X6U w2_split8(const float4& a0, const float4& a1) {
+    X6U b;
+    w2_split_pair(b, 0, a0.x, a0.y);
+    w2_split_pair(b, 1, a0.z, a0.w);
+    w2_split_pair(b, 2, a1.x, a1.y);
+    w2_split_pair(b, 3, a1.z, a1.w);
+    return b;
+}
+// w2_split_pair for operands known finite (the caller checked the whole wave's values): 48 instead of 106 VALU per
+// eight elements (split8's four-plane form: 74)
+DEVI void w2_split_pair_fin(X6U& b, int d, float x0, float x1) {
+    const unsigned us0 = __float_as_uint(x0), us1 = __float_as_uint(x1);
+    const unsigned h = __builtin_amdgcn_perm(us1, us0, 0x07060302u);
+    const float r0 = __fsub_rn(x0, __uint_as_float(us0 & 0xffff0000u));
+    const float r1 = __fsub_rn(x1, __uint_as_float(us1 & 0xffff0000u));
+    const unsigned m = w2_pk(r0, r1);
+    const unsigned l = w2_pk(__fsub_rn(r0, __uint_as_float(m << 16)), __fsub_rn(r1, __uint_as_float(m & 0xffff0000u)));
+    if (d == 0) { b.h.x = h; b.m.x = m; b.l.x = l; }
+    else if (d == 1) { b.h.y = h; b.m.y = m; b.l.y = l; }
+    else if (d == 2) { b.h.z = h; b.m.z = m; b.l.z = l; }
+    else { b.h.w = h; b.m.w = m; b.l.w = l; }
+}
+// true when a value every lane of the wave computed is finite (a sum of a lane's elements is non-finite when one of
+// them is; an overflowing sum only sends the wave down the general path)
+DEVI bool ws_wave_finite(float s) { return __builtin_amdgcn_ballot_w64(!__builtin_isfinite(s)) == 0; }
+DEVI float ws_sum8(const float4& a0, const float4& a1) {
+    return ((a0.x + a0.y) + (a0.z + a0.w)) + ((a1.x + a1.y) + (a1.z + a1.w));
+}
+// The activation operand in three planes for finite values (the wave-uniform fast path of the chain and wide
+// kernels' splits; x6_group / x6_group16 and ws_opnd)
+DEVI X6U w2_split8_fin(const float4& a0, const float4& a1) {
+    X6U b;
+    w2_split_pair_fin(b, 0, a0.x, a0.y);
+    w2_split_pair_fin(b, 1, a0.z, a0.w);
+    w2_split_pair_fin(b, 2, a1.x, a1.y);
+    w2_split_pair_fin(b, 3, a1.z, a1.w);
+    return b;
+}
+
 // Weight ring of the x6 form: D k groups (16 k each) x TN blocks x 3 planes of 1 KiB wave loads. Wp is the wave's
 // first block already offset by the lane (lane * 8 bf16); blocks wbs bf16 apart.
 template <int TN, int D>
@@ -1141,9 +1207,29 @@ DEVI void ring6_fill(uint4 (&wr)[D][TN][3], const unsigned short* Wp, long wbs, 
                 wr[d][j][p] = *(const uint4*)(Wp + j * wbs + ((size_t)min(g0 + d, gl) * 3 + p) * 512);
 }
 
+// -DCH_FAST (an A/B, off: the chain kernels measured 3-7 % slower with it, 192.5 vs 186 us per humanoid Q launch,
+// while the wide step kernel gains 2.7 % from the same split): the operand in three planes, split by the finite-only
+// form when all of the wave's eight-element groups are finite (a wave-uniform branch), by the general one otherwise;
+// the products are bitwise split8's for finite operands and carry a non-finite x through w_hi x alone, as split8's
+#ifdef CH_FAST
+struct X6C { bf16x8_t h, s, m, l; };   // s = h: the product table below reads b.s where split8 has its finite-zeroed hi
+DEVI X6C ch_split(const float4& a0, const float4& a1) {
+    X6U u;
+    if (__builtin_amdgcn_ballot_w64(!__builtin_isfinite(((a0.x + a0.y) + (a0.z + a0.w)) + ((a1.x + a1.y) + (a1.z + a1.w)))) == 0)
+        u = w2_split8_fin(a0, a1);
+    else
+        u = w2_split8(a0, a1);
+    X6C b;
+    b.h = as_bf16x8(u.h); b.s = b.h; b.m = as_bf16x8(u.m); b.l = as_bf16x8(u.l);
+    return b;
+}
+#else
+DEVI X6B ch_split(const float4& a0, const float4& a1) { return split8(a0, a1); }
+#endif
+
 template <int TN>
 DEVI void x6_group(floatx16 (&acc)[TN], const uint4 (&w)[TN][3], const float4& a0, const float4& a1) {
-    const X6B b = split8(a0, a1);
+    const auto b = ch_split(a0, a1);
     // small terms first, the hi.hi term last
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(w[j][1]), b.m, acc[j], 0, 0, 0);
@@ -1698,7 +1784,7 @@ DEVI void ring16x6_fill(uint4 (&wr)[D][NT][3], const unsigned short* Wb, int nf0
 
 template <int NT>
 DEVI void x6_group16(floatx4 (&acc)[NT], const uint4 (&w)[NT][3], const float4& a0, const float4& a1) {
-    const X6B b = split8(a0, a1);
+    const auto b = ch_split(a0, a1);
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j][1]), b.m, acc[j], 0, 0, 0);
 #pragma unroll
