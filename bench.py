@@ -53,6 +53,7 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector peak (spe
 # the dense BF16 MFMA peak / 6 in fp32-product FLOP/s (BF16 = 16 x the f32 MFMA rate, MI355X_MICROARCH.md)
 X6_PEAK_TFLOPS = round(FP32_PEAK_TFLOPS * 16 / 6, 1)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
+LDSDMA_CEILING_TBS = 6.4   # MI355X_MICROARCH.md price list, ldsdma-fill: LDS-DMA weight stream over the chip
 
 
 def plan_flops(cfg, executed: bool) -> float:
@@ -667,6 +668,21 @@ def step_roofline(cfg, B, agent, one_step, n_r, dev, pmc_prefix):
     if roof["traffic"]:
         roof["hbm_gbs_pmc"] = round(roof["traffic"] / avg_s / 1e9, 1)
         roof["hbm_frac_pmc"] = round(roof["hbm_gbs_pmc"] / HBM_PEAK_GBS, 4)
+    if n > 0 and wide:
+        # the roof that binds the wide kernel with every CU streaming: each workgroup fills its head's
+        # x6 weight fragments (3 KiB each, 8 per step) from L2 into LDS once per launch -- dynamics 8 chunks x
+        # (S1 + 8) steps + 2 NB3 layer-3 steps, reward 8 x (S1 + 8) -- against the LDS-DMA fill ceiling over the
+        # chip (MI355X_MICROARCH.md, ldsdma-fill: ~6.4 TB/s default policy)
+        g1, nb3 = (int(v) for v in name[name.index("<") + 1:name.index(">")].split(","))
+        s1 = (g1 + 1) // 2
+        nrb = -(-rows // 128)
+        fill = float(nrb * (8 * (s1 + 8) * 2 + 2 * nb3) * 8 * 3072)
+        tbs = fill / avg_s / 1e12
+        roof["weight_stream"] = {
+            "bytes_per_launch": fill, "achieved_tbs": round(tbs, 3), "ceiling_tbs": LDSDMA_CEILING_TBS,
+            "frac": round(tbs / LDSDMA_CEILING_TBS, 4),
+            "note": "L2 -> LDS x6 weight fills of all workgroups per launch; with half the CUs streaming (B = 16) the "
+                    "same kernel's per-CU stream cost drops from ~17 to ~6 us (profiles/r04/wide_diag_r4g.txt)"}
     return roof
 
 

@@ -105,6 +105,8 @@ class Engine:
         # and latency-bound rather than MFMA-bound) or the x6 form (TDMPC_LG_X6=1; set before the first update: the
         # captured graph keeps the choice)
         self.x6 = os.environ.get("TDMPC_LG_X6", "0") == "1"
+        # 64 x 64 tiles from this many 64 x 64 output tiles per launch (TDMPC_LG_T64, an A/B knob)
+        self.t64 = int(os.environ.get("TDMPC_LG_T64", "240"))
         # every product on the hand-written lg_gemm (grouped launches, fused ELU / ELU' epilogues); TDMPC_LG_BLAS=1
         # puts the plain M x M products back on hipBLASLt (torch.mm / addmm) for an A/B
         self.blas = os.environ.get("TDMPC_LG_BLAS", "0") == "1"
@@ -223,7 +225,7 @@ class Engine:
             # 64 x 64 tiles only for wide launches of row-major operands; a transposed weight operand (the
             # backward's dX) runs 15-25 % faster on 32 x 32 tiles (tools/lg_gemm_bench.py)
             tbw = any(sg[6] == 1 for j in jobs for sg in j["segs"])
-            tile = 2 if tiles64 >= 240 and not tbw else 1
+            tile = 2 if tiles64 >= self.t64 and not tbw else 1
         tile |= 0 if self.x6 else TILE_EXACT
         _lib.check(self.lib.tdmpc_lg_gemm(arr, len(jobs), tile, self._stream()), "tdmpc_lg_gemm")
 
