@@ -3819,11 +3819,24 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
 
 // defer = 1 (a loop of consecutive steps over the same rows, nothing reading X_{t+1}'s latents in between): on the
 // split path the finish of this step is folded into the next step's launch.
+// TDMPC_PSPLIT=1 (A/B): iteration 0's policy-row step launches (the rows the wide kernel leaves to the narrow
+// kernels by role) on the column-split kernel instead of the chain kernel
+static bool psplit_on() {
+    static const int v = [] { const char* e = getenv("TDMPC_PSPLIT"); return e ? atoi(e) : 0; }();
+    return v != 0;
+}
+static bool split_fits(const Ctx& c, int rows) {
+    const Layout& w = c.w;
+    return w.M == 512 && rows <= c.k.split_rows && (size_t)split_lds_floats(w.Kx, w.M) * 4 <= 64 * 1024 &&
+           (int)rup(w.Kx, 16) <= w.M / 2;
+}
+
 int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, int defer = 0,
               bool nowide = false) {
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
+    const bool psplit = nowide && psplit_on() && split_fits(c, rows);
     if (c.split_pend && (!use_split(c, rows) || rows != c.split_rows || t != c.split_t + 1 ||
                          memcmp(&map, &c.split_map, sizeof map)))
         if ((rc = flush_split(c))) return rc;
@@ -3850,7 +3863,7 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
             return launch_wide(c, t, rows, map, disc, first, last, z0c);
         }
     }
-    if (use_chain(c, rows, 2, CK_STEP)) {
+    if (!psplit && use_chain(c, rows, 2, CK_STEP)) {
         ChainArgs a = chain0(c, rows, map, t, c.Kx, 0, 2);
         ChainProb& d = a.p[0];
         d.W1 = c.pw + w.w1x; d.b1 = c.pw + w.b1x; d.W2 = c.pw + w.w2d; d.b2 = c.pw + w.b2d;
@@ -3868,7 +3881,7 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         if (t == 0 && c.z0c_ready && map.G % 32 == 0) { a.z0c = c.k.z0c; a.z0_G = map.G; a.k1c = z0c_k1c(c); }
         return launch_chain(CH_STEP, a, 2, c.s);
     }
-    if (use_split(c, rows)) {
+    if (psplit || use_split(c, rows)) {
         const int par = c.split_par;
         const size_t zs = (size_t)SPLIT_S * c.k.split_rows * std::max(w.Lr, w.Ar), rs = (size_t)SPLIT_S * c.k.split_rows;
         SplitArgs a;
@@ -3940,11 +3953,14 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
 
 // pi(z_t) with TruncatedNormal noise for `rows` rows of X_t -> X_t action columns (tdmpc.py:39-45).
 int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps_env, int eps_G, long eps_off,
-           float min_std, float* mu_out = nullptr) {
+           float min_std, float* mu_out = nullptr, bool prow = false) {
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
-    if (use_chain(c, rows, 1, CK_PI)) {
+    // (TDMPC_PSPLIT=1: the policy rows' pre-rollout pi on the column-split kernel, as their steps)
+    const bool psplit = prow && !mu_out && psplit_on() && w.M == 512 && rows <= c.k.split_rows &&
+                        (size_t)split_lds_floats(w.Lp, w.M) * 4 <= 64 * 1024 && (int)rup(w.Lp, 16) <= w.M / 2;
+    if (!psplit && use_chain(c, rows, 1, CK_PI)) {
         ChainArgs a = chain0(c, rows, map, t, w.Lp, w.Ap / 4, 1);
         ChainProb& p = a.p[0];
         p.W1 = c.pw + w.wp1; p.b1 = c.pw + w.bp1; p.W2 = c.pw + w.wp2; p.b2 = c.pw + w.bp2;
@@ -3956,7 +3972,7 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
         a.mu_out = mu_out;
         return launch_chain(CH_PI, a, 1, c.s);
     }
-    if (use_split_pi(c, rows)) {
+    if (psplit || use_split_pi(c, rows)) {
         if ((rc = flush_split(c))) return rc;
         SplitArgs a;
         memset(&a, 0, sizeof a);
@@ -4891,7 +4907,8 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     const RowMap rm = {N, T, 0};
     if (P > 0) {
         for (int t = 0; t < H; ++t) {
-            if ((rc = policy(c, t, B * P, pm, noise, c.eps_env, P, (long)t * P * c.A, prm->min_std))) return rc;
+            if ((rc = policy(c, t, B * P, pm, noise, c.eps_env, P, (long)t * P * c.A, prm->min_std, nullptr, true)))
+                return rc;
             if ((rc = step_next(c, t, B * T, all, prm->discount_pow[t], t == 0, t == H - 1)))
                 return rc;
         }
