@@ -214,6 +214,9 @@ struct Work {
     float* enc_tmp;  // pixel conv activations
     size_t x_stride; // floats per X_t
     int xrows;       // rup(B*T, 32)
+    float* XP;       // panel [pq_rows][Kx]: the policy rows' terminal inputs [a_H^i | z_H] of every CEM iteration i
+    float* qp;       // [2][pq_rows] their helper.q outputs (one launch at iteration 0; see terminal_q)
+    int pq_rows;     // rup(B * Imax * P, 32)
     char* p1;        // exchange region of the persistent one-env plan (plan1.inc), p1_bytes (0: not eligible)
     size_t p1_bytes;
     size_t total;
@@ -322,6 +325,9 @@ void make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k, int ex
     k->mean = (float*)take(B * H * w.A * 4);
     k->stdv = (float*)take(B * H * w.A * 4);
     k->enc_tmp = (float*)take(d->modality ? 2 * B * pixel_act_floats(w) * 4 : 256);
+    k->pq_rows = extra ? 0 : (int)rup(B * (size_t)d->max_iterations * P, 32);
+    k->XP = (float*)take((size_t)std::max(k->pq_rows, 32) * w.Kx * 4);
+    k->qp = (float*)take(2 * (size_t)std::max(k->pq_rows, 32) * 4);
     k->p1_bytes = p1_dims_ok(d, w) && !extra ? p1_region(d, w).total : 0;
     k->p1 = k->p1_bytes ? (char*)take(k->p1_bytes) : nullptr;
     k->total = o;
@@ -2427,7 +2433,7 @@ __global__ void __launch_bounds__(256) z0c_kernel(const float* W1, const float* 
 // cached (ChainArgs::mu_out); only the TruncatedNormal sample is redrawn, with the chain epilogue's arithmetic.
 // One thread per (row, action quad).
 struct PiMuArgs {
-    int rows; RowMap amap; const float* mu; int Ap, A; float* Xo; long x_ts;
+    int rows; RowMap amap; RowMap mmap; const float* mu; int Ap, A; float* Xo; long x_ts;   // mu row: map_row(mmap, row)
     const float* eps; int eps_G; long eps_env; long eps_off; float min_std, lo, hi;
 };
 
@@ -2439,7 +2445,7 @@ __global__ void __launch_bounds__(256) pi_from_mu_kernel(const PiMuArgs a) {
     const int xr = map_row(a.amap, row);
     const int e = row / a.eps_G, rr = row % a.eps_G;
     const float* ep = a.eps + (size_t)e * a.eps_env + a.eps_off + (size_t)rr * a.A;
-    const float4 m = *(const float4*)(a.mu + (size_t)xr * a.Ap + 4 * q);
+    const float4 m = *(const float4*)(a.mu + (size_t)map_row(a.mmap, row) * a.Ap + 4 * q);
     const float mv[4] = {m.x, m.y, m.z, m.w};
     float o[4];
 #pragma unroll
@@ -2456,6 +2462,29 @@ __global__ void __launch_bounds__(256) pi_from_mu_kernel(const PiMuArgs a) {
         o[cc] = x;
     }
     *(float4*)(a.Xo + (size_t)(xr >> 5) * a.x_ts + (size_t)q * 128 + (xr & 31) * 4) = make_float4(o[0], o[1], o[2], o[3]);
+}
+
+// The policy rows' terminal inputs of every CEM iteration (terminal_q's precompute): XP row (i B + e) P + p <- X_H
+// row e T + N + p, all Kx columns (iteration i's actions are rewritten by pi_from_mu_kernel for i >= 1).
+struct PqArgs {
+    const float* X; float* XP; long x_ts; int kq; int B, P, N, T, I;
+    const float* qp; float* qv; int qp_ld, q_ld, iter;   // pq_copy_kernel: iteration `iter`'s slice -> k.qv
+};
+__global__ void __launch_bounds__(256) pq_fill_kernel(const PqArgs a) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long rows = (long)a.I * a.B * a.P;
+    if (i >= rows * a.kq) return;
+    const int r = (int)(i / a.kq), qd = (int)(i % a.kq);
+    const int p = r % a.P, e = (r / a.P) % a.B;
+    const int xr = e * a.T + a.N + p;
+    const float4 v = *(const float4*)(a.X + (size_t)(xr >> 5) * a.x_ts + (size_t)qd * 128 + (xr & 31) * 4);
+    *(float4*)(a.XP + (size_t)(r >> 5) * a.x_ts + (size_t)qd * 128 + (r & 31) * 4) = v;
+}
+__global__ void __launch_bounds__(256) pq_copy_kernel(const PqArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 2 * a.B * a.P) return;
+    const int h = i / (a.B * a.P), r = i % (a.B * a.P), e = r / a.P, p = r % a.P;
+    a.qv[(size_t)h * a.q_ld + e * a.T + a.N + p] = a.qp[(size_t)h * a.qp_ld + (size_t)a.iter * a.B * a.P + r];
 }
 
 // estimate_value's terminal combination (tdmpc.py:91-92): G + gamma^H min(Q1, Q2), nan_to_num.
@@ -4038,11 +4067,11 @@ int pi_cache_on() {
 
 // pi(z_H) of `rows` rows from the cached means k.pimu (pi_from_mu_kernel) -> X_H action columns.
 int policy_from_mu(const Ctx& c, int rows, RowMap map, const float* eps, long eps_env, int eps_G, long eps_off,
-                   float min_std) {
+                   float min_std, float* Xo = nullptr, const RowMap* mmap = nullptr) {
     PiMuArgs f;
     memset(&f, 0, sizeof f);
-    f.rows = rows; f.amap = map; f.mu = c.k.pimu; f.Ap = c.w.Ap; f.A = c.w.A;
-    f.Xo = Xt(c, c.H); f.x_ts = (long)c.Kx * 32;
+    f.rows = rows; f.amap = map; f.mmap = mmap ? *mmap : map; f.mu = c.k.pimu; f.Ap = c.w.Ap; f.A = c.w.A;
+    f.Xo = Xo ? Xo : Xt(c, c.H); f.x_ts = (long)c.Kx * 32;
     f.eps = eps; f.eps_G = eps_G; f.eps_env = eps_env; f.eps_off = eps_off; f.min_std = min_std;
     f.lo = (float)(-1.0 + 1e-6); f.hi = (float)(1.0 - 1e-6);
     const long nth = (long)rows * (c.w.Ap / 4);
@@ -4075,10 +4104,11 @@ int prep(const Ctx& c, const float* noise, int iter, const float* z0) {
 
 // helper.q for both heads over `rows` rows of X_H mapped by `map`, on the chain kernel: q_p per row into k.qv
 // (the value combination happens where it is consumed: cem_kernel / qvalue_kernel).
-int q_chain(const Ctx& c, int rows, RowMap map) {
+int q_chain(const Ctx& c, int rows, RowMap map, const float* X = nullptr, float* qo = nullptr, int q_ld = 0) {
     const Layout& w = c.w;
     const int M = c.M;
     ChainArgs a = chain0(c, rows, map, c.H, c.Kx, 0, 2);
+    if (X) a.X = X;
     for (int q = 0; q < 2; ++q) {
         ChainProb& p = a.p[q];
         p.W1 = c.pw + w.wq1x + (size_t)q * M * c.Kx; p.b1 = c.pw + w.bq1x + q * M;
@@ -4091,7 +4121,7 @@ int q_chain(const Ctx& c, int rows, RowMap map) {
             p.X2 = x6p(c, X6_WQ2) + (size_t)q * (M / 32) * (M / 16) * 1536;
         }
     }
-    a.q = c.k.qv; a.q_ld = c.k.xrows;
+    a.q = qo ? qo : c.k.qv; a.q_ld = qo ? q_ld : c.k.xrows;
     return launch_chain(CH_Q, a, 2, c.s);
 }
 
@@ -4200,14 +4230,45 @@ int terminal_q_rows(const Ctx& c, int rows, RowMap map, float discH, bool chain)
     return 0;
 }
 
-int terminal_q(const Ctx& c, float discH) {
+// Sampled rows on the wide kernel, policy rows on the chain kernel (by role). The policy rows' terminal inputs
+// differ between CEM iterations only in the pre-drawn terminal noise (their z_H and cached pi mean are fixed), so with
+// `pq` (plan_cem's iteration loop, pi mean cache on) iteration 0 forms all I iterations' inputs and runs their Q in ONE
+// chain launch (one latency-bound launch instead of I); each iteration copies its slice into k.qv.
+bool use_pq(const Ctx& c, int I) {
+    static const int en = [] { const char* e = getenv("TDMPC_PQ"); return e ? atoi(e) : 1; }();
+    return en && c.P > 0 && I > 1 && c.k.pq_rows >= c.B * I * c.P && c.N + c.P == c.T;
+}
+int terminal_q(const Ctx& c, float discH, int iter = 0, int I = 1, bool pq = false, const float* noise = nullptr,
+               float min_std = 0.f) {
     const int rows = c.B * c.T;
     const bool chain = use_chain(c, rows, 2, CK_Q);
     const RowMap rm = {c.N, c.T, 0}, pm = {c.P, c.T, c.N};
-    if (chain && use_wide_q(c, c.B * c.N, rm)) {   // sampled rows wide, policy rows chain (by role)
+    if (chain && use_wide_q(c, c.B * c.N, rm)) {
         int rc;
         if ((rc = launch_wide_q(c, c.B * c.N, rm))) return rc;
-        return c.P > 0 ? q_chain(c, c.B * c.P, pm) : 0;
+        if (c.P == 0) return 0;
+        if (!pq) return q_chain(c, c.B * c.P, pm);
+        const int BP = c.B * c.P;
+        PqArgs a;
+        memset(&a, 0, sizeof a);
+        a.X = Xt(c, c.H); a.XP = c.k.XP; a.x_ts = (long)c.Kx * 32; a.kq = c.Kx / 4;
+        a.B = c.B; a.P = c.P; a.N = c.N; a.T = c.T; a.I = I;
+        a.qp = c.k.qp; a.qv = c.k.qv; a.qp_ld = c.k.pq_rows; a.q_ld = c.k.xrows; a.iter = iter;
+        if (iter == 0) {
+            const long nth = (long)I * BP * a.kq;
+            hipLaunchKernelGGL(pq_fill_kernel, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, c.s, a);
+            HIPCHK(hipGetLastError());
+            for (int i = 1; i < I; ++i) {   // iteration i's terminal actions, as policy_from_mu writes them then
+                const long toff = c.eps_cem_off + (long)i * c.eps_iter + c.eps_term_off;
+                const RowMap xm = {1 << 30, 0, i * BP};
+                if ((rc = policy_from_mu(c, BP, xm, noise, c.eps_env, c.P, toff + (long)c.N * c.A, min_std, c.k.XP, &pm)))
+                    return rc;
+            }
+            if ((rc = q_chain(c, I * BP, RowMap{1 << 30, 0, 0}, c.k.XP, c.k.qp, c.k.pq_rows))) return rc;
+        }
+        hipLaunchKernelGGL(pq_copy_kernel, dim3((unsigned)((2 * BP + 255) / 256)), dim3(256), 0, c.s, a);
+        HIPCHK(hipGetLastError());
+        return 0;
     }
     return terminal_q_rows(c, rows, RowMap{1 << 30, 0, 0}, discH, chain);
 }
@@ -4953,7 +5014,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
                                 pi_cache ? c.k.pimu : nullptr))) {
             return rc;
         }
-        if ((rc = terminal_q(c, prm->discount_pow[H]))) return rc;
+        if ((rc = terminal_q(c, prm->discount_pow[H], i, I, pi_cache && use_pq(c, I), noise, prm->min_std))) return rc;
         ca.final_iter = i == I - 1;
         ca.iter = i;
         hipLaunchKernelGGL(cem_kernel, dim3(B), dim3(1024), cem_lds, c.s, ca);
