@@ -76,6 +76,8 @@ int main(int argc, char** argv) {
     CK(hipStreamCreate(&s));
     void *packed, *ws;
     CK(hipMalloc(&packed, sz.packed_weight_bytes));
+    CK(hipMemset(packed, 0, sz.packed_weight_bytes));   // zero-filled once and announced (tdmpc_hip.h)
+    CT(tdmpc_pack_forget(packed));
     CK(hipMalloc(&ws, sz.workspace_bytes));
     CT(tdmpc_pack_weights(&d, tens, (int)dev.size(), packed, sz.packed_weight_bytes, s));
 

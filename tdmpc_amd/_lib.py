@@ -11,11 +11,11 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDMPC_LIB_PATH") or os.path.join(HERE, "libtdmpc_hip.so")   # override: A/B of builds
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 PATHS = {"auto": 0, "layered": 1, "chain": 2, "chain32": 3, "chain16": 4, "split": 5, "chain_x6": 6, "split_x6": 7, "chain64": 8, "persist": 9, "wide": 10}
 
 EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc_num_param_tensors",
-            "tdmpc_pack_weights", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_pi_rollout",
+            "tdmpc_pack_weights", "tdmpc_pack_forget", "tdmpc_encode", "tdmpc_plan", "tdmpc_estimate_value", "tdmpc_pi_rollout",
             "tdmpc_cem_iter", "tdmpc_reference_normals", "tdmpc_last_error", "tdmpc_debug_plan1_stamps",
             "tdmpc_debug_pack_check",
             "tdmpc_profile_begin", "tdmpc_profile_end", "tdmpc_profile_kernel", "tdmpc_icem_sizes_for", "tdmpc_plan_icem",
@@ -127,6 +127,7 @@ def lib():
     L.tdmpc_reference_normals.argtypes = [C.POINTER(Dims), vp, i32, C.c_int64, i32, i32, i32, C.c_uint64,
                                           C.c_uint64, vp, i32, C.POINTER(C.c_uint64), vp]
     L.tdmpc_pack_weights.argtypes = [C.POINTER(Dims), C.POINTER(vp), i32, vp, sz, vp]
+    L.tdmpc_pack_forget.argtypes = [vp]
     if hasattr(L, "tdmpc_debug_pack_check"):   # (diagnostic; absent from older builds used in A/B runs)
         L.tdmpc_debug_pack_check.argtypes = [C.POINTER(Dims), C.POINTER(C.c_int64), i32]
     L.tdmpc_encode.argtypes = [C.POINTER(Dims), vp, vp, i32, i32, vp, vp, vp]

@@ -27,7 +27,7 @@ def hipcc() -> str:
 def build(force: bool = False, verbose: bool = True, variant: str = "", defines=()) -> str:
     """The library (every source compiled in parallel, then linked); a variant (-DNAME defines, diagnostics or an A/B
     of a kernel knob) goes to libtdmpc_hip_<variant>.so, loaded with TDMPC_LIB_PATH."""
-    deps = SRCS + [os.path.join(HERE, "csrc", f) for f in ("plan1.inc", "wide_step.inc", "wide2.inc", "wide_q.inc")] + \
+    deps = SRCS + [os.path.join(HERE, "csrc", f) for f in ("plan1.inc", "wide_step.inc", "wide_heads.inc")] + \
         [os.path.join(REPO, "include", h) for h in ("tdmpc_hip.h", "tdmpc_replay.h", "tdmpc_learner.h")]
     out = OUT if not variant else os.path.join(HERE, f"libtdmpc_hip_{variant}.so")
     if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
@@ -35,7 +35,8 @@ def build(force: bool = False, verbose: bool = True, variant: str = "", defines=
     # -fno-slp-vectorize: no packed v_pk_add/mul_f32 from pairs of scalar f32 ops -- beside MFMAs a packed f32 VALU
     # instruction costs ~+22-26 cycles where two scalar ones are free (MI355X_MICROARCH.md, filler prices)
     base = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vectorize",
-            "-I", os.path.join(REPO, "include")] + [f"-D{d}" for d in defines]
+            "-I", os.path.join(REPO, "include")] + [f"-D{d}" for d in defines] + \
+        ([f"-DTDMPC_VARIANT={variant}"] if variant else [])
     objs, procs = [], []
     for src in SRCS:
         obj = os.path.join(HERE, "csrc", os.path.basename(src) + (f".{variant}" if variant else "") + ".o")

@@ -104,8 +104,16 @@ struct Layout {
     // k = 32 g + 16 (j >> 2) + 4 q + (j & 3) -- the v_mfma_f32_16x16x32_bf16 A fragment, in the k order in which a
     // 16x16 accumulator tile pair (a lane holding features 16t + 4q + i of its row) is the next layer's B fragment
     size_t x6q[9];   // (X6_N: every x6 matrix; the wide kernels read W1X .. W3D and WQ1X, WQ2)
+    size_t jobtab;   // the fused pack's job table (launch_pack): caller-owned, lives and dies with the packed buffer
+    // helper.q's LayerNorm-1 statistics block (wide_heads.inc; written by qstat_*_kernel after every pack) for planners
+    // whose batches reach the wide kernels: nqs = the first layer's real columns + its bias (A + L + 1), 0 = none
+    int nqs, nsr;          // columns of the Cholesky factor; statistics rows per Q head (16 x 8 or 16 x 16)
+    size_t x6qs, bqs;      // x6q [2][nsr][rup(Kx, 32)]; bias [2][nsr]
+    size_t qs_gram;        // fp64 scratch [2][nqs][nqs] (the Gram matrices)
     size_t total;
 };
+constexpr int PACK_MAX_JOBS = 96;              // job-table capacity (pack_jobs emits ~40-60)
+constexpr int PACK_JOB_BYTES = 192;            // >= sizeof(PackJob) (static_assert at its definition)
 
 // Matrices kept in the x6 layout: fp32 = hi + mid + lo, three bf16 planes. Block (nb, g) of 32 rows x 16 k is
 // [3 planes][64 lanes][8 bf16]: lane l (r = l & 31, h = l >> 5) element j holds row 32 nb + r,
@@ -182,6 +190,22 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
         x6_shape(*w, i, &r, &k);
         w->x6q[i] = take(rup(r, 16) * rup(k, 32) * 3 / 2);
     }
+    w->jobtab = take((size_t)PACK_MAX_JOBS * PACK_JOB_BYTES / 4);
+    // the statistics block: only where the wide heads may run (B N >= 4096 rows, M = 512) and the Cholesky's
+    // upper-packed fp64 factor fits one workgroup's LDS
+    w->nqs = w->nsr = 0;
+    w->x6qs = w->bqs = w->qs_gram = 0;
+    {
+        const int n = w->A + w->L + 1;
+        if (w->M == 512 && (long)d->max_batch * d->num_samples >= 4096 && n + 1 <= 256 &&
+            ((size_t)n * (n + 1) / 2 + n) * 8 <= 150 * 1024) {
+            w->nqs = n;
+            w->nsr = n + 1 <= 128 ? 128 : 256;
+            w->x6qs = take((size_t)2 * w->nsr * rup(w->Kx, 32) * 3 / 2);
+            w->bqs = take((size_t)2 * w->nsr);
+            w->qs_gram = take((size_t)2 * n * n * 2);
+        }
+    }
     w->total = o;
     return true;
 }
@@ -214,9 +238,6 @@ struct Work {
     float* enc_tmp;  // pixel conv activations
     size_t x_stride; // floats per X_t
     int xrows;       // rup(B*T, 32)
-    float* XP;       // panel [pq_rows][Kx]: the policy rows' terminal inputs [a_H^i | z_H] of every CEM iteration i
-    float* qp;       // [2][pq_rows] their helper.q outputs (one launch at iteration 0; see terminal_q)
-    int pq_rows;     // rup(B * Imax * P, 32)
     char* p1;        // exchange region of the persistent one-env plan (plan1.inc), p1_bytes (0: not eligible)
     size_t p1_bytes;
     size_t total;
@@ -325,9 +346,6 @@ void make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k, int ex
     k->mean = (float*)take(B * H * w.A * 4);
     k->stdv = (float*)take(B * H * w.A * 4);
     k->enc_tmp = (float*)take(d->modality ? 2 * B * pixel_act_floats(w) * 4 : 256);
-    k->pq_rows = extra ? 0 : (int)rup(B * (size_t)d->max_iterations * P, 32);
-    k->XP = (float*)take((size_t)std::max(k->pq_rows, 32) * w.Kx * 4);
-    k->qp = (float*)take(2 * (size_t)std::max(k->pq_rows, 32) * 4);
     k->p1_bytes = p1_dims_ok(d, w) && !extra ? p1_region(d, w).total : 0;
     k->p1 = k->p1_bytes ? (char*)take(k->p1_bytes) : nullptr;
     k->total = o;
@@ -1213,25 +1231,7 @@ DEVI void ring6_fill(uint4 (&wr)[D][TN][3], const unsigned short* Wp, long wbs, 
                 wr[d][j][p] = *(const uint4*)(Wp + j * wbs + ((size_t)min(g0 + d, gl) * 3 + p) * 512);
 }
 
-// -DCH_FAST (an A/B, off: the chain kernels measured 3-7 % slower with it, 192.5 vs 186 us per humanoid Q launch,
-// while the wide step kernel gains 2.7 % from the same split): the operand in three planes, split by the finite-only
-// form when all of the wave's eight-element groups are finite (a wave-uniform branch), by the general one otherwise;
-// the products are bitwise split8's for finite operands and carry a non-finite x through w_hi x alone, as split8's
-#ifdef CH_FAST
-struct X6C { bf16x8_t h, s, m, l; };   // s = h: the product table below reads b.s where split8 has its finite-zeroed hi
-DEVI X6C ch_split(const float4& a0, const float4& a1) {
-    X6U u;
-    if (__builtin_amdgcn_ballot_w64(!__builtin_isfinite(((a0.x + a0.y) + (a0.z + a0.w)) + ((a1.x + a1.y) + (a1.z + a1.w)))) == 0)
-        u = w2_split8_fin(a0, a1);
-    else
-        u = w2_split8(a0, a1);
-    X6C b;
-    b.h = as_bf16x8(u.h); b.s = b.h; b.m = as_bf16x8(u.m); b.l = as_bf16x8(u.l);
-    return b;
-}
-#else
 DEVI X6B ch_split(const float4& a0, const float4& a1) { return split8(a0, a1); }
-#endif
 
 template <int TN>
 DEVI void x6_group(floatx16 (&acc)[TN], const uint4 (&w)[TN][3], const float4& a0, const float4& a1) {
@@ -2464,28 +2464,6 @@ __global__ void __launch_bounds__(256) pi_from_mu_kernel(const PiMuArgs a) {
     *(float4*)(a.Xo + (size_t)(xr >> 5) * a.x_ts + (size_t)q * 128 + (xr & 31) * 4) = make_float4(o[0], o[1], o[2], o[3]);
 }
 
-// The policy rows' terminal inputs of every CEM iteration (terminal_q's precompute): XP row (i B + e) P + p <- X_H
-// row e T + N + p, all Kx columns (iteration i's actions are rewritten by pi_from_mu_kernel for i >= 1).
-struct PqArgs {
-    const float* X; float* XP; long x_ts; int kq; int B, P, N, T, I;
-    const float* qp; float* qv; int qp_ld, q_ld, iter;   // pq_copy_kernel: iteration `iter`'s slice -> k.qv
-};
-__global__ void __launch_bounds__(256) pq_fill_kernel(const PqArgs a) {
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long rows = (long)a.I * a.B * a.P;
-    if (i >= rows * a.kq) return;
-    const int r = (int)(i / a.kq), qd = (int)(i % a.kq);
-    const int p = r % a.P, e = (r / a.P) % a.B;
-    const int xr = e * a.T + a.N + p;
-    const float4 v = *(const float4*)(a.X + (size_t)(xr >> 5) * a.x_ts + (size_t)qd * 128 + (xr & 31) * 4);
-    *(float4*)(a.XP + (size_t)(r >> 5) * a.x_ts + (size_t)qd * 128 + (r & 31) * 4) = v;
-}
-__global__ void __launch_bounds__(256) pq_copy_kernel(const PqArgs a) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= 2 * a.B * a.P) return;
-    const int h = i / (a.B * a.P), r = i % (a.B * a.P), e = r / a.P, p = r % a.P;
-    a.qv[(size_t)h * a.q_ld + e * a.T + a.N + p] = a.qp[(size_t)h * a.qp_ld + (size_t)a.iter * a.B * a.P + r];
-}
 
 // estimate_value's terminal combination (tdmpc.py:91-92): G + gamma^H min(Q1, Q2), nan_to_num.
 DEVI float qvalue(float G, float q1, float q2, float discH) {
@@ -3171,8 +3149,7 @@ int set_lds_attr() {
 
 #include "plan1.inc"
 #include "wide_step.inc"
-#include "wide2.inc"
-#include "wide_q.inc"
+#include "wide_heads.inc"
 
 #define FOR_EACH_LINEAR(X)                                                                          \
     X(1, 1, 1, 1, 0, 32, false) X(1, 1, 1, 1, 0, 64, false) X(1, 1, 1, 1, 0, 128, false)              \
@@ -3193,14 +3170,14 @@ int init_attrs() {
     HIPCHK(hipFuncSetAttribute((const void*)plan1_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)plan1_kernel<6>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 #define WIDE_ATTR(G1, NB3) \
-    HIPCHK(hipFuncSetAttribute((const void*)wide_step_kernel<G1, NB3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)); \
-    HIPCHK(hipFuncSetAttribute((const void*)wide2_step_kernel<G1, NB3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIPCHK(hipFuncSetAttribute((const void*)wide_step_kernel<G1, NB3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     WIDE_FOR_EACH(WIDE_ATTR)
 #undef WIDE_ATTR
-#define WIDE_Q_ATTR(G1) \
-    HIPCHK(hipFuncSetAttribute((const void*)wide_q_kernel<G1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    WIDE_Q_FOR_EACH(WIDE_Q_ATTR)
-#undef WIDE_Q_ATTR
+#define WIDE_HEADS_ATTR(G1P, NB3P, G1Q, NSTQ) \
+    HIPCHK(hipFuncSetAttribute((const void*)wide_heads_kernel<G1P, NB3P, G1Q, NSTQ>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    WIDE_HEADS_FOR_EACH(WIDE_HEADS_ATTR)
+#undef WIDE_HEADS_ATTR
+    HIPCHK(hipFuncSetAttribute((const void*)qstat_chol_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)conv_tile_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -3775,12 +3752,6 @@ unsigned long long* g_p1_stamps = nullptr;   // tdmpc_debug_plan1_stamps (diagno
 
 // ---- the wide step kernel (wide_step.inc) for TOLD.next launches with >= one 128-row block per CU and head (B >= 32
 // envs at N = 512; TDMPC_WIDE=0 turns it off, TDMPC_PATH_WIDE forces it at every width it supports)
-// TDMPC_WIDE2=1: wide2_step_kernel (4 phases of 8 first-layer tiles, pipelined operand splits, wide2.inc) instead of
-// the round-3 wide_step_kernel (8 chunks of 4); an A/B switch while wide2 is measured, the default stays wide_step
-int wide_v2() {
-    static const int v = [] { const char* e = getenv("TDMPC_WIDE2"); return e ? atoi(e) : 0; }();
-    return v;
-}
 int wide_g1(const Ctx& c, bool z0c) {   // first-layer 32-k groups the kernel runs
     return (int)rup(z0c ? z0c_k1c(c) : c.Kx, 32) / 32;
 }
@@ -3823,14 +3794,13 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
     Profiler& pf = g_prof;
     const bool prof = pf.armed && pf.cfg == 4 + CH_STEP && pf.n + 2 <= pf.cap && (pf.rows == 0 || rows == pf.rows) && !z0c;
     if (prof) {
-        snprintf(pf.kernel, sizeof pf.kernel, "%s<%d, %d>", wide_v2() ? "wide2_step_kernel" : "wide_step_kernel", g1, nb3);
+        snprintf(pf.kernel, sizeof pf.kernel, "wide_step_kernel<%d, %d>", g1, nb3);
         HIPCHK(hipEventRecord(pf.ev[pf.n], c.s));
     }
     bool done = false;
 #define WIDE_LAUNCH(G1, NB3) \
     if (!done && g1 == G1 && nb3 == NB3) { \
-        if (wide_v2()) hipLaunchKernelGGL((wide2_step_kernel<G1, NB3>), grid, block, ws_lds<G1>(), c.s, a); \
-        else hipLaunchKernelGGL((wide_step_kernel<G1, NB3>), grid, block, ws_lds<G1>(), c.s, a); \
+        hipLaunchKernelGGL((wide_step_kernel<G1, NB3>), grid, block, ws_lds<G1>(), c.s, a); \
         done = true; \
     }
     WIDE_FOR_EACH(WIDE_LAUNCH)
@@ -3848,24 +3818,12 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
 
 // defer = 1 (a loop of consecutive steps over the same rows, nothing reading X_{t+1}'s latents in between): on the
 // split path the finish of this step is folded into the next step's launch.
-// TDMPC_PSPLIT=1 (A/B): iteration 0's policy-row step launches (the rows the wide kernel leaves to the narrow
-// kernels by role) on the column-split kernel instead of the chain kernel
-static bool psplit_on() {
-    static const int v = [] { const char* e = getenv("TDMPC_PSPLIT"); return e ? atoi(e) : 0; }();
-    return v != 0;
-}
-static bool split_fits(const Ctx& c, int rows) {
-    const Layout& w = c.w;
-    return w.M == 512 && rows <= c.k.split_rows && (size_t)split_lds_floats(w.Kx, w.M) * 4 <= 64 * 1024 &&
-           (int)rup(w.Kx, 16) <= w.M / 2;
-}
 
 int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, int defer = 0,
               bool nowide = false) {
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
-    const bool psplit = nowide && psplit_on() && split_fits(c, rows);
     if (c.split_pend && (!use_split(c, rows) || rows != c.split_rows || t != c.split_t + 1 ||
                          memcmp(&map, &c.split_map, sizeof map)))
         if ((rc = flush_split(c))) return rc;
@@ -3892,7 +3850,7 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
             return launch_wide(c, t, rows, map, disc, first, last, z0c);
         }
     }
-    if (!psplit && use_chain(c, rows, 2, CK_STEP)) {
+    if (use_chain(c, rows, 2, CK_STEP)) {
         ChainArgs a = chain0(c, rows, map, t, c.Kx, 0, 2);
         ChainProb& d = a.p[0];
         d.W1 = c.pw + w.w1x; d.b1 = c.pw + w.b1x; d.W2 = c.pw + w.w2d; d.b2 = c.pw + w.b2d;
@@ -3910,7 +3868,7 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         if (t == 0 && c.z0c_ready && map.G % 32 == 0) { a.z0c = c.k.z0c; a.z0_G = map.G; a.k1c = z0c_k1c(c); }
         return launch_chain(CH_STEP, a, 2, c.s);
     }
-    if (psplit || use_split(c, rows)) {
+    if (use_split(c, rows)) {
         const int par = c.split_par;
         const size_t zs = (size_t)SPLIT_S * c.k.split_rows * std::max(w.Lr, w.Ar), rs = (size_t)SPLIT_S * c.k.split_rows;
         SplitArgs a;
@@ -3982,14 +3940,11 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
 
 // pi(z_t) with TruncatedNormal noise for `rows` rows of X_t -> X_t action columns (tdmpc.py:39-45).
 int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps_env, int eps_G, long eps_off,
-           float min_std, float* mu_out = nullptr, bool prow = false) {
+           float min_std, float* mu_out = nullptr) {
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
-    // (TDMPC_PSPLIT=1: the policy rows' pre-rollout pi on the column-split kernel, as their steps)
-    const bool psplit = prow && !mu_out && psplit_on() && w.M == 512 && rows <= c.k.split_rows &&
-                        (size_t)split_lds_floats(w.Lp, w.M) * 4 <= 64 * 1024 && (int)rup(w.Lp, 16) <= w.M / 2;
-    if (!psplit && use_chain(c, rows, 1, CK_PI)) {
+    if (use_chain(c, rows, 1, CK_PI)) {
         ChainArgs a = chain0(c, rows, map, t, w.Lp, w.Ap / 4, 1);
         ChainProb& p = a.p[0];
         p.W1 = c.pw + w.wp1; p.b1 = c.pw + w.bp1; p.W2 = c.pw + w.wp2; p.b2 = c.pw + w.bp2;
@@ -4001,7 +3956,7 @@ int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps
         a.mu_out = mu_out;
         return launch_chain(CH_PI, a, 1, c.s);
     }
-    if (psplit || use_split_pi(c, rows)) {
+    if (use_split_pi(c, rows)) {
         if ((rc = flush_split(c))) return rc;
         SplitArgs a;
         memset(&a, 0, sizeof a);
@@ -4125,63 +4080,126 @@ int q_chain(const Ctx& c, int rows, RowMap map, const float* X = nullptr, float*
     return launch_chain(CH_Q, a, 2, c.s);
 }
 
-// helper.q for both heads on the wide kernel (wide_q.inc) over `rows` rows of X_H mapped by `map` -> k.qv. Used for
-// the N sampled rows of every env when their 128-row blocks cover the CUs (B >= 32 envs at N = 512); the policy rows
-// stay on the chain kernel -- a row's kernel follows its role, never the launch size, as in step_next.
-// TDMPC_WIDE_Q=1 turns it on (off by default until measured).
-int wide_q_g1(const Ctx& c) { return (int)rup(c.Kx, 32) / 32; }
-bool use_wide_q(const Ctx& c, int rows, const RowMap& map) {
-    static const int en = [] { const char* e = getenv("TDMPC_WIDE_Q"); return e ? atoi(e) : 0; }();
-    if (!en || c.w.M != 512 || !use_x6(c) || !num_cus()) return false;
-    if (c.path != TDMPC_PATH_AUTO && c.path != TDMPC_PATH_CHAIN && c.path != TDMPC_PATH_WIDE) return false;
-    if (rows % 16 || map.G % 16 || map.S % 16 || map.O % 16) return false;
-    const int g1 = wide_q_g1(c);
-    if (g1 < 2 || g1 > 5) return false;
-    return c.path == TDMPC_PATH_WIDE || (rows + 127) / 128 * 2 >= num_cus();
+// ---- the wide heads (wide_heads.inc): terminal pi and helper.q on the wide step kernel's design, for plans whose
+// sampled rows' steps run on the wide step kernel (B N rows fill 128-row blocks on every CU). TDMPC_WIDE_HEADS=0
+// keeps the chain kernels. A row's kernel follows its role, never the launch size (as in step_next): the sampled rows'
+// terminal pi and both Q heads and the policy rows' Q heads run here, the policy rows' cached pi mean on the chain
+// kernel (iteration 0) and pi_from_mu_kernel.
+int wh_g1p(const Ctx& c) { return (int)rup(c.w.Lp, 32) / 32; }
+int wh_nb3p(const Ctx& c) { return (int)rup(c.w.A, 16) / 16; }
+int wh_g1q(const Ctx& c) { return (int)rup(c.Kx, 32) / 32; }
+bool wh_instance(const Ctx& c) {
+    const int g1p = wh_g1p(c), nb3 = wh_nb3p(c), g1q = wh_g1q(c), nst = c.w.nsr / 16;
+#define WH_HAS(G1P, NB3P, G1Q, NSTQ) if (g1p == G1P && nb3 == NB3P && g1q == G1Q && nst == NSTQ) return true;
+    WIDE_HEADS_FOR_EACH(WH_HAS)
+#undef WH_HAS
+    return false;
 }
-int launch_wide_q(const Ctx& c, int rows, RowMap map) {
+bool use_wide_heads(const Ctx& c) {
+    static const int en = [] { const char* e = getenv("TDMPC_WIDE_HEADS"); return e ? atoi(e) : 1; }();
+    if (!en || !c.w.nqs || c.w.M != 512 || !use_x6(c) || !num_cus()) return false;
+    if (c.path != TDMPC_PATH_AUTO && c.path != TDMPC_PATH_CHAIN && c.path != TDMPC_PATH_WIDE) return false;
+    if (c.N + c.P != c.T || c.N % 16 || c.P % 16) return false;
+    if (!use_wide(c, c.B * c.N, RowMap{c.N, c.T, 0}, false) || !wh_instance(c)) return false;
+    // the policy rows' pi mean comes from the chain kernel (mu_out)
+    return c.P == 0 || use_chain(c, c.B * c.P, 1, CK_PI);
+}
+WHJob wh_job(int role, int head, int x0, int nx, int rows, RowMap map) {
+    WHJob j;
+    memset(&j, 0, sizeof j);
+    j.role = role; j.head = head; j.x0 = x0; j.nx = nx; j.rows = rows; j.nrb = (rows + 127) / 128; j.map = map;
+    j.eps_G = 1;
+    return j;
+}
+int launch_wide_heads(const Ctx& c, const WHJob* jobs, int nj, const float* eps, float min_std) {
     const Layout& w = c.w;
     const int M = c.M;
-    WideQArgs a;
+    WHArgs a;
     memset(&a, 0, sizeof a);
-    a.g1s = (int)(rup(c.Kx, 32) / 32);
-    const unsigned short* x1 = (const unsigned short*)(c.pw + w.x6q[X6_WQ1X]);
-    const unsigned short* x2 = (const unsigned short*)(c.pw + w.x6q[X6_WQ2]);
+    for (int i = 0; i < nj; ++i) a.job[i] = jobs[i];
+    a.njob = nj;
+    a.X = Xt(c, c.H); a.x_ts = (long)c.Kx * 32;
+    auto q6 = [&](int i) { return (const unsigned short*)(c.pw + w.x6q[i]); };
+    a.P1 = q6(X6_WP1); a.P2 = q6(X6_WP2); a.P3 = q6(X6_WP3);
+    a.pb1 = c.pw + w.bp1; a.pb2 = c.pw + w.bp2; a.pb3 = c.pw + w.bp3;
+    a.A = w.A; a.Ap = w.Ap; a.pq1 = w.Ap / 4; a.pkq = w.Lp / 4; a.pg1s = wh_g1p(c);
+    a.eps = eps; a.min_std = min_std; a.lo = (float)(-1.0 + 1e-6); a.hi = (float)(1.0 - 1e-6);
+    const int g1q = wh_g1q(c);
     for (int h = 0; h < 2; ++h) {
-        a.X1[h] = x1 + (size_t)h * (M / 16) * a.g1s * 1536;
-        a.X2[h] = x2 + (size_t)h * (M / 16) * (M / 32) * 1536;
-        a.b1[h] = c.pw + w.bq1x + h * M; a.g1[h] = c.pw + w.g1 + h * M; a.be1[h] = c.pw + w.be1 + h * M;
-        a.b2[h] = c.pw + w.bq2 + h * M; a.g2[h] = c.pw + w.g2 + h * M; a.be2[h] = c.pw + w.be2 + h * M;
-        a.w3[h] = c.pw + w.wq3 + h * M; a.b3[h] = c.pw + w.bq3 + h;
+        WHQHead& q = a.q[h];
+        q.S = (const unsigned short*)(c.pw + w.x6qs) + (size_t)h * (w.nsr / 16) * g1q * 1536;
+        q.X1 = q6(X6_WQ1X) + (size_t)h * (M / 16) * g1q * 1536;
+        q.X2 = q6(X6_WQ2) + (size_t)h * (M / 16) * (M / 32) * 1536;
+        q.bs = c.pw + w.bqs + (size_t)h * w.nsr;
+        q.b1 = c.pw + w.bq1x + h * M; q.g1 = c.pw + w.g1 + h * M; q.be1 = c.pw + w.be1 + h * M;
+        q.b2 = c.pw + w.bq2 + h * M; q.g2 = c.pw + w.g2 + h * M; q.be2 = c.pw + w.be2 + h * M;
+        q.w3 = c.pw + w.wq3 + h * M; q.b3 = c.pw + w.bq3 + h;
     }
-    a.rows = rows; a.nrb = (rows + 127) / 128; a.amap = map;
-    a.X = Xt(c, c.H); a.x_ts = (long)c.Kx * 32; a.kq = c.Kx / 4;
-    a.q = c.k.qv; a.q_ld = c.k.xrows;
-    const int g1 = wide_q_g1(c);
-    const dim3 grid((unsigned)rup(a.nrb, 4) * 2), block(64 * WS_NW);
-    // diagnostic timer (tdmpc_profile_begin cfg 4 + CH_Q, as the chain helper.q launches)
+    a.qkq = c.Kx / 4; a.qg1s = g1q;
+    a.qv = c.k.qv; a.q_ld = c.k.xrows;
+    int slots = 0;
+    bool allq = true;
+    double flops = 0.0;
+    for (int i = 0; i < nj; ++i) {
+        const WHJob& J = jobs[i];
+        if (J.rows % 16 || J.x0 < 0 || J.nx <= 0 || J.x0 + J.nx > 8) {
+            snprintf(g_err, sizeof g_err, "wide heads: bad job %d", i);
+            return TDMPC_E_DIMS;
+        }
+        slots = std::max(slots, (J.nrb + J.nx - 1) / J.nx);
+        allq = allq && J.role == WH_Q;
+        flops += 2.0 * J.rows * (J.role == WH_PI ? (double)w.L * M + (double)M * M + (double)M * w.A
+                                                 : (double)(w.L + w.A) * M + (double)M * M + M);
+    }
+    if (!slots) return 0;
+    const dim3 grid((unsigned)slots * 8), block(64 * WS_NW);
+    const int g1p = wh_g1p(c), nb3 = wh_nb3p(c), nst = w.nsr / 16;
+    // diagnostic timer (tdmpc_profile_begin cfg 4 + CH_Q: the all-Q launch, cfg 4 + CH_PI: the mixed one)
     Profiler& pf = g_prof;
-    const bool prof = pf.armed && pf.cfg == 4 + CH_Q && pf.n + 2 <= pf.cap && (pf.rows == 0 || rows == pf.rows);
+    const bool prof = pf.armed && pf.cfg == 4 + (allq ? CH_Q : CH_PI) && pf.n + 2 <= pf.cap &&
+                      (pf.rows == 0 || jobs[0].rows == pf.rows);
     if (prof) {
-        snprintf(pf.kernel, sizeof pf.kernel, "wide_q_kernel<%d>", g1);
+        snprintf(pf.kernel, sizeof pf.kernel, "wide_heads_kernel<%d, %d, %d, %d> (%s)", g1p, nb3, g1q, nst,
+                 allq ? "Q1 + Q2" : "pi + Q1 + Q2 of the policy rows");
         HIPCHK(hipEventRecord(pf.ev[pf.n], c.s));
     }
     bool done = false;
-#define WIDE_Q_LAUNCH(G1) \
-    if (!done && g1 == G1) { \
-        hipLaunchKernelGGL((wide_q_kernel<G1>), grid, block, ws_lds<G1>(), c.s, a); \
+#define WH_LAUNCH(G1P, NB3P, G1Q, NSTQ) \
+    if (!done && g1p == G1P && nb3 == NB3P && g1q == G1Q && nst == NSTQ) { \
+        hipLaunchKernelGGL((wide_heads_kernel<G1P, NB3P, G1Q, NSTQ>), grid, block, \
+                           ws_lds<(G1P > G1Q ? G1P : G1Q)>(), c.s, a); \
         done = true; \
     }
-    WIDE_Q_FOR_EACH(WIDE_Q_LAUNCH)
-#undef WIDE_Q_LAUNCH
-    if (!done) { snprintf(g_err, sizeof g_err, "wide q: no instance for G1 %d", g1); return TDMPC_E_DIMS; }
+    WIDE_HEADS_FOR_EACH(WH_LAUNCH)
+#undef WH_LAUNCH
+    if (!done) { snprintf(g_err, sizeof g_err, "wide heads: no instance"); return TDMPC_E_DIMS; }
     HIPCHK(hipGetLastError());
     if (prof) {
         HIPCHK(hipEventRecord(pf.ev[pf.n + 1], c.s));
         pf.n += 2;
-        pf.flops += 2.0 * rows * 2 * ((double)(w.L + w.A) * M + (double)M * M + M);   // algorithmic (one layer 1)
+        pf.flops += flops;
     }
     return 0;
+}
+
+// The terminal heads of one CEM iteration on the wide heads: launch A = the sampled rows' pi (XCD groups 0-3) beside the
+// policy rows' Q1 (4-5) and Q2 (6-7), launch B = the sampled rows' Q1 (0-3) and Q2 (4-7). The policy rows' actions at
+// X_H are in place (chain pi with the mean cache at iteration 0, pi_from_mu after).
+int terminal_wide(const Ctx& c, const float* noise, long toff, float min_std) {
+    const RowMap rm = {c.N, c.T, 0}, pm = {c.P, c.T, c.N};
+    WHJob ja[3];
+    int na = 0;
+    ja[na] = wh_job(WH_PI, 0, 0, c.P > 0 ? 4 : 8, c.B * c.N, rm);
+    ja[na].eps_env = c.eps_env; ja[na].eps_off = toff; ja[na].eps_G = c.N;
+    ++na;
+    if (c.P > 0) {
+        ja[na++] = wh_job(WH_Q, 0, 4, 2, c.B * c.P, pm);
+        ja[na++] = wh_job(WH_Q, 1, 6, 2, c.B * c.P, pm);
+    }
+    int rc;
+    if ((rc = launch_wide_heads(c, ja, na, noise, min_std))) return rc;
+    const WHJob jb[2] = {wh_job(WH_Q, 0, 0, 4, c.B * c.N, rm), wh_job(WH_Q, 1, 4, 4, c.B * c.N, rm)};
+    return launch_wide_heads(c, jb, 2, noise, min_std);
 }
 
 // Terminal value of `rows` rows of X_H mapped by `map`: the chain path leaves q1, q2 per row in k.qv (consumed
@@ -4230,47 +4248,9 @@ int terminal_q_rows(const Ctx& c, int rows, RowMap map, float discH, bool chain)
     return 0;
 }
 
-// Sampled rows on the wide kernel, policy rows on the chain kernel (by role). The policy rows' terminal inputs
-// differ between CEM iterations only in the pre-drawn terminal noise (their z_H and cached pi mean are fixed), so with
-// `pq` (plan_cem's iteration loop, pi mean cache on) iteration 0 forms all I iterations' inputs and runs their Q in ONE
-// chain launch (one latency-bound launch instead of I); each iteration copies its slice into k.qv.
-bool use_pq(const Ctx& c, int I) {
-    static const int en = [] { const char* e = getenv("TDMPC_PQ"); return e ? atoi(e) : 1; }();
-    return en && c.P > 0 && I > 1 && c.k.pq_rows >= c.B * I * c.P && c.N + c.P == c.T;
-}
-int terminal_q(const Ctx& c, float discH, int iter = 0, int I = 1, bool pq = false, const float* noise = nullptr,
-               float min_std = 0.f) {
+int terminal_q(const Ctx& c, float discH) {
     const int rows = c.B * c.T;
-    const bool chain = use_chain(c, rows, 2, CK_Q);
-    const RowMap rm = {c.N, c.T, 0}, pm = {c.P, c.T, c.N};
-    if (chain && use_wide_q(c, c.B * c.N, rm)) {
-        int rc;
-        if ((rc = launch_wide_q(c, c.B * c.N, rm))) return rc;
-        if (c.P == 0) return 0;
-        if (!pq) return q_chain(c, c.B * c.P, pm);
-        const int BP = c.B * c.P;
-        PqArgs a;
-        memset(&a, 0, sizeof a);
-        a.X = Xt(c, c.H); a.XP = c.k.XP; a.x_ts = (long)c.Kx * 32; a.kq = c.Kx / 4;
-        a.B = c.B; a.P = c.P; a.N = c.N; a.T = c.T; a.I = I;
-        a.qp = c.k.qp; a.qv = c.k.qv; a.qp_ld = c.k.pq_rows; a.q_ld = c.k.xrows; a.iter = iter;
-        if (iter == 0) {
-            const long nth = (long)I * BP * a.kq;
-            hipLaunchKernelGGL(pq_fill_kernel, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, c.s, a);
-            HIPCHK(hipGetLastError());
-            for (int i = 1; i < I; ++i) {   // iteration i's terminal actions, as policy_from_mu writes them then
-                const long toff = c.eps_cem_off + (long)i * c.eps_iter + c.eps_term_off;
-                const RowMap xm = {1 << 30, 0, i * BP};
-                if ((rc = policy_from_mu(c, BP, xm, noise, c.eps_env, c.P, toff + (long)c.N * c.A, min_std, c.k.XP, &pm)))
-                    return rc;
-            }
-            if ((rc = q_chain(c, I * BP, RowMap{1 << 30, 0, 0}, c.k.XP, c.k.qp, c.k.pq_rows))) return rc;
-        }
-        hipLaunchKernelGGL(pq_copy_kernel, dim3((unsigned)((2 * BP + 255) / 256)), dim3(256), 0, c.s, a);
-        HIPCHK(hipGetLastError());
-        return 0;
-    }
-    return terminal_q_rows(c, rows, RowMap{1 << 30, 0, 0}, discH, chain);
+    return terminal_q_rows(c, rows, RowMap{1 << 30, 0, 0}, discH, use_chain(c, rows, 2, CK_Q));
 }
 
 // TOLD.h for `batch` observations -> z0 [B][Lp]; optionally initialises the CEM mean/std.
@@ -4487,6 +4467,7 @@ struct PackJob {
     const float* src; int n, rows, cols;   // COPY: n values then zeros to `work`; TRANS: [rows][cols] -> [cols][rows]
     PackSrc m; int prow, pk;     // PANEL: [prow][pk] panel; X6 / X6Q: prow rows x pk k of the source map
 };
+static_assert(sizeof(PackJob) <= PACK_JOB_BYTES, "job-table slot");
 constexpr int PACK_WG = 256, PACK_PER = 8;   // threads per workgroup, items per thread
 
 __global__ void __launch_bounds__(PACK_WG) pack_fused_kernel(const PackJob* jobs, int nj, float* pw) {
@@ -4642,19 +4623,22 @@ void pack_jobs(const Layout& w, const float* const* t, std::vector<PackJob>& job
     }
 }
 
-// Job tables live in device memory, one immutable copy per distinct table and device (a HIP graph that captured a
-// pack keeps pointing at its table, whatever other planners pack later), uploaded on first use by a synchronous copy
-// -- not while the stream is being captured: the learner packs once before it captures its update. A table is keyed
-// by its content, i.e. by the source tensors' pointers: the host keeps those stable (tdmpc_amd.tdmpc.pack_told copies
-// non-live sources into per-planner staging tensors), so the set stays one table per planner and packed buffer.
-// Tables are never freed (a captured graph may still read one); past PACK_TABLES_WARN distinct tables the library
-// reports the growth once on stderr. Guarded by one mutex (planners on several host threads).
-struct PackTable { std::vector<PackJob> host; PackJob* dev; int device; };
-std::vector<PackTable> g_pack_tables;
+// The job table lives in the caller's packed buffer (Layout::jobtab), so it lives and dies with that buffer and the
+// HIP graphs the caller captured over it -- nothing device-side is global or leaks. It is uploaded by a synchronous
+// copy when it differs from the table last uploaded into that buffer, never while the stream is being captured (the
+// learner packs once before it captures its update). The host remembers the last table per packed buffer in a small
+// LRU (PACK_HOST_CACHE entries): forgetting one only costs a re-upload at that buffer's next pack. One mutex guards it
+// (planners on several host threads).
+struct PackTable { std::vector<PackJob> host; const float* pw; int device; };
+std::vector<PackTable> g_pack_tables;   // most recently used last
 std::mutex g_pack_mu;
-constexpr size_t PACK_TABLES_WARN = 256;
+constexpr size_t PACK_HOST_CACHE = 64;
 
-int launch_pack(std::vector<PackJob>& jobs, float* pw, hipStream_t s) {
+int launch_pack(std::vector<PackJob>& jobs, const Layout& w, float* pw, hipStream_t s) {
+    if (jobs.size() > (size_t)PACK_MAX_JOBS) {
+        snprintf(g_err, sizeof g_err, "tdmpc_pack_weights: %zu jobs > %d", jobs.size(), PACK_MAX_JOBS);
+        return TDMPC_E_SIZE;
+    }
     int blk = 0;
     for (PackJob& j : jobs) {
         j.blk0 = blk;
@@ -4663,44 +4647,29 @@ int launch_pack(std::vector<PackJob>& jobs, float* pw, hipStream_t s) {
     const size_t nb = jobs.size() * sizeof(PackJob);
     int device = 0;
     HIPCHK(hipGetDevice(&device));
-    const PackJob* dev = nullptr;
-    std::lock_guard<std::mutex> lock(g_pack_mu);
-    for (const PackTable& t : g_pack_tables)
-        if (t.device == device && t.host.size() == jobs.size() && !memcmp(t.host.data(), jobs.data(), nb)) {
-            dev = t.dev;
-            break;
+    PackJob* dev = (PackJob*)(pw + w.jobtab);
+    {
+        std::lock_guard<std::mutex> lock(g_pack_mu);
+        size_t hit = g_pack_tables.size();
+        for (size_t i = 0; i < g_pack_tables.size(); ++i)
+            if (g_pack_tables[i].pw == pw && g_pack_tables[i].device == device) { hit = i; break; }
+        const bool same = hit < g_pack_tables.size() && g_pack_tables[hit].host.size() == jobs.size() &&
+                          !memcmp(g_pack_tables[hit].host.data(), jobs.data(), nb);
+        if (!same) {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            HIPCHK(hipStreamIsCapturing(s, &cs));
+            if (cs != hipStreamCaptureStatusNone) {
+                snprintf(g_err, sizeof g_err, "tdmpc_pack_weights: new tensors while capturing (pack once before capture)");
+                return TDMPC_E_DIMS;
+            }
+            // drained before returning: the host vector is the copy's source
+            HIPCHK(hipMemcpyAsync(dev, jobs.data(), nb, hipMemcpyHostToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));
         }
-    if (!dev) {
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        HIPCHK(hipStreamIsCapturing(s, &cs));
-        if (cs != hipStreamCaptureStatusNone) {
-            snprintf(g_err, sizeof g_err, "tdmpc_pack_weights: new tensors while capturing (pack once before capture)");
-            return TDMPC_E_DIMS;
-        }
-        // tables are carved from 256 KiB device chunks (one current chunk per device) and written by a copy on the
-        // caller's stream, drained before returning (the host vector then dies)
-        struct Chunk { char* base; size_t used; };
-        static std::vector<Chunk> chunks;   // indexed by device
-        if ((int)chunks.size() <= device) chunks.resize(device + 1, Chunk{nullptr, 0});
-        Chunk& ch = chunks[device];
-        const size_t need = rup(nb, 256), CH = 256 * 1024;
-        if (need > CH) { snprintf(g_err, sizeof g_err, "tdmpc_pack_weights: job table too large"); return TDMPC_E_SIZE; }
-        if (!ch.base || ch.used + need > CH) {
-            HIPCHK(hipMalloc(&ch.base, CH));
-            ch.used = 0;
-        }
-        PackTable t;
-        t.host = jobs;
-        t.dev = (PackJob*)(ch.base + ch.used);
-        t.device = device;
-        ch.used += need;
-        HIPCHK(hipMemcpyAsync(t.dev, jobs.data(), nb, hipMemcpyHostToDevice, s));
-        HIPCHK(hipStreamSynchronize(s));
-        g_pack_tables.push_back(t);
-        if (g_pack_tables.size() == PACK_TABLES_WARN)
-            fprintf(stderr, "tdmpc_pack_weights: %zu distinct job tables (source tensors re-allocated per pack?)\n",
-                    g_pack_tables.size());
-        dev = t.dev;
+        PackTable t{jobs, pw, device};
+        if (hit < g_pack_tables.size()) g_pack_tables.erase(g_pack_tables.begin() + hit);
+        else if (g_pack_tables.size() >= PACK_HOST_CACHE) g_pack_tables.erase(g_pack_tables.begin());
+        g_pack_tables.push_back(std::move(t));
     }
     hipLaunchKernelGGL(pack_fused_kernel, dim3((unsigned)blk), dim3(PACK_WG), 0, s, dev, (int)jobs.size(), pw);
     HIPCHK(hipGetLastError());
@@ -4877,7 +4846,33 @@ int tdmpc_pack_weights(const tdmpc_dims* d, const float* const* t, int32_t n, vo
         if (!t[i]) return TDMPC_E_NULL;
     std::vector<PackJob> jobs;
     pack_jobs(w, t, jobs);
-    return launch_pack(jobs, (float*)packed, (hipStream_t)stream);
+    int rc = launch_pack(jobs, w, (float*)packed, (hipStream_t)stream);
+    if (rc || !w.nqs) return rc;
+    // helper.q's LayerNorm-1 statistics block from the packed first layer (wide_heads.inc): Gram, Cholesky, x6q
+    float* pw = (float*)packed;
+    QStatArgs q;
+    memset(&q, 0, sizeof q);
+    q.W1 = pw + w.wq1x; q.b1 = pw + w.bq1x; q.gram = (double*)(pw + w.qs_gram);
+    q.M = w.M; q.Kx = w.Kx; q.A = w.A; q.L = w.L; q.Ap = w.Ap; q.n = w.nqs;
+    q.S = (unsigned short*)(pw + w.x6qs); q.bs = pw + w.bqs; q.nsr = w.nsr; q.g1s = (int)(rup(w.Kx, 32) / 32);
+    const hipStream_t s = (hipStream_t)stream;
+    const int nt = (w.nqs + 15) / 16;
+    hipLaunchKernelGGL(qstat_gram_kernel, dim3(nt, nt, 2), dim3(256), 0, s, q);
+    HIPCHK(hipGetLastError());
+    const size_t lds = ((size_t)w.nqs * (w.nqs + 1) / 2 + w.nqs) * 8;
+    hipLaunchKernelGGL(qstat_chol_kernel, dim3(2), dim3(1024), lds, s, q);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int tdmpc_pack_forget(const void* packed) {
+    std::lock_guard<std::mutex> lock(g_pack_mu);
+    for (size_t i = 0; i < g_pack_tables.size(); ++i)
+        if (g_pack_tables[i].pw == (const float*)packed) {
+            g_pack_tables.erase(g_pack_tables.begin() + i);
+            break;
+        }
+    return 0;
 }
 
 int tdmpc_debug_pack_check(const tdmpc_dims* d, const int64_t* numel, int32_t n) {
@@ -4968,7 +4963,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     const RowMap rm = {N, T, 0};
     if (P > 0) {
         for (int t = 0; t < H; ++t) {
-            if ((rc = policy(c, t, B * P, pm, noise, c.eps_env, P, (long)t * P * c.A, prm->min_std, nullptr, true)))
+            if ((rc = policy(c, t, B * P, pm, noise, c.eps_env, P, (long)t * P * c.A, prm->min_std)))
                 return rc;
             if ((rc = step_next(c, t, B * T, all, prm->discount_pow[t], t == 0, t == H - 1)))
                 return rc;
@@ -4988,7 +4983,8 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     ca.std_floor_p = prm->std_floor_dev;
     ca.elite_out = elite_out; ca.score_out = score_out; ca.mean_out = mean_out; ca.std_out = std_out;
     ca.value_out = value_out;
-    if (use_chain(c, B * T, 2, CK_Q)) {   // terminal_q leaves q1, q2 per row; cem_kernel forms the values
+    const bool wide_heads = use_wide_heads(c);
+    if (wide_heads || use_chain(c, B * T, 2, CK_Q)) {   // q1, q2 per row in k.qv; cem_kernel forms the values
         ca.G = c.k.G; ca.qv = c.k.qv; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H];
     }
     const size_t cem_lds = cem_lds_bytes(T, H, ca.K, c.A);
@@ -5005,7 +5001,14 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
                 if ((rc = step_next(c, t, B * N, rm, prm->discount_pow[t], t == 0, t == H - 1, 1)))
                     return rc;
         const long toff = c.eps_cem_off + (long)i * c.eps_iter + c.eps_term_off;
-        if (pi_cache && i > 0) {
+        if (wide_heads) {
+            if (P > 0) {
+                if (i == 0) rc = policy(c, H, B * P, pmH, noise, c.eps_env, P, toff + (long)N * c.A, prm->min_std, c.k.pimu);
+                else rc = policy_from_mu(c, B * P, pmH, noise, c.eps_env, P, toff + (long)N * c.A, prm->min_std);
+                if (rc || (rc = flush_split(c))) return rc;
+            }
+            if ((rc = terminal_wide(c, noise, toff, prm->min_std))) return rc;
+        } else if (pi_cache && i > 0) {
             if ((rc = policy(c, H, B * N, rm, noise, c.eps_env, N, toff, prm->min_std))) return rc;
             if ((rc = flush_split(c))) return rc;
             if ((rc = policy_from_mu(c, B * P, pmH, noise, c.eps_env, P, toff + (long)N * c.A, prm->min_std)))
@@ -5014,7 +5017,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
                                 pi_cache ? c.k.pimu : nullptr))) {
             return rc;
         }
-        if ((rc = terminal_q(c, prm->discount_pow[H], i, I, pi_cache && use_pq(c, I), noise, prm->min_std))) return rc;
+        if (!wide_heads && (rc = terminal_q(c, prm->discount_pow[H]))) return rc;
         ca.final_iter = i == I - 1;
         ca.iter = i;
         hipLaunchKernelGGL(cem_kernel, dim3(B), dim3(1024), cem_lds, c.s, ca);

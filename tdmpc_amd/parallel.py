@@ -69,7 +69,9 @@ class EnvShardedPlanner:
     @torch.no_grad()
     def plan(self, global_obs, step, t0=True):
         """Plan this rank's envs of `global_obs` ([n_envs, ...]) and return every env's (actions, metrics).
-        `t0` is a bool for the whole batch or a sequence of n_envs per-env flags (global env order)."""
+        `t0` is a bool for the whole batch or a sequence of n_envs per-env flags (global env order).
+        On RCCL (and at world 1 on the GPU) a rank's device failure is raised on every rank two calls late (its
+        status word rides the gathered block); until then the affected envs' returned actions are NaN."""
         if not isinstance(t0, (bool, int)) and not (torch.is_tensor(t0) and t0.dim() == 0):
             t0 = list(t0)
             if len(t0) != self.n_envs:

@@ -122,6 +122,7 @@ class HipPlanner:
         # zeroed once: tdmpc_pack_weights writes every tensor's region (padding included) but not the alignment gaps
         # between them, which padded vector reads may touch
         self.packed = torch.zeros(sz.packed_weight_bytes // 4, dtype=torch.float32, device=dev)
+        self.L.tdmpc_pack_forget(C.c_void_p(self.packed.data_ptr()))   # (the address may be a freed buffer's)
         self.workspace = torch.empty(sz.workspace_bytes // 4, dtype=torch.float32, device=dev)
         d = self.dims
         self.N, self.P, self.A = d.num_samples, d.num_pi, d.action_dim
@@ -583,7 +584,12 @@ class TDMPC:
     def plan_batch(self, obs, eval_mode=False, step=None, t0=True, sync_metrics=True):
         """Plan B independent environments at once (obs: [B, *obs_shape]); `t0` may be a bool or a per-env
         sequence. Equivalent to B sequential reference `plan` calls on B agents sharing weights, with the
-        random draws taken env by env in reference order."""
+        random draws taken env by env in reference order.
+
+        sync_metrics=False returns (actions, metrics tensor [B, 2]) without a host sync. A device failure (the
+        persistent one-env plan giving up at a hand-off) then surfaces late: that call's actions are NaN, and the
+        raise comes at the next-but-one call (or at check_status()) -- the NaN actions of the failing call and of
+        the call after it may already have been returned by then."""
         cfg = self.cfg
         obs = obs if torch.is_tensor(obs) else np.asarray(obs)
         B = obs.shape[0]

@@ -104,11 +104,9 @@ for v, xs in d.items():
 PY
       ;;
     stamps)
-      for v in 1 0; do
-        TDMPC_WIDE2=$v TDMPC_LIB_PATH=$PWD/tdmpc_amd/libtdmpc_hip_ws.so timeout -k 10 200 python -u tools/ws_stamps.py 32 \
-          > "$OUT/stamps_v$v.txt" 2>&1 || exit 1
-        grep -v amdgpu.ids "$OUT/stamps_v$v.txt" | head -5
-      done ;;
+      TDMPC_LIB_PATH=$PWD/tdmpc_amd/libtdmpc_hip_ws.so timeout -k 10 200 python -u tools/ws_stamps.py 32 \
+        > "$OUT/stamps.txt" 2>&1 || exit 1
+      grep -v amdgpu.ids "$OUT/stamps.txt" | head -5 ;;
     learner:*)
       kv=${stage#learner:}; var=${kv%%=*}; vals=${kv#*=}
       timeout -k 10 600 python -u -m pytest tests/test_learner.py tests/test_gpu_train_loop.py tests/test_gpu_adam.py -m gpu -v -x \

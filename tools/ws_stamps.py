@@ -32,10 +32,7 @@ agent.plan_batch(obs, step=10**6, t0=False, sync_metrics=False)   # the last wid
 torch.cuda.synchronize()
 L.tdmpc_debug_plan1_stamps(None)
 st = buf.cpu().numpy().view(np.uint64).astype(np.int64)
-V2 = os.environ.get("TDMPC_WIDE2", "0") != "0"
-S1 = 2   # humanoid: 4 first-layer 32-k groups -> 2 steps per chunk, then 8 layer-2 steps
-if V2:
-    S1 = 4   # wide2: 4 phases of (4 layer-1 steps, 16 layer-2 steps)
+S1 = 4   # humanoid: 4 first-layer 32-k groups -> 4 steps per super-chunk, then 16 layer-2 steps
 for name, base in (("dynamics wg0", 0), ("reward wg4", 4096)):
     for w in range(8):
         s = st[base + w * 512: base + w * 512 + 512].reshape(256, 2)
