@@ -1,0 +1,130 @@
+// LDS-DMA weight-ring probe (development tool, not shipped): what bounds the wide kernels' L2 -> LDS weight stream.
+// One 512-thread workgroup per CU (256), 8 waves; per pipeline step every wave waits for its own DMAs up to the ring
+// depth (counted vmcnt), joins a workgroup barrier, issues D 1-KiB global_load_lds_dwordx4 of the next step into the
+// ring slot freed two steps ago, then (optionally) reads its step's fragments from LDS and runs MF MFMAs per fragment
+// -- the wide_step_kernel skeleton without its arithmetic. The source stream is a head's x6q fragment stream: every
+// workgroup of an XCD group (blockIdx % 8 in one half) walks the same SRC-byte panel in the same order.
+//   ./dma_ring NS D STEPS MF SRC_KB NT   -> us per launch, us per step, GB/s per CU, TB/s chip
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+template <int NT>
+__device__ __forceinline__ void glds(const void* g, unsigned voff, unsigned lds) {
+    unsigned keep;
+    if constexpr (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3 nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(voff), "s"(lds), "s"(g) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(voff), "s"(lds), "s"(g) : "memory");
+}
+
+template <int NS, int D, int MF, int NT, int V>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+ring_kernel(const char* src, long src_bytes, int steps, float* out) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int SLOT = 8 * D * 1024;
+    constexpr int VM = D * (NS - 3);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const unsigned base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)lds;
+    const unsigned voff = lane * 16;
+    const char* s0 = src + ((blockIdx.x & 7) >> 2) * src_bytes;   // XCD groups 0-3 / 4-7: two panels
+    auto addr = [&](int k, int d) -> const char* {
+        const long off = ((long)k * 8 * D + wave * D + d) * 1024 % src_bytes;
+        return s0 + off;
+    };
+    auto issue = [&](int k) {
+        if constexpr (V == 1 || V == 4 || V == 5) return;
+#pragma unroll
+        for (int d = 0; d < D; ++d) glds<NT>(addr(k, d), voff, base + (k % NS) * SLOT + (wave * D + d) * 1024);
+    };
+    for (int k = 0; k < NS - 1; ++k) issue(k);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    floatx4 acc[8];
+    for (int j = 0; j < 8; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < steps; ++k) {
+        if constexpr (V != 4) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(VM) : "memory");
+        issue(k + NS - 1);
+        if constexpr (MF > 0) {
+            const char* sl = lds + (k % NS) * SLOT + lane * 16;
+#pragma unroll
+            for (int f = 0; f < 8 * D / 3; ++f) {
+                uint4 w0, w1, w2;
+                if constexpr (V == 2 || V == 5) {
+                    w0 = make_uint4(f, lane, k, 1); w1 = make_uint4(f, 2, k, lane); w2 = make_uint4(3, f, lane, k);
+                } else {
+                    w0 = *(const uint4*)(sl + f * 3072); w1 = *(const uint4*)(sl + f * 3072 + 1024);
+                    w2 = *(const uint4*)(sl + f * 3072 + 2048);
+                }
+                const bf16x8_t a0 = __builtin_bit_cast(bf16x8_t, w0), a1 = __builtin_bit_cast(bf16x8_t, w1),
+                               a2 = __builtin_bit_cast(bf16x8_t, w2);
+                if constexpr (V == 3) { acc[f & 7][0] += __builtin_bit_cast(float, w0.x ^ w1.y ^ w2.z); continue; }
+#pragma unroll
+                for (int m = 0; m < MF; ++m) {
+                    const bf16x8_t a = m % 3 == 0 ? a0 : m % 3 == 1 ? a1 : a2;
+                    acc[(f + m) & 7] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, a1, acc[(f + m) & 7], 0, 0, 0);
+                }
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    float s = 0.f;
+    for (int j = 0; j < 8; ++j) s += acc[j][0] + acc[j][3];
+    if (s == 12345.f) out[tid] = s;
+}
+
+template <int NS, int D, int MF, int NT, int V = 0>
+void run(int steps, long src_kb, bool rnd = false) {
+    const long sb = src_kb * 1024;
+    char* src;
+    CK(hipMalloc(&src, 2 * sb));
+    CK(hipMemset(src, 0, 2 * sb));
+    if (rnd) {   // random bf16 bit patterns (finite: exponent kept moderate) -- the clock a real stream holds
+        std::vector<unsigned short> h(sb);
+        unsigned x = 12345;
+        for (auto& v : h) { x = x * 1664525u + 1013904223u; v = (unsigned short)(0x3c00 | ((x >> 8) & 0x83ff)); }
+        CK(hipMemcpy(src, h.data(), sb * 2 > 2 * sb ? 2 * sb : sb * 2, hipMemcpyHostToDevice));
+    }
+    float* out;
+    CK(hipMalloc(&out, 4096));
+    const size_t lds = (size_t)NS * 8 * D * 1024;
+    CK(hipFuncSetAttribute((const void*)ring_kernel<NS, D, MF, NT, V>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((ring_kernel<NS, D, MF, NT, V>), dim3(256), dim3(512), lds, 0, src, sb, steps, out);
+    CK(hipDeviceSynchronize());
+    const int R = 50;
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < R; ++i) hipLaunchKernelGGL((ring_kernel<NS, D, MF, NT, V>), dim3(256), dim3(512), lds, 0, src, sb, steps, out);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1e3 / R;
+    const double bytes = 256.0 * steps * 8 * D * 1024;
+    printf("V=%d rnd=%d NS=%d D=%d MF=%d NT=%d steps=%d src=%ldKB: %.2f us/launch, %.3f us/step, %.1f GB/s per CU, %.2f TB/s chip\n",
+           V, (int)rnd, NS, D, MF, NT, steps, src_kb, us, us / steps, bytes / 256 / (us * 1e-6) / 1e9, bytes / (us * 1e-6) / 1e12);
+    CK(hipFree(src));
+    CK(hipFree(out));
+}
+
+int main(int argc, char** argv) {
+    const int steps = argc > 1 ? atoi(argv[1]) : 94;
+    const long kb = argc > 2 ? atol(argv[2]) : 2304;
+    run<4, 3, 6, 0, 0>(steps, kb);          // full: DMA + LDS reads + 48 MFMAs per wave per step
+    run<4, 3, 6, 0, 1>(steps, kb);          // no DMA
+    run<4, 3, 6, 0, 4>(steps, kb);          // no DMA, no barrier: LDS reads + MFMA
+    run<4, 3, 6, 0, 5>(steps, kb);          // no DMA, no LDS reads: barrier + MFMA
+    run<4, 3, 12, 0, 5>(steps, kb);         // the same at twice the MFMAs per barrier
+    run<4, 3, 6, 0, 2>(steps, kb);          // DMA + MFMA, no LDS reads
+    return 0;
+}
