@@ -59,7 +59,7 @@ typedef struct tdmpc_lg_seg {
 } tdmpc_lg_seg;
 
 enum { TDMPC_LG_EPI_NONE = 0, TDMPC_LG_EPI_ELU = 1, TDMPC_LG_EPI_PI = 2, TDMPC_LG_EPI_ELU_BWD = 3,
-       TDMPC_LG_EPI_PI_BWD = 4 };
+       TDMPC_LG_EPI_PI_BWD = 4, TDMPC_LG_EPI_RELU_BWD = 5 };
 
 /* One GEMM of a grouped launch: C = epi(sum over segments + bias[n] + res[m][n]).
  *   EPI_ELU:     elu(x)                                   (nn.ELU)
@@ -67,6 +67,7 @@ enum { TDMPC_LG_EPI_NONE = 0, TDMPC_LG_EPI_ELU = 1, TDMPC_LG_EPI_PI = 2, TDMPC_L
  *                (TOLD.pi + TruncatedNormal.sample, helper.py:71-96; aux = the standard normal draws)
  *   EPI_ELU_BWD: x * (aux > 0 ? 1 : aux + 1)              (aux = the ELU's output)
  *   EPI_PI_BWD:  x * (1 - aux^2)                          (aux = mu: tanh' with the straight-through clamp)
+ *   EPI_RELU_BWD: aux > 0 ? x : 0                         (aux = the ReLU's output)
  *   c2 (EPI_NONE): a second copy of C (ldc2).
  * splits > 1: split-K over workgroups; slice s of the raw sum goes to c + s * slice (no bias / res / epi). */
 typedef struct tdmpc_lg_job {
@@ -124,13 +125,39 @@ int tdmpc_lg_finalize(const tdmpc_lg_gsrc* t, int32_t nt, float* g, float* normp
                       void* stream);
 
 /* clip_grad_norm_ (total norm = sqrt of the sum of normp [nblk]) + Adam (torch.optim.Adam, no weight decay) over n contiguous parameters;
- * norm_out[0] = the total norm (clip_grad_norm_'s return value). */
-int tdmpc_lg_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* normp, int32_t nblk,
+ * norm_out[0] = the total norm (clip_grad_norm_'s return value). g is left clipped, as clip_grad_norm_ leaves .grad. */
+int tdmpc_lg_adam(float* p, float* g, float* m, float* v, int64_t n, const float* normp, int32_t nblk,
                   const int32_t* step, float lr, float beta1, float beta2, float eps, float max_norm,
                   float* norm_out, void* stream);
 
 /* t <- lerp(t, p, w) elementwise (helper.ema, helper.py:48-52). */
 int tdmpc_lg_lerp(float* t, const float* p, int64_t n, float w, void* stream);
+
+/* The pixel encoder's convolutions (helper.enc, helper.py:119-133: Conv2d(cin -> 32, k, stride 2, no padding) + ReLU,
+ * NCHW fp32) for the learner, on the exact f32 MFMA (v_mfma_f32_32x32x2_f32), every sum in a fixed order.
+ * Forward: y_p = relu(conv(x / in_div (in_div > 0; NormalizeImg's x / 255), w_p) + b_p) for nprob <= 2 weight sets
+ * sharing the input (the online and target encoders on the same augmented frames). */
+typedef struct tdmpc_lg_conv {
+    const float* x;                  /* [n][cin][hin][hin] */
+    const float* w[2];               /* [32][cin][k][k] */
+    const float* b[2];               /* [32] */
+    float* y[2];                     /* [n][32][ho][ho], ho = (hin - k) / 2 + 1 */
+    int32_t nprob, n, cin, hin, k;
+    float in_div;
+} tdmpc_lg_conv;
+int tdmpc_lg_conv_fwd(const tdmpc_lg_conv* a, void* stream);
+
+/* Data gradient of a stride-2 conv masked by the ReLU that produced its input:
+ * dx[n][ci][y][x] = (sum_{co,ky,kx: y = 2oy + ky, x = 2ox + kx} w[co][ci][ky][kx] dy[n][co][oy][ox]) * (xact > 0). */
+int tdmpc_lg_conv_bwd_data(const float* dy, const float* w, const float* xact, float* dx, int32_t n, int32_t cin,
+                           int32_t hin, int32_t k, void* stream);
+
+/* Weight-gradient slices: part[s][co][c] = sum over the images of slice s (img_per_slice each, the last one short)
+ * and their output pixels p of dy[n][co][p] * patch(x / in_div, p)[c], c < cin k k (c = ci k k + ky k + kx); column
+ * c = cin k k is the bias gradient (sum of dy). part: [ceil(n / img_per_slice)][32][cin k k + 1], summed by
+ * tdmpc_lg_finalize. */
+int tdmpc_lg_conv_bwd_weight(const float* dy, const float* x, float in_div, float* part, int32_t n, int32_t cin,
+                             int32_t hin, int32_t k, int32_t img_per_slice, void* stream);
 
 /* In place over n elements: mode 0 x <- ELU(x) (nn.ELU, helper.py:172); mode 1 x <- x * ELU'(y) with y the saved
  * ELU output (y > 0 ? 1 : y + 1) -- the activation epilogues of a library GEMM's output. */

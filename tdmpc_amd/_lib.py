@@ -25,7 +25,8 @@ EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc
             # include/tdmpc_learner.h
             "tdmpc_loss_forward", "tdmpc_loss_backward", "tdmpc_random_shift",
             "tdmpc_lg_gemm", "tdmpc_lg_rows_fwd", "tdmpc_lg_rows_bwd", "tdmpc_lg_pi_loss", "tdmpc_lg_finalize",
-            "tdmpc_lg_adam", "tdmpc_lg_lerp", "tdmpc_lg_act")
+            "tdmpc_lg_adam", "tdmpc_lg_lerp", "tdmpc_lg_act", "tdmpc_lg_conv_fwd", "tdmpc_lg_conv_bwd_data",
+            "tdmpc_lg_conv_bwd_weight")
 
 
 class Dims(C.Structure):
@@ -92,6 +93,11 @@ class LgRows(C.Structure):      # tdmpc_lg_rows
     _fields_ = [("hd", LgRowHead * 3)] + [(n, C.c_int32) for n in ("nh", "rows", "m", "bsz")] + \
                [("reward", C.c_void_p), ("td", C.c_void_p), ("gamma", C.c_float),
                 ("q1", C.c_void_p), ("q2", C.c_void_p), ("rho", C.c_void_p)]
+
+
+class LgConv(C.Structure):      # tdmpc_lg_conv
+    _fields_ = [("x", C.c_void_p), ("w", C.c_void_p * 2), ("b", C.c_void_p * 2), ("y", C.c_void_p * 2)] + \
+               [(n, C.c_int32) for n in ("nprob", "n", "cin", "hin", "k")] + [("in_div", C.c_float)]
 
 
 class LgGsrc(C.Structure):      # tdmpc_lg_gsrc
@@ -163,6 +169,9 @@ def lib():
                                 C.c_float, C.c_float, vp, vp]
     L.tdmpc_lg_lerp.argtypes = [vp, vp, C.c_int64, C.c_float, vp]
     L.tdmpc_lg_act.argtypes = [vp, vp, C.c_int64, i32, vp]
+    L.tdmpc_lg_conv_fwd.argtypes = [C.POINTER(LgConv), vp]
+    L.tdmpc_lg_conv_bwd_data.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, vp]
+    L.tdmpc_lg_conv_bwd_weight.argtypes = [vp, vp, C.c_float, vp, i32, i32, i32, i32, i32, vp]
     for name in EXPORTED:
         if not hasattr(L, name) and not (name.startswith("tdmpc_debug_") and os.environ.get("TDMPC_LIB_PATH")):
             raise RuntimeError(f"{LIB_PATH} does not export {name}")

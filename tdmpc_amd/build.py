@@ -12,6 +12,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SRCS = [os.path.join(HERE, "csrc", "tdmpc_kernels.hip"), os.path.join(HERE, "csrc", "replay_kernels.hip"),
+        os.path.join(HERE, "csrc", "learner_conv.hip"),
         os.path.join(HERE, "csrc", "learner_kernels.hip"), os.path.join(HERE, "csrc", "learner_engine.hip")]
 OUT = os.path.join(HERE, "libtdmpc_hip.so")
 ARCH = os.environ.get("TDMPC_OFFLOAD_ARCH", "gfx950")

@@ -1,0 +1,279 @@
+// learner_conv.hip -- the pixel encoder's convolutions for the learner engine on MI355X (gfx950).
+//
+// Reference: helper.enc for pixels (/root/reference/src/algorithm/helper.py:119-133): NormalizeImg (x / 255), four
+// Conv2d(-> 32 channels, kernel 7 / 5 / 3 / 3, stride 2, no padding) + ReLU, Flatten, Linear; trained by
+// TDMPC.update (tdmpc.py:192-245) through the online encoder on the augmented observations, and run forward only
+// on the augmented next observations by the online (TD target, tdmpc.py:184-190) and the target encoder
+// (consistency target, tdmpc.py:206-207). The Linear and its backward are tdmpc_lg_gemm jobs; this file holds the
+// three convolution passes (include/tdmpc_learner.h), each an implicit GEMM on the exact f32 MFMA
+// (v_mfma_f32_32x32x2_f32, the learner's default product), with every sum in a fixed order (no atomics): a graph
+// replay equals the eager pass bit for bit.
+//   * conv_fwd: output pixels x 32 channels; a workgroup = 4 waves x 32 pixels of one image; the weights [K][32] and
+//     the im2col offset of every k in LDS, the input gathered from L2 (buffer loads, 8 MFMA steps in flight).
+//   * conv_bwd_data: the transposed conv, split by the input pixel's parity class (py, px) so that each class is a
+//     dense GEMM over only the (co, ky, kx) taps that reach it (ky = py (mod 2), kx = px (mod 2)); the ReLU mask of
+//     the layer below fused into the store.
+//   * conv_bwd_weight: 32 channels x (cin k k + 1) columns (the last one the bias), reduced over a slice of images
+//     and their output pixels; one partial slice per workgroup row, summed in order by tdmpc_lg_finalize.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "../../include/tdmpc_hip.h"
+#include "../../include/tdmpc_learner.h"
+
+namespace tdmpc_internal {
+void set_error(const char* msg);
+}
+
+namespace {
+
+#define DEVI __device__ __forceinline__
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+constexpr unsigned CV_OOB = 0x7ffffff0u;   // buffer offsets >= this read 0
+constexpr int CV_D = 8;                     // MFMA steps of operand loads in flight
+
+int cv_bad(const char* m) {
+    tdmpc_internal::set_error(m);
+    return TDMPC_E_DIMS;
+}
+
+DEVI float relu_f(float v) { return v != v ? v : fmaxf(v, 0.f); }   // (torch.relu keeps a NaN)
+DEVI __amdgpu_buffer_rsrc_t cv_rsrc(const float* p) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)CV_OOB, 0x00020000);
+}
+DEVI float cv_ld(__amdgpu_buffer_rsrc_t r, unsigned off_elems, bool ok) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, ok ? (int)(off_elems * 4u) : (int)CV_OOB, 0, 0));
+}
+
+// ---------------------------------------------------------------------------------------------------- forward
+// grid (ceil(ho^2 / 128), n, nprob), 256 threads; LDS sW [K2][32] | koff [K2] (K2 = K rounded up to even)
+__global__ void __launch_bounds__(256) conv_fwd_kernel(const tdmpc_lg_conv a, int ho, int K2) {
+    extern __shared__ float cv_sm[];
+    const int img = blockIdx.y, pr = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int kk = a.k * a.k, K = a.cin * kk, H = a.hin, HoHo = ho * ho;
+    const float* w = pr ? a.w[1] : a.w[0];
+    float* sW = cv_sm;
+    int* koff = (int*)(cv_sm + (size_t)K2 * 32);
+    for (int i = tid; i < K2 * 32; i += 256) {
+        const int k = i >> 5, co = i & 31;
+        sW[i] = k < K ? w[(size_t)co * K + k] : 0.f;
+    }
+    for (int k = tid; k < K2; k += 256) {
+        const int ci = k / kk, rem = k % kk;
+        koff[k] = k < K ? ci * H * H + (rem / a.k) * H + rem % a.k : 0;
+    }
+    __syncthreads();
+    const int p0 = blockIdx.x * 128 + wave * 32;
+    if (p0 >= HoHo) return;   // (wave-uniform; no barrier below)
+    const int p = p0 + r;
+    const int pp = p < HoHo ? p : HoHo - 1;
+    const int pixbase = 2 * (pp / ho) * H + 2 * (pp % ho);
+    const __amdgpu_buffer_rsrc_t rx = cv_rsrc(a.x + (size_t)img * a.cin * H * H);
+    const float div = a.in_div;
+    const int ns = K2 / 2;
+    floatx16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    float av[CV_D];
+#pragma unroll
+    for (int d = 0; d < CV_D - 1; ++d) av[d] = cv_ld(rx, (unsigned)(pixbase + koff[min(2 * d + h, K2 - 1)]), d < ns);
+    for (int s0 = 0; s0 < ns; s0 += CV_D) {
+#pragma unroll
+        for (int d = 0; d < CV_D; ++d) {
+            const int s = s0 + d, sl = s + CV_D - 1;
+            av[(d + CV_D - 1) % CV_D] = cv_ld(rx, (unsigned)(pixbase + koff[min(2 * sl + h, K2 - 1)]), sl < ns);
+            if (s < ns) {
+                float x = av[d];
+                if (div > 0.f) x = __fdiv_rn(x, div);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x, sW[(2 * s + h) * 32 + r], acc, 0, 0, 0);
+            }
+        }
+    }
+    // C/D map of the 32x32 MFMA: col = lane & 31 (the channel), row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5) (the pixel)
+    const float bias = (pr ? a.b[1] : a.b[0])[r];
+    float* y = (pr ? a.y[1] : a.y[0]) + ((size_t)img * 32 + r) * HoHo;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int pix = p0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (pix < HoHo) y[pix] = relu_f(acc[e] + bias);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ data gradient
+// grid (ceil(max class pixels / 128), 4 parity classes, n), 256 threads; LDS sW [Kc][32] | tab [Kc] (int2)
+__global__ void __launch_bounds__(256) conv_bwd_data_kernel(const float* dy, const float* w, const float* xact,
+                                                            float* dx, int cin, int H, int k, int ho) {
+    extern __shared__ float cv_sm[];
+    const int py = blockIdx.y >> 1, px = blockIdx.y & 1, img = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int Wc = (H - px + 1) / 2, Pc = ((H - py + 1) / 2) * Wc;
+    const int nky = (k - py + 1) / 2, nkx = (k - px + 1) / 2, Kc = 32 * nky * nkx;   // (even)
+    const int HoHo = ho * ho, kk = k * k;
+    float* sW = cv_sm;
+    int2* tab = (int2*)(cv_sm + (size_t)Kc * 32);
+    // tap j = (co nky + iy) nkx + ix: ky = py + 2 iy, kx = px + 2 ix; dy[co][cy - iy][cx - ix] for class pixel (cy, cx)
+    for (int i = tid; i < Kc * 32; i += 256) {
+        const int j = i >> 5, ci = i & 31;
+        const int ix = j % nkx, iy = (j / nkx) % nky, co = j / (nkx * nky);
+        sW[i] = w[((size_t)co * cin + ci) * kk + (py + 2 * iy) * k + px + 2 * ix];
+    }
+    for (int j = tid; j < Kc; j += 256) {
+        const int ix = j % nkx, iy = (j / nkx) % nky, co = j / (nkx * nky);
+        tab[j] = make_int2(co * HoHo - iy * ho - ix, iy | (ix << 8));
+    }
+    __syncthreads();
+    const int q0 = blockIdx.x * 128 + wave * 32;
+    if (q0 >= Pc) return;
+    const int q = min(q0 + r, Pc - 1);
+    const int cy = q / Wc, cx = q % Wc;
+    const __amdgpu_buffer_rsrc_t rd = cv_rsrc(dy + (size_t)img * 32 * HoHo);
+    const int ns = Kc / 2;
+    auto ld = [&](int s) -> float {
+        const int j = min(2 * s + h, Kc - 1);
+        const int2 t = tab[j];
+        const int oy = cy - (t.y & 255), ox = cx - (t.y >> 8);
+        const bool ok = s < ns && (unsigned)oy < (unsigned)ho && (unsigned)ox < (unsigned)ho;
+        return cv_ld(rd, (unsigned)(t.x + cy * ho + cx), ok);
+    };
+    floatx16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    float av[CV_D];
+#pragma unroll
+    for (int d = 0; d < CV_D - 1; ++d) av[d] = ld(d);
+    for (int s0 = 0; s0 < ns; s0 += CV_D) {
+#pragma unroll
+        for (int d = 0; d < CV_D; ++d) {
+            const int s = s0 + d;
+            av[(d + CV_D - 1) % CV_D] = ld(s + CV_D - 1);
+            if (s < ns) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[d], sW[(2 * s + h) * 32 + r], acc, 0, 0, 0);
+        }
+    }
+    // col = lane & 31: input channel ci; rows: class pixels
+    const size_t plane = ((size_t)img * cin + r) * H * H;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int qq = q0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (qq >= Pc) continue;
+        const int o = (2 * (qq / Wc) + py) * H + 2 * (qq % Wc) + px;
+        dx[plane + o] = xact[plane + o] > 0.f ? acc[e] : 0.f;   // (threshold_backward of the ReLU below)
+    }
+}
+
+// ---------------------------------------------------------------------------------------------- weight gradient
+// grid (ceil(column tiles / 4), slices), 256 threads: wave = one 32-column tile of [32][K + 1]
+__global__ void __launch_bounds__(256) conv_bwd_weight_kernel(const float* dy, const float* x, float div, float* part,
+                                                              int n, int cin, int H, int k, int ho, int ips) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int kk = k * k, K = cin * kk, K1 = K + 1, ntile = (K1 + 31) / 32;
+    const int t = blockIdx.x * 4 + wave;
+    if (t >= ntile) return;
+    const int slice = blockIdx.y, n0 = slice * ips, n1 = min(n, n0 + ips), HoHo = ho * ho;
+    // this lane's B column (t 32 + r): an im2col tap, the bias column (ones) or padding (zeros)
+    const int col = t * 32 + r;
+    const int ci = col / kk, rem = col % kk;
+    const int koff = col < K ? ci * H * H + (rem / k) * H + rem % k : 0;
+    const bool tap = col < K, one = col == K;
+    const int ns = (HoHo + 1) / 2;
+    floatx16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    for (int img = n0; img < n1; ++img) {
+        const __amdgpu_buffer_rsrc_t rd = cv_rsrc(dy + ((size_t)img * 32 + r) * HoHo);
+        const __amdgpu_buffer_rsrc_t rx = cv_rsrc(x + (size_t)img * cin * H * H);
+        // pixel 2s + h of the image; its (oy, ox) advanced incrementally (two pixels per step, 2 < ho)
+        int loy = 0, lox = h;   // the loads' position (CV_D - 1 steps ahead of the products)
+        float av[CV_D], bv[CV_D];
+        auto ld = [&](int s, float& A, float& Bv) {
+            const int pix = 2 * s + h;
+            const bool ok = s < ns && pix < HoHo;
+            A = cv_ld(rd, (unsigned)pix, ok);
+            const float xv = cv_ld(rx, (unsigned)(2 * loy * H + 2 * lox + koff), ok && tap);
+            Bv = one ? (ok ? 1.f : 0.f) : xv;
+            lox += 2;
+            if (lox >= ho) { lox -= ho; ++loy; }
+        };
+#pragma unroll
+        for (int d = 0; d < CV_D - 1; ++d) ld(d, av[d], bv[d]);
+        for (int s0 = 0; s0 < ns; s0 += CV_D) {
+#pragma unroll
+            for (int d = 0; d < CV_D; ++d) {
+                const int s = s0 + d;
+                ld(s + CV_D - 1, av[(d + CV_D - 1) % CV_D], bv[(d + CV_D - 1) % CV_D]);
+                if (s < ns) {
+                    float b = bv[d];
+                    if (div > 0.f && tap) b = __fdiv_rn(b, div);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[d], b, acc, 0, 0, 0);
+                }
+            }
+        }
+    }
+    // col = lane & 31 (the B column), row = (e & 3) + 8 (e >> 2) + 4 h (the output channel)
+    if (col >= K1) return;
+    float* o = part + (size_t)slice * 32 * K1 + col;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[(size_t)((e & 3) + 8 * (e >> 2) + 4 * h) * K1] = acc[e];
+}
+
+}  // namespace
+
+extern "C" {
+
+int tdmpc_lg_conv_fwd(const tdmpc_lg_conv* a, void* stream) {
+    if (!a || !a->x || !a->w[0] || !a->b[0] || !a->y[0]) return TDMPC_E_NULL;
+    if (a->nprob < 1 || a->nprob > 2 || (a->nprob == 2 && (!a->w[1] || !a->b[1] || !a->y[1])))
+        return cv_bad("tdmpc_lg_conv_fwd: nprob");
+    if (a->n <= 0 || a->cin <= 0 || a->k <= 0 || a->hin < a->k) return cv_bad("tdmpc_lg_conv_fwd: shape");
+    const int ho = (a->hin - a->k) / 2 + 1, K = a->cin * a->k * a->k, K2 = (K + 1) & ~1;
+    const size_t lds = (size_t)K2 * 32 * 4 + (size_t)K2 * 4;
+    if (lds > 160 * 1024) return cv_bad("tdmpc_lg_conv_fwd: cin k k too large");
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)conv_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+            hipSuccess)
+            return TDMPC_E_HIP;
+        attr = true;
+    }
+    hipLaunchKernelGGL(conv_fwd_kernel, dim3((ho * ho + 127) / 128, a->n, a->nprob), dim3(256), lds,
+                       (hipStream_t)stream, *a, ho, K2);
+    return hipGetLastError() == hipSuccess ? 0 : TDMPC_E_HIP;
+}
+
+int tdmpc_lg_conv_bwd_data(const float* dy, const float* w, const float* xact, float* dx, int32_t n, int32_t cin,
+                           int32_t hin, int32_t k, void* stream) {
+    if (!dy || !w || !xact || !dx) return TDMPC_E_NULL;
+    if (n <= 0 || cin != 32 || k <= 0 || hin < k) return cv_bad("tdmpc_lg_conv_bwd_data: shape (cin must be 32)");
+    const int ho = (hin - k) / 2 + 1, kh = (k + 1) / 2, Kmax = 32 * kh * kh;
+    const size_t lds = (size_t)Kmax * 32 * 4 + (size_t)Kmax * 8;
+    if (lds > 160 * 1024) return cv_bad("tdmpc_lg_conv_bwd_data: kernel too large");
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)conv_bwd_data_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess)
+            return TDMPC_E_HIP;
+        attr = true;
+    }
+    const int pmax = ((hin + 1) / 2) * ((hin + 1) / 2);
+    hipLaunchKernelGGL(conv_bwd_data_kernel, dim3((pmax + 127) / 128, 4, n), dim3(256), lds, (hipStream_t)stream, dy, w,
+                       xact, dx, cin, hin, k, ho);
+    return hipGetLastError() == hipSuccess ? 0 : TDMPC_E_HIP;
+}
+
+int tdmpc_lg_conv_bwd_weight(const float* dy, const float* x, float in_div, float* part, int32_t n, int32_t cin,
+                             int32_t hin, int32_t k, int32_t img_per_slice, void* stream) {
+    if (!dy || !x || !part) return TDMPC_E_NULL;
+    if (n <= 0 || cin <= 0 || k <= 0 || hin < k || img_per_slice <= 0) return cv_bad("tdmpc_lg_conv_bwd_weight: shape");
+    const int ho = (hin - k) / 2 + 1, ntile = (cin * k * k + 1 + 31) / 32;
+    const int nsl = (n + img_per_slice - 1) / img_per_slice;
+    hipLaunchKernelGGL(conv_bwd_weight_kernel, dim3((ntile + 3) / 4, nsl), dim3(256), 0, (hipStream_t)stream, dy, x,
+                       in_div, part, n, cin, hin, k, ho, img_per_slice);
+    return hipGetLastError() == hipSuccess ? 0 : TDMPC_E_HIP;
+}
+
+}  // extern "C"

@@ -324,6 +324,9 @@ __device__ __forceinline__ void lg_store(const tdmpc_lg_job& JJ, int splits, int
         x *= 1.f - mu * mu;
         break;
     }
+    case TDMPC_LG_EPI_RELU_BWD:   // (threshold_backward: the gradient where the ReLU's output is > 0, else 0)
+        x = JJ.aux[(size_t)row * JJ.ldaux + col] > 0.f ? x : 0.f;
+        break;
     default:
         if (JJ.c2) JJ.c2[(size_t)row * JJ.ldc2 + col] = x;
     }
@@ -627,7 +630,7 @@ __global__ void __launch_bounds__(256) lg_finalize_kernel(const FArgs F, float* 
     }
 }
 
-__global__ void __launch_bounds__(256) lg_adam_kernel(float* p, const float* g, float* m, float* v, long n,
+__global__ void __launch_bounds__(256) lg_adam_kernel(float* p, float* g, float* m, float* v, long n,
                                                       const float* normp, int nblk, const int* step, float lr,
                                                       float b1, float b2, float eps, float max_norm,
                                                       float* norm_out) {
@@ -647,6 +650,7 @@ __global__ void __launch_bounds__(256) lg_adam_kernel(float* p, const float* g, 
     const float bc2_sqrt = (float)sqrt(bc2);
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
         const float gi = g[i] * coef;
+        g[i] = gi;   // (clip_grad_norm_ leaves the clipped gradient in .grad)
         const float mi = m[i] + (1.f - b1) * (gi - m[i]);     // exp_avg.lerp_(grad, 1 - beta1)
         const float vi = v[i] * b2 + (1.f - b2) * gi * gi;  // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
         m[i] = mi;
@@ -716,7 +720,7 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
         if (j.splits > 1 && (j.bias || j.res || j.epi != TDMPC_LG_EPI_NONE || j.c2))
             return bad("tdmpc_lg_gemm: split-K job with an epilogue");
         if ((j.epi == TDMPC_LG_EPI_PI && (!j.aux || !j.c2)) ||
-            ((j.epi == TDMPC_LG_EPI_ELU_BWD || j.epi == TDMPC_LG_EPI_PI_BWD) && !j.aux))
+            ((j.epi == TDMPC_LG_EPI_ELU_BWD || j.epi == TDMPC_LG_EPI_PI_BWD || j.epi == TDMPC_LG_EPI_RELU_BWD) && !j.aux))
             return bad("tdmpc_lg_gemm: epilogue operand missing");
         P.job[q].j = j;
         for (int s = 0; s < j.nseg; ++s) {
@@ -809,7 +813,7 @@ int tdmpc_lg_finalize(const tdmpc_lg_gsrc* t, int32_t nt, float* g, float* normp
     return launched("finalize");
 }
 
-int tdmpc_lg_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* normp, int32_t nblk,
+int tdmpc_lg_adam(float* p, float* g, float* m, float* v, int64_t n, const float* normp, int32_t nblk,
                   const int32_t* step, float lr, float beta1, float beta2, float eps, float max_norm,
                   float* norm_out, void* stream) {
     if (!p || !g || !m || !v || !normp || !step) return TDMPC_E_NULL;

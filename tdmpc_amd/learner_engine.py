@@ -30,16 +30,23 @@ import torch
 from . import _lib
 
 ELU, TANH = 2, 1
-EPI_NONE, EPI_ELU, EPI_PI, EPI_ELU_BWD, EPI_PI_BWD = 0, 1, 2, 3, 4
+EPI_NONE, EPI_ELU, EPI_PI, EPI_ELU_BWD, EPI_PI_BWD, EPI_RELU_BWD = 0, 1, 2, 3, 4, 5
+CONV_K = (7, 5, 3, 3)                       # helper.enc's pixel convolutions (stride 2, no padding)
+CONV_NAMES = ("_encoder.1", "_encoder.3", "_encoder.5", "_encoder.7")
+LIN_NAME = "_encoder.10"                    # Flatten -> Linear(32 * 3 * 3 -> L)
 NBLK = 2048         # capacity of the norm partials (one per lg_finalize workgroup of 2048 gradients)
 ROWS_NWG = 256      # lg_rows_bwd workgroups (column-sum partials per head)
 TILE_EXACT = 0x100  # TDMPC_LG_TILE_EXACT (include/tdmpc_learner.h)
 
 
 def supported(cfg) -> bool:
-    """State observations, the plain encoder, hidden width 256 / 512 / 1024 (one wave per row in the row kernels)."""
-    return (getattr(cfg, "modality", "state") == "state" and not getattr(cfg, "enc_norm", False)
-            and int(cfg.mlp_dim) in (256, 512, 1024))
+    """The plain encoder (state MLP, or the pixel conv stack with 32 channels), hidden width 256 / 512 / 1024 (one
+    wave per row in the row kernels)."""
+    if getattr(cfg, "enc_norm", False) or int(cfg.mlp_dim) not in (256, 512, 1024):
+        return False
+    if getattr(cfg, "modality", "state") == "pixels":
+        return int(cfg.num_channels) == 32 and len(cfg.obs_shape) == 3 and cfg.obs_shape[1] == cfg.obs_shape[2]
+    return getattr(cfg, "modality", "state") == "state"
 
 
 def _p(t, off: int = 0) -> int:
@@ -70,6 +77,14 @@ class Engine:
         cfg = self.cfg = agent.cfg
         self.dev = torch.device(agent.device)
         self.O, self.E, self.L = int(cfg.obs_shape[0]), int(cfg.enc_dim), int(cfg.latent_dim)
+        # pixels: the conv stack's spatial sizes 84 -> 39 -> 18 -> 8 -> 3 and the flattened width
+        self.pix = getattr(cfg, "modality", "state") == "pixels"
+        if self.pix:
+            hw = [int(cfg.obs_shape[1])]
+            for k in CONV_K:
+                hw.append((hw[-1] - k) // 2 + 1)
+            self.hw, self.C0 = hw, int(cfg.obs_shape[0])
+            self.flat = 32 * hw[-1] * hw[-1]
         self.A, self.M, self.H = int(cfg.action_dim), int(cfg.mlp_dim), int(cfg.horizon)
         self.LA = self.L + self.A
         order = ["_encoder", "_dynamics", "_reward", "_Q1", "_Q2", "_pi"]
@@ -88,6 +103,11 @@ class Engine:
         self.n_main = self.off["_pi.0.weight"][0]
         self._alias(agent.model, self.P)
         self._alias(agent.model_target, self.PT)
+        # every parameter's .grad is a view of the flat gradient (lg_adam leaves the clipped gradient there, as
+        # clip_grad_norm_ leaves it in .grad)
+        for k, p in agent.model.named_parameters():
+            o, shape = self.off[k]
+            p.grad = self.G[o:o + p.numel()].view(shape)
         lr = float(cfg.lr)
         params = dict(agent.model.named_parameters())
         self.opt_main = _Adam([params[k] for k in names if not k.startswith("_pi.")], 0, self.n_main, lr, self.dev)
@@ -245,6 +265,45 @@ class Engine:
         else:
             _lib.check(self.lib.tdmpc_lg_rows_fwd(C.byref(a), self._stream()), "tdmpc_lg_rows_fwd")
 
+    def conv_stack(self, x, n, ys, targets=(False,)):
+        """helper.enc's conv stack (NormalizeImg, 4 x Conv2d + ReLU; helper.py:119-133) on n frame stacks x [n][C0][S][S]
+        (0..255) for one or two weight sets (targets[q]: set q is the target encoder's) -> ReLU outputs ys[q][layer].
+        The first layer runs both sets in one launch (same input); later layers read their own set's output."""
+        a = _lib.LgConv()
+        st = self._stream()
+        for i, k in enumerate(CONV_K):
+            for g in ([list(range(len(targets)))] if i == 0 else [[q] for q in range(len(targets))]):
+                a.x = _p(x) if i == 0 else _p(ys[g[0]][i - 1])
+                a.nprob, a.n, a.cin, a.hin, a.k = len(g), n, self.C0 if i == 0 else 32, self.hw[i], k
+                a.in_div = 255.0 if i == 0 else 0.0
+                for j, q in enumerate(g):
+                    a.w[j] = self.w(CONV_NAMES[i] + ".weight", targets[q])
+                    a.b[j] = self.w(CONV_NAMES[i] + ".bias", targets[q])
+                    a.y[j] = _p(ys[q][i])
+                _lib.check(self.lib.tdmpc_lg_conv_fwd(C.byref(a), st), "tdmpc_lg_conv_fwd")
+
+    def conv_backward(self, b, x, B):
+        """The conv stack's backward for the main batch (tdmpc.py:200 z = h(aug(obs))): from b["dy"][3] (the masked
+        gradient of the last conv's output) down to the first conv's weights -> {name: (slices ptr, K, nslices)}."""
+        st, out = self._stream(), {}
+        for i in range(3, -1, -1):
+            k, hin = CONV_K[i], self.hw[i]
+            cin = self.C0 if i == 0 else 32
+            K = cin * k * k
+            groups = -(-((K + 1 + 31) // 32) // 4)   # workgroup columns of the weight-gradient grid
+            ips = max(1, -(-B * groups // 256))          # images per slice: ~256 workgroups
+            nsl = -(-B // ips)
+            part = self.slot(b, f"conv{i}", nsl * 32 * (K + 1))
+            xin = x if i == 0 else b["ym"][i - 1]
+            _lib.check(self.lib.tdmpc_lg_conv_bwd_weight(_p(b["dy"][i]), _p(xin), 255.0 if i == 0 else 0.0, _p(part),
+                                                          B, cin, hin, k, ips, st), "tdmpc_lg_conv_bwd_weight")
+            out[CONV_NAMES[i]] = (_p(part), K, nsl)
+            if i > 0:   # the gradient of the layer below's ReLU output, masked by its ReLU
+                _lib.check(self.lib.tdmpc_lg_conv_bwd_data(_p(b["dy"][i]), self.w(CONV_NAMES[i] + ".weight"),
+                                                            _p(b["ym"][i - 1]), _p(b["dy"][i - 1]), B, 32, hin, k, st),
+                           "tdmpc_lg_conv_bwd_data")
+        return out
+
     def bufs(self, B):
         b = self._bufs.get(B)
         if b is not None:
@@ -269,6 +328,12 @@ class Engine:
             Yp1=z(R1, M), Yp2=z(R1, M), ACT=z(R1, A), MU=z(R1, A), dACT=z(R1, A), dPp2=z(R1, M), dPp1=z(R1, M),
             piloss=z(1), gnorm=z(1),
         )
+        if self.pix:   # the conv stacks' ReLU outputs (TD: target and online encoders; main: online) and gradients
+            hw, R = self.hw, H * B
+            b["yt"] = [z(R, 32, hw[i + 1], hw[i + 1]) for i in range(4)]
+            b["yo"] = [z(R, 32, hw[i + 1], hw[i + 1]) for i in range(4)]
+            b["ym"] = [z(B, 32, hw[i + 1], hw[i + 1]) for i in range(4)]
+            b["dy"] = [z(B, 32, hw[i + 1], hw[i + 1]) for i in range(4)]
         # weight-gradient slots: (name, out, in, dY, X, K) resolved per pass; sized for the largest pass
         self._bufs[B] = b
         b["slots"] = {}
@@ -281,19 +346,28 @@ class Engine:
         return s
 
     # ------------------------------------------------------------------------------------------- passes
-    def td_target(self, b, nxo, rew, R, eps):
+    def td_target(self, b, nxo_t, rew, R, eps):
         """tdmpc.py:184-190 for all H steps: online encoder + pi (TruncatedNormal draws `eps`), target Q, and the
         target encoder's next_z (tdmpc.py:206-207) -> b["TD"], b["NZ"]."""
         O, E, L, A, M, LA = self.O, self.E, self.L, self.A, self.M, self.LA
         w, wt = self.w, (lambda k: self.w(k, True))
-        self.gemm([dict(segs=[_seg(nxo, O, wt("_encoder.0.weight"), O, O)], m=R, n=E, c=_p(b["Yt1"]), ldc=E,
-                        bias=wt("_encoder.0.bias"), epi=EPI_ELU),
-                   dict(segs=[_seg(nxo, O, w("_encoder.0.weight"), O, O)], m=R, n=E, c=_p(b["Yo1"]), ldc=E,
-                        bias=w("_encoder.0.bias"), epi=EPI_ELU)])
-        self.gemm([dict(segs=[_seg(_p(b["Yt1"]), E, wt("_encoder.2.weight"), E, E)], m=R, n=L, c=_p(b["NZ"]),
-                        ldc=L, bias=wt("_encoder.2.bias")),
-                   dict(segs=[_seg(_p(b["Yo1"]), E, w("_encoder.2.weight"), E, E)], m=R, n=L, c=_p(b["Xtd"]),
-                        ldc=LA, bias=w("_encoder.2.bias"))])
+        nxo = _p(nxo_t)
+        if self.pix:   # the conv stacks of both encoders, then their Linear
+            F = self.flat
+            self.conv_stack(nxo_t, R, [b["yt"], b["yo"]], targets=(True, False))
+            self.gemm([dict(segs=[_seg(_p(b["yt"][3]), F, wt(LIN_NAME + ".weight"), F, F)], m=R, n=L, c=_p(b["NZ"]),
+                            ldc=L, bias=wt(LIN_NAME + ".bias")),
+                       dict(segs=[_seg(_p(b["yo"][3]), F, w(LIN_NAME + ".weight"), F, F)], m=R, n=L, c=_p(b["Xtd"]),
+                            ldc=LA, bias=w(LIN_NAME + ".bias"))])
+        else:
+            self.gemm([dict(segs=[_seg(nxo, O, wt("_encoder.0.weight"), O, O)], m=R, n=E, c=_p(b["Yt1"]), ldc=E,
+                            bias=wt("_encoder.0.bias"), epi=EPI_ELU),
+                       dict(segs=[_seg(nxo, O, w("_encoder.0.weight"), O, O)], m=R, n=E, c=_p(b["Yo1"]), ldc=E,
+                            bias=w("_encoder.0.bias"), epi=EPI_ELU)])
+            self.gemm([dict(segs=[_seg(_p(b["Yt1"]), E, wt("_encoder.2.weight"), E, E)], m=R, n=L, c=_p(b["NZ"]),
+                            ldc=L, bias=wt("_encoder.2.bias")),
+                       dict(segs=[_seg(_p(b["Yo1"]), E, w("_encoder.2.weight"), E, E)], m=R, n=L, c=_p(b["Xtd"]),
+                            ldc=LA, bias=w("_encoder.2.bias"))])
         self.prod([([(b["Xtd"][:, :L], 0, L)], "_pi.0.weight", b["T1"], "_pi.0.bias", False, False, EPI_ELU, None)])
         self.prod([([(b["T1"], 0, M)], "_pi.2.weight", b["T2"], "_pi.2.bias", False, False, EPI_ELU, None)])
         self.gemm([dict(segs=[_seg(_p(b["T2"]), M, w("_pi.4.weight"), M, M)], m=R, n=A, c=_p(b["Xtd"], L),
@@ -330,8 +404,15 @@ class Engine:
         B = obs.shape[0]
         R, R1 = H * B, (H + 1) * B
         b = self.bufs(B)
-        obs = obs.contiguous()
-        nxo_t = next_obses[:H].contiguous()
+        if self.pix:
+            # RandomShiftsAug (helper.py:250-283) on the H next-observation stacks, then on obs (tdmpc.py:200, 207), as
+            # the reference's update draws them; the frames may come as uint8 from the replay buffer
+            nx = next_obses[:H].reshape(H * B, *next_obses.shape[2:])
+            nxo_t = self.agent.aug(nx if nx.dtype == torch.float32 else nx.float()).contiguous()
+            obs = self.agent.aug(obs if obs.dtype == torch.float32 else obs.float()).contiguous()
+        else:
+            obs = obs.contiguous()
+            nxo_t = next_obses[:H].contiguous()
         rew_t = reward[:H].contiguous()
         weights = weights.contiguous()
         if noise is None:
@@ -339,21 +420,27 @@ class Engine:
         else:
             b["eps"].copy_(torch.cat([x.reshape(B, A) for x in noise]).to(dev))
         eps = b["eps"]
-        nxo, rew = _p(nxo_t), _p(rew_t)
+        rew = _p(rew_t)
         w = self.w
 
         # ---- TD targets and target latents (no gradient), on the side stream ----
         main = torch.cuda.current_stream(dev)
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
-            self.td_target(b, nxo, rew, R, _p(eps))
+            self.td_target(b, nxo_t, rew, R, _p(eps))
 
         # ---- forward: encoder, latent rollout, heads ----
         X0 = b["X0"]
-        self.gemm([dict(segs=[_seg(_p(obs), O, w("_encoder.0.weight"), O, O)], m=B, n=E, c=_p(b["Ye1"]), ldc=E,
-                        bias=w("_encoder.0.bias"), epi=EPI_ELU)])
-        self.gemm([dict(segs=[_seg(_p(b["Ye1"]), E, w("_encoder.2.weight"), E, E)], m=B, n=L, c=_p(X0), ldc=LA,
-                        bias=w("_encoder.2.bias"))])
+        if self.pix:
+            F = self.flat
+            self.conv_stack(obs, B, [b["ym"]])
+            self.gemm([dict(segs=[_seg(_p(b["ym"][3]), F, w(LIN_NAME + ".weight"), F, F)], m=B, n=L, c=_p(X0), ldc=LA,
+                            bias=w(LIN_NAME + ".bias"))])
+        else:
+            self.gemm([dict(segs=[_seg(_p(obs), O, w("_encoder.0.weight"), O, O)], m=B, n=E, c=_p(b["Ye1"]), ldc=E,
+                            bias=w("_encoder.0.bias"), epi=EPI_ELU)])
+            self.gemm([dict(segs=[_seg(_p(b["Ye1"]), E, w("_encoder.2.weight"), E, E)], m=B, n=L, c=_p(X0), ldc=LA,
+                            bias=w("_encoder.2.bias"))])
         X0.view(H + 1, B, LA)[:H, :, L:].copy_(action[:H])
         for t in range(H):
             self.gemm([dict(segs=[_seg(_p(X0, t * B * LA), LA, w("_dynamics.0.weight"), LA, LA)], m=B, n=M,
@@ -436,14 +523,23 @@ class Engine:
             out = _p(DG, (t - 1) * B * L) if t > 0 else _p(DZ0)
             self.gemm([dict(segs=[_seg(_p(dP1d, t * B * M), M, w("_dynamics.0.weight"), LA, M, bmode=1)], m=B,
                             n=L, c=out, ldc=L, res=_p(S, t * B * L), ldres=L)])
-        self.gemm([dict(segs=[_seg(_p(DZ0), L, w("_encoder.2.weight"), E, L, bmode=1)], m=B, n=E,
-                        c=_p(b["dP1e"]), ldc=E, epi=EPI_ELU_BWD, aux=_p(b["Ye1"]), ldaux=E)])
+        conv = {}
+        if self.pix:   # Linear backward with the last conv's ReLU mask, then the conv stack's backward
+            F = self.flat
+            self.gemm([dict(segs=[_seg(_p(DZ0), L, w(LIN_NAME + ".weight"), F, L, bmode=1)], m=B, n=F,
+                            c=_p(b["dy"][3]), ldc=F, epi=EPI_RELU_BWD, aux=_p(b["ym"][3]), ldaux=F)])
+            conv = self.conv_backward(b, obs, B)
+            dw_enc = [(LIN_NAME, L, F, [_seg(_p(DZ0), L, _p(b["ym"][3]), F, B, 1, 1, F)], 1)]
+        else:
+            self.gemm([dict(segs=[_seg(_p(DZ0), L, w("_encoder.2.weight"), E, L, bmode=1)], m=B, n=E,
+                            c=_p(b["dP1e"]), ldc=E, epi=EPI_ELU_BWD, aux=_p(b["Ye1"]), ldaux=E)])
+            dw_enc = [("_encoder.2", L, E, [_seg(_p(DZ0), L, _p(b["Ye1"]), E, B, 1, 1, E)], 1),
+                      ("_encoder.0", E, O, [_seg(_p(b["dP1e"]), E, _p(obs), O, B, 1, 1, O)], 1)]
 
         # ---- the rollout's weight gradients (one grouped launch) ----
         g_dyn3 = ([_seg(_p(DG), L, _p(b["Yd2"]), M, R - B, 1, 1, M)] if H > 1 else []) + \
             [_seg(_p(dZP, H * B * L), L, _p(b["Yd2"], (H - 1) * B * M), M, B, 1, 1, M)]
-        dw = [("_encoder.2", L, E, [_seg(_p(DZ0), L, _p(b["Ye1"]), E, B, 1, 1, E)], 1),
-              ("_encoder.0", E, O, [_seg(_p(b["dP1e"]), E, _p(obs), O, B, 1, 1, O)], 1),
+        dw = dw_enc + [
               ("_dynamics.4", L, M, g_dyn3, sp),
               ("_dynamics.2", M, M, [_seg(_p(dP2d), M, _p(b["Yd1"]), M, R, 1, 1, M)], sp),
               ("_dynamics.0", M, LA, [_seg(_p(dP1d), M, _p(X0), LA, R, 1, 1, LA)], sp)]
@@ -464,6 +560,9 @@ class Engine:
             src[q + ".4.bias"] = (_p(part2[h], M), 1, M, M, ROWS_NWG, PW2)
             src[q + ".6.weight"] = (_p(part2[h], 2 * M), 1, M, M, ROWS_NWG, PW2)
             src[q + ".6.bias"] = (_p(part2[h], 3 * M), 1, 1, 1, ROWS_NWG, PW2)
+        for name, (ptr, K, nsl) in conv.items():   # the conv weight-gradient slices [nsl][32][K + 1]
+            src[name + ".weight"] = (ptr, 32, K, K + 1, nsl, 32 * (K + 1))
+            src[name + ".bias"] = (ptr + 4 * K, 32, 1, K + 1, nsl, 32 * (K + 1))
         src["_reward.4.weight"] = (_p(partr), 1, M, M, ROWS_NWG, PWr)
         src["_reward.4.bias"] = (_p(partr, M), 1, 1, 1, ROWS_NWG, PWr)
         self._optimise(self.opt_main, src, 0, _p(b["gnorm"]))
