@@ -41,12 +41,30 @@ ring_kernel(const char* src, long src_bytes, int steps, float* out) {
         const long off = ((long)k * 8 * D + wave * D + d) * 1024 % src_bytes;
         return s0 + off;
     };
+    // V 6 / 7: only waves 4-7 / 0-3 issue (each the step's DMAs of itself and its SIMD partner wave ^ 4)
     auto issue = [&](int k) {
-        if constexpr (V == 1 || V == 4 || V == 5) return;
+        if constexpr (V == 1 || V == 4 || V == 5 || V == 8) return;
+        if constexpr (V == 6 || V == 7) {
+            if ((V == 6) != (wave >= 4)) return;
+#pragma unroll
+            for (int d = 0; d < 2 * D; ++d) {
+                const int w = d < D ? wave : wave ^ 4, dd = d % D;
+                const long off = ((long)k * 8 * D + w * D + dd) * 1024 % src_bytes;
+                glds<NT>(s0 + off, voff, base + (k % NS) * SLOT + (w * D + dd) * 1024);
+            }
+            return;
+        }
 #pragma unroll
         for (int d = 0; d < D; ++d) glds<NT>(addr(k, d), voff, base + (k % NS) * SLOT + (wave * D + d) * 1024);
     };
-    for (int k = 0; k < NS - 1; ++k) issue(k);
+    // V 8: every wave issues its D DMAs spread over the step, one after fragment 2d + 1
+    auto issue_one = [&](int k, int d) {
+        glds<NT>(addr(k, d), voff, base + (k % NS) * SLOT + (wave * D + d) * 1024);
+    };
+    for (int k = 0; k < NS - 1; ++k) {
+        if constexpr (V == 8) { for (int d = 0; d < D; ++d) issue_one(k, d); }
+        else issue(k);
+    }
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     floatx4 acc[8];
     for (int j = 0; j < 8; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -67,6 +85,7 @@ ring_kernel(const char* src, long src_bytes, int steps, float* out) {
                 const bf16x8_t a0 = __builtin_bit_cast(bf16x8_t, w0), a1 = __builtin_bit_cast(bf16x8_t, w1),
                                a2 = __builtin_bit_cast(bf16x8_t, w2);
                 if constexpr (V == 3) { acc[f & 7][0] += __builtin_bit_cast(float, w0.x ^ w1.y ^ w2.z); continue; }
+                if constexpr (V == 8) { if ((f & 1) && f / 2 < D) issue_one(k + NS - 1, f / 2); }
 #pragma unroll
                 for (int m = 0; m < MF; ++m) {
                     const bf16x8_t a = m % 3 == 0 ? a0 : m % 3 == 1 ? a1 : a2;
@@ -120,11 +139,12 @@ void run(int steps, long src_kb, bool rnd = false) {
 int main(int argc, char** argv) {
     const int steps = argc > 1 ? atoi(argv[1]) : 94;
     const long kb = argc > 2 ? atol(argv[2]) : 2304;
-    run<4, 3, 6, 0, 0>(steps, kb);          // full: DMA + LDS reads + 48 MFMAs per wave per step
-    run<4, 3, 6, 0, 1>(steps, kb);          // no DMA
-    run<4, 3, 6, 0, 4>(steps, kb);          // no DMA, no barrier: LDS reads + MFMA
-    run<4, 3, 6, 0, 5>(steps, kb);          // no DMA, no LDS reads: barrier + MFMA
-    run<4, 3, 12, 0, 5>(steps, kb);         // the same at twice the MFMAs per barrier
-    run<4, 3, 6, 0, 2>(steps, kb);          // DMA + MFMA, no LDS reads
+    run<4, 3, 6, 0, 0>(steps, kb);          // full: every wave issues 3 DMAs right after the barrier
+    run<4, 3, 6, 0, 5>(steps, kb);          // MFMA + barrier only (the floor)
+    run<4, 3, 6, 0, 6>(steps, kb);          // waves 4-7 issue all 24 DMAs (6 each)
+    run<4, 3, 6, 0, 7>(steps, kb);          // waves 0-3 issue all 24
+    run<4, 3, 6, 0, 8>(steps, kb);          // every wave, its 3 DMAs spread over the step
+    run<4, 3, 6, 1, 0>(steps, kb);          // nt
+    run<5, 3, 6, 0, 6>(steps, kb);
     return 0;
 }
