@@ -53,7 +53,7 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector peak (spe
 # the dense BF16 MFMA peak / 6 in fp32-product FLOP/s (BF16 = 16 x the f32 MFMA rate, MI355X_MICROARCH.md)
 X6_PEAK_TFLOPS = round(FP32_PEAK_TFLOPS * 16 / 6, 1)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
-LDSDMA_CEILING_TBS = 6.4   # MI355X_MICROARCH.md price list, ldsdma-fill: LDS-DMA weight stream over the chip
+LDSDMA_CEILING_TBS = 16.4  # measured: the wide kernel's own LDS-DMA ring alone, 256 CUs (tools/mb/dma_ring.hip, profiles/r05/)
 
 
 def plan_flops(cfg, executed: bool) -> float:
@@ -416,6 +416,7 @@ def learner_bench(cfg, dev, cpu=True, reps=30):
             out[mode]["note"] = ("the same graph-replayed update with lg_gemm on the x6 products (six "
                                  "v_mfma_f32_32x32x16_bf16 per fp32 product) instead of the exact v_mfma_f32_32x32x2_f32")
     out["graph_speedup_vs_eager"] = round(out["eager"]["ms_per_update"] / out["graph"]["ms_per_update"], 2)
+    out["pixels"] = pixel_learner_bench(dev)
     if cpu:
         from oracle.learner_ref import RefLearner
         ref = RefLearner(lcfg, synthetic_state_dict(lcfg, 0), synthetic_state_dict(lcfg, 1))
@@ -429,6 +430,61 @@ def learner_bench(cfg, dev, cpu=True, reps=30):
                                "cores": torch.get_num_threads(),
                                "sample": f"{n} oracle update() calls (reference math on torch CPU)"}
         out["speedup_vs_cpu"] = round(cdt / out["graph"]["ms_per_update"] * 1e3, 1)
+    return out
+
+
+class _FixedBatch:
+    """A replay stand-in that hands out one device batch (graph-safe: the same tensors every call)."""
+    graph_safe, idx, _full = True, 0, False
+
+    def __init__(self, b):
+        self.b = b
+        self.prio = torch.zeros(b[0].shape[0], 1, device=b[0].device)
+
+    def sample(self):
+        return self.b
+
+    def update_priorities(self, idxs, p):
+        self.prio.copy_(p)
+
+
+def pixel_learner_bench(dev, reps=10):
+    """The pixel learner (quadruped-run pixels: 9 x 84 x 84 frame stacks, conv encoder, batch 512, horizon 5;
+    tdmpc.py:192-245 with RandomShiftsAug and the conv stack, helper.py:119-133, 250-283) on the learner engine
+    (learner_conv.hip's conv kernels, HIP-graph replay) against the same update through autograd (PyTorch conv =
+    MIOpen), one fixed device batch."""
+    cfg = bench_cfg("quadruped-run-pixels", batch_size=512)
+    cfg.device = str(dev)
+    B, H, A = cfg.batch_size, cfg.horizon, cfg.action_dim
+    shape = tuple(cfg.obs_shape)
+    g = torch.Generator(device=dev).manual_seed(0)
+    b = (torch.randint(0, 256, (B,) + shape, generator=g, device=dev).float(),
+         torch.randint(0, 256, (H + 1, B) + shape, generator=g, device=dev).float(),
+         torch.rand(H + 1, B, A, generator=g, device=dev) * 2 - 1, torch.randn(H + 1, B, 1, generator=g, device=dev),
+         torch.arange(B, device=dev), torch.ones(B, device=dev))
+    out = {"config": f"{cfg.task} pixels: batch {B}, horizon {H}, frames {shape}, latent {cfg.latent_dim}"}
+    for mode, engine in (("engine_graph", "1"), ("autograd_miopen", "0")):
+        os.environ["TDMPC_LEARNER_ENGINE"] = engine
+        try:
+            agent = TDMPC(cfg)
+            agent.model.load_state_dict(synthetic_state_dict(cfg, 0))
+            agent.model_target.load_state_dict(synthetic_state_dict(cfg, 1))
+            agent.learner(graph=engine == "1", warmup=3)
+            buf = _FixedBatch(b)
+            for i in range(5):
+                agent.update(buf, i + 1, sync_metrics=False)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for i in range(reps):
+                agent.update(buf, 6 + i, sync_metrics=False)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t) / reps
+            out[mode] = {"value": round(1.0 / dt, 2), "unit": "updates/s", "ms_per_update": round(dt * 1e3, 3)}
+            del agent
+        finally:
+            os.environ.pop("TDMPC_LEARNER_ENGINE", None)
+    out["engine_speedup_vs_autograd"] = round(out["autograd_miopen"]["ms_per_update"] /
+                                              out["engine_graph"]["ms_per_update"], 2)
     return out
 
 
@@ -669,30 +725,32 @@ def step_roofline(cfg, B, agent, one_step, n_r, dev, pmc_prefix):
         roof["hbm_gbs_pmc"] = round(roof["traffic"] / avg_s / 1e9, 1)
         roof["hbm_frac_pmc"] = round(roof["hbm_gbs_pmc"] / HBM_PEAK_GBS, 4)
     if n > 0 and wide:
-        # the roof that binds the wide kernel with every CU streaming: each workgroup fills its head's
-        # x6 weight fragments (3 KiB each, 8 per step) from L2 into LDS once per launch -- dynamics 8 chunks x
-        # (S1 + 8) steps + 2 NB3 layer-3 steps, reward 8 x (S1 + 8) -- against the LDS-DMA fill ceiling over the
-        # chip (MI355X_MICROARCH.md, ldsdma-fill: ~6.4 TB/s default policy)
+        # the wide kernel's weight stream: each workgroup fills its head's x6 weight fragments (3 KiB
+        # each, 8 per step) from L2 into LDS once per launch -- 4 super-chunks x (G1 + 16) steps per head + 2 NB3
+        # layer-3 steps of the dynamics head -- against the LDS-DMA rate measured with nothing else running
+        # (tools/mb/dma_ring.hip: the kernel's own ring, 16.4-16.7 TB/s over the chip, profiles/r05/dma_ring_probe_*.txt)
         g1, nb3 = (int(v) for v in name[name.index("<") + 1:name.index(">")].split(","))
-        s1 = (g1 + 1) // 2
         nrb = -(-rows // 128)
-        fill = float(nrb * (8 * (s1 + 8) * 2 + 2 * nb3) * 8 * 3072)
+        fill = float(nrb * (4 * (g1 + 16) * 2 + 2 * nb3) * 8 * 3072)
         tbs = fill / avg_s / 1e12
         roof["weight_stream"] = {
             "bytes_per_launch": fill, "achieved_tbs": round(tbs, 3), "ceiling_tbs": LDSDMA_CEILING_TBS,
             "frac": round(tbs / LDSDMA_CEILING_TBS, 4),
-            "note": "L2 -> LDS x6 weight fills of all workgroups per launch; with half the CUs streaming (B = 16) the "
-                    "same kernel's per-CU stream cost drops from ~17 to ~6 us (profiles/r04/wide_diag_r4g.txt)"}
+            "note": "L2 -> LDS x6 weight fills of all workgroups per launch. The probe with the kernel's ring: the "
+                    "stream alone 0.38 us per step, its 48 MFMAs per wave alone 0.71, both 1.12 -- they do not "
+                    "overlap (profiles/r05/dma_ring_probe_isolation.txt)"}
     return roof
 
 
-def q_roofline(cfg, B, agent, one_step, n_r):
-    """helper.q (both Q heads, tdmpc.py:47-50) at every iteration's terminal value: HIP events around its launches
-    (library profile cfg 4 + CH_Q over the N + P rows of every env), FLOPs counted by the library."""
+def q_roofline(cfg, B, agent, one_step, n_r, cfg_id=6, rows=0):
+    """The terminal heads (tdmpc.py:91-92): cfg_id 6 = helper.q (both Q heads, tdmpc.py:47-50) -- on the wide heads
+    kernel the sampled rows' Q1 + Q2 launch, else the chain launch over the N + P rows of every env; cfg_id 5 with
+    rows = B N = the wide heads kernel's mixed launch (the sampled rows' TOLD.pi beside the policy rows' Q1 + Q2).
+    HIP events around the launches (library profiler), FLOPs counted by the library."""
     L = _lib.lib()
     graph = agent.graph
     agent.graph = False
-    _lib.check(L.tdmpc_profile_begin(6, -1, 0, 0, 8192), "profile_begin")
+    _lib.check(L.tdmpc_profile_begin(cfg_id, -1, 0, rows, 8192), "profile_begin")
     for i in range(n_r):
         one_step(1 + i)
     n, ms, fl = C.c_int32(), C.c_double(), C.c_double()
@@ -702,8 +760,9 @@ def q_roofline(cfg, B, agent, one_step, n_r):
         return None
     avg_s = ms.value / n.value * 1e-3
     per = fl.value / n.value
-    return {"launches": n.value, "avg_launch_us": round(avg_s * 1e6, 3), "flops_per_launch": per,
-            "achieved": round(per / avg_s / 1e12, 3), "frac_of_x6_peak": round(per / avg_s / 1e12 / X6_PEAK_TFLOPS, 4)}
+    return {"kernel": L.tdmpc_profile_kernel().decode(), "launches": n.value, "avg_launch_us": round(avg_s * 1e6, 3),
+            "flops_per_launch": per, "achieved": round(per / avg_s / 1e12, 3),
+            "frac_of_x6_peak": round(per / avg_s / 1e12 / X6_PEAK_TFLOPS, 4)}
 
 
 def _sync():
@@ -801,6 +860,7 @@ def main():
     if not args.no_roofline:
         roof = step_roofline(cfg, B, agent, one_step, max(3, min(args.steps, 10)), dev, f"{args.config}/B{B}")
         roof["q_head"] = q_roofline(cfg, B, agent, one_step, max(3, min(args.steps, 10)))
+        roof["pi_head"] = q_roofline(cfg, B, agent, one_step, max(3, min(args.steps, 10)), 5, B * cfg.num_samples)
 
     fl_alg = plan_flops(cfg, executed=False)
     fl_exec = plan_flops(cfg, executed=True)
@@ -926,7 +986,6 @@ def main():
             "roofline": roof,
             "plan_roofline": plan_roof,
             "exact_f32_mfma": exact,
-            "single_env": single,
             "batch_sweep": sweep,
             "configs": others,
             "replay_sampler": replay,
@@ -938,7 +997,8 @@ def main():
         if cpu:
             out["speedup_vs_cpu"] = round(value / world / cpu["value"], 2)
             if single:
-                out["single_env"]["speedup_vs_cpu"] = round(single["value"] / cpu["value"], 2)
+                single["speedup_vs_cpu"] = round(single["value"] / cpu["value"], 2)
+        out["single_env"] = single   # (last: the driver keeps the tail of the line)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -152,9 +152,10 @@ int tdmpc_num_param_tensors(const tdmpc_dims* dims);
 
 /* Pack the TOLD parameters (device pointers, reference state_dict order, fp32, contiguous nn.Linear
  * [out,in] / Conv2d [out,in,kh,kw] layout) into `packed` (replaces TDMPC.model for planning). ONE kernel
- * launch enqueued on `stream`. Its job table lives in `packed` itself (no library-global device memory): it is
- * uploaded, with a synchronising copy, whenever the pointer set differs from the one last packed into this
- * buffer, so such a call must not be inside a stream capture; later ones may be. Re-run whenever the
+ * launch enqueued on `stream`. Its job table lives in `packed` itself (no library-global device memory): every
+ * call outside a stream capture uploads it (an async copy queued before the launch); a call inside a capture
+ * uploads nothing and requires the same tensors as this buffer's last uncaptured pack (pack once before
+ * capturing). Re-run whenever the
  * parameters change (after TDMPC.update -- the learner does so from its flat parameter buffer inside its
  * update graph). When allocated, `packed` must be zero-filled once (every tensor's region is rewritten whole,
  * padding included, but the alignment gaps between regions are not, and padded vector reads may touch them)
@@ -162,8 +163,9 @@ int tdmpc_num_param_tensors(const tdmpc_dims* dims);
 int tdmpc_pack_weights(const tdmpc_dims* dims, const float* const* tensors, int32_t n_tensors,
                        void* packed, size_t packed_bytes, void* stream);
 
-/* A packed buffer was (re)allocated at `packed`: forget the job table the library last uploaded at that
- * address, so the next tdmpc_pack_weights into it uploads its own. Host only, no HIP call. Returns 0. */
+/* A packed buffer was (re)allocated at `packed`: forget the job table the library last uploaded at that address
+ * (and free its pinned staging buffer), so that a captured pack into the new buffer cannot pass on the old buffer's
+ * record. Returns 0. */
 int tdmpc_pack_forget(const void* packed);
 
 /* Diagnostic, host only (no HIP call): bounds-checks tdmpc_pack_weights' job table for these dims, given the

@@ -403,6 +403,98 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
     }
 }
 
+// The LDS-staged form (tile 3 of tdmpc_lg_gemm; jobs whose segments all read A row-major, no split-K, exact f32
+// products): per 32 x 32 output tile, K in chunks of 64 -- every chunk's A rows and B columns loaded by the whole
+// workgroup with coalesced 4-byte buffer loads (a wave reads 256 contiguous bytes per instruction; the direct form
+// reads 16 bytes from each of 32 rows per instruction and is bound by those scattered requests) into LDS (row stride
+// 65 floats: the MFMA operand reads down a column are conflict-free), the next chunk's loads in flight while this
+// chunk's MFMAs run, one barrier per chunk; the four waves split each chunk's K and add through LDS at the end.
+constexpr int LGS_K = 64, LGS_P = LGS_K + 1;
+
+__global__ void __launch_bounds__(256) lg_gemm_lds_kernel(const KArgs P) {
+    __shared__ float sA[2][32 * LGS_P], sB[2][32 * LGS_P];
+    __shared__ float red[4][16][64];
+    int jb = 0;
+    for (int q = 1; q < P.njobs; ++q)
+        if ((int)blockIdx.x >= P.job[q].block0) jb = q;
+    const KJob& J = P.job[jb];
+    const int tile = (int)blockIdx.x - J.block0;
+    const int m0 = (tile % J.tiles_m) * 32, n0 = (tile / J.tiles_m) * 32;
+    const int M = J.j.m, N = J.j.n;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    // the chunk sequence: every segment's K in chunks of 64
+    int nch[3], nchunks = 0;
+    for (int s2 = 0; s2 < 3; ++s2) {
+        nch[s2] = s2 < J.j.nseg ? (J.j.seg[s2].k + LGS_K - 1) / LGS_K : 0;
+        nchunks += nch[s2];
+    }
+    float ra[8], rb[8];
+    // loads of chunk c into registers: A element e = tid + 256 i of [32 rows][64 k]; B the same over [32 n][64 k]
+    // (bmode 0, weight rows) or [64 k][32 n] (bmode 1)
+    auto load = [&](int c) {
+        int s2 = 0, cc = c;
+        while (s2 < 2 && cc >= nch[s2]) { cc -= nch[s2]; ++s2; }
+        const tdmpc_lg_seg& S = J.j.seg[s2];
+        const int k0 = cc * LGS_K;
+        const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)S.a, (short)0, (int)LG_OOB, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)S.b, (short)0, (int)LG_OOB, 0x00020000);
+        const int nbm = J.nb_mem[s2];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int e = tid + 256 * i;
+            const int row = e >> 6, k = k0 + (e & 63);
+            const bool ok = m0 + row < M && k < S.k;
+            ra[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                rsa, ok ? (int)((unsigned)((m0 + row) * S.lda + k) * 4u) : (int)LG_OOB, 0, 0));
+            int n, kb;
+            if (S.bmode == 0) { n = n0 + (e >> 6); kb = k; }
+            else { n = n0 + (e & 31); kb = k0 + (e >> 5); }
+            const bool okb = n < nbm && kb < S.k;
+            const unsigned idx = S.bmode == 0 ? (unsigned)(n * S.ldb + kb) : (unsigned)(kb * S.ldb + n);
+            rb[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsb, okb ? (int)(idx * 4u) : (int)LG_OOB, 0, 0));
+        }
+        return S.bmode;
+    };
+    auto store = [&](int buf, int bmode) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int e = tid + 256 * i;
+            sA[buf][(e >> 6) * LGS_P + (e & 63)] = ra[i];
+            if (bmode == 0) sB[buf][(e >> 6) * LGS_P + (e & 63)] = rb[i];
+            else sB[buf][(e & 31) * LGS_P + (e >> 5)] = rb[i];
+        }
+    };
+    floatx16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    if (nchunks > 0) {
+        store(0, load(0));
+        __syncthreads();
+        for (int c = 0; c < nchunks; ++c) {
+            const int buf = c & 1;
+            int bm = 0;
+            if (c + 1 < nchunks) bm = load(c + 1);
+            // this wave's 16 k of the chunk: MFMA step t sums k = 16 wave + 2t + h
+            const float* a = sA[buf] + r * LGS_P + 16 * wave + h;
+            const float* b = sB[buf] + r * LGS_P + 16 * wave + h;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2 * t], b[2 * t], acc, 0, 0, 0);
+            if (c + 1 < nchunks) store(buf ^ 1, bm);
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[wave][e][lane] = acc[e];
+    __syncthreads();
+    const tdmpc_lg_job& JJ = J.j;
+    for (int q = wave * 4; q < wave * 4 + 4; ++q) {
+        const float v = red[0][q][lane] + red[1][q][lane] + red[2][q][lane] + red[3][q][lane];
+        const int row = m0 + (q & 3) + 8 * (q >> 2) + 4 * h, col = n0 + r;
+        if (row >= M || col >= N) continue;
+        lg_store(JJ, 1, 0, row, col, v);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------------- rows
 template <int NC>
 __global__ void __launch_bounds__(256) lg_rows_fwd_kernel(const tdmpc_lg_rows a) {
@@ -708,10 +800,19 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
     if (!jobs) return TDMPC_E_NULL;
     const bool x6 = !(tile & TDMPC_LG_TILE_EXACT);   // x6 products unless the caller asks for the exact f32 MFMA
     tile &= ~TDMPC_LG_TILE_EXACT;
-    if (njobs <= 0 || njobs > LG_MAXJ || (tile != 1 && tile != 2)) return bad("tdmpc_lg_gemm: njobs / tile");
+    if (njobs <= 0 || njobs > LG_MAXJ || tile < 1 || tile > 3) return bad("tdmpc_lg_gemm: njobs / tile");
+    if (tile == 3) {   // the LDS-staged form where every job allows it (A row-major, no ones column, no split-K), else tile 1
+        bool ok = !x6;
+        for (int q = 0; q < njobs && ok; ++q) {
+            ok = jobs[q].splits == 1;
+            for (int s2 = 0; s2 < jobs[q].nseg && ok; ++s2)
+                ok = jobs[q].seg[s2].amode == 0 && jobs[q].seg[s2].ones_col < 0;
+        }
+        if (!ok) tile = 1;
+    }
     KArgs P;
     memset(&P, 0, sizeof P);
-    const int tw = 32 * tile;
+    const int tw = tile == 2 ? 64 : 32;
     long blocks = 0;
     for (int q = 0; q < njobs; ++q) {
         const tdmpc_lg_job& j = jobs[q];
@@ -739,7 +840,8 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
     P.njobs = njobs;
     if (blocks >= (1L << 31)) return bad("tdmpc_lg_gemm: grid");
     const dim3 g((unsigned)blocks), b(256);
-    if (tile == 1 && x6) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, true>), g, b, 0, (hipStream_t)stream, P);
+    if (tile == 3) hipLaunchKernelGGL(lg_gemm_lds_kernel, g, b, 0, (hipStream_t)stream, P);
+    else if (tile == 1 && x6) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, true>), g, b, 0, (hipStream_t)stream, P);
     else if (tile == 1) hipLaunchKernelGGL((lg_gemm_kernel<1, 1>), g, b, 0, (hipStream_t)stream, P);
     else if (x6) hipLaunchKernelGGL((lg_gemm_kernel<2, 2, true>), g, b, 0, (hipStream_t)stream, P);
     else hipLaunchKernelGGL((lg_gemm_kernel<2, 2>), g, b, 0, (hipStream_t)stream, P);

@@ -1008,7 +1008,7 @@ struct ChainArgs {
     int rb;                              // row block: 32 (chain_kernel) or 16 (chain16_kernel)
     int nw;                              // waves per workgroup of chain_kernel: 8 or 16
     int hfl;                             // floats of the LDS activation block (max(K1, M) * rb, K1 to 16)
-    int il;                              // > 0: the problems interleaved along blockIdx.x (pb = x % il)
+    int il;                              // (retired: 0, the problems along blockIdx.y)
     int x6;                              // chain_kernel<..., X6 = true>: fp32 products from split bf16
     RowMap amap;                         // logical row -> X row (input and output)
     const float* X; long x_ts;           // X_t panel (input)
@@ -1392,10 +1392,10 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     // il > 0: heads interleaved along x; il < 0: XCD-grouped heads (blocks b, b + 8, ... share an XCD: dispatch
     // groups 0-3 run head 0, 4-7 head 1, so each XCD's L2 holds one head's weights); else head = blockIdx.y
     const int bx = blockIdx.x;
-    const int pb = a.il > 0 ? bx % a.il : a.il < 0 ? (bx & 7) >> 2 : blockIdx.y;
+    const int pb = blockIdx.y;
     const ChainProb& P = a.p[pb];
     const int M = a.M;
-    const int m0 = (a.il > 0 ? bx / a.il : a.il < 0 ? (bx >> 3) * 4 + (bx & 3) : bx) * 32;
+    const int m0 = bx * 32;
     if (m0 >= a.rows) return;   // (XCD-grouped grids are padded to a multiple of 4 blocks per head)
     float* sH = smem;                       // activation block [max(K1, M)/4][32][4]
     float* red0 = smem + a.hfl;             // [NW][32]
@@ -1913,10 +1913,10 @@ template <int MODE, int NT, int D = 4, int D3 = 4, int X6 = 0>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) chain16_kernel(const ChainArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = lane & 15, h4 = lane >> 4;
-    const int pb = a.il ? blockIdx.x % a.il : blockIdx.y;
+    const int pb = blockIdx.y;
     const ChainProb& P = a.p[pb];
     const int M = a.M;
-    const int m0 = (a.il ? blockIdx.x / a.il : blockIdx.x) * 16;
+    const int m0 = blockIdx.x * 16;
     float* sH = smem;                       // activation block [max(K1, M)/4][16][4]
     float* red0 = smem + a.hfl;             // [8][16]
     float* red1 = red0 + 128;               // [8][16]
@@ -3156,8 +3156,7 @@ int set_lds_attr() {
     X(1, 2, 1, 1, 0, 32, false) X(1, 2, 1, 1, 0, 64, false) X(1, 2, 1, 1, 0, 128, false)              \
     X(1, 1, 1, 1, 1, 32, false) X(1, 1, 1, 1, 1, 64, false) X(1, 1, 1, 1, 1, 128, false)              \
     X(1, 2, 1, 1, 1, 32, false) X(1, 2, 1, 1, 1, 64, false) X(1, 2, 1, 1, 1, 128, false)              \
-    X(2, 2, 2, 2, 0, 1, true) X(2, 2, 2, 2, 1, 1, true) X(2, 2, 2, 2, 0, 2, true) X(2, 2, 2, 2, 1, 2, true) \
-    X(2, 1, 2, 2, 0, 1, true) X(2, 1, 2, 2, 0, 2, true) X(1, 2, 4, 2, 0, 1, true)
+    X(2, 2, 2, 2, 1, 1, true)
 
 int init_attrs() {
     static int done = 0;
@@ -3184,7 +3183,7 @@ int init_attrs() {
 #define LDS_ATTR1(...) \
     HIPCHK(hipFuncSetAttribute((const void*)linear_lds_kernel<__VA_ARGS__>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 #define LDS_ATTR(...) LDS_ATTR1(__VA_ARGS__, true) LDS_ATTR1(__VA_ARGS__, false)
-    LDS_ATTR(2, 2, 2, 2, 32) LDS_ATTR(2, 1, 2, 4, 32) LDS_ATTR(3, 1, 2, 4, 32) LDS_ATTR(1, 1, 2, 2, 32)
+    LDS_ATTR(2, 1, 2, 4, 32) LDS_ATTR(3, 1, 2, 4, 32) LDS_ATTR(1, 1, 2, 2, 32)
 #undef LDS_ATTR
 #undef LDS_ATTR1
 #define CHAIN_ATTR(MODE, TN) \
@@ -3243,27 +3242,12 @@ int thr_rows() {
     return v;
 }
 
-// throughput tile variant (development knob TDMPC_THR_VARIANT): 0 = LDS-staged 128x128 (default),
-// register-direct: 5 = 128x128 4 waves, 1 = 128x128 8 waves (K split in 2), 2 = 128x64 4 waves,
-// 3 = 128x64 8 waves (K split), 4 = 128x128 8 waves (32x64 each)
-int thr_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("TDMPC_THR_VARIANT");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
-}
-
 // Tile choice by shape (tools/mb/mb_linear.hip "sweep" on MI355X): the LDS-staged throughput tiles from
 // thr_rows() rows on; below that the K-split latency tiles, 32x64 where K and N are wide enough to feed
 // its 8 waves (512x512 hidden layers from 512 rows, the 100-wide latent layer from 2048 rows) or where the
 // epilogue needs 64-column row blocks (wide64: LayerNorm moments are kept per 64 columns).
 LinCfg pick_cfg(int M, int nmax, int K, int wide64) {
-    if (M >= thr_rows() && nmax >= 256 && K >= 64) {
-        const int v = thr_variant();
-        return LinCfg{3, (v == 2 || v == 3) ? 64 : 128, 64};
-    }
+    if (M >= thr_rows() && nmax >= 256 && K >= 64) return LinCfg{3, 128, 64};
     if (wide64 || (nmax >= 256 ? (K >= 256 && M >= 512) : M >= 2048)) return LinCfg{2, 64, 64};
     return LinCfg{1, 32, 32};
 }
@@ -3333,18 +3317,8 @@ int num_cus() {
     return n;
 }
 
-int lds_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("TDMPC_LDS_VARIANT");
-        v = e ? atoi(e) : 1;
-    }
-    return v;
-}
-
 // LDS-staged throughput tiles: 128x128 with 8 waves (64x32 each, 2 waves per SIMD) by default, 192x128
-// (8 waves of 96x32) or 64x64 (4 waves of 32x32) when the work per CU says so; TDMPC_LDS_VARIANT=0 selects
-// the 4-wave 128x128 tile (kept for comparison).
+// (8 waves of 96x32) or 64x64 (4 waves of 32x32) when the work per CU says so.
 int launch_lds(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
     const int ctiles128 = (nmax + 127) / 128, rtiles = (a.M + 127) / 128;
     {   // Tile by the work of the busiest CU: ceil(WGs / CUs) x tile area, over the tile's efficiency.
@@ -3360,8 +3334,6 @@ int launch_lds(const LinArgs& a, int nprob, int nmax, hipStream_t s) {
         if (c192 < c128 && c192 <= c64) return launch_lds_t<3, 1, 2, 4, 32>(a, nprob, nmax, s);
         if (c64 < c128) return launch_lds_t<1, 1, 2, 2, 32>(a, nprob, nmax, s);
     }
-    const int v = lds_variant();
-    if (v == 0) return launch_lds_t<2, 2, 2, 2, 32>(a, nprob, nmax, s);
     return launch_lds_t<2, 1, 2, 4, 32>(a, nprob, nmax, s);
 }
 
@@ -3370,17 +3342,8 @@ int launch_lin(const LinArgs& a, int nprob, int nmax, int wide64, int pro, hipSt
     if (a.M <= 0) return 0;
     if (a.K % 8) { snprintf(g_err, sizeof g_err, "bad K %d", a.K); return TDMPC_E_DIMS; }
     const LinCfg cfg = pick_cfg(a.M, nmax, a.K, wide64);
-    if (cfg.id == 3) {
-        const int v = thr_variant();
-        if (v == 0 && pro == PRO_PLAIN) return launch_lds(a, nprob, nmax, s);
-        if (pro == PRO_PLAIN) {
-            if (v == 1) return launch_lin_t<2, 2, 2, 2, 0, 2, true>(a, nprob, nmax, 3, s);
-            if (v == 2) return launch_lin_t<2, 1, 2, 2, 0, 1, true>(a, nprob, nmax, 3, s);
-            if (v == 3) return launch_lin_t<2, 1, 2, 2, 0, 2, true>(a, nprob, nmax, 3, s);
-            if (v == 4) return launch_lin_t<1, 2, 4, 2, 0, 1, true>(a, nprob, nmax, 3, s);
-            return launch_lin_t<2, 2, 2, 2, 0, 1, true>(a, nprob, nmax, 3, s);
-        }
-        if (v == 1) return launch_lin_t<2, 2, 2, 2, 1, 2, true>(a, nprob, nmax, 3, s);
+    if (cfg.id == 3) {   // (the register-direct 128-row variants of rounds 1-2 measured slower: git history)
+        if (pro == PRO_PLAIN) return launch_lds(a, nprob, nmax, s);
         return launch_lin_t<2, 2, 2, 2, 1, 1, true>(a, nprob, nmax, 3, s);
     }
     int kch = 32;
@@ -3452,29 +3415,6 @@ double chain_macs_per_row(int mode, const ChainArgs& a, int nprob) {
     return nprob * (K1 * M + M * M + M);
 }
 
-// TDMPC_CHAIN_IL=1: the two problems of a launch (dynamics / reward, Q1 / Q2) alternate along blockIdx.x, so a
-// CU's co-resident workgroups are one of each (different layer-3 phases) instead of two of the same head. Off by
-// default: measured on MI355X (humanoid-run, round-1 run) 9.50 vs 8.99 ms per B = 32 plan, 3.08 vs 3.04 at
-// B = 8 -- two workgroups of the same head on a CU stream the same weight panels at about the same time and
-// share them through the CU's L1, which the mixed pair loses.
-int chain_il() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("TDMPC_CHAIN_IL");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
-}
-
-int chain_xcd() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("TDMPC_CHAIN_XCD");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
-}
-
 int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
     if (a0.rows <= 0) return 0;
     ChainArgs a = a0;
@@ -3482,13 +3422,10 @@ int launch_chain(int mode, const ChainArgs& a0, int nprob, hipStream_t s) {
     const int nw = a.rb == 16 ? 8 : a.nw;
     const size_t lds = ((size_t)a.hfl + (a.rb == 16 ? 256 : 64 * nw) + chain_param_floats(mode, a.M, a.n3)) * 4;
     const int nblk = (a.rows + a.rb - 1) / a.rb;
-    a.il = nprob > 1 && chain_il() ? nprob : 0;
-    // XCD-grouped heads for two-head 32-row launches (TDMPC_CHAIN_XCD=1): each XCD streams one head's (x6: 2.15 MB)
-    // weights instead of both (4.3 MB). Off by default: measured on MI355X (humanoid-run B = 32) 6.41 vs 6.09 ms per
-    // plan -- co-resident same-head workgroups on a CU already share the weight stream, and halving the heads per
-    // XCD halves the workgroups that stream each weight line at the same time
-    if (!a.il && nprob == 2 && a.rb == 32 && chain_xcd()) a.il = -1;
-    const dim3 grid(a.il > 0 ? nblk * nprob : a.il < 0 ? (unsigned)rup(nblk, 4) * 2 : nblk, a.il ? 1 : nprob), block(64 * nw);
+    // (the problems along blockIdx.y: co-resident same-head workgroups on a CU share the weight stream through its L1;
+    // interleaving the heads along x, or grouping them by XCD, measured 3-6 % slower -- round 1, git history)
+    a.il = 0;
+    const dim3 grid(nblk, nprob), block(64 * nw);
     const int tn = a.M / (32 * nw);
     // diagnostic timer (tdmpc_profile_begin cfg 4 + mode): HIP events around matching chain launches
     Profiler& pf = g_prof;
@@ -4624,15 +4561,27 @@ void pack_jobs(const Layout& w, const float* const* t, std::vector<PackJob>& job
 }
 
 // The job table lives in the caller's packed buffer (Layout::jobtab), so it lives and dies with that buffer and the
-// HIP graphs the caller captured over it -- nothing device-side is global or leaks. It is uploaded by a synchronous
-// copy when it differs from the table last uploaded into that buffer, never while the stream is being captured (the
-// learner packs once before it captures its update). The host remembers the last table per packed buffer in a small
-// LRU (PACK_HOST_CACHE entries): forgetting one only costs a re-upload at that buffer's next pack. One mutex guards it
-// (planners on several host threads).
-struct PackTable { std::vector<PackJob> host; const float* pw; int device; };
+// HIP graphs the caller captured over it -- nothing device-side is global or leaks. Every pack outside a stream
+// capture uploads the table (an async copy from a pinned staging buffer kept per packed buffer, whose previous copy's
+// event is waited for before it is rewritten -- long done by then); a pack inside a capture uploads nothing and
+// requires the table last uploaded into that buffer to be this one (pack once before capturing, as the learner
+// does). The host keeps the staging buffers in a small LRU (PACK_HOST_CACHE entries, freed on eviction);
+// tdmpc_pack_forget drops a buffer's entry when its address is re-allocated. One mutex guards it.
+struct PackTable {
+    std::vector<PackJob> host; const float* pw; int device;
+    PackJob* pinned; hipEvent_t done; bool recorded;
+};
 std::vector<PackTable> g_pack_tables;   // most recently used last
 std::mutex g_pack_mu;
 constexpr size_t PACK_HOST_CACHE = 64;
+
+void pack_table_free(PackTable& t) {
+    if (t.recorded) (void)hipEventSynchronize(t.done);
+    if (t.done) (void)hipEventDestroy(t.done);
+    if (t.pinned) (void)hipHostFree(t.pinned);
+    t.pinned = nullptr;
+    t.done = nullptr;
+}
 
 int launch_pack(std::vector<PackJob>& jobs, const Layout& w, float* pw, hipStream_t s) {
     if (jobs.size() > (size_t)PACK_MAX_JOBS) {
@@ -4653,22 +4602,36 @@ int launch_pack(std::vector<PackJob>& jobs, const Layout& w, float* pw, hipStrea
         size_t hit = g_pack_tables.size();
         for (size_t i = 0; i < g_pack_tables.size(); ++i)
             if (g_pack_tables[i].pw == pw && g_pack_tables[i].device == device) { hit = i; break; }
-        const bool same = hit < g_pack_tables.size() && g_pack_tables[hit].host.size() == jobs.size() &&
-                          !memcmp(g_pack_tables[hit].host.data(), jobs.data(), nb);
-        if (!same) {
-            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-            HIPCHK(hipStreamIsCapturing(s, &cs));
-            if (cs != hipStreamCaptureStatusNone) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIPCHK(hipStreamIsCapturing(s, &cs));
+        if (cs != hipStreamCaptureStatusNone) {
+            if (hit == g_pack_tables.size() || g_pack_tables[hit].host.size() != jobs.size() ||
+                memcmp(g_pack_tables[hit].host.data(), jobs.data(), nb)) {
                 snprintf(g_err, sizeof g_err, "tdmpc_pack_weights: new tensors while capturing (pack once before capture)");
                 return TDMPC_E_DIMS;
             }
-            // drained before returning: the host vector is the copy's source
-            HIPCHK(hipMemcpyAsync(dev, jobs.data(), nb, hipMemcpyHostToDevice, s));
-            HIPCHK(hipStreamSynchronize(s));
+        } else {
+            if (hit == g_pack_tables.size()) {
+                if (g_pack_tables.size() >= PACK_HOST_CACHE) {
+                    pack_table_free(g_pack_tables.front());
+                    g_pack_tables.erase(g_pack_tables.begin());
+                }
+                PackTable t{{}, pw, device, nullptr, nullptr, false};
+                HIPCHK(hipHostMalloc((void**)&t.pinned, (size_t)PACK_MAX_JOBS * sizeof(PackJob), hipHostMallocDefault));
+                HIPCHK(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
+                g_pack_tables.push_back(std::move(t));
+                hit = g_pack_tables.size() - 1;
+            }
+            PackTable& t = g_pack_tables[hit];
+            if (t.recorded) HIPCHK(hipEventSynchronize(t.done));
+            memcpy(t.pinned, jobs.data(), nb);
+            HIPCHK(hipMemcpyAsync(dev, t.pinned, nb, hipMemcpyHostToDevice, s));
+            HIPCHK(hipEventRecord(t.done, s));
+            t.recorded = true;
+            t.host = jobs;
         }
-        PackTable t{jobs, pw, device};
-        if (hit < g_pack_tables.size()) g_pack_tables.erase(g_pack_tables.begin() + hit);
-        else if (g_pack_tables.size() >= PACK_HOST_CACHE) g_pack_tables.erase(g_pack_tables.begin());
+        PackTable t = std::move(g_pack_tables[hit]);   // most recently used last
+        g_pack_tables.erase(g_pack_tables.begin() + hit);
         g_pack_tables.push_back(std::move(t));
     }
     hipLaunchKernelGGL(pack_fused_kernel, dim3((unsigned)blk), dim3(PACK_WG), 0, s, dev, (int)jobs.size(), pw);
@@ -4869,6 +4832,7 @@ int tdmpc_pack_forget(const void* packed) {
     std::lock_guard<std::mutex> lock(g_pack_mu);
     for (size_t i = 0; i < g_pack_tables.size(); ++i)
         if (g_pack_tables[i].pw == (const float*)packed) {
+            pack_table_free(g_pack_tables[i]);
             g_pack_tables.erase(g_pack_tables.begin() + i);
             break;
         }

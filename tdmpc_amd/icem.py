@@ -76,6 +76,7 @@ class TdICEM:
         _lib.check(self.L.tdmpc_icem_sizes_for(C.byref(d), C.byref(sz)), "tdmpc_icem_sizes_for")
         dev = self.device
         self.packed = torch.zeros(sz.packed_weight_bytes // 4, dtype=torch.float32, device=dev)   # (gaps stay 0)
+        self.L.tdmpc_pack_forget(C.c_void_p(self.packed.data_ptr()))   # (the address may be a freed buffer's)
         self.workspace = torch.empty(sz.workspace_bytes // 4, dtype=torch.float32, device=dev)
         self.E_max = int(cfg.fraction_elites_reused * K)
         T_max = N + self.E_max + self.P_max

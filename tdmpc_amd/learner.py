@@ -25,6 +25,7 @@ into ONE HIP graph per (buffer fill, EMA) shape and replayed: no Python in the l
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 import torch.nn.functional as F
@@ -146,7 +147,9 @@ class Learner:
         self.target_params = list(agent.model_target.parameters())
         from . import learner_engine
         self.engine = None
-        if str(agent.device).startswith("cuda") and learner_engine.supported(self.cfg):
+        # (TDMPC_LEARNER_ENGINE=0: the autograd path with PyTorch's kernels, the bench's comparison leg)
+        if (str(agent.device).startswith("cuda") and learner_engine.supported(self.cfg) and
+                os.environ.get("TDMPC_LEARNER_ENGINE", "1") != "0"):
             # explicit forward / backward kernels over flat parameters (tdmpc_amd/learner_engine.py); its two
             # Adam states stand in for the reference's optimisers
             self.engine = learner_engine.Engine(agent)

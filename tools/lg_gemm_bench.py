@@ -45,6 +45,14 @@ def run(m, n, k, amode, bmode, tile, splits=1, reps=50):
 
 
 import sys as _s
+if "--lds" in _s.argv:   # the learner's forward / dX shapes: direct tiles (1, 2) vs the LDS-staged tile (3), exact f32
+    EX = 0x100
+    for (m, n, k, am, bm) in [(512, 512, 512, 0, 0), (512, 512, 121, 0, 0), (512, 100, 512, 0, 0), (512, 512, 100, 0, 1),
+                              (512, 512, 512, 0, 1), (2560, 512, 512, 0, 0), (2560, 512, 121, 0, 0), (2560, 21, 512, 0, 0),
+                              (3072, 512, 512, 0, 0), (3072, 512, 100, 0, 0), (2560, 512, 512, 0, 1)]:
+        for tile in (1, 2, 3):
+            run(m, n, k, am, bm, tile | EX)
+    _s.exit(0)
 if "--small" in _s.argv:
     for (m, n, k, am, bm) in [(512, 512, 512, 0, 0), (512, 512, 121, 0, 0), (512, 100, 512, 0, 0),
                               (512, 512, 100, 0, 1), (512, 512, 512, 0, 1), (512, 100, 512, 0, 1)]:
