@@ -563,3 +563,48 @@ def test_plan_returns_its_own_action():
     assert torch.equal(a1, agent.planner.action[0])
     assert a0.shape == (cfg.action_dim,) and a0.is_contiguous()
     assert np.isfinite([m0["current_std"], m0["external_reward_mean"], m1["current_std"]]).all()
+
+
+@pytest.mark.parametrize("stress", ["ln_shift", "ln_scale"])
+def test_wide_heads_layernorm_stress_vs_oracle(stress):
+    """The wide heads kernel's LayerNorm-1 moments come from the pack's statistics block (mean = wbar . x + bbar,
+    var = |R [x; 1]|^2 / M), not from the 512 layer-1 outputs. Stressed here at the bench shape (32
+    humanoid envs, the wide step + wide heads kernels) against the oracle, every env: ln_shift puts the first Q
+    layers' outputs far from zero mean (bias + 30 / - 20: |mean| ~ 10-30 sigma, where an E[y^2] - mean^2 variance
+    would cancel), ln_scale shrinks their spread (weights x 1e-2: sigma ~ 1e-2, the LayerNorm eps 1e-5 matters) and
+    randomises both LayerNorms' affine parameters. The first iteration's values row by row at the fp32 tolerance
+    (parity_util: 1e-5 + 1e-4 |ref|), then every iteration while the elite sets agree."""
+    cfg = make_cfg("humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5)
+    B = 32
+    sd = synthetic_state_dict(cfg, 17)
+    g = torch.Generator().manual_seed(5)
+    for q, sh in (("_Q1", 30.0), ("_Q2", -20.0)):
+        if stress == "ln_shift":
+            sd[f"{q}.0.bias"] = sd[f"{q}.0.bias"] + sh
+        else:
+            sd[f"{q}.0.weight"] = sd[f"{q}.0.weight"] * 1e-2
+            sd[f"{q}.0.bias"] = sd[f"{q}.0.bias"] * 1e-2
+        for ln in ("1", "4"):
+            sd[f"{q}.{ln}.weight"] = 1.0 + 0.5 * torch.randn(sd[f"{q}.{ln}.weight"].shape, generator=g)
+            sd[f"{q}.{ln}.bias"] = 0.3 * torch.randn(sd[f"{q}.{ln}.bias"].shape, generator=g)
+    agent = TDMPC(cfg, max_batch=B)
+    agent.model.load_state_dict(sd)
+    agent.std = 0.05
+    told = tdmpc_ref.RefTOLD(sd, cfg)
+    rs = np.random.RandomState(7)
+    obs = rs.standard_normal((B, cfg.obs_shape[0])).astype(np.float32)
+    torch.manual_seed(8)
+    np.random.seed(8)
+    noises = [tdmpc_ref.draw_noise(cfg, 10**6, False) for _ in range(B)]
+    tr = {}
+    agent._plan_envs(obs, False, 10**6, [True] * B, trace=tr, noise=noises)
+    full = 0
+    for e in range(B):
+        rtr = {}
+        tdmpc_ref.plan(told, cfg, tdmpc_ref.PlanState(0.05), obs[e], noises[e], eval_mode=False, step=10**6, t0=True,
+                       trace=rtr)
+        ref_vals = torch.stack(rtr["value"]).squeeze(-1).numpy()
+        same = _compare_iterations(tr["value"][e].cpu().numpy(), ref_vals, cfg.num_elites)
+        record(same, f"wide_heads_{stress}/env{e}")
+        full += int(same)
+    assert full >= B - 2, f"{full} of {B} envs compared to the end"
