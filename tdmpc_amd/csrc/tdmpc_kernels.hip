@@ -109,6 +109,7 @@ struct Layout {
     // whose batches reach the wide kernels: nqs = the first layer's real columns + its bias (A + L + 1), 0 = none
     int nqs, nsr;          // columns of the Cholesky factor; statistics rows per Q head (16 x 8 or 16 x 16)
     size_t x6qs, bqs;      // x6q [2][nsr][rup(Kx, 32)]; bias [2][nsr]
+    size_t x6qf, bqf;      // the folded first layer diag(g1) (W1 - 1 wbar^T): x6q [2][M][rup(Kx, 32)]; g1 (b1 - bbar) [2][M]
     size_t qs_gram;        // fp64 scratch [2][nqs][nqs] (the Gram matrices)
     size_t total;
 };
@@ -194,7 +195,7 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
     // the statistics block: only where the wide heads may run (B N >= 4096 rows, M = 512) and the Cholesky's
     // upper-packed fp64 factor fits one workgroup's LDS
     w->nqs = w->nsr = 0;
-    w->x6qs = w->bqs = w->qs_gram = 0;
+    w->x6qs = w->bqs = w->x6qf = w->bqf = w->qs_gram = 0;
     {
         const int n = w->A + w->L + 1;
         if (w->M == 512 && (long)d->max_batch * d->num_samples >= 4096 && n + 1 <= 256 &&
@@ -203,6 +204,8 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
             w->nsr = n + 1 <= 128 ? 128 : 256;
             w->x6qs = take((size_t)2 * w->nsr * rup(w->Kx, 32) * 3 / 2);
             w->bqs = take((size_t)2 * w->nsr);
+            w->x6qf = take((size_t)2 * w->M * rup(w->Kx, 32) * 3 / 2);
+            w->bqf = take((size_t)2 * w->M);
             w->qs_gram = take((size_t)2 * n * n * 2);
         }
     }
@@ -4065,10 +4068,10 @@ int launch_wide_heads(const Ctx& c, const WHJob* jobs, int nj, const float* eps,
     for (int h = 0; h < 2; ++h) {
         WHQHead& q = a.q[h];
         q.S = (const unsigned short*)(c.pw + w.x6qs) + (size_t)h * (w.nsr / 16) * g1q * 1536;
-        q.X1 = q6(X6_WQ1X) + (size_t)h * (M / 16) * g1q * 1536;
+        q.X1 = (const unsigned short*)(c.pw + w.x6qf) + (size_t)h * (M / 16) * g1q * 1536;   // (folded, see wide_heads.inc)
         q.X2 = q6(X6_WQ2) + (size_t)h * (M / 16) * (M / 32) * 1536;
         q.bs = c.pw + w.bqs + (size_t)h * w.nsr;
-        q.b1 = c.pw + w.bq1x + h * M; q.g1 = c.pw + w.g1 + h * M; q.be1 = c.pw + w.be1 + h * M;
+        q.b1 = c.pw + w.bqf + h * M; q.g1 = c.pw + w.g1 + h * M; q.be1 = c.pw + w.be1 + h * M;
         q.b2 = c.pw + w.bq2 + h * M; q.g2 = c.pw + w.g2 + h * M; q.be2 = c.pw + w.be2 + h * M;
         q.w3 = c.pw + w.wq3 + h * M; q.b3 = c.pw + w.bq3 + h;
     }
@@ -4818,6 +4821,7 @@ int tdmpc_pack_weights(const tdmpc_dims* d, const float* const* t, int32_t n, vo
     q.W1 = pw + w.wq1x; q.b1 = pw + w.bq1x; q.gram = (double*)(pw + w.qs_gram);
     q.M = w.M; q.Kx = w.Kx; q.A = w.A; q.L = w.L; q.Ap = w.Ap; q.n = w.nqs;
     q.S = (unsigned short*)(pw + w.x6qs); q.bs = pw + w.bqs; q.nsr = w.nsr; q.g1s = (int)(rup(w.Kx, 32) / 32);
+    q.F = (unsigned short*)(pw + w.x6qf); q.bf = pw + w.bqf; q.g1 = pw + w.g1;
     const hipStream_t s = (hipStream_t)stream;
     const int nt = (w.nqs + 15) / 16;
     hipLaunchKernelGGL(qstat_gram_kernel, dim3(nt, nt, 2), dim3(256), 0, s, q);

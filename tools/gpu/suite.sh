@@ -15,6 +15,9 @@
 #   single:v1,v2     literal single-env plan() per library variant (6 rounds of 150 calls, median per variant)
 #   stamps           per-step shader stamps of the wide step kernel (needs the `ws` variant: -DWS_STAMPS)
 #   learner:VAR=v1,v2  the learner / train-loop / adam tests, then an A/B of VAR on the humanoid update time
+#   lgbench          lg_gemm tile timings of the learner's products (tools/lg_gemm_bench.py --lds)
+#   p1stamps         per-hand-off timeline of the one-env persistent plan (tools/p1_stamps.py)
+#   qt               tools/quick_time.py on CONFIG / ENVS (qt.txt)
 # Environment: CONFIG (default humanoid-run), ENVS (default 32).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -118,6 +121,15 @@ PY
             python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('$var=$v', d['graph'])" || exit 1
         done
       done ;;
+    lgbench)
+      timeout -k 10 200 python -u tools/lg_gemm_bench.py --lds > "$OUT/lg_gemm.txt" 2>&1 || { tail -20 "$OUT/lg_gemm.txt"; exit 1; }
+      grep -v amdgpu.ids "$OUT/lg_gemm.txt" | tail -30 ;;
+    p1stamps)
+      timeout -k 10 120 python -u tools/p1_stamps.py "$CONFIG" > "$OUT/p1_stamps.txt" 2>&1 || { tail -20 "$OUT/p1_stamps.txt"; exit 1; }
+      tail -4 "$OUT/p1_stamps.txt" ;;
+    qt)
+      timeout -k 10 120 python -u tools/quick_time.py "$CONFIG" "$ENVS" > "$OUT/qt.txt" 2>&1 || { tail -20 "$OUT/qt.txt"; exit 1; }
+      grep -v amdgpu.ids "$OUT/qt.txt" ;;
     *) echo "unknown stage $stage"; exit 2 ;;
   esac
 done
