@@ -403,14 +403,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
     }
 }
 
-// The LDS-staged form (tile 3 of tdmpc_lg_gemm; jobs whose segments all read A row-major, no split-K, exact f32
-// products): per 32 x 32 output tile, K in chunks of 64 -- every chunk's A rows and B columns loaded by the whole
+// The LDS-staged form (tiles 3 and 4 of tdmpc_lg_gemm; jobs whose segments all read A row-major, no split-K, exact
+// f32 products): per 32 x 32 output tile, K in chunks of 64 -- every chunk's A rows and B columns loaded by the whole
 // workgroup with coalesced 4-byte buffer loads (a wave reads 256 contiguous bytes per instruction; the direct form
 // reads 16 bytes from each of 32 rows per instruction and is bound by those scattered requests) into LDS (row stride
-// 65 floats: the MFMA operand reads down a column are conflict-free), the next chunk's loads in flight while this
-// chunk's MFMAs run, one barrier per chunk; the four waves split each chunk's K and add through LDS at the end.
+// 65 floats: the MFMA operand reads down a column are conflict-free), one barrier per chunk; the four waves split each
+// chunk's K and add through LDS at the end. D chunks' loads are in flight in registers (tile 3: D = 1, tile 4: D = 4):
+// one workgroup per CU at the learner's sizes (256 tiles of a 512 x 512 product), so nothing else hides a chunk's L2
+// latency behind its eight MFMAs (~0.2 us) -- D chunks ahead cover ~0.9 us.
 constexpr int LGS_K = 64, LGS_P = LGS_K + 1;
 
+template <int D>
 __global__ void __launch_bounds__(256) lg_gemm_lds_kernel(const KArgs P) {
     __shared__ float sA[2][32 * LGS_P], sB[2][32 * LGS_P];
     __shared__ float red[4][16][64];
@@ -428,10 +431,11 @@ __global__ void __launch_bounds__(256) lg_gemm_lds_kernel(const KArgs P) {
         nch[s2] = s2 < J.j.nseg ? (J.j.seg[s2].k + LGS_K - 1) / LGS_K : 0;
         nchunks += nch[s2];
     }
-    float ra[8], rb[8];
+    float ra[D][8], rb[D][8];
+    int bmq[D];
     // loads of chunk c into registers: A element e = tid + 256 i of [32 rows][64 k]; B the same over [32 n][64 k]
     // (bmode 0, weight rows) or [64 k][32 n] (bmode 1)
-    auto load = [&](int c) {
+    auto load = [&](int c, float (&xa)[8], float (&xb)[8]) __attribute__((always_inline)) -> int {
         int s2 = 0, cc = c;
         while (s2 < 2 && cc >= nch[s2]) { cc -= nch[s2]; ++s2; }
         const tdmpc_lg_seg& S = J.j.seg[s2];
@@ -444,43 +448,50 @@ __global__ void __launch_bounds__(256) lg_gemm_lds_kernel(const KArgs P) {
             const int e = tid + 256 * i;
             const int row = e >> 6, k = k0 + (e & 63);
             const bool ok = m0 + row < M && k < S.k;
-            ra[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            xa[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
                 rsa, ok ? (int)((unsigned)((m0 + row) * S.lda + k) * 4u) : (int)LG_OOB, 0, 0));
             int n, kb;
             if (S.bmode == 0) { n = n0 + (e >> 6); kb = k; }
             else { n = n0 + (e & 31); kb = k0 + (e >> 5); }
             const bool okb = n < nbm && kb < S.k;
             const unsigned idx = S.bmode == 0 ? (unsigned)(n * S.ldb + kb) : (unsigned)(kb * S.ldb + n);
-            rb[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsb, okb ? (int)(idx * 4u) : (int)LG_OOB, 0, 0));
+            xb[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsb, okb ? (int)(idx * 4u) : (int)LG_OOB, 0, 0));
         }
         return S.bmode;
     };
-    auto store = [&](int buf, int bmode) {
+    auto store = [&](int buf, const float (&xa)[8], const float (&xb)[8], int bmode) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int e = tid + 256 * i;
-            sA[buf][(e >> 6) * LGS_P + (e & 63)] = ra[i];
-            if (bmode == 0) sB[buf][(e >> 6) * LGS_P + (e & 63)] = rb[i];
-            else sB[buf][(e & 31) * LGS_P + (e >> 5)] = rb[i];
+            sA[buf][(e >> 6) * LGS_P + (e & 63)] = xa[i];
+            if (bmode == 0) sB[buf][(e >> 6) * LGS_P + (e & 63)] = xb[i];
+            else sB[buf][(e & 31) * LGS_P + (e >> 5)] = xb[i];
         }
     };
     floatx16 acc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-    if (nchunks > 0) {
-        store(0, load(0));
-        __syncthreads();
-        for (int c = 0; c < nchunks; ++c) {
-            const int buf = c & 1;
-            int bm = 0;
-            if (c + 1 < nchunks) bm = load(c + 1);
-            // this wave's 16 k of the chunk: MFMA step t sums k = 16 wave + 2t + h
-            const float* a = sA[buf] + r * LGS_P + 16 * wave + h;
-            const float* b = sB[buf] + r * LGS_P + 16 * wave + h;
 #pragma unroll
-            for (int t = 0; t < 8; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2 * t], b[2 * t], acc, 0, 0, 0);
-            if (c + 1 < nchunks) store(buf ^ 1, bm);
-            __syncthreads();
+    for (int d = 0; d < D; ++d)
+        if (d < nchunks) bmq[d] = load(d, ra[d], rb[d]);
+    // chunk c: stored into LDS buffer c & 1, its registers refilled with chunk c + D, one barrier, the MFMAs. (A wave
+    // stores chunk c + 1 into the other buffer only after the barrier of chunk c, which every wave reaches after its
+    // MFMAs of chunk c - 1: two buffers suffice.)
+    for (int c0 = 0; c0 < nchunks; c0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int c = c0 + d;
+            if (c < nchunks) {
+                const int buf = c & 1;
+                store(buf, ra[d], rb[d], bmq[d]);
+                if (c + D < nchunks) bmq[d] = load(c + D, ra[d], rb[d]);
+                __syncthreads();
+                // this wave's 16 k of the chunk: MFMA step t sums k = 16 wave + 2t + h
+                const float* a = sA[buf] + r * LGS_P + 16 * wave + h;
+                const float* b = sB[buf] + r * LGS_P + 16 * wave + h;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2 * t], b[2 * t], acc, 0, 0, 0);
+            }
         }
     }
 #pragma unroll
@@ -800,8 +811,8 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
     if (!jobs) return TDMPC_E_NULL;
     const bool x6 = !(tile & TDMPC_LG_TILE_EXACT);   // x6 products unless the caller asks for the exact f32 MFMA
     tile &= ~TDMPC_LG_TILE_EXACT;
-    if (njobs <= 0 || njobs > LG_MAXJ || tile < 1 || tile > 3) return bad("tdmpc_lg_gemm: njobs / tile");
-    if (tile == 3) {   // the LDS-staged form where every job allows it (A row-major, no ones column, no split-K), else tile 1
+    if (njobs <= 0 || njobs > LG_MAXJ || tile < 1 || tile > 4) return bad("tdmpc_lg_gemm: njobs / tile");
+    if (tile >= 3) {   // the LDS-staged forms where every job allows it (A row-major, no ones column, no split-K), else tile 1
         bool ok = !x6;
         for (int q = 0; q < njobs && ok; ++q) {
             ok = jobs[q].splits == 1;
@@ -840,7 +851,8 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
     P.njobs = njobs;
     if (blocks >= (1L << 31)) return bad("tdmpc_lg_gemm: grid");
     const dim3 g((unsigned)blocks), b(256);
-    if (tile == 3) hipLaunchKernelGGL(lg_gemm_lds_kernel, g, b, 0, (hipStream_t)stream, P);
+    if (tile == 4) hipLaunchKernelGGL(lg_gemm_lds_kernel<4>, g, b, 0, (hipStream_t)stream, P);
+    else if (tile == 3) hipLaunchKernelGGL(lg_gemm_lds_kernel<1>, g, b, 0, (hipStream_t)stream, P);
     else if (tile == 1 && x6) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, true>), g, b, 0, (hipStream_t)stream, P);
     else if (tile == 1) hipLaunchKernelGGL((lg_gemm_kernel<1, 1>), g, b, 0, (hipStream_t)stream, P);
     else if (x6) hipLaunchKernelGGL((lg_gemm_kernel<2, 2, true>), g, b, 0, (hipStream_t)stream, P);

@@ -130,8 +130,9 @@ class Engine:
         # every product on the hand-written lg_gemm (grouped launches, fused ELU / ELU' epilogues); TDMPC_LG_BLAS=1
         # puts the plain M x M products back on hipBLASLt (torch.mm / addmm) for an A/B
         self.blas = os.environ.get("TDMPC_LG_BLAS", "0") == "1"
-        # lg_gemm's LDS-staged tile (3) for the forward / data-gradient products (TDMPC_LG_LDS=0: the direct tiles)
-        self.lds = os.environ.get("TDMPC_LG_LDS", "1") != "0"
+        # lg_gemm's LDS-staged tile for the forward / data-gradient products: TDMPC_LG_LDS = 4 (four K chunks in
+        # flight, default), 3 (one), 0 (the direct tiles)
+        self.lds = int(os.environ.get("TDMPC_LG_LDS", "4"))
         self._aux = {}
 
     def _alias(self, model, flat):
@@ -247,7 +248,7 @@ class Engine:
             # 64 x 64 tiles only for wide launches of row-major operands; a transposed weight operand (the
             # backward's dX) runs 15-25 % faster on 32 x 32 tiles (tools/lg_gemm_bench.py)
             tbw = any(sg[6] == 1 for j in jobs for sg in j["segs"])
-            tile = 3 if self.lds and not self.x6 else 2 if tiles64 >= self.t64 and not tbw else 1
+            tile = self.lds if self.lds in (3, 4) and not self.x6 else 2 if tiles64 >= self.t64 and not tbw else 1
         tile |= 0 if self.x6 else TILE_EXACT
         _lib.check(self.lib.tdmpc_lg_gemm(arr, len(jobs), tile, self._stream()), "tdmpc_lg_gemm")
 

@@ -70,7 +70,11 @@ def status_main(out):
 def main(out):
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    backend = os.environ.get("TDMPC_SHARD_BACKEND", "gloo")   # "nccl" (RCCL): one rank per device only
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     if len(sys.argv) > 2 and sys.argv[2] == "status":
         try:
             status_main(out)
@@ -91,6 +95,13 @@ def main(out):
             position_rngs(agent, planner.lo, k, H, I)
             a, m = planner.plan(torch.from_numpy(obs), 10**6, t0=(k == 0))
             res[f"a{k}"], res[f"m{k}"] = a.cpu().numpy(), m.cpu().numpy()
+        if world == 1:
+            # (plan() skips the exchange at world 1: run the planner's gather itself, so the RCCL device-tensor
+            # all_gather_into_tensor executes on the hardware; its output must be the local block, byte for byte)
+            planner._all.fill_(float("nan"))
+            planner._all_gather()
+            torch.cuda.synchronize()
+            res["gather_equal"] = np.array(bool(torch.equal(planner._all, planner._local)))
         np.savez(os.path.join(out, f"rank{rank}.npz"), **res)
     finally:
         dist.destroy_process_group()

@@ -29,9 +29,10 @@ def _free_port():
     return p
 
 
-def _run_world(tmp_path, world, *mode):
+def _run_world(tmp_path, world, *mode, backend="gloo"):
     port = _free_port()
-    env = dict(os.environ, WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    env = dict(os.environ, WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               TDMPC_SHARD_BACKEND=backend)
     env.pop("TDMPC_P1_DEBUG_SKIP", None)
     here = os.path.dirname(os.path.abspath(__file__))
     procs = [subprocess.Popen([sys.executable, os.path.join(here, "shard_worker.py"), str(tmp_path), *mode],
@@ -59,9 +60,7 @@ def test_sharded_status_raises_on_every_rank(tmp_path):
         assert finite == "True" and st == "0", (r, finite, st)
 
 
-def test_sharded_dog64_world2_equals_single_process(tmp_path):
-    world = 2
-    _run_world(tmp_path, world)
+def _check_against_single_process(tmp_path, world):
     got = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(world)]
     # single process, all 64 envs, same weights and generator states
     c = W.cfg()
@@ -77,3 +76,19 @@ def test_sharded_dog64_world2_equals_single_process(tmp_path):
         for r in range(world):   # every rank holds the whole gathered batch
             np.testing.assert_array_equal(got[r][f"a{k}"], a, err_msg=f"call {k} rank {r} actions")
             np.testing.assert_array_equal(got[r][f"m{k}"], m, err_msg=f"call {k} rank {r} metrics")
+
+
+def test_sharded_dog64_world2_equals_single_process(tmp_path):
+    world = 2
+    _run_world(tmp_path, world)
+    _check_against_single_process(tmp_path, world)
+
+
+def test_sharded_dog64_rccl_world1_equals_single_process(tmp_path):
+    """The RCCL ("nccl") branch of EnvShardedPlanner on hardware: one rank owning the box's GPU, the device-tensor
+    all_gather_into_tensor over RCCL (parallel.py's nccl path, the one `bench.py --gpus N` takes under torchrun), the
+    gathered batch bitwise equal to the single-process plan_batch. (Two ranks on one device are refused by RCCL, so
+    the multi-rank exchange itself is covered by the gloo test above and tests/test_parallel_cpu.py.)"""
+    _run_world(tmp_path, 1, backend="nccl")
+    _check_against_single_process(tmp_path, 1)
+    assert bool(np.load(os.path.join(tmp_path, "rank0.npz"))["gather_equal"])

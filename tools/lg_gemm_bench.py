@@ -50,13 +50,13 @@ if "--lds" in _s.argv:   # the learner's forward / dX shapes: direct tiles (1, 2
     for (m, n, k, am, bm) in [(512, 512, 512, 0, 0), (512, 512, 121, 0, 0), (512, 100, 512, 0, 0), (512, 512, 100, 0, 1),
                               (512, 512, 512, 0, 1), (2560, 512, 512, 0, 0), (2560, 512, 121, 0, 0), (2560, 21, 512, 0, 0),
                               (3072, 512, 512, 0, 0), (3072, 512, 100, 0, 0), (2560, 512, 512, 0, 1)]:
-        for tile in (1, 2, 3):
+        for tile in (1, 2, 3, 4):
             run(m, n, k, am, bm, tile | EX)
     _s.exit(0)
 if "--small" in _s.argv:
     for (m, n, k, am, bm) in [(512, 512, 512, 0, 0), (512, 512, 121, 0, 0), (512, 100, 512, 0, 0),
                               (512, 512, 100, 0, 1), (512, 512, 512, 0, 1), (512, 100, 512, 0, 1)]:
-        for tile in (1, 3):
+        for tile in (1, 3, 4):
             run(m, n, k, am, bm, tile)
     _s.exit(0)
 for (m, n, k) in ([] if "--dw" in _s.argv else [(2560, 512, 512), (3072, 512, 512), (512, 512, 512), (2560, 512, 121), (2560, 21, 512)]):
