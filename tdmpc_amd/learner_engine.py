@@ -584,8 +584,8 @@ class Engine:
             slots[name] = _p(buf)
             jobs.append(dict(segs=segs, m=o, n=i + 1, c=_p(buf), ldc=i + 1, splits=s, slice=o * (i + 1)))
         # 32 x 32 tiles, K (the rows) split 4 ways: 2-3x faster than 64 x 64 tiles for these narrow-N / long-K
-        # products on MI355X (tools/lg_gemm_bench.py --dw: 512 x 122 x 2560 12 vs 38 us)
-        self.gemm(jobs, tile=1)
+        # products on MI355X (tools/lg_gemm_bench.py --dw: 512 x 122 x 2560 12 vs 38 us); LDS-staged as the rest
+        self.gemm(jobs, tile=self.lds if self.lds in (3, 4) and not self.x6 else 1)
         return slots
 
     def _optimise(self, opt, src, g_lo, norm_out):
