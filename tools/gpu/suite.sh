@@ -15,6 +15,7 @@
 #   single:v1,v2     literal single-env plan() per library variant (6 rounds of 150 calls, median per variant)
 #   stamps           per-step shader stamps of the wide step kernel (needs the `ws` variant: -DWS_STAMPS)
 #   learner:VAR=v1,v2  the learner / train-loop / adam tests, then an A/B of VAR on the humanoid update time
+#   lab:VAR=v1,v2    the humanoid update-time A/B of `learner:` without its tests
 #   lgbench          lg_gemm tile timings of the learner's products (tools/lg_gemm_bench.py --lds)
 #   p1stamps         per-hand-off timeline of the one-env persistent plan (tools/p1_stamps.py)
 #   qt               tools/quick_time.py on CONFIG / ENVS (qt.txt)
@@ -115,6 +116,14 @@ PY
       timeout -k 10 600 python -u -m pytest tests/test_learner.py tests/test_gpu_train_loop.py tests/test_gpu_adam.py -m gpu -v -x \
         --timeout 300 --timeout-method thread > "$OUT/learner_tests.txt" 2>&1 || { echo "tests failed"; tail -40 "$OUT/learner_tests.txt"; exit 1; }
       grep -E "passed|failed" "$OUT/learner_tests.txt" | tail -1
+      for i in 1 2 3; do
+        for v in ${vals//,/ }; do
+          env "$var=$v" timeout -k 10 120 python -u tools/quick_learner.py humanoid-run 2>&1 | grep -v amdgpu.ids | \
+            python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('$var=$v', d['graph'])" || exit 1
+        done
+      done ;;
+    lab:*)
+      kv=${stage#lab:}; var=${kv%%=*}; vals=${kv#*=}
       for i in 1 2 3; do
         for v in ${vals//,/ }; do
           env "$var=$v" timeout -k 10 120 python -u tools/quick_learner.py humanoid-run 2>&1 | grep -v amdgpu.ids | \
