@@ -592,7 +592,8 @@ def test_wide_heads_layernorm_stress_vs_oracle(stress):
     eps 1e-5 matters) and randomises both LayerNorms' affine parameters.
     A stressed LayerNorm amplifies every fp32 rounding of its input by |y| / sigma, the reference's own included, so
     the yardstick is the oracle with helper.q in float64: iteration 0's 768 values (identical candidates on all
-    sides) must be no further from it than 2x the fp32 oracle's own distance from it (+ 2e-6). Then every iteration
+    sides) must be no further from it than 2x the fp32 oracle's own distance from it + the fp32 tolerance's 1e-5
+    (the rollout before helper.q rounds differently too: x6 products vs the reference's fp32 GEMMs). Then every iteration
     is compared with the fp32 oracle while the elite sets agree, at the fp32 tolerance (parity_util: 1e-5 + 1e-4
     |ref|) widened by 4x that measured reference error (two fp32 evaluations each that far from exact)."""
     cfg = make_cfg("humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5)
@@ -631,7 +632,7 @@ def test_wide_heads_layernorm_stress_vs_oracle(stress):
         gpu = tr["value"][e].cpu().numpy().astype(np.float64)
         ref_err = np.abs(vals["f32"][0] - vals["f64"][0]).max()
         gpu_err = np.abs(gpu[0] - vals["f64"][0]).max()
-        assert gpu_err <= 2 * ref_err + 2e-6, f"env {e}: |gpu - exact| {gpu_err:.3e} vs fp32 reference {ref_err:.3e}"
+        assert gpu_err <= 2 * ref_err + ATOL, f"env {e}: |gpu - exact| {gpu_err:.3e} vs fp32 reference {ref_err:.3e}"
         same = True
         for i in range(vals["f32"].shape[0]):
             ok = _close(gpu[i], vals["f32"][i], atol=ATOL + 4 * ref_err)
