@@ -78,10 +78,7 @@ typedef struct tdmpc_lg_job {
     float std_; int32_t splits; int64_t slice;
 } tdmpc_lg_job;
 
-/* Up to 12 GEMMs in one launch; tile 1: 32x32 output tiles, 2: 64x64 (4 waves split K inside a workgroup); 3: 32x32
- * tiles with every K chunk staged through LDS by coalesced loads, one chunk's loads ahead; 4: the same with four
- * chunks' loads in flight (exact products only: with x6 products they fall back to tile 1). Tiles 3 and 4 compute the
- * same sums in the same order (bitwise equal).
+/* Up to 12 GEMMs in one launch; tile 1: 32x32 output tiles, 2: 64x64 (4 waves split K inside a workgroup).
  * Products are fp32-accurate x6 (three bf16 parts per operand, six bf16 MFMAs per pair, fp32 accumulation);
  * tile | TDMPC_LG_TILE_EXACT runs the exact v_mfma_f32_32x32x2_f32 products instead. */
 #define TDMPC_LG_TILE_EXACT 0x100

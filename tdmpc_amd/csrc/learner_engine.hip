@@ -403,124 +403,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
     }
 }
 
-// The LDS-staged form (tiles 3 and 4 of tdmpc_lg_gemm; exact f32 products): per 32 x 32 output tile, K in chunks of
-// 64 -- every chunk's A rows and B columns loaded by the whole workgroup with coalesced 4-byte buffer loads (a wave
-// reads 256 contiguous bytes per instruction for a row-major operand, 2 x 128 for a transposed one; the direct form
-// reads 16 bytes from each of 32 rows per instruction and is bound by those scattered requests) into LDS (row stride
-// 65 floats: the MFMA operand reads down a column are conflict-free), one barrier per chunk; the four waves split each
-// chunk's K and add through LDS at the end. D chunks' loads are in flight in registers (tile 3: D = 1, tile 4: D = 4):
-// one workgroup per CU at the learner's sizes (256 tiles of a 512 x 512 product), so nothing else hides a chunk's L2
-// latency behind its eight MFMAs (~0.2 us) -- D chunks ahead cover ~0.9 us. Split-K jobs (the weight gradients: A =
-// dY^T read as amode 1, B = X^T as bmode 1, the bias as the ones column) take the direct form's K ranges per split.
-constexpr int LGS_K = 64, LGS_P = LGS_K + 1;
-
-template <int D>
-__global__ void __launch_bounds__(256) lg_gemm_lds_kernel(const KArgs P) {
-    __shared__ float sA[2][32 * LGS_P], sB[2][32 * LGS_P];
-    __shared__ float red[4][16][64];
-    int jb = 0;
-    for (int q = 1; q < P.njobs; ++q)
-        if ((int)blockIdx.x >= P.job[q].block0) jb = q;
-    const KJob& J = P.job[jb];
-    const int local = (int)blockIdx.x - J.block0;
-    const int splits = J.j.splits, split = local % splits, tile = local / splits;
-    const int m0 = (tile % J.tiles_m) * 32, n0 = (tile / J.tiles_m) * 32;
-    const int M = J.j.m, N = J.j.n;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-    // the chunk sequence: every segment's K range (this split's, as the direct form cuts it) in chunks of 64
-    int nch[3], klo[3], khi[3], nchunks = 0;
-    for (int s2 = 0; s2 < 3; ++s2) {
-        klo[s2] = khi[s2] = 0;
-        if (s2 < J.j.nseg) {
-            const int k = J.j.seg[s2].k;
-            khi[s2] = k;
-            if (splits > 1) {
-                const int chunk = ((k + splits - 1) / splits + 7) & ~7;
-                klo[s2] = min(k, split * chunk);
-                khi[s2] = min(k, klo[s2] + chunk);
-            }
-        }
-        nch[s2] = (khi[s2] - klo[s2] + LGS_K - 1) / LGS_K;
-        nchunks += nch[s2];
-    }
-    float ra[D][8], rb[D][8];
-    int bmq[D];
-    // loads of chunk c into registers, element e = tid + 256 i: A over [32 rows][64 k] (amode 0: A[m][k], the k run
-    // contiguous; amode 1: A[k][m], the m run contiguous), B over [32 n][64 k] (bmode 0: B[n][k]) or [64 k][32 n]
-    // (bmode 1: B[k][n]); the ones column's entries are 1 inside the K range, no load. Returns the modes (bit 0 a, 1 b).
-    auto load = [&](int c, float (&xa)[8], float (&xb)[8]) __attribute__((always_inline)) -> int {
-        int s2 = 0, cc = c;
-        while (s2 < 2 && cc >= nch[s2]) { cc -= nch[s2]; ++s2; }
-        const tdmpc_lg_seg& S = J.j.seg[s2];
-        const int k0 = klo[s2] + cc * LGS_K, kend = khi[s2];
-        const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)S.a, (short)0, (int)LG_OOB, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)S.b, (short)0, (int)LG_OOB, 0x00020000);
-        const int nbm = J.nb_mem[s2];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int e = tid + 256 * i;
-            const int row = S.amode == 0 ? e >> 6 : e & 31, k = k0 + (S.amode == 0 ? e & 63 : e >> 5);
-            const bool ok = m0 + row < M && k < kend;
-            const unsigned ia = S.amode == 0 ? (unsigned)((m0 + row) * S.lda + k) : (unsigned)(k * S.lda + m0 + row);
-            xa[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsa, ok ? (int)(ia * 4u) : (int)LG_OOB, 0, 0));
-            int n, kb;
-            if (S.bmode == 0) { n = n0 + (e >> 6); kb = k0 + (e & 63); }
-            else { n = n0 + (e & 31); kb = k0 + (e >> 5); }
-            const bool okb = n < nbm && kb < kend;
-            const unsigned idx = S.bmode == 0 ? (unsigned)(n * S.ldb + kb) : (unsigned)(kb * S.ldb + n);
-            const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsb, okb ? (int)(idx * 4u) : (int)LG_OOB, 0, 0));
-            xb[i] = n == S.ones_col ? (kb < kend ? 1.f : 0.f) : v;
-        }
-        return S.amode | (S.bmode << 1);
-    };
-    auto store = [&](int buf, const float (&xa)[8], const float (&xb)[8], int modes) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int e = tid + 256 * i;
-            if (!(modes & 1)) sA[buf][(e >> 6) * LGS_P + (e & 63)] = xa[i];
-            else sA[buf][(e & 31) * LGS_P + (e >> 5)] = xa[i];
-            if (!(modes & 2)) sB[buf][(e >> 6) * LGS_P + (e & 63)] = xb[i];
-            else sB[buf][(e & 31) * LGS_P + (e >> 5)] = xb[i];
-        }
-    };
-    floatx16 acc;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-#pragma unroll
-    for (int d = 0; d < D; ++d)
-        if (d < nchunks) bmq[d] = load(d, ra[d], rb[d]);
-    // chunk c: stored into LDS buffer c & 1, its registers refilled with chunk c + D, one barrier, the MFMAs. (A wave
-    // stores chunk c + 1 into the other buffer only after the barrier of chunk c, which every wave reaches after its
-    // MFMAs of chunk c - 1: two buffers suffice.)
-    for (int c0 = 0; c0 < nchunks; c0 += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const int c = c0 + d;
-            if (c < nchunks) {
-                const int buf = c & 1;
-                store(buf, ra[d], rb[d], bmq[d]);
-                if (c + D < nchunks) bmq[d] = load(c + D, ra[d], rb[d]);
-                __syncthreads();
-                // this wave's 16 k of the chunk: MFMA step t sums k = 16 wave + 2t + h
-                const float* a = sA[buf] + r * LGS_P + 16 * wave + h;
-                const float* b = sB[buf] + r * LGS_P + 16 * wave + h;
-#pragma unroll
-                for (int t = 0; t < 8; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2 * t], b[2 * t], acc, 0, 0, 0);
-            }
-        }
-    }
-#pragma unroll
-    for (int e = 0; e < 16; ++e) red[wave][e][lane] = acc[e];
-    __syncthreads();
-    const tdmpc_lg_job& JJ = J.j;
-    for (int q = wave * 4; q < wave * 4 + 4; ++q) {
-        const float v = red[0][q][lane] + red[1][q][lane] + red[2][q][lane] + red[3][q][lane];
-        const int row = m0 + (q & 3) + 8 * (q >> 2) + 4 * h, col = n0 + r;
-        if (row >= M || col >= N) continue;
-        lg_store(JJ, splits, split, row, col, v);
-    }
-}
-
 // ---------------------------------------------------------------------------------------------------- rows
 template <int NC>
 __global__ void __launch_bounds__(256) lg_rows_fwd_kernel(const tdmpc_lg_rows a) {
@@ -826,8 +708,7 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
     if (!jobs) return TDMPC_E_NULL;
     const bool x6 = !(tile & TDMPC_LG_TILE_EXACT);   // x6 products unless the caller asks for the exact f32 MFMA
     tile &= ~TDMPC_LG_TILE_EXACT;
-    if (njobs <= 0 || njobs > LG_MAXJ || tile < 1 || tile > 4) return bad("tdmpc_lg_gemm: njobs / tile");
-    if (tile >= 3 && x6) tile = 1;   // (the LDS-staged forms run the exact products only)
+    if (njobs <= 0 || njobs > LG_MAXJ || tile < 1 || tile > 2) return bad("tdmpc_lg_gemm: njobs / tile");
     KArgs P;
     memset(&P, 0, sizeof P);
     const int tw = tile == 2 ? 64 : 32;
@@ -858,9 +739,7 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
     P.njobs = njobs;
     if (blocks >= (1L << 31)) return bad("tdmpc_lg_gemm: grid");
     const dim3 g((unsigned)blocks), b(256);
-    if (tile == 4) hipLaunchKernelGGL(lg_gemm_lds_kernel<4>, g, b, 0, (hipStream_t)stream, P);
-    else if (tile == 3) hipLaunchKernelGGL(lg_gemm_lds_kernel<1>, g, b, 0, (hipStream_t)stream, P);
-    else if (tile == 1 && x6) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, true>), g, b, 0, (hipStream_t)stream, P);
+    if (tile == 1 && x6) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, true>), g, b, 0, (hipStream_t)stream, P);
     else if (tile == 1) hipLaunchKernelGGL((lg_gemm_kernel<1, 1>), g, b, 0, (hipStream_t)stream, P);
     else if (x6) hipLaunchKernelGGL((lg_gemm_kernel<2, 2, true>), g, b, 0, (hipStream_t)stream, P);
     else hipLaunchKernelGGL((lg_gemm_kernel<2, 2>), g, b, 0, (hipStream_t)stream, P);

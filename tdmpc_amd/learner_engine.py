@@ -130,9 +130,6 @@ class Engine:
         # every product on the hand-written lg_gemm (grouped launches, fused ELU / ELU' epilogues); TDMPC_LG_BLAS=1
         # puts the plain M x M products back on hipBLASLt (torch.mm / addmm) for an A/B
         self.blas = os.environ.get("TDMPC_LG_BLAS", "0") == "1"
-        # lg_gemm's LDS-staged tile for the forward / data-gradient products: TDMPC_LG_LDS = 4 (four K chunks in
-        # flight, default), 3 (one), 0 (the direct tiles)
-        self.lds = int(os.environ.get("TDMPC_LG_LDS", "4"))
         self._aux = {}
 
     def _alias(self, model, flat):
@@ -248,7 +245,7 @@ class Engine:
             # 64 x 64 tiles only for wide launches of row-major operands; a transposed weight operand (the
             # backward's dX) runs 15-25 % faster on 32 x 32 tiles (tools/lg_gemm_bench.py)
             tbw = any(sg[6] == 1 for j in jobs for sg in j["segs"])
-            tile = self.lds if self.lds in (3, 4) and not self.x6 else 2 if tiles64 >= self.t64 and not tbw else 1
+            tile = 2 if tiles64 >= self.t64 and not tbw else 1
         tile |= 0 if self.x6 else TILE_EXACT
         _lib.check(self.lib.tdmpc_lg_gemm(arr, len(jobs), tile, self._stream()), "tdmpc_lg_gemm")
 
@@ -584,8 +581,8 @@ class Engine:
             slots[name] = _p(buf)
             jobs.append(dict(segs=segs, m=o, n=i + 1, c=_p(buf), ldc=i + 1, splits=s, slice=o * (i + 1)))
         # 32 x 32 tiles, K (the rows) split 4 ways: 2-3x faster than 64 x 64 tiles for these narrow-N / long-K
-        # products on MI355X (tools/lg_gemm_bench.py --dw: 512 x 122 x 2560 12 vs 38 us); LDS-staged as the rest
-        self.gemm(jobs, tile=self.lds if self.lds in (3, 4) and not self.x6 else 1)
+        # products on MI355X (tools/lg_gemm_bench.py --dw: 512 x 122 x 2560 12 vs 38 us)
+        self.gemm(jobs, tile=1)
         return slots
 
     def _optimise(self, opt, src, g_lo, norm_out):

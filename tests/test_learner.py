@@ -456,79 +456,3 @@ def test_gpu_conv_kernels_match_torch(layer):
     if layer > 0:
         close(dx, dx_ref, "data gradient")
 
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(512, 512, 512, 0), (512, 512, 121, 0), (512, 100, 512, 1), (70, 45, 300, 1),
-                                   (2560, 21, 512, 0)])
-def test_gpu_lg_gemm_lds_tiles(shape):
-    """tdmpc_lg_gemm's LDS-staged tiles (3: one K chunk's loads ahead, 4: four) on the learner's forward / data-gradient
-    shapes (bmode 0: B = a Linear weight [n][k], 1: its transpose [k][n]), plus a ragged one and a two-segment job,
-    exact f32 products: within 1e-5 of each output's largest |sum| of the float64 product, tiles 3 and 4 bitwise
-    equal (the same chunks in the same order), and tile 1 within the same tolerance."""
-    import ctypes as C
-    from tdmpc_amd import _lib
-    L = _lib.lib()
-    m, n, k, bmode = shape
-    g = torch.Generator().manual_seed(m + n + k)
-    A = torch.randn(m, k, generator=g, dtype=torch.float64)
-    A2 = torch.randn(m, 37, generator=g, dtype=torch.float64)
-    Bw = torch.randn(n, k, generator=g, dtype=torch.float64)
-    B2 = torch.randn(n, 37, generator=g, dtype=torch.float64)
-    ref = A @ Bw.T + A2 @ B2.T
-    scale = (A.abs() @ Bw.abs().T + A2.abs() @ B2.abs().T).max()
-    dev = "cuda"
-    Ad, A2d = A.float().contiguous().to(dev), A2.float().contiguous().to(dev)
-    Bd = (Bw if bmode == 0 else Bw.T).float().contiguous().to(dev)
-    B2d = (B2 if bmode == 0 else B2.T).float().contiguous().to(dev)
-    outs = {}
-    for tile in (1, 3, 4):
-        Cm = torch.full((m, n), float("nan"), device=dev)
-        arr = (_lib.LgJob * 1)()
-        J = arr[0]
-        for s, (a, b, kk) in enumerate([(Ad, Bd, k), (A2d, B2d, 37)]):
-            J.seg[s].a, J.seg[s].b, J.seg[s].lda = a.data_ptr(), b.data_ptr(), kk
-            J.seg[s].ldb = kk if bmode == 0 else n
-            J.seg[s].k, J.seg[s].amode, J.seg[s].bmode, J.seg[s].ones_col = kk, 0, bmode, -1
-        J.nseg, J.m, J.n, J.epi, J.c, J.ldc, J.splits, J.slice = 2, m, n, 0, Cm.data_ptr(), n, 1, m * n
-        _lib.check(L.tdmpc_lg_gemm(arr, 1, tile | 0x100, C.c_void_p(torch.cuda.current_stream().cuda_stream)),
-                   "lg_gemm")
-        torch.cuda.synchronize()
-        outs[tile] = Cm.cpu().double()
-        assert ((outs[tile] - ref).abs().max() / scale) < 1e-5, (tile, float((outs[tile] - ref).abs().max() / scale))
-    assert torch.equal(outs[3], outs[4])
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(512, 122, 2560, 4), (100, 513, 2560, 4), (21, 513, 777, 3), (64, 40, 100, 1)])
-def test_gpu_lg_gemm_lds_weight_gradient(shape):
-    """The weight-gradient form on the LDS-staged tiles: dW = dY^T X with the bias gradient as a column of ones
-    (A = dY read transposed, amode 1; B = X read transposed, bmode 1; ones column n - 1), K = the rows split `splits`
-    ways into slices that are summed here: tiles 1, 3, 4 within 1e-5 of each output's largest |sum| of the float64
-    product, tiles 3 and 4 bitwise equal."""
-    import ctypes as C
-    from tdmpc_amd import _lib
-    L = _lib.lib()
-    o, n1, R, splits = shape
-    i = n1 - 1
-    g = torch.Generator().manual_seed(o + n1 + R)
-    dY = torch.randn(R, o, generator=g, dtype=torch.float64)
-    X = torch.randn(R, i, generator=g, dtype=torch.float64)
-    ref = torch.cat([dY.T @ X, dY.sum(0)[:, None]], 1)
-    scale = torch.cat([dY.abs().T @ X.abs(), dY.abs().sum(0)[:, None]], 1).max()
-    dev = "cuda"
-    dYd, Xd = dY.float().contiguous().to(dev), X.float().contiguous().to(dev)
-    outs = {}
-    for tile in (1, 3, 4):
-        Cm = torch.full((splits, o, n1), float("nan"), device=dev)
-        arr = (_lib.LgJob * 1)()
-        J = arr[0]
-        J.seg[0].a, J.seg[0].b, J.seg[0].lda, J.seg[0].ldb = dYd.data_ptr(), Xd.data_ptr(), o, i
-        J.seg[0].k, J.seg[0].amode, J.seg[0].bmode, J.seg[0].ones_col = R, 1, 1, i
-        J.nseg, J.m, J.n, J.epi, J.c, J.ldc, J.splits, J.slice = 1, o, n1, 0, Cm.data_ptr(), n1, splits, o * n1
-        _lib.check(L.tdmpc_lg_gemm(arr, 1, tile | 0x100, C.c_void_p(torch.cuda.current_stream().cuda_stream)),
-                   "lg_gemm")
-        torch.cuda.synchronize()
-        outs[tile] = Cm.cpu().double()
-        got = outs[tile].sum(0)
-        assert ((got - ref).abs().max() / scale) < 1e-5, (tile, float((got - ref).abs().max() / scale))
-    assert torch.equal(outs[3], outs[4])
