@@ -448,7 +448,7 @@ class _FixedBatch:
         self.prio.copy_(p)
 
 
-def pixel_learner_bench(dev, reps=10):
+def pixel_learner_bench(dev, reps=10, modes=None):
     """The pixel learner (quadruped-run pixels: 9 x 84 x 84 frame stacks, conv encoder, batch 512, horizon 5;
     tdmpc.py:192-245 with RandomShiftsAug and the conv stack, helper.py:119-133, 250-283) on the learner engine
     (learner_conv.hip's conv kernels, HIP-graph replay) against the same update through autograd (PyTorch conv =
@@ -464,6 +464,8 @@ def pixel_learner_bench(dev, reps=10):
          torch.arange(B, device=dev), torch.ones(B, device=dev))
     out = {"config": f"{cfg.task} pixels: batch {B}, horizon {H}, frames {shape}, latent {cfg.latent_dim}"}
     for mode, engine in (("engine_graph", "1"), ("autograd_miopen", "0")):
+        if modes is not None and mode.split("_")[0] not in modes:
+            continue
         os.environ["TDMPC_LEARNER_ENGINE"] = engine
         try:
             agent = TDMPC(cfg)
@@ -483,8 +485,9 @@ def pixel_learner_bench(dev, reps=10):
             del agent
         finally:
             os.environ.pop("TDMPC_LEARNER_ENGINE", None)
-    out["engine_speedup_vs_autograd"] = round(out["autograd_miopen"]["ms_per_update"] /
-                                              out["engine_graph"]["ms_per_update"], 2)
+    if "autograd_miopen" in out and "engine_graph" in out:
+        out["engine_speedup_vs_autograd"] = round(out["autograd_miopen"]["ms_per_update"] /
+                                                  out["engine_graph"]["ms_per_update"], 2)
     return out
 
 
