@@ -42,6 +42,10 @@ int tdmpc_loss_backward(const tdmpc_loss_args* a, const float* rows, const float
  * shift: float [n][2] integers in [0, 2 pad] (the reference's torch.randint draw, x then y). */
 int tdmpc_random_shift(const float* x, const float* shift, int32_t n, int32_t c, int32_t h, int32_t w, int32_t pad,
                        float* out, void* stream);
+/* The same with the output divided by div (> 0; 0 = no division), rounded as helper.enc's NormalizeImg x / 255: the
+ * learner engine augments straight into normalised frames for its conv stack (tdmpc_lg_conv_* with in_div = 0). */
+int tdmpc_random_shift_scaled(const float* x, const float* shift, int32_t n, int32_t c, int32_t h, int32_t w,
+                              int32_t pad, float div, float* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * The learner engine: TDMPC.update / update_pi / _td_target (tdmpc.py:165-245) as explicit forward and backward

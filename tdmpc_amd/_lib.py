@@ -23,7 +23,7 @@ EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc
             "tdmpc_replay_workspace_bytes", "tdmpc_replay_add_priorities", "tdmpc_replay_update_priorities",
             "tdmpc_replay_sample",
             # include/tdmpc_learner.h
-            "tdmpc_loss_forward", "tdmpc_loss_backward", "tdmpc_random_shift",
+            "tdmpc_loss_forward", "tdmpc_loss_backward", "tdmpc_random_shift", "tdmpc_random_shift_scaled",
             "tdmpc_lg_gemm", "tdmpc_lg_rows_fwd", "tdmpc_lg_rows_bwd", "tdmpc_lg_pi_loss", "tdmpc_lg_finalize",
             "tdmpc_lg_adam", "tdmpc_lg_lerp", "tdmpc_lg_act", "tdmpc_lg_conv_fwd", "tdmpc_lg_conv_bwd_data",
             "tdmpc_lg_conv_bwd_weight")
@@ -160,6 +160,7 @@ def lib():
     L.tdmpc_loss_forward.argtypes = [C.POINTER(LossArgs), vp, vp, vp]
     L.tdmpc_loss_backward.argtypes = [C.POINTER(LossArgs), vp, vp, vp, vp, vp, vp, vp, vp]
     L.tdmpc_random_shift.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp]
+    L.tdmpc_random_shift_scaled.argtypes = [vp, vp, i32, i32, i32, i32, i32, C.c_float, vp, vp]
     L.tdmpc_lg_gemm.argtypes = [C.POINTER(LgJob), i32, i32, vp]
     L.tdmpc_lg_rows_fwd.argtypes = [C.POINTER(LgRows), vp]
     L.tdmpc_lg_rows_bwd.argtypes = [C.POINTER(LgRows), i32, vp]

@@ -35,7 +35,7 @@ namespace {
 #define DEVI __device__ __forceinline__
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr unsigned CV_OOB = 0x7ffffff0u;   // buffer offsets >= this read 0
-constexpr int CV_D = 8;                     // MFMA steps of operand loads in flight
+constexpr int CV_D = 16;                    // MFMA steps of operand loads in flight
 
 int cv_bad(const char* m) {
     tdmpc_internal::set_error(m);

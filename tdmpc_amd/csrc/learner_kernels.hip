@@ -137,8 +137,10 @@ bool args_ok(const tdmpc_loss_args* a) {
 // (i, j) of stacked image k is the padded image at (i + sy_k, j + sx_k) = the input at
 // (clamp(i + sy_k - pad), clamp(j + sx_k - pad)). One thread per output pixel, a row per 64 consecutive lanes
 // (coalesced, HBM-bound: 4 B read + 4 B written per pixel). shift: the reference's own draw, float [n][2] (x, y).
+// div > 0: the output is x / div, rounded as helper.enc's NormalizeImg rounds it (the learner engine's conv stack
+// then reads normalised frames: the division leaves its inner loops).
 __global__ void __launch_bounds__(256) random_shift_kernel(const float* x, const float* shift, int C, int h, int w,
-                                                           int pad, float* out) {
+                                                           int pad, float div, float* out) {
     const int k = blockIdx.y;                        // stacked image
     const int sx = (int)shift[2 * k], sy = (int)shift[2 * k + 1];
     const size_t plane = (size_t)h * w;
@@ -146,7 +148,8 @@ __global__ void __launch_bounds__(256) random_shift_kernel(const float* x, const
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
         const int c = e / (h * w), r = e % (h * w), i = r / w, j = r % w;
         const int si = min(max(i + sy - pad, 0), h - 1), sj = min(max(j + sx - pad, 0), w - 1);
-        out[(size_t)k * C * plane + e] = x[(size_t)k * C * plane + c * plane + (size_t)si * w + sj];
+        const float v = x[(size_t)k * C * plane + c * plane + (size_t)si * w + sj];
+        out[(size_t)k * C * plane + e] = div > 0.f ? __fdiv_rn(v, div) : v;
     }
 }
 
@@ -156,11 +159,16 @@ extern "C" {
 
 int tdmpc_random_shift(const float* x, const float* shift, int32_t n, int32_t c, int32_t h, int32_t w, int32_t pad,
                        float* out, void* stream) {
+    return tdmpc_random_shift_scaled(x, shift, n, c, h, w, pad, 0.f, out, stream);
+}
+
+int tdmpc_random_shift_scaled(const float* x, const float* shift, int32_t n, int32_t c, int32_t h, int32_t w,
+                              int32_t pad, float div, float* out, void* stream) {
     if (!x || !shift || !out) return TDMPC_E_NULL;
     if (n <= 0 || c <= 0 || h <= 0 || w <= 0 || pad < 0 || (long)c * h * w >= (1L << 31)) return TDMPC_E_DIMS;
     const int per = c * h * w;
     hipLaunchKernelGGL(random_shift_kernel, dim3(std::min((per + 255) / 256, 64), n), dim3(256), 0,
-                       (hipStream_t)stream, x, shift, c, h, w, pad, out);
+                       (hipStream_t)stream, x, shift, c, h, w, pad, div, out);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         tdmpc_internal::set_error(hipGetErrorString(e));

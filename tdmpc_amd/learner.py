@@ -57,8 +57,9 @@ class RandomShiftsAug(torch.nn.Module):
         super().__init__()
         self.pad = int(cfg.img_size / 21) if cfg.modality == "pixels" else None
 
-    def forward(self, x, shift=None):
-        """shift: optional explicit [n, 2] (x, y) integer shifts instead of the draw (parity tests)."""
+    def forward(self, x, shift=None, div=0.0):
+        """shift: optional explicit [n, 2] (x, y) integer shifts instead of the draw (parity tests). div > 0: the
+        frames come back divided by div (NormalizeImg's x / 255 folded into the gather; the learner engine)."""
         if not self.pad:
             return x
         from . import _lib
@@ -75,9 +76,9 @@ class RandomShiftsAug(torch.nn.Module):
         x = x.contiguous()
         out = torch.empty_like(x)
         L = _lib.lib()
-        _lib.check(L.tdmpc_random_shift(C.c_void_p(x.data_ptr()), C.c_void_p(shift.data_ptr()), n, c, hh, ww,
-                                        self.pad, C.c_void_p(out.data_ptr()),
-                                        C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)),
+        _lib.check(L.tdmpc_random_shift_scaled(C.c_void_p(x.data_ptr()), C.c_void_p(shift.data_ptr()), n, c, hh, ww,
+                                               self.pad, float(div), C.c_void_p(out.data_ptr()),
+                                               C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)),
                    "tdmpc_random_shift")
         return out.reshape(shape)
 

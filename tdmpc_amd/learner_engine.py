@@ -266,8 +266,8 @@ class Engine:
             _lib.check(self.lib.tdmpc_lg_rows_fwd(C.byref(a), self._stream()), "tdmpc_lg_rows_fwd")
 
     def conv_stack(self, x, n, ys, targets=(False,)):
-        """helper.enc's conv stack (NormalizeImg, 4 x Conv2d + ReLU; helper.py:119-133) on n frame stacks x [n][C0][S][S]
-        (0..255) for one or two weight sets (targets[q]: set q is the target encoder's) -> ReLU outputs ys[q][layer].
+        """helper.enc's conv stack (4 x Conv2d + ReLU after NormalizeImg; helper.py:119-133) on n normalised frame
+        stacks x [n][C0][S][S] (x / 255: the augmentation divides) for one or two weight sets (targets[q]: set q is the target encoder's) -> ReLU outputs ys[q][layer].
         The first layer runs both sets in one launch (same input); later layers read their own set's output."""
         a = _lib.LgConv()
         st = self._stream()
@@ -275,7 +275,7 @@ class Engine:
             for g in ([list(range(len(targets)))] if i == 0 else [[q] for q in range(len(targets))]):
                 a.x = _p(x) if i == 0 else _p(ys[g[0]][i - 1])
                 a.nprob, a.n, a.cin, a.hin, a.k = len(g), n, self.C0 if i == 0 else 32, self.hw[i], k
-                a.in_div = 255.0 if i == 0 else 0.0
+                a.in_div = 0.0
                 for j, q in enumerate(g):
                     a.w[j] = self.w(CONV_NAMES[i] + ".weight", targets[q])
                     a.b[j] = self.w(CONV_NAMES[i] + ".bias", targets[q])
@@ -290,12 +290,11 @@ class Engine:
             k, hin = CONV_K[i], self.hw[i]
             cin = self.C0 if i == 0 else 32
             K = cin * k * k
-            groups = -(-((K + 1 + 31) // 32) // 4)   # workgroup columns of the weight-gradient grid
-            ips = max(1, -(-B * groups // 256))          # images per slice: ~256 workgroups
+            ips = 1                                      # one image per slice: B x ceil(tiles / 4) workgroups
             nsl = -(-B // ips)
             part = self.slot(b, f"conv{i}", nsl * 32 * (K + 1))
             xin = x if i == 0 else b["ym"][i - 1]
-            _lib.check(self.lib.tdmpc_lg_conv_bwd_weight(_p(b["dy"][i]), _p(xin), 255.0 if i == 0 else 0.0, _p(part),
+            _lib.check(self.lib.tdmpc_lg_conv_bwd_weight(_p(b["dy"][i]), _p(xin), 0.0, _p(part),
                                                           B, cin, hin, k, ips, st), "tdmpc_lg_conv_bwd_weight")
             out[CONV_NAMES[i]] = (_p(part), K, nsl)
             if i > 0:   # the gradient of the layer below's ReLU output, masked by its ReLU
@@ -407,9 +406,10 @@ class Engine:
         if self.pix:
             # RandomShiftsAug (helper.py:250-283) on the H next-observation stacks, then on obs (tdmpc.py:200, 207), as
             # the reference's update draws them; the frames may come as uint8 from the replay buffer
+            # (NormalizeImg's x / 255 folded into the shift's gather: the conv stack reads normalised frames)
             nx = next_obses[:H].reshape(H * B, *next_obses.shape[2:])
-            nxo_t = self.agent.aug(nx if nx.dtype == torch.float32 else nx.float()).contiguous()
-            obs = self.agent.aug(obs if obs.dtype == torch.float32 else obs.float()).contiguous()
+            nxo_t = self.agent.aug(nx if nx.dtype == torch.float32 else nx.float(), div=255.0).contiguous()
+            obs = self.agent.aug(obs if obs.dtype == torch.float32 else obs.float(), div=255.0).contiguous()
         else:
             obs = obs.contiguous()
             nxo_t = next_obses[:H].contiguous()
