@@ -19,6 +19,7 @@
 
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -102,6 +103,114 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const tdmpc_lg_conv a, in
     for (int e = 0; e < 16; ++e) {
         const int pix = p0 + (e & 3) + 8 * (e >> 2) + 4 * h;
         if (pix < HoHo) y[pix] = relu_f(acc[e] + bias);
+    }
+}
+
+// The same forward for the large layers (ho^2 >= 256: the first two), input staged in LDS: a workgroup = 8 waves x
+// 32 output pixels = the 256-pixel block [P0, P0 + 256) of one image, for both weight sets of the launch (NP). The
+// block's output rows need input rows [2 oy0, 2 oy1 + k): a contiguous run of SR rows per channel, copied in chunks of
+// CC channels (<= 32 KB of slab, <= 208 k-values of weights) with coalesced loads; the next chunk's loads are in
+// flight in registers while this chunk's MFMAs run on LDS operands (one ds_read of the slab per MFMA step and set,
+// no global-latency chain). The division by in_div (NormalizeImg) happens once per staged element, the same rounding.
+// Sums: chunk by chunk in k order, every chunk but the last an even number of k-values -- the direct kernel's MFMA
+// pairs and order, so both give the same bits (tests/test_learner.py). TDMPC_CONV_DIRECT=1: the direct kernel (A/B).
+constexpr int CVS_SLAB = 8192, CVS_KC = 208;   // slab floats, k-values per chunk
+
+template <int NP>
+__global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv a, int ho, int CC, int SRM) {
+    extern __shared__ float cv_sm[];
+    const int img = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int k = a.k, kk = k * k, H = a.hin, HoHo = ho * ho, cin = a.cin;
+    const int P0 = blockIdx.x * 256;
+    const int oy0 = P0 / ho, oy1 = min(ho - 1, (P0 + 255) / ho);
+    const int SR = 2 * (oy1 - oy0) + k, plane = SR * H;
+    const int KCM = (CC * kk + 1) & ~1;
+    float* slab = cv_sm;                                   // [CC][SR][H]
+    float* sW = slab + (size_t)CC * SRM * H;               // [NP][KCM][32]
+    int* koff = (int*)(sW + (size_t)NP * KCM * 32);        // [KCM]
+    const __amdgpu_buffer_rsrc_t rx = cv_rsrc(a.x + ((size_t)img * cin * H + 2 * oy0) * H);
+    __amdgpu_buffer_rsrc_t rw[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) rw[q] = cv_rsrc(a.w[q]);
+    const float div = a.in_div;
+    const int nchunk = (cin + CC - 1) / CC;
+    const bool live = P0 + wave * 32 < HoHo;   // (wave-uniform)
+    const int pp = min(P0 + wave * 32 + r, HoHo - 1);
+    const int pixbase = 2 * (pp / ho - oy0) * H + 2 * (pp % ho);
+    constexpr int NS = CVS_SLAB / 512, NW = (CVS_KC * 32 + 511) / 512;
+    float sv[NS], wv[NP][NW];
+    auto fetch = [&](int c) __attribute__((always_inline)) {
+        const int c0 = c * CC, cc = min(CC, cin - c0), ns = cc * plane, nk = cc * kk;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const int e = tid + 512 * i, ci = e / plane;
+            sv[i] = cv_ld(rx, (unsigned)((c0 + ci) * H * H + e - ci * plane), e < ns);
+        }
+#pragma unroll
+        for (int q = 0; q < NP; ++q)
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const int e = tid + 512 * i, kl = e >> 5, co = e & 31;
+                wv[q][i] = cv_ld(rw[q], (unsigned)(co * cin * kk + c0 * kk + kl), kl < nk);
+            }
+    };
+    auto stash = [&](int c) __attribute__((always_inline)) {
+        const int c0 = c * CC, cc = min(CC, cin - c0), ns = cc * plane, nk = cc * kk;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const int e = tid + 512 * i;
+            if (e < ns) slab[e] = div > 0.f ? __fdiv_rn(sv[i], div) : sv[i];
+        }
+#pragma unroll
+        for (int q = 0; q < NP; ++q)
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const int e = tid + 512 * i;
+                if ((e >> 5) < KCM) sW[(q * KCM) * 32 + e] = wv[q][i];
+            }
+        for (int j = tid; j < KCM; j += 512) {
+            const int ci = j / kk, t = j % kk;
+            koff[j] = j < nk ? ci * plane + (t / k) * H + t % k : 0;
+        }
+    };
+    floatx16 acc[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
+    fetch(0);
+    stash(0);
+    __syncthreads();
+    for (int c = 0; c < nchunk; ++c) {
+        if (c + 1 < nchunk) fetch(c + 1);
+        if (live) {
+            const int nst = (min(CC, cin - c * CC) * kk + 1) / 2;
+#pragma unroll 4
+            for (int s = 0; s < nst; ++s) {
+                const float av = slab[pixbase + koff[2 * s + h]];
+#pragma unroll
+                for (int q = 0; q < NP; ++q)
+                    acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, sW[(q * KCM + 2 * s + h) * 32 + r], acc[q], 0, 0, 0);
+            }
+        }
+        if (c + 1 < nchunk) {
+            __syncthreads();
+            stash(c + 1);
+            __syncthreads();
+        }
+    }
+    if (!live) return;
+    const int p0 = P0 + wave * 32;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+        const float bias = a.b[q][r];
+        float* y = a.y[q] + ((size_t)img * 32 + r) * HoHo;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int pix = p0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            if (pix < HoHo) y[pix] = relu_f(acc[q][e] + bias);
+        }
     }
 }
 
@@ -231,15 +340,35 @@ int tdmpc_lg_conv_fwd(const tdmpc_lg_conv* a, void* stream) {
         return cv_bad("tdmpc_lg_conv_fwd: nprob");
     if (a->n <= 0 || a->cin <= 0 || a->k <= 0 || a->hin < a->k) return cv_bad("tdmpc_lg_conv_fwd: shape");
     const int ho = (a->hin - a->k) / 2 + 1, K = a->cin * a->k * a->k, K2 = (K + 1) & ~1;
-    const size_t lds = (size_t)K2 * 32 * 4 + (size_t)K2 * 4;
-    if (lds > 160 * 1024) return cv_bad("tdmpc_lg_conv_fwd: cin k k too large");
     static bool attr = false;
     if (!attr) {
         if (hipFuncSetAttribute((const void*)conv_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
-            hipSuccess)
+                hipSuccess ||
+            hipFuncSetAttribute((const void*)conv_fwd_slab_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess ||
+            hipFuncSetAttribute((const void*)conv_fwd_slab_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess)
             return TDMPC_E_HIP;
         attr = true;
     }
+    const int kk = a->k * a->k, H = a->hin;
+    // the LDS-staged form for the large layers: slab rows of a 256-pixel block, channels per chunk within both caps
+    const int SRM = std::min(H, 2 * (std::min(ho, 255 / ho + 2) - 1) + a->k);
+    int CC = std::min(a->cin, std::min(CVS_SLAB / (SRM * H), CVS_KC / kk));
+    if ((kk & 1) && CC < a->cin) CC &= ~1;   // (even k-values per chunk but the last: the direct kernel's MFMA pairs)
+    if (ho * ho >= 256 && CC >= 1 && getenv("TDMPC_CONV_DIRECT") == nullptr) {
+        const int KCM = (CC * kk + 1) & ~1;
+        const size_t lds = ((size_t)CC * SRM * H + (size_t)a->nprob * KCM * 32 + KCM) * 4;
+        if (a->nprob == 2)
+            hipLaunchKernelGGL(conv_fwd_slab_kernel<2>, dim3((ho * ho + 255) / 256, a->n), dim3(512), lds,
+                               (hipStream_t)stream, *a, ho, CC, SRM);
+        else
+            hipLaunchKernelGGL(conv_fwd_slab_kernel<1>, dim3((ho * ho + 255) / 256, a->n), dim3(512), lds,
+                               (hipStream_t)stream, *a, ho, CC, SRM);
+        return hipGetLastError() == hipSuccess ? 0 : TDMPC_E_HIP;
+    }
+    const size_t lds = (size_t)K2 * 32 * 4 + (size_t)K2 * 4;
+    if (lds > 160 * 1024) return cv_bad("tdmpc_lg_conv_fwd: cin k k too large");
     hipLaunchKernelGGL(conv_fwd_kernel, dim3((ho * ho + 127) / 128, a->n, a->nprob), dim3(256), lds,
                        (hipStream_t)stream, *a, ho, K2);
     return hipGetLastError() == hipSuccess ? 0 : TDMPC_E_HIP;

@@ -317,9 +317,16 @@ def test_gpu_pixel_update_matches_oracle():
     buf = _DeviceBatchBuffer(b)
     rec, aug = [], agent.aug
 
-    def recording_aug(x):
-        y = aug(x)
-        rec.append(y.detach().cpu())
+    def recording_aug(x, div=0.0):
+        # (the engine augments straight into normalised frames, div = 255: the integer frames are recovered for the
+        # oracle, which normalises them itself -- and torch's own x / 255 of them must be the kernel's output)
+        y = aug(x, div=div)
+        r = y.detach().cpu()
+        if div:
+            raw = torch.round(r * div)
+            assert torch.equal(raw / div, r)
+            r = raw
+        rec.append(r)
         return y
 
     agent.aug = recording_aug
@@ -432,6 +439,17 @@ def test_gpu_conv_kernels_match_torch(layer):
     a.w[0], a.b[0], a.y[0] = wd.data_ptr(), bd.data_ptr(), y.data_ptr()
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     _lib.check(L.tdmpc_lg_conv_fwd(C.byref(a), st), "conv_fwd")
+    # the large layers run the LDS-staged forward; the direct kernel (TDMPC_CONV_DIRECT) must give the same bits
+    y_direct = torch.full_like(y, float("nan"))
+    a.y[0] = y_direct.data_ptr()
+    os.environ["TDMPC_CONV_DIRECT"] = "1"
+    try:
+        _lib.check(L.tdmpc_lg_conv_fwd(C.byref(a), st), "conv_fwd direct")
+    finally:
+        del os.environ["TDMPC_CONV_DIRECT"]
+    a.y[0] = y.data_ptr()
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_direct), float((y - y_direct).abs().max())
     ips = 4
     nsl = -(-n // ips)
     K = cin * k * k
