@@ -128,7 +128,6 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv 
     const int KCM = (CC * kk + 1) & ~1;
     float* slab = cv_sm;                                   // [CC][SR][H]
     float* sW = slab + (size_t)CC * SRM * H;               // [NP][KCM][32]
-    int* koff = (int*)(sW + (size_t)NP * KCM * 32);        // [KCM]
     const __amdgpu_buffer_rsrc_t rx = cv_rsrc(a.x + ((size_t)img * cin * H + 2 * oy0) * H);
     __amdgpu_buffer_rsrc_t rw[NP];
 #pragma unroll
@@ -169,10 +168,6 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv 
                 const int e = tid + 512 * i;
                 if ((e >> 5) < KCM) sW[(q * KCM) * 32 + e] = wv[q][i];
             }
-        for (int j = tid; j < KCM; j += 512) {
-            const int ci = j / kk, t = j % kk;
-            koff[j] = j < nk ? ci * plane + (t / k) * H + t % k : 0;
-        }
     };
     floatx16 acc[NP];
 #pragma unroll
@@ -185,13 +180,25 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv 
     for (int c = 0; c < nchunk; ++c) {
         if (c + 1 < nchunk) fetch(c + 1);
         if (live) {
-            const int nst = (min(CC, cin - c * CC) * kk + 1) / 2;
+            // k-value j = 2 s + h of the chunk is tap (ci, ky, kx) at slab offset ci plane + ky H + kx from the pixel's
+            // base, advanced incrementally (no index table: its LDS read would sit in front of every slab read)
+            const int nk = min(CC, cin - c * CC) * kk, nst = (nk + 1) / 2;
+            int kx = h, ky = 0, off = pixbase + h;
 #pragma unroll 4
             for (int s = 0; s < nst; ++s) {
-                const float av = slab[pixbase + koff[2 * s + h]];
+                float av = slab[off];
+                if (2 * s + h >= nk) av = 0.f;   // (the odd chunk's pad: whatever lies past the slab, times 0)
 #pragma unroll
                 for (int q = 0; q < NP; ++q)
                     acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, sW[(q * KCM + 2 * s + h) * 32 + r], acc[q], 0, 0, 0);
+                kx += 2;
+                const bool wx = kx >= k;
+                kx -= wx ? k : 0;
+                ky += wx ? 1 : 0;
+                off += wx ? 2 + H - k : 2;
+                const bool wy = ky >= k;
+                ky -= wy ? k : 0;
+                off += wy ? plane - k * H : 0;
             }
         }
         if (c + 1 < nchunk) {
@@ -358,7 +365,7 @@ int tdmpc_lg_conv_fwd(const tdmpc_lg_conv* a, void* stream) {
     if ((kk & 1) && CC < a->cin) CC &= ~1;   // (even k-values per chunk but the last: the direct kernel's MFMA pairs)
     if (ho * ho >= 256 && CC >= 1 && getenv("TDMPC_CONV_DIRECT") == nullptr) {
         const int KCM = (CC * kk + 1) & ~1;
-        const size_t lds = ((size_t)CC * SRM * H + (size_t)a->nprob * KCM * 32 + KCM) * 4;
+        const size_t lds = ((size_t)CC * SRM * H + (size_t)a->nprob * KCM * 32) * 4;
         if (a->nprob == 2)
             hipLaunchKernelGGL(conv_fwd_slab_kernel<2>, dim3((ho * ho + 255) / 256, a->n), dim3(512), lds,
                                (hipStream_t)stream, *a, ho, CC, SRM);
