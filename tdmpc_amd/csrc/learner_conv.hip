@@ -337,6 +337,85 @@ __global__ void __launch_bounds__(256) conv_bwd_weight_kernel(const float* dy, c
     for (int e = 0; e < 16; ++e) o[(size_t)((e & 3) + 8 * (e >> 2) + 4 * h) * K1] = acc[e];
 }
 
+// The weight gradient with its operands staged in LDS: a workgroup = 8 waves over the images of one slice, the
+// image's output pixels in blocks of PB (dy [32][PB] and the block's input slab [cin][SR][H] copied with coalesced
+// loads), wave w owning the 32-column tiles w + 8 u (u < TPW: one dy read feeds TPW MFMAs). Pixel pairs and their
+// order are the direct kernel's (PB even), so both give the same bits; TDMPC_CONV_DIRECT=1 runs the direct one.
+template <int TPW>
+__global__ void __launch_bounds__(512) conv_bwd_weight_slab_kernel(const float* dy, const float* x, float div,
+                                                                   float* part, int n, int cin, int H, int k, int ho,
+                                                                   int ips, int PB, int SRM) {
+    extern __shared__ float cv_sm[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int kk = k * k, K = cin * kk, K1 = K + 1, HoHo = ho * ho;
+    const int slice = blockIdx.x, n0 = slice * ips, n1 = min(n, n0 + ips);
+    const int PBP = PB + 1;
+    float* dyl = cv_sm;                              // [32][PB + 1]
+    float* slab = cv_sm + 32 * PBP;                  // [cin][SR][H]
+    int tapoff[TPW];
+    bool tap[TPW], one[TPW];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        const int col = (wave + 8 * u) * 32 + r;
+        const int ci = col / kk, rem = col % kk;
+        tap[u] = col < K;
+        one[u] = col == K;
+        tapoff[u] = tap[u] ? ci * SRM * H + (rem / k) * H + rem % k : 0;   // (plane stride SRM H: see the staging)
+    }
+    floatx16 acc[TPW];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[u][e] = 0.f;
+    for (int img = n0; img < n1; ++img) {
+        const float* dyi = dy + (size_t)img * 32 * HoHo;
+        const float* xi = x + (size_t)img * cin * H * H;
+        for (int P0 = 0; P0 < HoHo; P0 += PB) {
+            const int npx = min(PB, HoHo - P0);
+            const int oy0 = P0 / ho, oy1 = (P0 + npx - 1) / ho;
+            const int SR = 2 * (oy1 - oy0) + k, plane = SR * H;
+            __syncthreads();   // (the previous block's reads are done)
+            for (int e = tid; e < 32 * npx; e += 512) {
+                const int co = e / npx, p = e - co * npx;
+                dyl[co * PBP + p] = dyi[(size_t)co * HoHo + P0 + p];
+            }
+            for (int e = tid; e < cin * plane; e += 512) {
+                const int ci = e / plane, o = e - ci * plane;
+                const float v = xi[(size_t)ci * H * H + (size_t)(2 * oy0) * H + o];
+                slab[ci * SRM * H + o] = div > 0.f ? __fdiv_rn(v, div) : v;
+            }
+            __syncthreads();
+            const int nst = (npx + 1) / 2;
+            int P = P0 + h, ox = P % ho;
+            int po = 2 * (P / ho - oy0) * H + 2 * ox;
+#pragma unroll 2
+            for (int s = 0; s < nst; ++s) {
+                const bool pv = 2 * s + h < npx;
+                const float av = pv ? dyl[r * PBP + 2 * s + h] : 0.f;
+#pragma unroll
+                for (int u = 0; u < TPW; ++u) {
+                    const float xv = slab[(pv && tap[u]) ? tapoff[u] + po : 0];
+                    const float bv = tap[u] ? (pv ? xv : 0.f) : (one[u] && pv ? 1.f : 0.f);
+                    acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[u], 0, 0, 0);
+                }
+                ox += 2;
+                const bool w = ox >= ho;
+                ox -= w ? ho : 0;
+                po += w ? 4 + 2 * H - 2 * ho : 4;
+            }
+        }
+    }
+    // col = lane & 31 (the B column), row = (e & 3) + 8 (e >> 2) + 4 h (the output channel)
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        const int col = (wave + 8 * u) * 32 + r;
+        if (col >= K1) continue;
+        float* o = part + (size_t)slice * 32 * K1 + col;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[(size_t)((e & 3) + 8 * (e >> 2) + 4 * h) * K1] = acc[u][e];
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -407,6 +486,33 @@ int tdmpc_lg_conv_bwd_weight(const float* dy, const float* x, float in_div, floa
     if (n <= 0 || cin <= 0 || k <= 0 || hin < k || img_per_slice <= 0) return cv_bad("tdmpc_lg_conv_bwd_weight: shape");
     const int ho = (hin - k) / 2 + 1, ntile = (cin * k * k + 1 + 31) / 32;
     const int nsl = (n + img_per_slice - 1) / img_per_slice;
+    if (ntile <= 32 && getenv("TDMPC_CONV_DIRECT") == nullptr) {
+        // the largest even pixel block whose input slab fits 64 KB of LDS
+        int PB = 0, SRM = 0;
+        for (int pb = 256; pb >= 2 && !PB; pb /= 2) {
+            const int srm = std::min(hin, 2 * (std::min(ho, (pb - 1) / ho + 2) - 1) + k);
+            if (cin * srm * hin <= 16384) PB = pb, SRM = srm;
+        }
+        if (PB) {
+            static bool attr = false;
+            if (!attr) {
+                if (hipFuncSetAttribute((const void*)conv_bwd_weight_slab_kernel<2>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+                    hipFuncSetAttribute((const void*)conv_bwd_weight_slab_kernel<4>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+                    return TDMPC_E_HIP;
+                attr = true;
+            }
+            const size_t lds = ((size_t)32 * (PB + 1) + (size_t)cin * SRM * hin) * 4;
+            if (ntile <= 16)
+                hipLaunchKernelGGL(conv_bwd_weight_slab_kernel<2>, dim3(nsl), dim3(512), lds, (hipStream_t)stream, dy, x,
+                                   in_div, part, n, cin, hin, k, ho, img_per_slice, PB, SRM);
+            else
+                hipLaunchKernelGGL(conv_bwd_weight_slab_kernel<4>, dim3(nsl), dim3(512), lds, (hipStream_t)stream, dy, x,
+                                   in_div, part, n, cin, hin, k, ho, img_per_slice, PB, SRM);
+            return hipGetLastError() == hipSuccess ? 0 : TDMPC_E_HIP;
+        }
+    }
     hipLaunchKernelGGL(conv_bwd_weight_kernel, dim3((ntile + 3) / 4, nsl), dim3(256), 0, (hipStream_t)stream, dy, x,
                        in_div, part, n, cin, hin, k, ho, img_per_slice);
     return hipGetLastError() == hipSuccess ? 0 : TDMPC_E_HIP;

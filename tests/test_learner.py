@@ -456,6 +456,16 @@ def test_gpu_conv_kernels_match_torch(layer):
     part = torch.zeros(nsl, 32, K + 1, device=dev)
     _lib.check(L.tdmpc_lg_conv_bwd_weight(dyd.data_ptr(), xd.data_ptr(), 255.0 if layer == 0 else 0.0, part.data_ptr(),
                                           n, cin, hin, k, ips, st), "conv_bwd_weight")
+    # (the LDS-staged weight gradient; the direct kernel must give the same bits)
+    part_direct = torch.full_like(part, float("nan"))
+    os.environ["TDMPC_CONV_DIRECT"] = "1"
+    try:
+        _lib.check(L.tdmpc_lg_conv_bwd_weight(dyd.data_ptr(), xd.data_ptr(), 255.0 if layer == 0 else 0.0,
+                                              part_direct.data_ptr(), n, cin, hin, k, ips, st), "conv_bwd_weight direct")
+    finally:
+        del os.environ["TDMPC_CONV_DIRECT"]
+    torch.cuda.synchronize()
+    assert torch.equal(part, part_direct), float((part - part_direct).abs().max())
     if layer > 0:
         dx = torch.zeros(n, cin, hin, hin, device=dev)
         _lib.check(L.tdmpc_lg_conv_bwd_data(dyd.data_ptr(), wd.data_ptr(), xd.data_ptr(), dx.data_ptr(), n, cin, hin, k,
