@@ -116,14 +116,15 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const tdmpc_lg_conv a, in
 // pairs and order, so both give the same bits (tests/test_learner.py). TDMPC_CONV_DIRECT=1: the direct kernel (A/B).
 constexpr int CVS_SLAB = 8192, CVS_KC = 208;   // slab floats, k-values per chunk
 
-template <int NP>
+template <int NP, int TP>
 __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv a, int ho, int CC, int SRM) {
     extern __shared__ float cv_sm[];
     const int img = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     const int k = a.k, kk = k * k, H = a.hin, HoHo = ho * ho, cin = a.cin;
-    const int P0 = blockIdx.x * 256;
-    const int oy0 = P0 / ho, oy1 = min(ho - 1, (P0 + 255) / ho);
+    constexpr int BP = 256 * TP;   // block pixels: 8 waves x TP tiles of 32
+    const int P0 = blockIdx.x * BP;
+    const int oy0 = P0 / ho, oy1 = min(ho - 1, (P0 + BP - 1) / ho);
     const int SR = 2 * (oy1 - oy0) + k, plane = SR * H;
     const int KCM = (CC * kk + 1) & ~1;
     float* slab = cv_sm;                                   // [CC][SR][H]
@@ -134,9 +135,14 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv 
     for (int q = 0; q < NP; ++q) rw[q] = cv_rsrc(a.w[q]);
     const float div = a.in_div;
     const int nchunk = (cin + CC - 1) / CC;
-    const bool live = P0 + wave * 32 < HoHo;   // (wave-uniform)
-    const int pp = min(P0 + wave * 32 + r, HoHo - 1);
-    const int pixbase = 2 * (pp / ho - oy0) * H + 2 * (pp % ho);
+    const int pw0 = P0 + wave * 32 * TP;       // this wave's TP tiles: pixels [pw0, pw0 + 32 TP)
+    const bool live = pw0 < HoHo;              // (wave-uniform)
+    int pixbase[TP];
+#pragma unroll
+    for (int t = 0; t < TP; ++t) {
+        const int pp = min(pw0 + 32 * t + r, HoHo - 1);
+        pixbase[t] = 2 * (pp / ho - oy0) * H + 2 * (pp % ho);
+    }
     constexpr int NS = CVS_SLAB / 512, NW = (CVS_KC * 32 + 511) / 512;
     float sv[NS], wv[NP][NW];
     auto fetch = [&](int c) __attribute__((always_inline)) {
@@ -169,11 +175,13 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv 
                 if ((e >> 5) < KCM) sW[(q * KCM) * 32 + e] = wv[q][i];
             }
     };
-    floatx16 acc[NP];
+    floatx16 acc[NP][TP];
 #pragma unroll
     for (int q = 0; q < NP; ++q)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
+        for (int t = 0; t < TP; ++t)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[q][t][e] = 0.f;
     fetch(0);
     stash(0);
     __syncthreads();
@@ -183,14 +191,22 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv 
             // k-value j = 2 s + h of the chunk is tap (ci, ky, kx) at slab offset ci plane + ky H + kx from the pixel's
             // base, advanced incrementally (no index table: its LDS read would sit in front of every slab read)
             const int nk = min(CC, cin - c * CC) * kk, nst = (nk + 1) / 2;
-            int kx = h, ky = 0, off = pixbase + h;
+            int kx = h, ky = 0, off = h;
 #pragma unroll 4
             for (int s = 0; s < nst; ++s) {
-                float av = slab[off];
-                if (2 * s + h >= nk) av = 0.f;   // (the odd chunk's pad: whatever lies past the slab, times 0)
+                float av[TP];
 #pragma unroll
-                for (int q = 0; q < NP; ++q)
-                    acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, sW[(q * KCM + 2 * s + h) * 32 + r], acc[q], 0, 0, 0);
+                for (int t = 0; t < TP; ++t) {
+                    av[t] = slab[pixbase[t] + off];
+                    if (2 * s + h >= nk) av[t] = 0.f;   // (the odd chunk's pad: whatever lies past the slab, times 0)
+                }
+#pragma unroll
+                for (int q = 0; q < NP; ++q) {
+                    const float bw = sW[(q * KCM + 2 * s + h) * 32 + r];
+#pragma unroll
+                    for (int t = 0; t < TP; ++t)
+                        acc[q][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t], bw, acc[q][t], 0, 0, 0);
+                }
                 kx += 2;
                 const bool wx = kx >= k;
                 kx -= wx ? k : 0;
@@ -208,16 +224,17 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv 
         }
     }
     if (!live) return;
-    const int p0 = P0 + wave * 32;
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
         const float bias = a.b[q][r];
         float* y = a.y[q] + ((size_t)img * 32 + r) * HoHo;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int pix = p0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            if (pix < HoHo) y[pix] = relu_f(acc[q][e] + bias);
-        }
+        for (int t = 0; t < TP; ++t)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int pix = pw0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (pix < HoHo) y[pix] = relu_f(acc[q][t][e] + bias);
+            }
     }
 }
 
@@ -430,27 +447,36 @@ int tdmpc_lg_conv_fwd(const tdmpc_lg_conv* a, void* stream) {
     if (!attr) {
         if (hipFuncSetAttribute((const void*)conv_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
                 hipSuccess ||
-            hipFuncSetAttribute((const void*)conv_fwd_slab_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+            hipFuncSetAttribute((const void*)conv_fwd_slab_kernel<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess ||
-            hipFuncSetAttribute((const void*)conv_fwd_slab_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+            hipFuncSetAttribute((const void*)conv_fwd_slab_kernel<2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess ||
+            hipFuncSetAttribute((const void*)conv_fwd_slab_kernel<1, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess ||
+            hipFuncSetAttribute((const void*)conv_fwd_slab_kernel<2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess)
             return TDMPC_E_HIP;
         attr = true;
     }
     const int kk = a->k * a->k, H = a->hin;
-    // the LDS-staged form for the large layers: slab rows of a 256-pixel block, channels per chunk within both caps
-    const int SRM = std::min(H, 2 * (std::min(ho, 255 / ho + 2) - 1) + a->k);
+    // the LDS-staged form for the large layers: slab rows of a 256 TP-pixel block (TP = 2 tiles per wave where the
+    // image fills the blocks: the first layer), channels per chunk within both caps
+    const int TP = ho * ho >= 1024 ? 2 : 1, BP = 256 * TP;
+    const int SRM = std::min(H, 2 * (std::min(ho, (BP - 1) / ho + 2) - 1) + a->k);
     int CC = std::min(a->cin, std::min(CVS_SLAB / (SRM * H), CVS_KC / kk));
     if ((kk & 1) && CC < a->cin) CC &= ~1;   // (even k-values per chunk but the last: the direct kernel's MFMA pairs)
     if (ho * ho >= 256 && CC >= 1 && getenv("TDMPC_CONV_DIRECT") == nullptr) {
         const int KCM = (CC * kk + 1) & ~1;
         const size_t lds = ((size_t)CC * SRM * H + (size_t)a->nprob * KCM * 32) * 4;
-        if (a->nprob == 2)
-            hipLaunchKernelGGL(conv_fwd_slab_kernel<2>, dim3((ho * ho + 255) / 256, a->n), dim3(512), lds,
-                               (hipStream_t)stream, *a, ho, CC, SRM);
+        const dim3 grid((ho * ho + BP - 1) / BP, a->n);
+        if (a->nprob == 2 && TP == 2)
+            hipLaunchKernelGGL((conv_fwd_slab_kernel<2, 2>), grid, dim3(512), lds, (hipStream_t)stream, *a, ho, CC, SRM);
+        else if (a->nprob == 2)
+            hipLaunchKernelGGL((conv_fwd_slab_kernel<2, 1>), grid, dim3(512), lds, (hipStream_t)stream, *a, ho, CC, SRM);
+        else if (TP == 2)
+            hipLaunchKernelGGL((conv_fwd_slab_kernel<1, 2>), grid, dim3(512), lds, (hipStream_t)stream, *a, ho, CC, SRM);
         else
-            hipLaunchKernelGGL(conv_fwd_slab_kernel<1>, dim3((ho * ho + 255) / 256, a->n), dim3(512), lds,
-                               (hipStream_t)stream, *a, ho, CC, SRM);
+            hipLaunchKernelGGL((conv_fwd_slab_kernel<1, 1>), grid, dim3(512), lds, (hipStream_t)stream, *a, ho, CC, SRM);
         return hipGetLastError() == hipSuccess ? 0 : TDMPC_E_HIP;
     }
     const size_t lds = (size_t)K2 * 32 * 4 + (size_t)K2 * 4;
