@@ -126,9 +126,10 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv 
     const int P0 = blockIdx.x * BP;
     const int oy0 = P0 / ho, oy1 = min(ho - 1, (P0 + BP - 1) / ho);
     const int SR = 2 * (oy1 - oy0) + k, plane = SR * H;
-    const int KCM = (CC * kk + 1) & ~1;
-    float* slab = cv_sm;                                   // [CC][SR][H]
-    float* sW = slab + (size_t)CC * SRM * H;               // [NP][KCM][32]
+    const int KCM = (CC * kk + 1) & ~1, KT = ((KCM / 2) + 3) & ~3;
+    float* slab = cv_sm;                                   // [CC + 1][SR][H] (plane cc: zeros for an odd chunk's pad)
+    float* sW = slab + (((CC + 1) * SRM * H + 3) & ~3);    // [NP][KCM][32] (16-byte aligned: kt's int4 reads)
+    int* kt = (int*)(sW + (size_t)NP * KCM * 32);          // [2][KT]: slab offset of k-value 2 s + h, step s
     const __amdgpu_buffer_rsrc_t rx = cv_rsrc(a.x + ((size_t)img * cin * H + 2 * oy0) * H);
     __amdgpu_buffer_rsrc_t rw[NP];
 #pragma unroll
@@ -167,6 +168,13 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv 
             const int e = tid + 512 * i;
             if (e < ns) slab[e] = div > 0.f ? __fdiv_rn(sv[i], div) : sv[i];
         }
+        if (nk & 1)   // the pad k-value nk reads plane cc at the pixel's base: zeros (times a zero weight)
+            for (int e = tid; e < plane; e += 512) slab[ns + e] = 0.f;
+        for (int e = tid; e < 2 * KT; e += 512) {
+            const int hh = e / KT, st = e - hh * KT, j = 2 * st + hh;
+            const int ci = j / kk, t = j - ci * kk;
+            kt[e] = j < nk ? ci * plane + (t / k) * H + t % k : cc * plane;
+        }
 #pragma unroll
         for (int q = 0; q < NP; ++q)
 #pragma unroll
@@ -188,33 +196,29 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv 
     for (int c = 0; c < nchunk; ++c) {
         if (c + 1 < nchunk) fetch(c + 1);
         if (live) {
-            // k-value j = 2 s + h of the chunk is tap (ci, ky, kx) at slab offset ci plane + ky H + kx from the pixel's
-            // base, advanced incrementally (no index table: its LDS read would sit in front of every slab read)
+            // k-value j = 2 s + h of the chunk is tap (ci, ky, kx) at slab offset kt[h][s] = ci plane + ky H + kx from
+            // the pixel's base: four steps' offsets per 16-byte LDS read, a step's reads then independent of each other
             const int nk = min(CC, cin - c * CC) * kk, nst = (nk + 1) / 2;
-            int kx = h, ky = 0, off = h;
-#pragma unroll 4
-            for (int s = 0; s < nst; ++s) {
-                float av[TP];
+            const int* kth = kt + h * KT;
+            for (int s0 = 0; s0 < nst; s0 += 4) {
+                const int4 o4 = *(const int4*)(kth + s0);
+                const int ov[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
-                for (int t = 0; t < TP; ++t) {
-                    av[t] = slab[pixbase[t] + off];
-                    if (2 * s + h >= nk) av[t] = 0.f;   // (the odd chunk's pad: whatever lies past the slab, times 0)
+                for (int u = 0; u < 4; ++u) {
+                    const int s = s0 + u;
+                    if (s < nst) {
+                        float av[TP];
+#pragma unroll
+                        for (int t = 0; t < TP; ++t) av[t] = slab[pixbase[t] + ov[u]];
+#pragma unroll
+                        for (int q = 0; q < NP; ++q) {
+                            const float bw = sW[(q * KCM + 2 * s + h) * 32 + r];
+#pragma unroll
+                            for (int t = 0; t < TP; ++t)
+                                acc[q][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t], bw, acc[q][t], 0, 0, 0);
+                        }
+                    }
                 }
-#pragma unroll
-                for (int q = 0; q < NP; ++q) {
-                    const float bw = sW[(q * KCM + 2 * s + h) * 32 + r];
-#pragma unroll
-                    for (int t = 0; t < TP; ++t)
-                        acc[q][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t], bw, acc[q][t], 0, 0, 0);
-                }
-                kx += 2;
-                const bool wx = kx >= k;
-                kx -= wx ? k : 0;
-                ky += wx ? 1 : 0;
-                off += wx ? 2 + H - k : 2;
-                const bool wy = ky >= k;
-                ky -= wy ? k : 0;
-                off += wy ? plane - k * H : 0;
             }
         }
         if (c + 1 < nchunk) {
@@ -466,8 +470,8 @@ int tdmpc_lg_conv_fwd(const tdmpc_lg_conv* a, void* stream) {
     int CC = std::min(a->cin, std::min(CVS_SLAB / (SRM * H), CVS_KC / kk));
     if ((kk & 1) && CC < a->cin) CC &= ~1;   // (even k-values per chunk but the last: the direct kernel's MFMA pairs)
     if (ho * ho >= 256 && CC >= 1 && getenv("TDMPC_CONV_DIRECT") == nullptr) {
-        const int KCM = (CC * kk + 1) & ~1;
-        const size_t lds = ((size_t)CC * SRM * H + (size_t)a->nprob * KCM * 32) * 4;
+        const int KCM = (CC * kk + 1) & ~1, KT = ((KCM / 2) + 3) & ~3;
+        const size_t lds = ((size_t)(((CC + 1) * SRM * H + 3) & ~3) + (size_t)a->nprob * KCM * 32 + 2 * KT) * 4;
         const dim3 grid((ho * ho + BP - 1) / BP, a->n);
         if (a->nprob == 2 && TP == 2)
             hipLaunchKernelGGL((conv_fwd_slab_kernel<2, 2>), grid, dim3(512), lds, (hipStream_t)stream, *a, ho, CC, SRM);
