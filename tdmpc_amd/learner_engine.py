@@ -127,9 +127,12 @@ class Engine:
         self.x6 = os.environ.get("TDMPC_LG_X6", "0") == "1"
         # 64 x 64 tiles from this many 64 x 64 output tiles per launch (TDMPC_LG_T64, an A/B knob)
         self.t64 = int(os.environ.get("TDMPC_LG_T64", "240"))
-        # every product on the hand-written lg_gemm (grouped launches, fused ELU / ELU' epilogues); TDMPC_LG_BLAS=1
-        # puts the plain M x M products back on hipBLASLt (torch.mm / addmm) for an A/B
-        self.blas = os.environ.get("TDMPC_LG_BLAS", "0") == "1"
+        # the heads' plain M x M products (R = H B rows, no fused epilogue) on hipBLASLt (torch.mm / addmm), the
+        # library GEMM for a plain GEMM: 1.25 vs 1.37 ms per humanoid update with them on lg_gemm, graph replay
+        # (profiles/r05/learner_blas_ab.txt). Everything else -- the rollout's chained products with their fused ELU /
+        # ELU' epilogues, the grouped weight gradients, rows, losses, Adam -- stays on the hand-written kernels.
+        # TDMPC_LG_BLAS=0 puts those products on lg_gemm too (set before the first update: the graph keeps it).
+        self.blas = os.environ.get("TDMPC_LG_BLAS", "1") == "1"
         self._aux = {}
 
     def _alias(self, model, flat):
@@ -153,9 +156,8 @@ class Engine:
         return (self.PT if target else self.P)[o:o + n].view(shape)
 
     def mm(self, x, k, out, bias=None, target=False, transpose=False, cols=None, acc=False):
-        """out = x @ W^T (+ bias) -- or x @ W with transpose=True (the backward's dX) -- on hipBLASLt; kept only for
-        the TDMPC_LG_BLAS=1 A/B of the products `job` puts on lg_gemm. cols: W's input columns [c0, c1) only;
-        acc: out += x @ W^T."""
+        """out = x @ W^T (+ bias) -- or x @ W with transpose=True (the backward's dX) -- on hipBLASLt (the heads'
+        plain products, see self.blas). cols: W's input columns [c0, c1) only; acc: out += x @ W^T."""
         w = self.wv(k, target)
         if cols is not None:
             w = w[:, cols[0]:cols[1]]
@@ -187,8 +189,8 @@ class Engine:
         return j
 
     def mms(self, jobs, blas):
-        """Run a group of `job` products: ONE lg_gemm launch (default), or -- TDMPC_LG_BLAS=1, the A/B -- each on
-        hipBLASLt through `mm` plus a tdmpc_lg_act launch for a fused epilogue. blas: the mm() arguments per job."""
+        """Run a group of `job` products: each on hipBLASLt through `mm` plus a tdmpc_lg_act launch for a fused
+        epilogue (default), or -- TDMPC_LG_BLAS=0 -- ONE grouped lg_gemm launch. blas: the mm() arguments per job."""
         if not self.blas:
             self.gemm(jobs)
             return
