@@ -10,4 +10,6 @@ import bench
 from tdmpc_amd.config import bench_cfg
 
 cfg = bench_cfg(sys.argv[1] if len(sys.argv) > 1 else "humanoid-run")
-print(json.dumps(bench.learner_bench(cfg, torch.device("cuda"), cpu=False, reps=int(os.environ.get("REPS", 30)))))
+modes = tuple(os.environ.get("MODES", "graph").split(","))
+print(json.dumps(bench.learner_bench(cfg, torch.device("cuda"), cpu=False, reps=int(os.environ.get("REPS", 30)),
+                                     pixels=False, modes=modes)))
