@@ -92,3 +92,37 @@ def test_sharded_dog64_rccl_world1_equals_single_process(tmp_path):
     _run_world(tmp_path, 1, backend="nccl")
     _check_against_single_process(tmp_path, 1)
     assert bool(np.load(os.path.join(tmp_path, "rank0.npz"))["gather_equal"])
+
+
+def test_world1_deferred_status_raises_two_calls_late():
+    """The deferred status path of EnvShardedPlanner (world 1 on the GPU; RCCL ranks take the same path after their
+    gather): call 0's one-env persistent plan fails on the device (TDMPC_P1_DEBUG_SKIP), its actions come back NaN
+    without a host sync, call 1 (healthy) returns finite actions, and call 2 raises from EnvShardedPlanner's own
+    check -- before the agent's HipPlanner check, which it clears -- naming rank 0 and the status; the sticky word is
+    cleared, so call 3 plans normally."""
+    from tdmpc_amd import TDMPC, EnvShardedPlanner
+    from tdmpc_amd.config import make_cfg
+    from tdmpc_amd.told import synthetic_state_dict
+    c = make_cfg("humanoid", num_samples=512, num_elites=64, iterations=6, horizon=5)
+    agent = TDMPC(c, max_batch=1, path="persist")
+    agent.model.load_state_dict(synthetic_state_dict(c, 13))
+    agent.std = 0.05
+    planner = EnvShardedPlanner(1, c.action_dim, agent=agent)
+    assert planner.world == 1
+    obs = torch.from_numpy(np.random.RandomState(3).standard_normal((1, c.obs_shape[0])).astype(np.float32))
+    os.environ["TDMPC_P1_DEBUG_SKIP"] = "1"
+    try:
+        a0, _ = planner.plan(obs, 10**6, t0=True)
+    finally:
+        del os.environ["TDMPC_P1_DEBUG_SKIP"]
+    agent.planner._graphs.clear()   # (the captured graph keeps the knob's launch arguments)
+    assert not bool(torch.isfinite(a0).all())
+    a1, _ = planner.plan(obs, 10**6, t0=True)
+    assert bool(torch.isfinite(a1).all())
+    with pytest.raises(RuntimeError, match=r"rank\(s\) \[0\] \(status 1\)"):
+        planner.plan(obs, 10**6, t0=True)
+    assert int(agent.planner.status.item()) == 0
+    a3, _ = planner.plan(obs, 10**6, t0=True)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(a3).all())
+    planner.check_status()   # (nothing pending or set)
