@@ -100,6 +100,115 @@ ring_kernel(const char* src, long src_bytes, int steps, float* out) {
     if (s == 12345.f) out[tid] = s;
 }
 
+// V 10: the weights streamed as fp32 (2 KiB per wave per step, 2/3 of the x6 bytes) into an fp32 ring, each step's
+// landed slot split once per workgroup into the three bf16 planes of a double-buffered plane buffer (each thread 8
+// weights: 2 ds_read_b128, the three-way split, 3 ds_write_b128), the MFMAs reading the planes split one step earlier.
+__device__ __forceinline__ void split8(const float4& a, const float4& b, uint4& h, uint4& m, uint4& l) {
+    const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    unsigned short hh[8], mm[8], ll[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const __bf16 bh = (__bf16)x[i];
+        const float r1 = x[i] - (float)bh;
+        const __bf16 bm = (__bf16)r1;
+        const __bf16 bl = (__bf16)(r1 - (float)bm);
+        hh[i] = __builtin_bit_cast(unsigned short, bh);
+        mm[i] = __builtin_bit_cast(unsigned short, bm);
+        ll[i] = __builtin_bit_cast(unsigned short, bl);
+    }
+    h = make_uint4(hh[0] | (hh[1] << 16), hh[2] | (hh[3] << 16), hh[4] | (hh[5] << 16), hh[6] | (hh[7] << 16));
+    m = make_uint4(mm[0] | (mm[1] << 16), mm[2] | (mm[3] << 16), mm[4] | (mm[5] << 16), mm[6] | (mm[7] << 16));
+    l = make_uint4(ll[0] | (ll[1] << 16), ll[2] | (ll[3] << 16), ll[4] | (ll[5] << 16), ll[6] | (ll[7] << 16));
+}
+
+template <int NS, int MF>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+ring10_kernel(const char* src, long src_bytes, int steps, float* out) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int SLOT = 16 * 1024, PLANES = 24 * 1024;
+    constexpr int VM = 2 * (NS - 3);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const unsigned base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)lds;
+    const unsigned voff = lane * 16;
+    char* pb = lds + NS * SLOT;
+    const char* s0 = src + ((blockIdx.x & 7) >> 2) * src_bytes;
+    auto issue = [&](int k) {
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            const long off = ((long)k * 16 + wave * 2 + d) * 1024 % src_bytes;
+            glds<0>(s0 + off, voff, base + (k % NS) * SLOT + (wave * 2 + d) * 1024);
+        }
+    };
+    auto split = [&](int k) {   // slot of step k -> plane buffer k & 1
+        const char* sl = lds + (k % NS) * SLOT + tid * 32;
+        const float4 a = *(const float4*)sl, b = *(const float4*)(sl + 16);
+        uint4 h, m, l;
+        split8(a, b, h, m, l);
+        char* d = pb + (k & 1) * PLANES;
+        *(uint4*)(d + tid * 16) = h;
+        *(uint4*)(d + 8192 + tid * 16) = m;
+        *(uint4*)(d + 16384 + tid * 16) = l;
+    };
+    for (int k = 0; k < NS - 1; ++k) issue(k);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    split(0);
+    floatx4 acc[8];
+    for (int j = 0; j < 8; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < steps; ++k) {
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(VM) : "memory");
+        issue(k + NS - 1);
+        split(k + 1);
+        const char* sl = pb + (k & 1) * PLANES + lane * 16;
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+            // fragment f's three planes (the probe's layout: 1 KiB per plane and fragment)
+            const uint4 w0 = *(const uint4*)(sl + f * 1024), w1 = *(const uint4*)(sl + 8192 + f * 1024),
+                        w2 = *(const uint4*)(sl + 16384 + f * 1024);
+            const bf16x8_t a0 = __builtin_bit_cast(bf16x8_t, w0), a1 = __builtin_bit_cast(bf16x8_t, w1),
+                           a2 = __builtin_bit_cast(bf16x8_t, w2);
+#pragma unroll
+            for (int mm = 0; mm < MF; ++mm) {
+                const bf16x8_t a = mm % 3 == 0 ? a0 : mm % 3 == 1 ? a1 : a2;
+                acc[(f + mm) & 7] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, a1, acc[(f + mm) & 7], 0, 0, 0);
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    float s = 0.f;
+    for (int j = 0; j < 8; ++j) s += acc[j][0] + acc[j][3];
+    if (s == 12345.f) out[tid] = s;
+}
+
+template <int NS, int MF>
+void run10(int steps, long src_kb) {
+    const long sb = src_kb * 1024;
+    char* src;
+    CK(hipMalloc(&src, 2 * sb));
+    CK(hipMemset(src, 0, 2 * sb));
+    float* out;
+    CK(hipMalloc(&out, 4096));
+    const size_t lds = (size_t)NS * 16 * 1024 + 2 * 24 * 1024;
+    CK(hipFuncSetAttribute((const void*)ring10_kernel<NS, MF>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((ring10_kernel<NS, MF>), dim3(256), dim3(512), lds, 0, src, sb, steps, out);
+    CK(hipDeviceSynchronize());
+    const int R = 50;
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < R; ++i) hipLaunchKernelGGL((ring10_kernel<NS, MF>), dim3(256), dim3(512), lds, 0, src, sb, steps, out);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1e3 / R;
+    printf("V=10 (fp32 stream + split) NS=%d MF=%d steps=%d src=%ldKB: %.2f us/launch, %.3f us/step\n", NS, MF, steps,
+           src_kb, us, us / steps);
+    CK(hipFree(src));
+    CK(hipFree(out));
+}
+
 template <int NS, int D, int MF, int NT, int V = 0>
 void run(int steps, long src_kb, bool rnd = false) {
     const long sb = src_kb * 1024;
@@ -141,10 +250,9 @@ int main(int argc, char** argv) {
     const long kb = argc > 2 ? atol(argv[2]) : 2304;
     run<4, 3, 6, 0, 0>(steps, kb);          // full: every wave issues 3 DMAs right after the barrier
     run<4, 3, 6, 0, 5>(steps, kb);          // MFMA + barrier only (the floor)
-    run<4, 3, 6, 0, 6>(steps, kb);          // waves 4-7 issue all 24 DMAs (6 each)
-    run<4, 3, 6, 0, 7>(steps, kb);          // waves 0-3 issue all 24
-    run<4, 3, 6, 0, 8>(steps, kb);          // every wave, its 3 DMAs spread over the step
-    run<4, 3, 6, 1, 0>(steps, kb);          // nt
-    run<5, 3, 6, 0, 6>(steps, kb);
+    run10<4, 6>(steps, kb);                 // fp32 stream + one split per workgroup
+    run10<5, 6>(steps, kb);
+    run10<4, 0>(steps, kb);                 // (its stream + split alone)
+    run<4, 3, 0, 0, 0>(steps, kb);          // (the x6 stream alone)
     return 0;
 }
