@@ -2,8 +2,9 @@
 
 * `test_plan_fullsize_configs`: whole `plan()` calls (N=512, H=5, 6 iterations, K=64) for cheetah-run,
   humanoid-run with latent 512, quadruped-run pixels and dog-run, at one env per call (the drop-in) and at
-  8 envs per call (configs[3]'s per-GPU share of 64 dog envs) -- and latent 512 at the bench's 32 envs per call
-  too --, cold start, warm start and a mixed t0 batch,
+  8 envs per call (configs[3]'s per-GPU share of 64 dog envs) and at the bench's 32 envs per call (the wide step
+  and wide heads kernels, each config its own instance; latent 512 on the chain kernels), cold start, warm start and
+  a mixed t0 batch,
   every env against the oracle (the CPU restatement of tdmpc.py:94-163, pinned to the reference) on the same
   noise. Tolerances as tests/test_gpu_plan.py (parity_util): values 1e-5 + 1e-4 |ref|, action / mean / std /
   metrics 2e-5 while the elite sets agree; near-tie escapes are counted (tests/test_zz_parity_budget.py).
@@ -52,9 +53,6 @@ def _obs(cfg, rs, B):
 @pytest.mark.parametrize("B", [1, 8, 32])
 @pytest.mark.parametrize("name", list(CONFIGS))
 def test_plan_fullsize_configs(name, B):
-    if B == 32 and name != "humanoid-run-l512":
-        pytest.skip("the 32-env bench shape runs the wide kernels: covered by test_gpu_plan.py (L100) and here "
-                    "for BASELINE's literal humanoid config (latent 512) only")
     task, ov = CONFIGS[name]
     cfg = make_cfg(task, **ov)
     agent = _agent(cfg, 21, B=B)
@@ -94,6 +92,31 @@ def test_plan_fullsize_configs(name, B):
                                        [rm["external_reward_mean"], rm["current_std"]], atol=2e-5, rtol=1e-4)
             pm = agent.planner.prev_mean_view(5, B)[e].cpu().numpy()
             np.testing.assert_allclose(pm, states[e].prev_mean.numpy(), atol=2e-5, rtol=0)
+    if B == 32:   # the kernels that ran: the wide ones where the bench runs them (latent 512: the chain kernels)
+        step_k, q_k = _kernel_of(agent, cfg, 4), _kernel_of(agent, cfg, 6)
+        want = "chain_kernel" if name == "humanoid-run-l512" else ("wide_step_kernel", "wide_heads_kernel")
+        assert step_k.startswith(want if isinstance(want, str) else want[0]), step_k
+        assert q_k.startswith(want if isinstance(want, str) else want[1]), q_k
+
+
+def _kernel_of(agent, cfg, prof_cfg):
+    """Name of the kernel the library's profiler (tdmpc_profile_begin cfg: 4 the step launches, 6 helper.q) timed
+    over one eager plan of the agent's batch."""
+    import ctypes as C
+    from tdmpc_amd import _lib
+    L = _lib.lib()
+    B = agent.planner.max_batch if hasattr(agent.planner, "max_batch") else 32
+    obs = _obs(cfg, np.random.RandomState(1), B)
+    graph, agent.graph = agent.graph, False
+    try:
+        _lib.check(L.tdmpc_profile_begin(prof_cfg, -1, 0, 0, 256), "profile_begin")
+        agent.plan_batch(obs, step=10**6, t0=False, sync_metrics=False)
+        n, ms, fl = C.c_int32(), C.c_double(), C.c_double()
+        _lib.check(L.tdmpc_profile_end(C.byref(n), C.byref(ms), C.byref(fl)), "profile_end")
+    finally:
+        agent.graph = graph
+    assert n.value > 0, prof_cfg
+    return L.tdmpc_profile_kernel().decode()
 
 
 @pytest.mark.parametrize("path", ["auto", "chain_x6", "layered"])
