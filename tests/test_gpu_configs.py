@@ -310,3 +310,42 @@ def test_default_plan_graph_equals_eager():
         assert graph == (len(agent.planner._graphs) == 2)   # (eval_mode False, True)
     for (a1, m1), (a2, m2) in zip(*outs):
         assert torch.equal(a1, a2) and m1 == m2
+
+
+@pytest.mark.parametrize("case", NF_CASES)
+def test_plan_wide_nonfinite(case):
+    """The non-finite cases of test_estimate_value_nonfinite through the whole plan at the bench shape (32 humanoid
+    envs: the wide step and wide heads kernels, the statistics-block LayerNorm included), where estimate_value's
+    entry point does not reach the wide heads. A start-latent case sets the encoder's last bias (z0 = h(obs) then
+    carries the value in column 3 for every env). Iteration 0's 768 values of every env (the same candidates on
+    both sides) against the oracle's: exactly where the oracle's are nan_to_num's specials (0, +-FLT_MAX),
+    elsewhere within 1e-5 (of the largest |G| for the large cases)."""
+    cfg = make_cfg("humanoid", **FULL)
+    B = 32
+    sd = synthetic_state_dict(cfg, 7)
+    z0 = torch.zeros(1, cfg.latent_dim)
+    _nf_case(case, sd, z0)
+    if case in ("beyond_bf16", "inf_latent", "nan_latent"):
+        sd["_encoder.2.bias"][3] = z0[0, 3]
+    agent = TDMPC(cfg, max_batch=B)
+    agent.model.load_state_dict(sd)
+    agent.std = 0.05
+    told = tdmpc_ref.RefTOLD(sd, cfg)
+    rs = np.random.RandomState(4)
+    obs = rs.standard_normal((B, cfg.obs_shape[0])).astype(np.float32)
+    torch.manual_seed(8)
+    np.random.seed(8)
+    noises = [tdmpc_ref.draw_noise(cfg, 10**6, False) for _ in range(B)]
+    tr = {}
+    agent._plan_envs(obs, False, 10**6, [True] * B, trace=tr, noise=noises)
+    for e in range(B):
+        rtr = {}
+        tdmpc_ref.plan(told, cfg, tdmpc_ref.PlanState(0.05), obs[e], noises[e], eval_mode=False, step=10**6, t0=True,
+                       trace=rtr)
+        rv = rtr["value"][0].squeeze(-1).numpy()
+        gv = tr["value"][e][0].cpu().numpy()
+        assert np.isfinite(gv).all(), f"env {e}: nan_to_num left a non-finite value"
+        special = (np.abs(rv) == FMAX) | (rv == 0)
+        np.testing.assert_array_equal(gv[special], rv[special], err_msg=f"env {e}")
+        atol = 1e-5 * float(np.abs(rv).max()) if case in ("large_finite", "beyond_bf16") else 1e-5
+        assert close(gv[~special], rv[~special], atol=atol).all(), (e, np.abs(gv - rv)[~special].max())
