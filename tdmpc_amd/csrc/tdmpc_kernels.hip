@@ -3236,14 +3236,7 @@ struct LinCfg {
     int bw;      // row-reduction block width (64 or 32)
 };
 
-int thr_rows() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("TDMPC_THR_ROWS");
-        v = e ? atoi(e) : 4096;
-    }
-    return v;
-}
+int thr_rows() { return 4096; }
 
 // Tile choice by shape (tools/mb/mb_linear.hip "sweep" on MI355X): the LDS-staged throughput tiles from
 // thr_rows() rows on; below that the K-split latency tiles, 32x64 where K and N are wide enough to feed
@@ -3370,14 +3363,7 @@ int launch_lin(const LinArgs& a, int nprob, int nmax, int wide64, int pro, hipSt
 // GEMMs, whose K-split tiles spread the same rows over more CUs, finish first. Measured on MI355X (humanoid
 // plan, round-1 run): threshold 64 vs 128: B = 2 envs 1.65 vs 1.87 ms, B = 4 1.88 vs 1.98 ms; 32 loses
 // at one env (1.56 vs 1.38 ms).
-int chain_wgs() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("TDMPC_CHAIN_WGS");
-        v = e ? atoi(e) : 64;
-    }
-    return v;
-}
+int chain_wgs() { return 64; }
 
 // Shapes the chain kernel supports: M = 256 * TN (TN = 1, 2, 4); the last layer's (block, K-part) items
 // (<= 16) fit the activation block as 32x32 partial tiles.
@@ -3544,14 +3530,7 @@ bool chain_nw16_ok(const Layout& w) {
 }
 
 // Waves per 32-row chain workgroup (TDMPC_CHAIN_NW: 8 or 16; 16 needs M = 512).
-int chain_nw() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("TDMPC_CHAIN_NW");
-        v = e ? atoi(e) : 8;
-    }
-    return v;
-}
+int chain_nw() { return 8; }
 
 // x6 chain kernels (fp32 products from a three-way bf16 split, chain_kernel<..., X6>) for 32-row chain launches:
 // forced by TDMPC_PATH_CHAIN_X6, the default of the auto / chain paths (TDMPC_X6=0 turns it off there); the
@@ -3584,12 +3563,6 @@ int chain_rb(const Ctx& c, int rows, int nprob) {
         c.path == TDMPC_PATH_WIDE)
         return 32;
     if (c.path == TDMPC_PATH_CHAIN16) return 16;
-    static int forced = -1;
-    if (forced < 0) {
-        const char* e = getenv("TDMPC_CHAIN_RB");
-        forced = e ? atoi(e) : 0;
-    }
-    if (forced == 16 || forced == 32) return forced;
     return (rows + 31) / 32 * nprob > num_cus() / 2 ? 32 : 16;
 }
 
@@ -3625,12 +3598,7 @@ bool use_split(const Ctx& c, int rows) {
     // auto: only while the first layer, repeated per slice, stays cheap next to the slice of the M x M layer
     // (humanoid-run L512: K1 = 536 made the one-env plan 1.3x slower than the layered path)
     if (c.path != TDMPC_PATH_AUTO || (int)rup(w.Kx, 16) > w.M / 2) return false;
-    static int en = -1;
-    if (en < 0) {
-        const char* e = getenv("TDMPC_SPLIT");
-        en = e ? atoi(e) : 1;
-    }
-    return en && !use_chain(c, rows, 2, CK_STEP);
+    return !use_chain(c, rows, 2, CK_STEP);
 }
 
 // split_step_kernel for the pi head (grid z = 1: no reward head; its finish is split_pi_finish_kernel).
@@ -3639,12 +3607,7 @@ bool use_split_pi(const Ctx& c, int rows) {
     if (w.M != 512 || rows > c.k.split_rows || (size_t)split_lds_floats(w.Lp, w.M) * 4 > 64 * 1024) return false;
     if (c.path == TDMPC_PATH_SPLIT || c.path == TDMPC_PATH_SPLIT_X6) return true;
     if (c.path != TDMPC_PATH_AUTO || (int)rup(w.Lp, 16) > w.M / 2) return false;
-    static int en = -1;
-    if (en < 0) {
-        const char* e = getenv("TDMPC_SPLIT_PI");
-        en = e ? atoi(e) : 1;
-    }
-    return en && !use_chain(c, rows, 1, CK_PI);
+    return !use_chain(c, rows, 1, CK_PI);
 }
 
 // One TOLD.next step (tdmpc.py:34-37) for `rows` logical rows mapped onto X rows, plus the return update
@@ -3777,12 +3740,11 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
             // split is by a row's role, never by the launch's size or a row's position in it, so a row's kernel (and
             // its rounding) does not depend on the batch size (tests/test_gpu_sharded.py: two 32-env shards equal
             // the 64-env batch bitwise). At t = 0 both parts keep the z0c first layer (the per-env bias is indexed by
-            // logical row / G, and G is the per-env row count of each part's map). TDMPC_WIDE_SPLIT=0 turns it off.
-            static const int split = [] { const char* e = getenv("TDMPC_WIDE_SPLIT"); return e ? atoi(e) : 1; }();
+            // logical row / G, and G is the per-env row count of each part's map).
             const RowMap rm = {c.N, map.S, 0}, pm = {c.P, map.S, c.N};
             const int envs = rows / std::max(1, map.G);
             const bool z0c_rm = t == 0 && c.z0c_ready;   // (rm.G = N: use_wide checks N % 128 for the z0c bias)
-            if (split && c.P > 0 && c.N + c.P == c.T && map.G == c.T && map.S == c.T && map.O == 0 && rows == envs * c.T &&
+            if (c.P > 0 && c.N + c.P == c.T && map.G == c.T && map.S == c.T && map.O == 0 && rows == envs * c.T &&
                 use_wide(c, envs * c.N, rm, z0c_rm)) {
                 if ((rc = launch_wide(c, t, envs * c.N, rm, disc, first, last, z0c_rm))) return rc;
                 return step_next(c, t, envs * c.P, pm, disc, first, last, 0, true);

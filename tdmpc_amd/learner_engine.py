@@ -125,8 +125,8 @@ class Engine:
         # and latency-bound rather than MFMA-bound) or the x6 form (TDMPC_LG_X6=1; set before the first update: the
         # captured graph keeps the choice)
         self.x6 = os.environ.get("TDMPC_LG_X6", "0") == "1"
-        # 64 x 64 tiles from this many 64 x 64 output tiles per launch (TDMPC_LG_T64, an A/B knob)
-        self.t64 = int(os.environ.get("TDMPC_LG_T64", "240"))
+        # 64 x 64 tiles from this many 64 x 64 output tiles per launch (measured: profiles/r04/learner_tile_ab.txt)
+        self.t64 = 240
         # the heads' plain M x M products (R = H B rows, no fused epilogue) on hipBLASLt (torch.mm / addmm), the
         # library GEMM for a plain GEMM: 1.25 vs 1.37 ms per humanoid update with them on lg_gemm, graph replay
         # (profiles/r05/learner_blas_ab.txt). Everything else -- the rollout's chained products with their fused ELU /
