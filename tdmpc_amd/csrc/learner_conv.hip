@@ -43,6 +43,9 @@ int cv_bad(const char* m) {
     return TDMPC_E_DIMS;
 }
 
+// q = e / d for 0 <= e < 2^16 and 0 < d <= 2^16 by a float multiply (exact: (e + 0.5) / d sits >= 0.5 / d away from an
+// integer, far beyond the product's rounding) -- the staging loops' index splits without an integer division
+DEVI int cv_div(int e, float inv_d) { return (int)__fmul_rn((float)e + 0.5f, inv_d); }
 DEVI float relu_f(float v) { return v != v ? v : fmaxf(v, 0.f); }   // (torch.relu keeps a NaN)
 DEVI __amdgpu_buffer_rsrc_t cv_rsrc(const float* p) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)CV_OOB, 0x00020000);
@@ -126,6 +129,7 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv 
     const int P0 = blockIdx.x * BP;
     const int oy0 = P0 / ho, oy1 = min(ho - 1, (P0 + BP - 1) / ho);
     const int SR = 2 * (oy1 - oy0) + k, plane = SR * H;
+    const float inv_plane = 1.0f / (float)plane;
     const int KCM = (CC * kk + 1) & ~1, KT = ((KCM / 2) + 3) & ~3;
     float* slab = cv_sm;                                   // [CC + 1][SR][H] (plane cc: zeros for an odd chunk's pad)
     float* sW = slab + (((CC + 1) * SRM * H + 3) & ~3);    // [NP][KCM][32] (16-byte aligned: kt's int4 reads)
@@ -150,7 +154,7 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv 
         const int c0 = c * CC, cc = min(CC, cin - c0), ns = cc * plane, nk = cc * kk;
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
-            const int e = tid + 512 * i, ci = e / plane;
+            const int e = tid + 512 * i, ci = cv_div(e, inv_plane);
             sv[i] = cv_ld(rx, (unsigned)((c0 + ci) * H * H + e - ci * plane), e < ns);
         }
 #pragma unroll
@@ -163,10 +167,18 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv 
     };
     auto stash = [&](int c) __attribute__((always_inline)) {
         const int c0 = c * CC, cc = min(CC, cin - c0), ns = cc * plane, nk = cc * kk;
+        if (div > 0.f) {   // (a uniform branch: the division is not computed when there is none)
 #pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            const int e = tid + 512 * i;
-            if (e < ns) slab[e] = div > 0.f ? __fdiv_rn(sv[i], div) : sv[i];
+            for (int i = 0; i < NS; ++i) {
+                const int e = tid + 512 * i;
+                if (e < ns) slab[e] = __fdiv_rn(sv[i], div);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                const int e = tid + 512 * i;
+                if (e < ns) slab[e] = sv[i];
+            }
         }
         if (nk & 1)   // the pad k-value nk reads plane cc at the pixel's base: zeros (times a zero weight)
             for (int e = tid; e < plane; e += 512) slab[ns + e] = 0.f;
@@ -395,16 +407,22 @@ __global__ void __launch_bounds__(512) conv_bwd_weight_slab_kernel(const float* 
             const int npx = min(PB, HoHo - P0);
             const int oy0 = P0 / ho, oy1 = (P0 + npx - 1) / ho;
             const int SR = 2 * (oy1 - oy0) + k, plane = SR * H;
+            const float inv_npx = 1.0f / (float)npx, inv_plane = 1.0f / (float)plane;
             __syncthreads();   // (the previous block's reads are done)
             for (int e = tid; e < 32 * npx; e += 512) {
-                const int co = e / npx, p = e - co * npx;
+                const int co = cv_div(e, inv_npx), p = e - co * npx;
                 dyl[co * PBP + p] = dyi[(size_t)co * HoHo + P0 + p];
             }
-            for (int e = tid; e < cin * plane; e += 512) {
-                const int ci = e / plane, o = e - ci * plane;
-                const float v = xi[(size_t)ci * H * H + (size_t)(2 * oy0) * H + o];
-                slab[ci * SRM * H + o] = div > 0.f ? __fdiv_rn(v, div) : v;
-            }
+            if (div > 0.f)
+                for (int e = tid; e < cin * plane; e += 512) {
+                    const int ci = cv_div(e, inv_plane), o = e - ci * plane;
+                    slab[ci * SRM * H + o] = __fdiv_rn(xi[(size_t)ci * H * H + (size_t)(2 * oy0) * H + o], div);
+                }
+            else
+                for (int e = tid; e < cin * plane; e += 512) {
+                    const int ci = cv_div(e, inv_plane), o = e - ci * plane;
+                    slab[ci * SRM * H + o] = xi[(size_t)ci * H * H + (size_t)(2 * oy0) * H + o];
+                }
             __syncthreads();
             const int nst = (npx + 1) / 2;
             int P = P0 + h, ox = P % ho;
