@@ -481,9 +481,9 @@ int tdmpc_lg_conv_fwd(const tdmpc_lg_conv* a, void* stream) {
         attr = true;
     }
     const int kk = a->k * a->k, H = a->hin;
-    // the LDS-staged form for the large layers: slab rows of a 256 TP-pixel block (TP = 2 tiles per wave where the
-    // image fills the blocks: the first layer), channels per chunk within both caps
-    const int TP = ho * ho >= 1024 ? 2 : 1, BP = 256 * TP;
+    // the LDS-staged form for the large layers: slab rows of a 256 TP-pixel block (TP = 2 tiles per wave on both
+    // large layers: two MFMA chains per weight read), channels per chunk within both caps
+    const int TP = ho * ho >= 300 ? 2 : 1, BP = 256 * TP;
     const int SRM = std::min(H, 2 * (std::min(ho, (BP - 1) / ho + 2) - 1) + a->k);
     int CC = std::min(a->cin, std::min(CVS_SLAB / (SRM * H), CVS_KC / kk));
     if ((kk & 1) && CC < a->cin) CC &= ~1;   // (even k-values per chunk but the last: the direct kernel's MFMA pairs)
