@@ -29,9 +29,6 @@
 
 namespace tdmpc_internal {
 void set_error(const char* msg);
-int conv_fwd(const void* x, int x_u8, long xbs, const float* w, const float* b, float* y, long ybs, int n, int cin,
-             int hin, int k, float in_div, hipStream_t s);
-int conv_fwd_init();
 }
 
 namespace {
@@ -57,31 +54,9 @@ DEVI float cv_ld(__amdgpu_buffer_rsrc_t r, unsigned off_elems, bool ok) {
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, ok ? (int)(off_elems * 4u) : (int)CV_OOB, 0, 0));
 }
 
-// The forward's arguments: the C ABI's tdmpc_lg_conv (dense [n][c][h][w] images) or the planner's encoder
-// (tdmpc_internal::conv_fwd: per-image strides, uint8 frames on the first layer).
-struct CvArgs {
-    const void* x; int x_u8; long xbs;   // input image e at x + e * xbs elements (float, or uint8 when x_u8)
-    const float* w[2]; const float* b[2];
-    float* y[2]; long ybs;               // output image e at y + e * ybs floats ([32][ho][ho] each)
-    int nprob, n, cin, hin, k;
-    float in_div;
-};
-// one input element (the buffer offset in elements; uint8 frames as bytes)
-DEVI float cv_ldx(__amdgpu_buffer_rsrc_t r, int u8, unsigned off_elems, bool ok) {
-    if (u8) {
-        const unsigned char v = __builtin_amdgcn_raw_buffer_load_b8(r, ok ? (int)off_elems : (int)CV_OOB, 0, 0);
-        return (float)v;
-    }
-    return cv_ld(r, off_elems, ok);
-}
-DEVI __amdgpu_buffer_rsrc_t cv_rsrc_x(const CvArgs& a, size_t off_elems) {
-    const char* p = (const char*)a.x + off_elems * (a.x_u8 ? 1 : 4);
-    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)CV_OOB, 0x00020000);
-}
-
 // ---------------------------------------------------------------------------------------------------- forward
 // grid (ceil(ho^2 / 128), n, nprob), 256 threads; LDS sW [K2][32] | koff [K2] (K2 = K rounded up to even)
-__global__ void __launch_bounds__(256) conv_fwd_kernel(const CvArgs a, int ho, int K2) {
+__global__ void __launch_bounds__(256) conv_fwd_kernel(const tdmpc_lg_conv a, int ho, int K2) {
     extern __shared__ float cv_sm[];
     const int img = blockIdx.y, pr = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
@@ -103,8 +78,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const CvArgs a, int ho, i
     const int p = p0 + r;
     const int pp = p < HoHo ? p : HoHo - 1;
     const int pixbase = 2 * (pp / ho) * H + 2 * (pp % ho);
-    const __amdgpu_buffer_rsrc_t rx = cv_rsrc_x(a, (size_t)img * a.xbs);
-    const int u8 = a.x_u8;
+    const __amdgpu_buffer_rsrc_t rx = cv_rsrc(a.x + (size_t)img * a.cin * H * H);
     const float div = a.in_div;
     const int ns = K2 / 2;
     floatx16 acc;
@@ -112,12 +86,12 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const CvArgs a, int ho, i
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
     float av[CV_D];
 #pragma unroll
-    for (int d = 0; d < CV_D - 1; ++d) av[d] = cv_ldx(rx, u8, (unsigned)(pixbase + koff[min(2 * d + h, K2 - 1)]), d < ns);
+    for (int d = 0; d < CV_D - 1; ++d) av[d] = cv_ld(rx, (unsigned)(pixbase + koff[min(2 * d + h, K2 - 1)]), d < ns);
     for (int s0 = 0; s0 < ns; s0 += CV_D) {
 #pragma unroll
         for (int d = 0; d < CV_D; ++d) {
             const int s = s0 + d, sl = s + CV_D - 1;
-            av[(d + CV_D - 1) % CV_D] = cv_ldx(rx, u8, (unsigned)(pixbase + koff[min(2 * sl + h, K2 - 1)]), sl < ns);
+            av[(d + CV_D - 1) % CV_D] = cv_ld(rx, (unsigned)(pixbase + koff[min(2 * sl + h, K2 - 1)]), sl < ns);
             if (s < ns) {
                 float x = av[d];
                 if (div > 0.f) x = __fdiv_rn(x, div);
@@ -127,7 +101,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const CvArgs a, int ho, i
     }
     // C/D map of the 32x32 MFMA: col = lane & 31 (the channel), row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5) (the pixel)
     const float bias = (pr ? a.b[1] : a.b[0])[r];
-    float* y = (pr ? a.y[1] : a.y[0]) + (size_t)img * a.ybs + (size_t)r * HoHo;
+    float* y = (pr ? a.y[1] : a.y[0]) + ((size_t)img * 32 + r) * HoHo;
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
         const int pix = p0 + (e & 3) + 8 * (e >> 2) + 4 * h;
@@ -146,7 +120,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(const CvArgs a, int ho, i
 constexpr int CVS_SLAB = 8192, CVS_KC = 208;   // slab floats, k-values per chunk
 
 template <int NP, int TP>
-__global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const CvArgs a, int ho, int CC, int SRM) {
+__global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const tdmpc_lg_conv a, int ho, int CC, int SRM) {
     extern __shared__ float cv_sm[];
     const int img = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
@@ -160,8 +134,7 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const CvArgs a, int 
     float* slab = cv_sm;                                   // [CC + 1][SR][H] (plane cc: zeros for an odd chunk's pad)
     float* sW = slab + (((CC + 1) * SRM * H + 3) & ~3);    // [NP][KCM][32] (16-byte aligned: kt's int4 reads)
     int* kt = (int*)(sW + (size_t)NP * KCM * 32);          // [2][KT]: slab offset of k-value 2 s + h, step s
-    const __amdgpu_buffer_rsrc_t rx = cv_rsrc_x(a, (size_t)img * a.xbs + (size_t)(2 * oy0) * H);
-    const int u8 = a.x_u8;
+    const __amdgpu_buffer_rsrc_t rx = cv_rsrc(a.x + ((size_t)img * cin * H + 2 * oy0) * H);
     __amdgpu_buffer_rsrc_t rw[NP];
 #pragma unroll
     for (int q = 0; q < NP; ++q) rw[q] = cv_rsrc(a.w[q]);
@@ -182,7 +155,7 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const CvArgs a, int 
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
             const int e = tid + 512 * i, ci = cv_div(e, inv_plane);
-            sv[i] = cv_ldx(rx, u8, (unsigned)((c0 + ci) * H * H + e - ci * plane), e < ns);
+            sv[i] = cv_ld(rx, (unsigned)((c0 + ci) * H * H + e - ci * plane), e < ns);
         }
 #pragma unroll
         for (int q = 0; q < NP; ++q)
@@ -270,7 +243,7 @@ __global__ void __launch_bounds__(512) conv_fwd_slab_kernel(const CvArgs a, int 
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
         const float bias = a.b[q][r];
-        float* y = a.y[q] + (size_t)img * a.ybs + (size_t)r * HoHo;
+        float* y = a.y[q] + ((size_t)img * 32 + r) * HoHo;
 #pragma unroll
         for (int t = 0; t < TP; ++t)
 #pragma unroll
@@ -482,26 +455,31 @@ __global__ void __launch_bounds__(512) conv_bwd_weight_slab_kernel(const float* 
     }
 }
 
-// The forward kernels' dynamic-LDS limits, set once (the planner calls it from its own init_attrs, before any capture).
-int conv_init() {
-    static int rc = -1;
-    if (rc < 0) {
-        rc = 0;
-        const void* ks[5] = {(const void*)conv_fwd_kernel, (const void*)conv_fwd_slab_kernel<1, 1>,
-                             (const void*)conv_fwd_slab_kernel<2, 1>, (const void*)conv_fwd_slab_kernel<1, 2>,
-                             (const void*)conv_fwd_slab_kernel<2, 2>};
-        for (const void* k : ks)
-            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-                rc = TDMPC_E_HIP;
-    }
-    return rc;
-}
+}  // namespace
 
-// The forward's launch for either caller: the LDS-staged kernel for the large layers, the direct one otherwise.
-int conv_fwd_launch(const CvArgs& ca, hipStream_t stream) {
-    const CvArgs* a = &ca;
+extern "C" {
+
+int tdmpc_lg_conv_fwd(const tdmpc_lg_conv* a, void* stream) {
+    if (!a || !a->x || !a->w[0] || !a->b[0] || !a->y[0]) return TDMPC_E_NULL;
+    if (a->nprob < 1 || a->nprob > 2 || (a->nprob == 2 && (!a->w[1] || !a->b[1] || !a->y[1])))
+        return cv_bad("tdmpc_lg_conv_fwd: nprob");
+    if (a->n <= 0 || a->cin <= 0 || a->k <= 0 || a->hin < a->k) return cv_bad("tdmpc_lg_conv_fwd: shape");
     const int ho = (a->hin - a->k) / 2 + 1, K = a->cin * a->k * a->k, K2 = (K + 1) & ~1;
-    if (int rc = conv_init()) return rc;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)conv_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+                hipSuccess ||
+            hipFuncSetAttribute((const void*)conv_fwd_slab_kernel<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess ||
+            hipFuncSetAttribute((const void*)conv_fwd_slab_kernel<2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess ||
+            hipFuncSetAttribute((const void*)conv_fwd_slab_kernel<1, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess ||
+            hipFuncSetAttribute((const void*)conv_fwd_slab_kernel<2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess)
+            return TDMPC_E_HIP;
+        attr = true;
+    }
     const int kk = a->k * a->k, H = a->hin;
     // the LDS-staged form for the large layers: slab rows of a 256 TP-pixel block (TP = 2 tiles per wave on both
     // large layers: two MFMA chains per weight read), channels per chunk within both caps
@@ -514,38 +492,20 @@ int conv_fwd_launch(const CvArgs& ca, hipStream_t stream) {
         const size_t lds = ((size_t)(((CC + 1) * SRM * H + 3) & ~3) + (size_t)a->nprob * KCM * 32 + 2 * KT) * 4;
         const dim3 grid((ho * ho + BP - 1) / BP, a->n);
         if (a->nprob == 2 && TP == 2)
-            hipLaunchKernelGGL((conv_fwd_slab_kernel<2, 2>), grid, dim3(512), lds, stream, *a, ho, CC, SRM);
+            hipLaunchKernelGGL((conv_fwd_slab_kernel<2, 2>), grid, dim3(512), lds, (hipStream_t)stream, *a, ho, CC, SRM);
         else if (a->nprob == 2)
-            hipLaunchKernelGGL((conv_fwd_slab_kernel<2, 1>), grid, dim3(512), lds, stream, *a, ho, CC, SRM);
+            hipLaunchKernelGGL((conv_fwd_slab_kernel<2, 1>), grid, dim3(512), lds, (hipStream_t)stream, *a, ho, CC, SRM);
         else if (TP == 2)
-            hipLaunchKernelGGL((conv_fwd_slab_kernel<1, 2>), grid, dim3(512), lds, stream, *a, ho, CC, SRM);
+            hipLaunchKernelGGL((conv_fwd_slab_kernel<1, 2>), grid, dim3(512), lds, (hipStream_t)stream, *a, ho, CC, SRM);
         else
-            hipLaunchKernelGGL((conv_fwd_slab_kernel<1, 1>), grid, dim3(512), lds, stream, *a, ho, CC, SRM);
+            hipLaunchKernelGGL((conv_fwd_slab_kernel<1, 1>), grid, dim3(512), lds, (hipStream_t)stream, *a, ho, CC, SRM);
         return hipGetLastError() == hipSuccess ? 0 : TDMPC_E_HIP;
     }
     const size_t lds = (size_t)K2 * 32 * 4 + (size_t)K2 * 4;
     if (lds > 160 * 1024) return cv_bad("tdmpc_lg_conv_fwd: cin k k too large");
     hipLaunchKernelGGL(conv_fwd_kernel, dim3((ho * ho + 127) / 128, a->n, a->nprob), dim3(256), lds,
-                       stream, *a, ho, K2);
+                       (hipStream_t)stream, *a, ho, K2);
     return hipGetLastError() == hipSuccess ? 0 : TDMPC_E_HIP;
-}
-
-}  // namespace
-
-extern "C" {
-
-int tdmpc_lg_conv_fwd(const tdmpc_lg_conv* a, void* stream) {
-    if (!a || !a->x || !a->w[0] || !a->b[0] || !a->y[0]) return TDMPC_E_NULL;
-    if (a->nprob < 1 || a->nprob > 2 || (a->nprob == 2 && (!a->w[1] || !a->b[1] || !a->y[1])))
-        return cv_bad("tdmpc_lg_conv_fwd: nprob");
-    if (a->n <= 0 || a->cin <= 0 || a->k <= 0 || a->hin < a->k) return cv_bad("tdmpc_lg_conv_fwd: shape");
-    const int ho = (a->hin - a->k) / 2 + 1;
-    CvArgs c;
-    c.x = a->x; c.x_u8 = 0; c.xbs = (long)a->cin * a->hin * a->hin;
-    for (int q = 0; q < 2; ++q) { c.w[q] = a->w[q]; c.b[q] = a->b[q]; c.y[q] = a->y[q]; }
-    c.ybs = 32L * ho * ho;
-    c.nprob = a->nprob; c.n = a->n; c.cin = a->cin; c.hin = a->hin; c.k = a->k; c.in_div = a->in_div;
-    return conv_fwd_launch(c, (hipStream_t)stream);
 }
 
 int tdmpc_lg_conv_bwd_data(const float* dy, const float* w, const float* xact, float* dx, int32_t n, int32_t cin,
@@ -607,16 +567,3 @@ int tdmpc_lg_conv_bwd_weight(const float* dy, const float* x, float in_div, floa
 }
 
 }  // extern "C"
-
-int tdmpc_internal::conv_fwd_init() { return conv_init(); }
-
-// The planner's pixel encoder (tdmpc_kernels.hip, encode): one conv layer + ReLU over n images with per-image strides,
-// uint8 frames read directly on the first layer (x_u8), the same kernels as the learner's forward.
-int tdmpc_internal::conv_fwd(const void* x, int x_u8, long xbs, const float* w, const float* b, float* y, long ybs,
-                             int n, int cin, int hin, int k, float in_div, hipStream_t s) {
-    CvArgs c;
-    c.x = x; c.x_u8 = x_u8; c.xbs = xbs;
-    c.w[0] = c.w[1] = w; c.b[0] = c.b[1] = b; c.y[0] = c.y[1] = y; c.ybs = ybs;
-    c.nprob = 1; c.n = n; c.cin = cin; c.hin = hin; c.k = k; c.in_div = in_div;
-    return conv_fwd_launch(c, s);
-}

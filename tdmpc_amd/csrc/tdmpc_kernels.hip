@@ -36,12 +36,6 @@
 
 #include "../../include/tdmpc_hip.h"
 
-namespace tdmpc_internal {   // learner_conv.hip: the conv forward shared with the learner (the pixel encoder)
-int conv_fwd(const void* x, int x_u8, long xbs, const float* w, const float* b, float* y, long ybs, int n, int cin,
-             int hin, int k, float in_div, hipStream_t s);
-int conv_fwd_init();
-}
-
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 #define DEVI __device__ __forceinline__
@@ -3170,7 +3164,7 @@ int set_lds_attr() {
 int init_attrs() {
     static int done = 0;
     if (done) return 0;
-    int rc = tdmpc_internal::conv_fwd_init();
+    int rc = 0;
 #define SET_ATTR(TM, TN, WGM, WGN, PRO, KCH, ROLL) rc |= set_lds_attr<TM, TN, WGM, WGN, PRO, KCH, ROLL>();
     FOR_EACH_LINEAR(SET_ATTR)
 #undef SET_ATTR
@@ -4188,16 +4182,6 @@ int encode(const Ctx& c, const void* obs, int obs_is_u8, int batch, const float*
             // tiled form when the channels split into groups of 8: (pixels per item, output rows per tile) by a
             // cost model -- rounds of workgroups over the CUs x rounds of items over 256 threads x an item's
             // instructions, plus the staging -- among the shapes whose tile fits LDS
-            if (w.nch == 32) {
-                // 32 channels (the reference's num_channels): the learner's conv kernels on the exact f32 MFMA
-                // (learner_conv.hip: LDS-staged input slabs for the two large layers), uint8 frames / 255 read
-                // directly on the first layer
-                if (int rc = tdmpc_internal::conv_fwd(in, in_u8, in_bs, pw + w.cw[i], pw + w.cb[i], out, (long)act,
-                                                      batch, cin, hi, ks[i], in_u8 ? 255.f : 0.f, c.s))
-                    return rc;
-                in = out; in_u8 = 0; in_bs = (long)act; cin = w.nch;
-                continue;
-            }
             int toy = 0, px = 1;
             if (w.nch % 8 == 0) {
                 double best = 1e300;
