@@ -222,6 +222,20 @@ class Engine:
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
 
+    def _pair(self, main_steps, side_steps):
+        """Issue two independent launch sequences (generators that yield after each launch): main_steps on the
+        caller's stream, side_steps on self.side (forked from it here; the caller joins it back), one launch from
+        each in turn. In the captured graph the main branch (the critical path) then leads: 1.20 vs 1.21 ms per
+        humanoid update against capturing the side branch whole first (profiles/r05/learner_branches.txt)."""
+        main = torch.cuda.current_stream(self.dev)
+        self.side.wait_stream(main)
+        live = [(main, main_steps), (self.side, side_steps)]
+        while live:
+            for e in list(live):
+                with torch.cuda.stream(e[0]):
+                    if next(e[1], StopIteration) is StopIteration:
+                        live.remove(e)
+
     def gemm(self, jobs, tile=None):
         """jobs: dicts (segs, m, n, c, ldc, bias, epi, aux, ldaux, res, ldres, c2, ldc2, std, splits, slice)."""
         arr = (_lib.LgJob * len(jobs))()
@@ -347,43 +361,125 @@ class Engine:
         return s
 
     # ------------------------------------------------------------------------------------------- passes
-    def td_target(self, b, nxo_t, rew, R, eps):
+    def _td_steps(self, b, nxo_t, rew, R, eps):
         """tdmpc.py:184-190 for all H steps: online encoder + pi (TruncatedNormal draws `eps`), target Q, and the
-        target encoder's next_z (tdmpc.py:206-207) -> b["TD"], b["NZ"]."""
+        target encoder's next_z (tdmpc.py:206-207) -> b["TD"], b["NZ"]. A generator: yields after each launch
+        (see _pair)."""
         O, E, L, A, M, LA = self.O, self.E, self.L, self.A, self.M, self.LA
         w, wt = self.w, (lambda k: self.w(k, True))
         nxo = _p(nxo_t)
         if self.pix:   # the conv stacks of both encoders, then their Linear
             F = self.flat
             self.conv_stack(nxo_t, R, [b["yt"], b["yo"]], targets=(True, False))
+            yield
             self.gemm([dict(segs=[_seg(_p(b["yt"][3]), F, wt(LIN_NAME + ".weight"), F, F)], m=R, n=L, c=_p(b["NZ"]),
                             ldc=L, bias=wt(LIN_NAME + ".bias")),
                        dict(segs=[_seg(_p(b["yo"][3]), F, w(LIN_NAME + ".weight"), F, F)], m=R, n=L, c=_p(b["Xtd"]),
                             ldc=LA, bias=w(LIN_NAME + ".bias"))])
+            yield
         else:
             self.gemm([dict(segs=[_seg(nxo, O, wt("_encoder.0.weight"), O, O)], m=R, n=E, c=_p(b["Yt1"]), ldc=E,
                             bias=wt("_encoder.0.bias"), epi=EPI_ELU),
                        dict(segs=[_seg(nxo, O, w("_encoder.0.weight"), O, O)], m=R, n=E, c=_p(b["Yo1"]), ldc=E,
                             bias=w("_encoder.0.bias"), epi=EPI_ELU)])
+            yield
             self.gemm([dict(segs=[_seg(_p(b["Yt1"]), E, wt("_encoder.2.weight"), E, E)], m=R, n=L, c=_p(b["NZ"]),
                             ldc=L, bias=wt("_encoder.2.bias")),
                        dict(segs=[_seg(_p(b["Yo1"]), E, w("_encoder.2.weight"), E, E)], m=R, n=L, c=_p(b["Xtd"]),
                             ldc=LA, bias=w("_encoder.2.bias"))])
+            yield
         self.prod([([(b["Xtd"][:, :L], 0, L)], "_pi.0.weight", b["T1"], "_pi.0.bias", False, False, EPI_ELU, None)])
+        yield
         self.prod([([(b["T1"], 0, M)], "_pi.2.weight", b["T2"], "_pi.2.bias", False, False, EPI_ELU, None)])
+        yield
         self.gemm([dict(segs=[_seg(_p(b["T2"]), M, w("_pi.4.weight"), M, M)], m=R, n=A, c=_p(b["Xtd"], L),
                         ldc=LA, bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MUtd"]), ldc2=A,
                         std=float(self.cfg.min_std))])
+        yield
         PA, PB = b["PAt"], b["PBt"]
         self.prod([([(b["Xtd"], 0, LA)], f"_Q{h + 1}.0.weight", PA[h, :R], f"_Q{h + 1}.0.bias", True, False,
                     EPI_NONE, None) for h in range(2)])
+        yield
         self.rows([dict(x=_p(PA[h]), y=_p(PB[h]), ln=1, g=wt(f"_Q{h + 1}.1.weight"), beta=wt(f"_Q{h + 1}.1.bias"),
                         act=TANH) for h in range(2)], R)
+        yield
         self.prod([([(PB[h, :R], 0, M)], f"_Q{h + 1}.3.weight", PA[h, :R], f"_Q{h + 1}.3.bias", True, False,
                     EPI_NONE, None) for h in range(2)])
+        yield
         self.rows([dict(x=_p(PA[h]), ln=1, g=wt(f"_Q{h + 1}.4.weight"), beta=wt(f"_Q{h + 1}.4.bias"), act=ELU,
                         tail=1, w3=wt(f"_Q{h + 1}.6.weight"), b3=wt(f"_Q{h + 1}.6.bias"), out=_p(b["TQ"][h]))
                    for h in range(2)], R, reward=rew, td=_p(b["TD"]), gamma=float(self.cfg.discount))
+
+    def _fwd_steps(self, b, obs, action, B):
+        """The update's forward (tdmpc.py:199-213): encoder, latent rollout, heads over the H B rollout rows. A
+        generator: yields after each launch (see _pair)."""
+        H, O, E, L, M, LA = self.H, self.O, self.E, self.L, self.M, self.LA
+        R = H * B
+        w, X0 = self.w, b["X0"]
+        if self.pix:
+            F = self.flat
+            self.conv_stack(obs, B, [b["ym"]])
+            yield
+            self.gemm([dict(segs=[_seg(_p(b["ym"][3]), F, w(LIN_NAME + ".weight"), F, F)], m=B, n=L, c=_p(X0), ldc=LA,
+                            bias=w(LIN_NAME + ".bias"))])
+            yield
+        else:
+            self.gemm([dict(segs=[_seg(_p(obs), O, w("_encoder.0.weight"), O, O)], m=B, n=E, c=_p(b["Ye1"]), ldc=E,
+                            bias=w("_encoder.0.bias"), epi=EPI_ELU)])
+            yield
+            self.gemm([dict(segs=[_seg(_p(b["Ye1"]), E, w("_encoder.2.weight"), E, E)], m=B, n=L, c=_p(X0), ldc=LA,
+                            bias=w("_encoder.2.bias"))])
+            yield
+        X0.view(H + 1, B, LA)[:H, :, L:].copy_(action[:H])
+        yield
+        for t in range(H):
+            self.gemm([dict(segs=[_seg(_p(X0, t * B * LA), LA, w("_dynamics.0.weight"), LA, LA)], m=B, n=M,
+                            c=_p(b["Yd1"], t * B * M), ldc=M, bias=w("_dynamics.0.bias"), epi=EPI_ELU)])
+            yield
+            self.gemm([dict(segs=[_seg(_p(b["Yd1"], t * B * M), M, w("_dynamics.2.weight"), M, M)], m=B, n=M,
+                            c=_p(b["Yd2"], t * B * M), ldc=M, bias=w("_dynamics.2.bias"), epi=EPI_ELU)])
+            yield
+            self.gemm([dict(segs=[_seg(_p(b["Yd2"], t * B * M), M, w("_dynamics.4.weight"), M, M)], m=B, n=L,
+                            c=_p(X0, (t + 1) * B * LA), ldc=LA, bias=w("_dynamics.4.bias"),
+                            c2=_p(b["ZP"], t * B * L), ldc2=L)])
+            yield
+        # reward head layer 1 (ELU) rides in its own slot 2 of PA / Y2 buffers, in the Q heads' first-layer launch
+        PA = b["PA"]
+        PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(
+            b, R, [(X0[:R], 0, LA)], extra=[([(X0[:R], 0, LA)], "_reward.0.weight", PA[2, :R], "_reward.0.bias",
+                                              False, False, EPI_ELU, None)])
+        yield
+        self.prod([([(Y1[h, :R], 0, M)], f"_Q{h + 1}.3.weight", PB[h, :R], f"_Q{h + 1}.3.bias", False, False,
+                    EPI_NONE, None) for h in range(2)] +
+                  [([(PA[2, :R], 0, M)], "_reward.2.weight", PB[2, :R], "_reward.2.bias", False, False, EPI_NONE,
+                    None)])
+        yield
+        Q = b["Q"]
+        heads = [dict(x=_p(PB[h]), y=_p(Y2[h]), xhat=_p(XH2[h]), rstd=_p(RS2[h]), ln=1, g=w(f"_Q{h + 1}.4.weight"),
+                      beta=w(f"_Q{h + 1}.4.bias"), act=ELU, tail=1, w3=w(f"_Q{h + 1}.6.weight"),
+                      b3=w(f"_Q{h + 1}.6.bias"), out=_p(Q[h])) for h in range(2)]
+        heads.append(dict(x=_p(PB[2]), y=_p(Y2[2]), act=ELU, tail=1, w3=w("_reward.4.weight"),
+                          b3=w("_reward.4.bias"), out=_p(Q[2])))
+        self.rows(heads, R)
+
+    def _rollout_bwd_steps(self, b, B):
+        """Backward through the latent rollout (tdmpc.py:203-205), newest step first: b["S"] (the heads' gradient
+        of z_t) and dZP -> DG / DZ0. A generator: yields after each launch (see _pair)."""
+        H, L, M, LA = self.H, self.L, self.M, self.LA
+        w, S, dZP = self.w, b["S"], b["dZP"]
+        DG, dP2d, dP1d, DZ0 = b["DG"], b["dP2d"], b["dP1d"], b["DZ0"]
+        for t in range(H - 1, -1, -1):
+            g_t = _p(dZP, H * B * L) if t == H - 1 else _p(DG, t * B * L)     # d loss / d z_{t+1}
+            self.gemm([dict(segs=[_seg(g_t, L, w("_dynamics.4.weight"), M, L, bmode=1)], m=B, n=M,
+                            c=_p(dP2d, t * B * M), ldc=M, epi=EPI_ELU_BWD, aux=_p(b["Yd2"], t * B * M), ldaux=M)])
+            yield
+            self.gemm([dict(segs=[_seg(_p(dP2d, t * B * M), M, w("_dynamics.2.weight"), M, M, bmode=1)], m=B, n=M,
+                            c=_p(dP1d, t * B * M), ldc=M, epi=EPI_ELU_BWD, aux=_p(b["Yd1"], t * B * M), ldaux=M)])
+            yield
+            out = _p(DG, (t - 1) * B * L) if t > 0 else _p(DZ0)
+            self.gemm([dict(segs=[_seg(_p(dP1d, t * B * M), M, w("_dynamics.0.weight"), LA, M, bmode=1)], m=B,
+                            n=L, c=out, ldc=L, res=_p(S, t * B * L), ldres=L)])
+            yield
 
     def q_forward(self, b, n, parts, extra=()):
         """helper.q layer 1 + LayerNorm + Tanh for both Q heads over n rows; the input is the concatenation of
@@ -425,49 +521,11 @@ class Engine:
         rew = _p(rew_t)
         w = self.w
 
-        # ---- TD targets and target latents (no gradient), on the side stream ----
+        # ---- forward (encoder, latent rollout, heads) beside the TD targets and target latents (no gradient) ----
         main = torch.cuda.current_stream(dev)
-        self.side.wait_stream(main)
-        with torch.cuda.stream(self.side):
-            self.td_target(b, nxo_t, rew, R, _p(eps))
-
-        # ---- forward: encoder, latent rollout, heads ----
-        X0 = b["X0"]
-        if self.pix:
-            F = self.flat
-            self.conv_stack(obs, B, [b["ym"]])
-            self.gemm([dict(segs=[_seg(_p(b["ym"][3]), F, w(LIN_NAME + ".weight"), F, F)], m=B, n=L, c=_p(X0), ldc=LA,
-                            bias=w(LIN_NAME + ".bias"))])
-        else:
-            self.gemm([dict(segs=[_seg(_p(obs), O, w("_encoder.0.weight"), O, O)], m=B, n=E, c=_p(b["Ye1"]), ldc=E,
-                            bias=w("_encoder.0.bias"), epi=EPI_ELU)])
-            self.gemm([dict(segs=[_seg(_p(b["Ye1"]), E, w("_encoder.2.weight"), E, E)], m=B, n=L, c=_p(X0), ldc=LA,
-                            bias=w("_encoder.2.bias"))])
-        X0.view(H + 1, B, LA)[:H, :, L:].copy_(action[:H])
-        for t in range(H):
-            self.gemm([dict(segs=[_seg(_p(X0, t * B * LA), LA, w("_dynamics.0.weight"), LA, LA)], m=B, n=M,
-                            c=_p(b["Yd1"], t * B * M), ldc=M, bias=w("_dynamics.0.bias"), epi=EPI_ELU)])
-            self.gemm([dict(segs=[_seg(_p(b["Yd1"], t * B * M), M, w("_dynamics.2.weight"), M, M)], m=B, n=M,
-                            c=_p(b["Yd2"], t * B * M), ldc=M, bias=w("_dynamics.2.bias"), epi=EPI_ELU)])
-            self.gemm([dict(segs=[_seg(_p(b["Yd2"], t * B * M), M, w("_dynamics.4.weight"), M, M)], m=B, n=L,
-                            c=_p(X0, (t + 1) * B * LA), ldc=LA, bias=w("_dynamics.4.bias"),
-                            c2=_p(b["ZP"], t * B * L), ldc2=L)])
-        # reward head layer 1 (ELU) rides in its own slot 2 of PA / Y2 buffers, in the Q heads' first-layer launch
-        PA = b["PA"]
-        PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(
-            b, R, [(X0[:R], 0, LA)], extra=[([(X0[:R], 0, LA)], "_reward.0.weight", PA[2, :R], "_reward.0.bias",
-                                              False, False, EPI_ELU, None)])
-        self.prod([([(Y1[h, :R], 0, M)], f"_Q{h + 1}.3.weight", PB[h, :R], f"_Q{h + 1}.3.bias", False, False,
-                    EPI_NONE, None) for h in range(2)] +
-                  [([(PA[2, :R], 0, M)], "_reward.2.weight", PB[2, :R], "_reward.2.bias", False, False, EPI_NONE,
-                    None)])
-        Q = b["Q"]
-        heads = [dict(x=_p(PB[h]), y=_p(Y2[h]), xhat=_p(XH2[h]), rstd=_p(RS2[h]), ln=1, g=w(f"_Q{h + 1}.4.weight"),
-                      beta=w(f"_Q{h + 1}.4.bias"), act=ELU, tail=1, w3=w(f"_Q{h + 1}.6.weight"),
-                      b3=w(f"_Q{h + 1}.6.bias"), out=_p(Q[h])) for h in range(2)]
-        heads.append(dict(x=_p(PB[2]), y=_p(Y2[2]), act=ELU, tail=1, w3=w("_reward.4.weight"),
-                          b3=w("_reward.4.bias"), out=_p(Q[2])))
-        self.rows(heads, R)
+        self._pair(self._fwd_steps(b, obs, action, B), self._td_steps(b, nxo_t, rew, R, _p(eps)))
+        X0, Q = b["X0"], b["Q"]
+        PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = (b[k] for k in ("PA", "PB", "Y1", "Y2", "XH1", "XH2", "RS1", "RS2"))
 
         main.wait_stream(self.side)   # TD / NZ ready
         # ---- losses (fused HIP loss, include/tdmpc_learner.h) ----
@@ -511,20 +569,17 @@ class Engine:
         for h in range(2):
             dw_h += [(f"_Q{h + 1}.3", M, M, [_seg(_p(dP2[h]), M, _p(Y1[h]), M, R, 1, 1, M)], sp),
                      (f"_Q{h + 1}.0", M, LA, [_seg(_p(dP1[h]), M, _p(X0), LA, R, 1, 1, LA)], sp)]
-        self.side.wait_stream(main)
-        with torch.cuda.stream(self.side):
-            slots = self._dw(b, "mainh", dw_h)
-        # ---- backward through the latent rollout (tdmpc.py:203-205), newest step first ----
+        # pi's forward over the detached latents z_0..z_H for update_pi (reads X0 and pi's weights only, which the
+        # main optimiser step does not touch) rides on the side stream after them
+        slots = {}
+
+        def side_steps():
+            slots.update(self._dw(b, "mainh", dw_h))
+            yield
+            yield from self._pi_fwd_steps(b, X0[:, :L], R1, _p(eps, R * A))
+
+        self._pair(self._rollout_bwd_steps(b, B), side_steps())
         DG, dP2d, dP1d, DZ0 = b["DG"], b["dP2d"], b["dP1d"], b["DZ0"]
-        for t in range(H - 1, -1, -1):
-            g_t = _p(dZP, H * B * L) if t == H - 1 else _p(DG, t * B * L)     # d loss / d z_{t+1}
-            self.gemm([dict(segs=[_seg(g_t, L, w("_dynamics.4.weight"), M, L, bmode=1)], m=B, n=M,
-                            c=_p(dP2d, t * B * M), ldc=M, epi=EPI_ELU_BWD, aux=_p(b["Yd2"], t * B * M), ldaux=M)])
-            self.gemm([dict(segs=[_seg(_p(dP2d, t * B * M), M, w("_dynamics.2.weight"), M, M, bmode=1)], m=B, n=M,
-                            c=_p(dP1d, t * B * M), ldc=M, epi=EPI_ELU_BWD, aux=_p(b["Yd1"], t * B * M), ldaux=M)])
-            out = _p(DG, (t - 1) * B * L) if t > 0 else _p(DZ0)
-            self.gemm([dict(segs=[_seg(_p(dP1d, t * B * M), M, w("_dynamics.0.weight"), LA, M, bmode=1)], m=B,
-                            n=L, c=out, ldc=L, res=_p(S, t * B * L), ldres=L)])
         conv = {}
         if self.pix:   # Linear backward with the last conv's ReLU mask, then the conv stack's backward
             F = self.flat
@@ -571,7 +626,7 @@ class Engine:
         buffer.update_priorities(idxs, b["lrows"][3].view(B, 1))
 
         # ---- update_pi on the detached latents z_0..z_H (tdmpc.py:165-182) ----
-        pi_loss = self._update_pi(b, X0[:, :L], H + 1, B, _p(eps, R * A))
+        pi_loss = self._update_pi(b, X0[:, :L], H + 1, B, _p(eps, R * A), pi_fwd_done=True)
         scal = b["scal"]
         return torch.cat([scal[0:3], pi_loss, scal[3:5], b["gnorm"]])
 
@@ -609,18 +664,30 @@ class Engine:
                                           opt.lr, 0.9, 0.999, 1e-8, float(self.cfg.grad_clip_norm), norm_out, st),
                    "tdmpc_lg_adam")
 
-    def _update_pi(self, b, zt, nt, B, eps):
+    def _pi_fwd_steps(self, b, zt, n, eps):
+        """pi's forward for update_pi over the n rows of zt (TruncatedNormal draws `eps`) -> b["Yp1"], b["Yp2"],
+        b["ACT"], b["MU"]. A generator: yields after each launch (see _pair)."""
+        L, A, M = self.L, self.A, self.M
+        w = self.w
+        self.prod([([(zt, 0, L)], "_pi.0.weight", b["Yp1"][:n], "_pi.0.bias", False, False, EPI_ELU, None)])
+        yield
+        self.prod([([(b["Yp1"][:n], 0, M)], "_pi.2.weight", b["Yp2"][:n], "_pi.2.bias", False, False, EPI_ELU, None)])
+        yield
+        self.gemm([dict(segs=[_seg(_p(b["Yp2"]), M, w("_pi.4.weight"), M, M)], m=n, n=A, c=_p(b["ACT"]), ldc=A,
+                        bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MU"]), ldc2=A,
+                        std=float(self.cfg.min_std))])
+        yield
+
+    def _update_pi(self, b, zt, nt, B, eps, pi_fwd_done=False):
         """TDMPC.update_pi over the nt latent blocks of B rows of zt ([nt B, L], rows may be strided) -> pi_loss
-        tensor [1]."""
+        tensor [1]. pi_fwd_done: _pi_fwd_steps already ran over the same rows and draws."""
         L, A, M, LA = self.L, self.A, self.M, self.LA
         n = nt * B
         w = self.w
         z, ldz = _p(zt), zt.stride(0)
-        self.prod([([(zt, 0, L)], "_pi.0.weight", b["Yp1"][:n], "_pi.0.bias", False, False, EPI_ELU, None)])
-        self.prod([([(b["Yp1"][:n], 0, M)], "_pi.2.weight", b["Yp2"][:n], "_pi.2.bias", False, False, EPI_ELU, None)])
-        self.gemm([dict(segs=[_seg(_p(b["Yp2"]), M, w("_pi.4.weight"), M, M)], m=n, n=A, c=_p(b["ACT"]), ldc=A,
-                        bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MU"]), ldc2=A,
-                        std=float(self.cfg.min_std))])
+        if not pi_fwd_done:
+            for _ in self._pi_fwd_steps(b, zt, n, eps):
+                pass
         PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(b, n, [(zt, 0, L), (b["ACT"][:n], L, LA)])
         self.prod([([(Y1[h, :n], 0, M)], f"_Q{h + 1}.3.weight", PB[h, :n], f"_Q{h + 1}.3.bias", False, False,
                     EPI_NONE, None) for h in range(2)])

@@ -16,7 +16,7 @@
 #   stamps           per-step shader stamps of the wide step kernel (needs the `ws` variant: -DWS_STAMPS)
 #   learner:VAR=v1,v2  the learner / train-loop / adam tests, then an A/B of VAR on the humanoid update time
 #   lab:VAR=v1,v2    the humanoid update-time A/B of `learner:` without its tests
-#   lgbench          lg_gemm tile timings of the learner's products (tools/lg_gemm_bench.py --lds)
+#   lgbench          lg_gemm tile timings of the learner's products (tools/lg_gemm_bench.py)
 #   p1stamps         per-hand-off timeline of the one-env persistent plan (tools/p1_stamps.py)
 #   qt               tools/quick_time.py on CONFIG / ENVS (qt.txt)
 # Environment: CONFIG (default humanoid-run), ENVS (default 32).
@@ -131,7 +131,7 @@ PY
         done
       done ;;
     lgbench)
-      timeout -k 10 200 python -u tools/lg_gemm_bench.py --lds > "$OUT/lg_gemm.txt" 2>&1 || { tail -20 "$OUT/lg_gemm.txt"; exit 1; }
+      timeout -k 10 200 python -u tools/lg_gemm_bench.py > "$OUT/lg_gemm.txt" 2>&1 || { tail -20 "$OUT/lg_gemm.txt"; exit 1; }
       grep -v amdgpu.ids "$OUT/lg_gemm.txt" | tail -30 ;;
     p1stamps)
       timeout -k 10 120 python -u tools/p1_stamps.py "$CONFIG" > "$OUT/p1_stamps.txt" 2>&1 || { tail -20 "$OUT/p1_stamps.txt"; exit 1; }
