@@ -806,6 +806,32 @@ def job_rate(elapsed, units_per_rank, dist, device):
     return elapsed, world * units_per_rank / elapsed
 
 
+def summary_line(out, cfg):
+    """A compact record of every leg (the driver keeps only the tail of the JSON line): per config its plan-steps/s,
+    the dominant step kernel's fraction of its roof and helper.q's; then the single env, the learner, iCEM and the
+    CPU speedup. Keys name the latent explicitly: BASELINE.json configs[2] says latent 512, the reference's
+    cfgs/tasks/humanoid.yaml:6 says 100 -- both are measured."""
+    def leg(v, roof):
+        if v is None:
+            return None
+        r = roof or {}
+        q = r.get("q_head") or {}
+        return [round(v, 1), r.get("frac"), q.get("frac_of_x6_peak"), (r.get("kernel") or "").split(" (")[0]]
+    s = {f"{out['config']['workload'].split(':')[0]} L{cfg.latent_dim} B{out['config']['envs_per_gpu']}":
+         leg(out["value"], out.get("roofline"))}
+    for k, v in (out.get("configs") or {}).items():
+        s[k] = leg(v.get("value"), v.get("roofline"))
+    s["_fields"] = "[plan-steps/s, step-kernel frac of x6 roof, helper.q frac, step kernel]"
+    se = out.get("single_env") or {}
+    s["single_env_plan"] = se.get("value")
+    ln = out.get("learner") or {}
+    s["learner_graph_ms"] = (ln.get("graph") or {}).get("ms_per_update") if isinstance(ln.get("graph"), dict) else ln.get("graph")
+    ic = out.get("icem") or {}
+    s["icem_single_b32"] = [ic.get("value"), (ic.get("batch32") or {}).get("value")]
+    s["x_cpu"] = out.get("speedup_vs_cpu")
+    return s
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1005,7 +1031,8 @@ def main():
             out["speedup_vs_cpu"] = round(value / world / cpu["value"], 2)
             if single:
                 single["speedup_vs_cpu"] = round(single["value"] / cpu["value"], 2)
-        out["single_env"] = single   # (last: the driver keeps the tail of the line)
+        out["single_env"] = single
+        out["summary"] = summary_line(out, cfg)   # (last: the driver keeps the tail of the line)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

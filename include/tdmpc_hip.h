@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define TDMPC_ABI_VERSION 7
+#define TDMPC_ABI_VERSION 8
 
 #define TDMPC_OK 0
 #define TDMPC_E_DIMS (-1)     /* unsupported or inconsistent dims / params */
@@ -92,6 +92,13 @@ typedef struct tdmpc_plan_params {
 /* tdmpc_plan_params.status bits */
 #define TDMPC_STATUS_P1_TIMEOUT 1   /* the persistent one-env plan (path 9 / auto at batch 1) gave up at a hand-off:
                                        not every workgroup of its grid was resident (e.g. other work held CUs) */
+#define TDMPC_STATUS_PACK_STALE 2   /* ABI 8: a tdmpc_pack_weights launch found another job table in `packed` than the
+                                       one it was issued for (the buffer was re-allocated or zeroed at a recorded
+                                       address without tdmpc_pack_forget and packed under capture, or a captured
+                                       graph's pack replayed after the buffer was re-keyed): it packed nothing and
+                                       poisoned the weights with NaN. Sticky in the packed buffer until the next
+                                       uncaptured pack; tdmpc_plan, tdmpc_plan_icem and tdmpc_cem_iter OR it into
+                                       their status word and return NaN actions / metrics. */
 
 #define TDMPC_PATH_AUTO 0
 #define TDMPC_PATH_LAYERED 1
@@ -153,19 +160,23 @@ int tdmpc_num_param_tensors(const tdmpc_dims* dims);
 /* Pack the TOLD parameters (device pointers, reference state_dict order, fp32, contiguous nn.Linear
  * [out,in] / Conv2d [out,in,kh,kw] layout) into `packed` (replaces TDMPC.model for planning). ONE kernel
  * launch enqueued on `stream`. Its job table lives in `packed` itself (no library-global device memory): every
- * call outside a stream capture uploads it (an async copy queued before the launch); a call inside a capture
- * uploads nothing and requires the same tensors as this buffer's last uncaptured pack (pack once before
- * capturing). Re-run whenever the
- * parameters change (after TDMPC.update -- the learner does so from its flat parameter buffer inside its
- * update graph). When allocated, `packed` must be zero-filled once (every tensor's region is rewritten whole,
- * padding included, but the alignment gaps between regions are not, and padded vector reads may touch them)
- * and announced with tdmpc_pack_forget (its address may be a freed buffer's). */
+ * call outside a stream capture uploads it with a header naming it (a nonce); a call inside a capture uploads
+ * nothing and requires the same tensors as this buffer's last uncaptured pack (pack once before capturing).
+ * The kernel checks the header's nonce against the table the call was issued for: a mismatch (a buffer
+ * re-allocated or zeroed at a known address and packed first under capture, a replayed graph whose buffer was
+ * re-keyed since) packs nothing, NaN-poisons the weights and raises TDMPC_STATUS_PACK_STALE, which the next plan
+ * passes on -- never silently zero or stale weights. Once a capture has packed into `packed`, an uncaptured pack
+ * from OTHER tensors returns TDMPC_E_DIMS until tdmpc_pack_forget(packed). Re-run whenever the parameters change
+ * (after TDMPC.update -- the learner does so from its flat parameter buffer inside its update graph). When
+ * allocated, `packed` must be zero-filled once (every tensor's region is rewritten whole, padding included, but
+ * the alignment gaps between regions are not, and padded vector reads may touch them); announcing it with
+ * tdmpc_pack_forget is good practice (a skipped call is caught by the nonce check, not silently wrong). */
 int tdmpc_pack_weights(const tdmpc_dims* dims, const float* const* tensors, int32_t n_tensors,
                        void* packed, size_t packed_bytes, void* stream);
 
-/* A packed buffer was (re)allocated at `packed`: forget the job table the library last uploaded at that address
- * (and free its pinned staging buffer), so that a captured pack into the new buffer cannot pass on the old buffer's
- * record. Returns 0. */
+/* A packed buffer was (re)allocated or is re-keyed at `packed`: forget the job table the library last uploaded at
+ * that address (and free its pinned staging buffer). The next uncaptured pack uploads a table with a new nonce;
+ * graphs captured over the old table then fail loudly (TDMPC_STATUS_PACK_STALE) if replayed. Returns 0. */
 int tdmpc_pack_forget(const void* packed);
 
 /* Diagnostic, host only (no HIP call): bounds-checks tdmpc_pack_weights' job table for these dims, given the
@@ -221,6 +232,7 @@ typedef struct tdmpc_icem_params {
     int64_t env_stride;       /* floats per env noise stream */
     float min_std, temperature, momentum, one_minus_momentum, std_floor, init_std;
     float discount_pow[17];
+    int32_t* status;          /* ABI 8: optional device int32, sticky (tdmpc_plan_params.status) */
 } tdmpc_icem_params;
 
 /* Sizes for tdmpc_plan_icem (the workspace holds N + K + num_pi rows per env). */

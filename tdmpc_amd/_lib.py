@@ -11,7 +11,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TDMPC_LIB_PATH") or os.path.join(HERE, "libtdmpc_hip.so")   # override: A/B of builds
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 PATHS = {"auto": 0, "layered": 1, "chain": 2, "chain32": 3, "chain16": 4, "split": 5, "chain_x6": 6, "split_x6": 7, "chain64": 8, "persist": 9, "wide": 10}
 
 EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc_num_param_tensors",
@@ -27,6 +27,26 @@ EXPORTED = ("tdmpc_abi_version", "tdmpc_sizes_for", "tdmpc_noise_floats", "tdmpc
             "tdmpc_lg_gemm", "tdmpc_lg_rows_fwd", "tdmpc_lg_rows_bwd", "tdmpc_lg_pi_loss", "tdmpc_lg_finalize",
             "tdmpc_lg_adam", "tdmpc_lg_lerp", "tdmpc_lg_act", "tdmpc_lg_conv_fwd", "tdmpc_lg_conv_bwd_data",
             "tdmpc_lg_conv_bwd_weight")
+
+
+# tdmpc_plan_params.status bits (include/tdmpc_hip.h)
+STATUS_P1_TIMEOUT = 1
+STATUS_PACK_STALE = 2
+
+
+def status_text(st: int) -> str:
+    """What a nonzero device status word means (each set bit)."""
+    parts = []
+    if st & STATUS_P1_TIMEOUT:
+        parts.append("the persistent one-env plan timed out at a hand-off -- not every workgroup of its grid was "
+                     "resident; set TDMPC_PERSIST=0 to plan on the launch chain instead")
+    if st & STATUS_PACK_STALE:
+        parts.append("the weight pack found another job table in the packed buffer than the one it was issued for "
+                     "(a re-allocated or re-keyed buffer packed under capture without tdmpc_pack_forget): the "
+                     "weights are NaN until the next uncaptured pack")
+    if st & ~(STATUS_P1_TIMEOUT | STATUS_PACK_STALE):
+        parts.append(f"unknown bits {st & ~(STATUS_P1_TIMEOUT | STATUS_PACK_STALE):#x}")
+    return "; ".join(parts)
 
 
 class Dims(C.Structure):
@@ -52,7 +72,7 @@ class IcemParams(C.Structure):
                 ("samp_off", C.c_int64 * 16), ("term_off", C.c_int64 * 16)] + \
                [(n, C.c_int64) for n in ("reuse_off", "pi_off", "act_off", "env_stride")] + \
                [(n, C.c_float) for n in ("min_std", "temperature", "momentum", "one_minus_momentum", "std_floor",
-                                         "init_std")] + [("discount_pow", C.c_float * 17)]
+                                         "init_std")] + [("discount_pow", C.c_float * 17), ("status", C.c_void_p)]
 
 
 class ReplayDims(C.Structure):

@@ -28,8 +28,11 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <mutex>
 #include <type_traits>
 #include <vector>
@@ -104,7 +107,8 @@ struct Layout {
     // k = 32 g + 16 (j >> 2) + 4 q + (j & 3) -- the v_mfma_f32_16x16x32_bf16 A fragment, in the k order in which a
     // 16x16 accumulator tile pair (a lane holding features 16t + 4q + i of its row) is the next layer's B fragment
     size_t x6q[9];   // (X6_N: every x6 matrix; the wide kernels read W1X .. W3D and WQ1X, WQ2)
-    size_t jobtab;   // the fused pack's job table (launch_pack): caller-owned, lives and dies with the packed buffer
+    size_t jobtab;   // the fused pack's header (PackHdr: table nonce, sticky status) + job table (launch_pack):
+                     // caller-owned, lives and dies with the packed buffer
     // helper.q's LayerNorm-1 statistics block (wide_heads.inc; written by qstat_*_kernel after every pack) for planners
     // whose batches reach the wide kernels: nqs = the first layer's real columns + its bias (A + L + 1), 0 = none
     int nqs, nsr;          // columns of the Cholesky factor; statistics rows per Q head (16 x 8 or 16 x 16)
@@ -115,6 +119,16 @@ struct Layout {
 };
 constexpr int PACK_MAX_JOBS = 96;              // job-table capacity (pack_jobs emits ~40-60)
 constexpr int PACK_JOB_BYTES = 192;            // >= sizeof(PackJob) (static_assert at its definition)
+constexpr int PACK_HDR_BYTES = 256;            // PackHdr slot ahead of the job table
+// The header of the packed buffer's job table. `nonce` names the table last uploaded into the buffer; every pack
+// launch carries the nonce of the table its host record says is there and checks it on the device, so a pack that
+// would read another table (a re-allocated or re-zeroed buffer, a captured graph whose buffer was re-keyed) poisons
+// the weights and raises `status` instead of packing from stale pointers. `status` is sticky until the next upload;
+// every plan ORs it into the caller's status word (TDMPC_STATUS_PACK_STALE).
+struct PackHdr {
+    unsigned long long nonce;
+    int status, njobs;
+};
 
 // Matrices kept in the x6 layout: fp32 = hi + mid + lo, three bf16 planes. Block (nb, g) of 32 rows x 16 k is
 // [3 planes][64 lanes][8 bf16]: lane l (r = l & 31, h = l >> 5) element j holds row 32 nb + r,
@@ -191,7 +205,7 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
         x6_shape(*w, i, &r, &k);
         w->x6q[i] = take(rup(r, 16) * rup(k, 32) * 3 / 2);
     }
-    w->jobtab = take((size_t)PACK_MAX_JOBS * PACK_JOB_BYTES / 4);
+    w->jobtab = take((size_t)(PACK_HDR_BYTES + PACK_MAX_JOBS * PACK_JOB_BYTES) / 4);
     // the statistics block: only where the wide heads may run (B N >= 4096 rows, M = 512) and the Cholesky's
     // upper-packed fp64 factor fits one workgroup's LDS
     w->nqs = w->nsr = 0;
@@ -2714,6 +2728,7 @@ struct CemArgs {
     float* action; float* metrics;
     float* elite_out; float* score_out; float* mean_out; float* std_out;
     int no_pick; float* reward_out;     // tdmpc_cem_iter: stop after the refit; reward mean -> reward_out [B]
+    const int* pstatus; int* status;    // the packed buffer's sticky pack status -> the caller's status word
 };
 
 DEVI uint32_t f2ord(float v) {
@@ -2859,6 +2874,10 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
     if (a.elite_store)
         for (int i = tid; i < HKA; i += nt) a.elite_store[(size_t)e * a.Hmax * a.K * A + i] = EA[i];
     if (!a.final_iter) return;
+    // a stale pack (PackHdr.status) poisoned the weights: raise it into the caller's word, NaN the outputs below
+    const int pst = a.pstatus ? *a.pstatus : 0;
+    if (pst && tid == 0 && a.status)
+        __hip_atomic_fetch_or(a.status, pst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (a.elite_out)
         for (int i = tid; i < HKA; i += nt) a.elite_out[(size_t)e * HKA + i] = EA[i];
     if (a.score_out && tid < K) a.score_out[(size_t)e * K + tid] = sc[tid];
@@ -2895,14 +2914,15 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
         for (int w = 0; w < nwv; ++w) rs += red[1 + w];
         float cs = 0.f;
         for (int c = 0; c < A; ++c) cs += sstd[c];
-        a.metrics[(size_t)e * 2 + 0] = rs / (float)T;   // estimate_value's reward.mean() (last iteration)
-        a.metrics[(size_t)e * 2 + 1] = cs / (float)A;   // _std[0].mean()
+        a.metrics[(size_t)e * 2 + 0] = pst ? __builtin_nanf("") : rs / (float)T;   // estimate_value's reward.mean()
+        a.metrics[(size_t)e * 2 + 1] = pst ? __builtin_nanf("") : cs / (float)A;   // _std[0].mean()
     }
     __syncthreads();
     const int j = *jsel;
     for (int c = tid; c < A; c += nt) {
         float v = EA[(size_t)j * A + c];
         if (!a.eval_mode) v = fadd(v, fmul(sstd[c], a.eps[(size_t)e * a.eps_env + a.eps_act_off + c]));
+        if (pst) v = __builtin_nanf("");
         a.action[(size_t)e * A + c] = v;
         // the reference adds the action noise in place to a view of its stored elites (`a = actions[0]`,
         // tdmpc_icem_similarity_mlp.py:255-259): the kept elite[0][j] carries it
@@ -4269,6 +4289,11 @@ __global__ void zero_words_kernel(unsigned* p, int n) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0u;
 }
 
+// the packed buffer's sticky pack status (PackHdr::status, TDMPC_STATUS_PACK_STALE)
+inline const int* pack_status(const Ctx& c) {
+    return (const int*)((const char*)(c.pw + c.w.jobtab) + offsetof(PackHdr, status));
+}
+
 int plan1_launch(const Ctx& c, const tdmpc_plan_params* prm, const float* noise, const double* u, float* prev_mean,
                  float* action, float* metrics, float* elite_out, float* score_out, float* value_out, float* mean_out,
                  float* std_out) {
@@ -4297,6 +4322,7 @@ int plan1_launch(const Ctx& c, const tdmpc_plan_params* prm, const float* noise,
     a.o_qm = rg.o_qm; a.o_qp = rg.o_qp; a.o_val = rg.o_val; a.o_rl = rg.o_rl; a.o_mu = rg.o_mu; a.o_y2 = rg.o_y2; a.pi_cache = pi_cache_on(); a.xb_t = rg.xb_t; a.xb_g = rg.xb_g;
     a.stamps = g_p1_stamps;
     a.status = prm->status;
+    a.pstatus = pack_status(c);
     {
         const char* e = getenv("TDMPC_P1_DEBUG_SKIP");   // test knob, read per launch (captured with the graph)
         a.debug_skip = e && atoi(e) ? 1 : 0;
@@ -4372,7 +4398,17 @@ struct PackJob {
 static_assert(sizeof(PackJob) <= PACK_JOB_BYTES, "job-table slot");
 constexpr int PACK_WG = 256, PACK_PER = 8;   // threads per workgroup, items per thread
 
-__global__ void __launch_bounds__(PACK_WG) pack_fused_kernel(const PackJob* jobs, int nj, float* pw) {
+__global__ void __launch_bounds__(PACK_WG) pack_fused_kernel(PackHdr* hdr, const PackJob* jobs, int nj, float* pw,
+                                                              unsigned long long nonce, long nweights) {
+    if (hdr->nonce != nonce) {
+        // not the table this launch was issued for (the buffer was re-allocated, re-zeroed or re-keyed since): pack
+        // nothing from it, poison every weight region and raise the buffer's sticky status (plans pass it on)
+        for (long i = (long)blockIdx.x * PACK_WG + threadIdx.x; i < nweights; i += (long)gridDim.x * PACK_WG)
+            pw[i] = __builtin_nanf("");
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            __hip_atomic_fetch_or(&hdr->status, TDMPC_STATUS_PACK_STALE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     // the workgroup's job: last job whose blk0 <= blockIdx.x (binary search over the job table)
     int lo = 0, hi = nj - 1;
     while (lo < hi) {
@@ -4527,25 +4563,49 @@ void pack_jobs(const Layout& w, const float* const* t, std::vector<PackJob>& job
 
 // The job table lives in the caller's packed buffer (Layout::jobtab), so it lives and dies with that buffer and the
 // HIP graphs the caller captured over it -- nothing device-side is global or leaks. Every pack outside a stream
-// capture uploads the table (an async copy from a pinned staging buffer kept per packed buffer, whose previous copy's
-// event is waited for before it is rewritten -- long done by then); a pack inside a capture uploads nothing and
-// requires the table last uploaded into that buffer to be this one (pack once before capturing, as the learner
-// does). The host keeps the staging buffers in a small LRU (PACK_HOST_CACHE entries, freed on eviction);
-// tdmpc_pack_forget drops a buffer's entry when its address is re-allocated. One mutex guards it.
+// capture uploads header + table (an async copy from a pinned staging buffer kept per packed buffer, whose previous
+// copy's event is waited for before it is rewritten -- long done by then); a pack inside a capture uploads nothing and
+// requires the table last uploaded into that buffer to be this one (pack once before capturing, as the learner does).
+// Staleness is checked on the device, not trusted from the host record: every launch carries the nonce of the table
+// the record says is in the buffer and pack_fused_kernel compares it with the header's (a buffer re-allocated at a
+// recorded address or zeroed again fails loudly: NaN weights + TDMPC_STATUS_PACK_STALE). An uncaptured pack keeps the
+// record's nonce when its table is unchanged (graphs captured over the buffer stay valid) and draws a new one
+// otherwise; once a capture has packed from a buffer, an uncaptured pack with OTHER tensors is refused (it would
+// silently re-point the captured graph) until tdmpc_pack_forget drops the record -- after which such a graph's pack
+// sees a nonce mismatch and fails loudly. Records live until tdmpc_pack_forget; only their pinned staging buffers are
+// recycled (PACK_PINNED of them, least recently used first). One mutex guards it.
 struct PackTable {
     std::vector<PackJob> host; const float* pw; int device;
-    PackJob* pinned; hipEvent_t done; bool recorded;
+    unsigned long long nonce; bool captured;
+    char* pinned; hipEvent_t done; bool recorded;
 };
 std::vector<PackTable> g_pack_tables;   // most recently used last
 std::mutex g_pack_mu;
-constexpr size_t PACK_HOST_CACHE = 64;
+constexpr size_t PACK_PINNED = 64;
+constexpr size_t PACK_UPLOAD_BYTES = (size_t)PACK_HDR_BYTES + (size_t)PACK_MAX_JOBS * sizeof(PackJob);
 
-void pack_table_free(PackTable& t) {
+void pack_table_unpin(PackTable& t) {
     if (t.recorded) (void)hipEventSynchronize(t.done);
     if (t.done) (void)hipEventDestroy(t.done);
     if (t.pinned) (void)hipHostFree(t.pinned);
     t.pinned = nullptr;
     t.done = nullptr;
+    t.recorded = false;
+}
+
+// table nonces: never 0 (a zeroed buffer's header) and distinct across processes and buffers with high probability
+unsigned long long pack_next_nonce() {
+    static std::atomic<unsigned long long> ctr{0};
+    static const unsigned long long base =
+        ((unsigned long long)std::chrono::high_resolution_clock::now().time_since_epoch().count() * 0x9E3779B97F4A7C15ull) ^
+        ((unsigned long long)getpid() << 32);
+    for (;;) {
+        unsigned long long z = base + 0x9E3779B97F4A7C15ull * (ctr.fetch_add(1) + 1);   // splitmix64 finaliser
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        if (z) return z;
+    }
 }
 
 int launch_pack(std::vector<PackJob>& jobs, const Layout& w, float* pw, hipStream_t s) {
@@ -4561,45 +4621,65 @@ int launch_pack(std::vector<PackJob>& jobs, const Layout& w, float* pw, hipStrea
     const size_t nb = jobs.size() * sizeof(PackJob);
     int device = 0;
     HIPCHK(hipGetDevice(&device));
-    PackJob* dev = (PackJob*)(pw + w.jobtab);
+    PackHdr* hdr = (PackHdr*)(pw + w.jobtab);
+    PackJob* dev = (PackJob*)((char*)hdr + PACK_HDR_BYTES);
+    unsigned long long nonce = 0;
     {
         std::lock_guard<std::mutex> lock(g_pack_mu);
         size_t hit = g_pack_tables.size();
         for (size_t i = 0; i < g_pack_tables.size(); ++i)
             if (g_pack_tables[i].pw == pw && g_pack_tables[i].device == device) { hit = i; break; }
+        const bool same = hit < g_pack_tables.size() && g_pack_tables[hit].host.size() == jobs.size() &&
+                          !memcmp(g_pack_tables[hit].host.data(), jobs.data(), nb);
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         HIPCHK(hipStreamIsCapturing(s, &cs));
         if (cs != hipStreamCaptureStatusNone) {
-            if (hit == g_pack_tables.size() || g_pack_tables[hit].host.size() != jobs.size() ||
-                memcmp(g_pack_tables[hit].host.data(), jobs.data(), nb)) {
-                snprintf(g_err, sizeof g_err, "tdmpc_pack_weights: new tensors while capturing (pack once before capture)");
+            if (!same) {
+                snprintf(g_err, sizeof g_err, hit == g_pack_tables.size()
+                         ? "tdmpc_pack_weights: no table uploaded into this buffer while capturing (pack once before capture)"
+                         : "tdmpc_pack_weights: new tensors while capturing (pack once before capture)");
                 return TDMPC_E_DIMS;
             }
+            g_pack_tables[hit].captured = true;
         } else {
+            if (hit < g_pack_tables.size() && g_pack_tables[hit].captured && !same) {
+                snprintf(g_err, sizeof g_err, "tdmpc_pack_weights: a captured graph packs into this buffer from other "
+                         "tensors; call tdmpc_pack_forget(packed) first (that graph's pack then fails loudly)");
+                return TDMPC_E_DIMS;
+            }
             if (hit == g_pack_tables.size()) {
-                if (g_pack_tables.size() >= PACK_HOST_CACHE) {
-                    pack_table_free(g_pack_tables.front());
-                    g_pack_tables.erase(g_pack_tables.begin());
-                }
-                PackTable t{{}, pw, device, nullptr, nullptr, false};
-                HIPCHK(hipHostMalloc((void**)&t.pinned, (size_t)PACK_MAX_JOBS * sizeof(PackJob), hipHostMallocDefault));
-                HIPCHK(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
-                g_pack_tables.push_back(std::move(t));
+                g_pack_tables.push_back(PackTable{{}, pw, device, 0, false, nullptr, nullptr, false});
                 hit = g_pack_tables.size() - 1;
             }
             PackTable& t = g_pack_tables[hit];
+            if (!same || !t.nonce) t.nonce = pack_next_nonce();
+            if (!t.pinned) {
+                size_t npin = 0;
+                for (const PackTable& o : g_pack_tables) npin += o.pinned != nullptr;
+                for (size_t i = 0; npin >= PACK_PINNED && i < g_pack_tables.size(); ++i)
+                    if (g_pack_tables[i].pinned) { pack_table_unpin(g_pack_tables[i]); --npin; }
+                HIPCHK(hipHostMalloc((void**)&t.pinned, PACK_UPLOAD_BYTES, hipHostMallocDefault));
+                HIPCHK(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
+            }
             if (t.recorded) HIPCHK(hipEventSynchronize(t.done));
-            memcpy(t.pinned, jobs.data(), nb);
-            HIPCHK(hipMemcpyAsync(dev, t.pinned, nb, hipMemcpyHostToDevice, s));
+            PackHdr h;
+            memset(&h, 0, sizeof h);
+            h.nonce = t.nonce; h.status = 0; h.njobs = (int)jobs.size();
+            memset(t.pinned, 0, PACK_HDR_BYTES);
+            memcpy(t.pinned, &h, sizeof h);
+            memcpy(t.pinned + PACK_HDR_BYTES, jobs.data(), nb);
+            HIPCHK(hipMemcpyAsync(hdr, t.pinned, PACK_HDR_BYTES + nb, hipMemcpyHostToDevice, s));
             HIPCHK(hipEventRecord(t.done, s));
             t.recorded = true;
             t.host = jobs;
         }
+        nonce = g_pack_tables[hit].nonce;
         PackTable t = std::move(g_pack_tables[hit]);   // most recently used last
         g_pack_tables.erase(g_pack_tables.begin() + hit);
         g_pack_tables.push_back(std::move(t));
     }
-    hipLaunchKernelGGL(pack_fused_kernel, dim3((unsigned)blk), dim3(PACK_WG), 0, s, dev, (int)jobs.size(), pw);
+    hipLaunchKernelGGL(pack_fused_kernel, dim3((unsigned)blk), dim3(PACK_WG), 0, s, hdr, (const PackJob*)dev,
+                       (int)jobs.size(), pw, nonce, (long)w.jobtab);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -4798,7 +4878,7 @@ int tdmpc_pack_forget(const void* packed) {
     std::lock_guard<std::mutex> lock(g_pack_mu);
     for (size_t i = 0; i < g_pack_tables.size(); ++i)
         if (g_pack_tables[i].pw == (const float*)packed) {
-            pack_table_free(g_pack_tables[i]);
+            pack_table_unpin(g_pack_tables[i]);
             g_pack_tables.erase(g_pack_tables.begin() + i);
             break;
         }
@@ -4913,6 +4993,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     ca.std_floor_p = prm->std_floor_dev;
     ca.elite_out = elite_out; ca.score_out = score_out; ca.mean_out = mean_out; ca.std_out = std_out;
     ca.value_out = value_out;
+    ca.pstatus = pack_status(c); ca.status = prm->status;
     const bool wide_heads = use_wide_heads(c);
     if (wide_heads || use_chain(c, B * T, 2, CK_Q)) {   // q1, q2 per row in k.qv; cem_kernel forms the values
         ca.G = c.k.G; ca.qv = c.k.qv; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H];
@@ -5022,6 +5103,7 @@ int tdmpc_plan_icem(const tdmpc_dims* d, const tdmpc_icem_params* prm, const voi
     ca.omm = prm->one_minus_momentum; ca.std_floor = prm->std_floor; ca.action = action; ca.metrics = metrics;
     ca.mean_out = mean_out; ca.std_out = std_out; ca.elite_store = elites;
     ca.G = c.k.G; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H]; ca.value_out = value_out;
+    ca.pstatus = pack_status(c); ca.status = prm->status;
     const size_t cem_lds = cem_lds_bytes(Tw, H, K, c.A);
     for (int i = 0; i < I; ++i) {
         const int Ni = prm->n_samples[i], Pi = prm->n_pi[i], Ei = prm->n_elite[i], NE = Ni + Ei;
@@ -5190,6 +5272,7 @@ int tdmpc_cem_iter(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void
     ca.temperature = prm->temperature; ca.momentum = prm->momentum; ca.omm = prm->one_minus_momentum;
     ca.std_floor = prm->std_floor; ca.std_floor_p = prm->std_floor_dev;
     ca.elite_out = elite_actions; ca.score_out = score; ca.value_out = value; ca.reward_out = reward_mean;
+    ca.pstatus = pack_status(c); ca.status = prm->status;
     if (use_chain(c, B * T, 2, CK_Q)) { ca.G = c.k.G; ca.qv = c.k.qv; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H]; }
     hipLaunchKernelGGL(cem_kernel, dim3(B), dim3(1024), cem_lds_bytes(T, H, ca.K, A), c.s, ca);
     HIPCHK(hipGetLastError());

@@ -87,7 +87,11 @@ class TdICEM:
         self.prev_mean_flat = torch.zeros(max_batch * H * A, dtype=torch.float32, device=dev)
         self.elites = torch.zeros(max_batch, H, K, A, dtype=torch.float32, device=dev)
         self.action = torch.zeros(max_batch, A, dtype=torch.float32, device=dev)
-        self.metrics = torch.zeros(max_batch, 2, dtype=torch.float32, device=dev)
+        # [status word | 3 pad words | metrics [max_batch, 2]]: a call's sticky device status (tdmpc_icem_params.status:
+        # TDMPC_STATUS_PACK_STALE) comes down with its metrics in one copy
+        self._ms_dev = torch.zeros(4 + 2 * max_batch, dtype=torch.float32, device=dev)
+        self.status = self._ms_dev[:1].view(torch.int32)
+        self.metrics = self._ms_dev[4:].view(max_batch, 2)
         self.obs_buf = torch.zeros(max_batch, cfg.obs_shape[0], dtype=torch.float32, device=dev)
         col_max = cfg.iterations * H * N * A + H * self.E_max * A   # coloured floats of one env and call
         self._stage = torch.empty(col_max, dtype=torch.float32, device=dev)
@@ -300,7 +304,9 @@ class TdICEM:
             return torch.empty(cfg.action_dim, dtype=torch.float32, device=self.device).uniform_(-1, 1), metrics
         obs = torch.as_tensor(np.asarray(obs), dtype=torch.float32).view(1, -1)
         a, m = self._plan_envs(obs, eval_mode, step, t0, [noise] if noise is not None else None, trace)
-        m = m[0].double().cpu().numpy()
+        ms = self._ms_dev[:6].cpu()
+        self._raise_status(int(ms[:1].view(torch.int32)))
+        m = ms[4:6].double().numpy()
         metrics.update({"external_reward_mean": float(m[0]), "current_std": float(m[1])})
         return a[0].clone(), metrics
 
@@ -315,7 +321,21 @@ class TdICEM:
         a, m = self._plan_envs(obs.view(obs.shape[0], -1), eval_mode, step, t0, None, None)
         if not sync_metrics:
             return a, m
-        return a, [{"external_reward_mean": float(r), "current_std": float(sd)} for r, sd in m.double().cpu().numpy()]
+        B = obs.shape[0]
+        ms = self._ms_dev[:4 + 2 * B].cpu()
+        self._raise_status(int(ms[:1].view(torch.int32)))
+        return a, [{"external_reward_mean": float(r), "current_std": float(sd)}
+                   for r, sd in ms[4:].view(B, 2).double().numpy()]
+
+    def check_status(self):
+        """Synchronising check of the sticky device status word (for plan_batch(sync_metrics=False) callers)."""
+        self._raise_status(int(self.status.item()))
+
+    def _raise_status(self, st: int):
+        if st:
+            self.status.zero_()
+            raise RuntimeError(f"tdmpc_plan_icem failed on the device (status {st}): "
+                               + _lib.status_text(st) + "; its actions are NaN")
 
     def _plan_envs(self, obs, eval_mode, step, t0, noise, trace):
         cfg = self.cfg
@@ -367,6 +387,7 @@ class TdICEM:
         p.std_floor, p.init_std = float(self.std), 0.5
         for t, v in enumerate(_discount_pows(cfg.discount, H)):
             p.discount_pow[t] = v
+        p.status = self.status.data_ptr()
         dev = self.device
         value_out = mean_out = std_out = None
         if trace is not None:

@@ -48,8 +48,9 @@ def clip_grad_norm_19(params, max_norm):
 
 class RandomShiftsAug(torch.nn.Module):
     """helper.py:250-283: random-shift augmentation of pixel observations (identity for state). The shifts are
-    drawn exactly as the reference draws them (one torch.randint of [n, 1, 1, 2] on the input's device, so the
-    generator advances identically); the shift itself runs as one HIP gather kernel (tdmpc_random_shift,
+    drawn as the reference draws them per call (one torch.randint of [n, 1, 1, 2] on the input's device, so one
+    call advances the generator identically; the engine's update makes its calls in another order than the
+    reference's, learner_engine.update); the shift itself runs as one HIP gather kernel (tdmpc_random_shift,
     include/tdmpc_learner.h): the reference's pad + grid_sample lands on integer pixel centres, so it is a
     clamped-index copy (tests/test_learner.py holds it to the reference's outputs)."""
 
@@ -270,6 +271,19 @@ class Learner:
 
     def update(self, buffer, step, noise=None):
         """TDMPC.update semantics -> metrics tensor [7] on the device (no sync)."""
+        # the engine's hipBLASLt products (learner_engine.mm) follow torch's process-wide fp32 matmul setting: pin
+        # full fp32 around every eager pass and capture, whatever the caller set (ADVICE r5)
+        prec = torch.get_float32_matmul_precision()
+        tf32 = torch.backends.cuda.matmul.allow_tf32
+        torch.set_float32_matmul_precision("highest")
+        torch.backends.cuda.matmul.allow_tf32 = False
+        try:
+            return self._update(buffer, step, noise)
+        finally:
+            torch.set_float32_matmul_precision(prec)
+            torch.backends.cuda.matmul.allow_tf32 = tf32
+
+    def _update(self, buffer, step, noise=None):
         self.agent.model.train()
         if noise is not None or not self._capturable(buffer) or self.calls < self.warmup:
             if self._capturable(buffer) and self.calls == self.warmup - 1:

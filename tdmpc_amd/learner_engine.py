@@ -127,11 +127,14 @@ class Engine:
         self.x6 = os.environ.get("TDMPC_LG_X6", "0") == "1"
         # 64 x 64 tiles from this many 64 x 64 output tiles per launch (measured: profiles/r04/learner_tile_ab.txt)
         self.t64 = 240
-        # the heads' plain M x M products (R = H B rows, no fused epilogue) on hipBLASLt (torch.mm / addmm), the
-        # library GEMM for a plain GEMM: 1.25 vs 1.37 ms per humanoid update with them on lg_gemm, graph replay
-        # (profiles/r05/learner_blas_ab.txt). Everything else -- the rollout's chained products with their fused ELU /
-        # ELU' epilogues, the grouped weight gradients, rows, losses, Adam -- stays on the hand-written kernels.
-        # TDMPC_LG_BLAS=0 puts those products on lg_gemm too (set before the first update: the graph keeps it).
+        # every grouped product of prod() -- the heads' Q / reward / policy layers over R = H B rows and their dX,
+        # including the ones whose ELU (pi's layers, the Q / reward first layers) or ELU' (dX) epilogue lg_gemm would
+        # fuse: those run torch.mm / addmm plus one tdmpc_lg_act launch -- on hipBLASLt: 1.25 vs 1.37 ms per humanoid
+        # update with them on lg_gemm, graph replay (profiles/r05/learner_blas_ab.txt). The products inside the
+        # rollout chain (gemm() / _pair), the grouped weight gradients, rows, losses and Adam stay on the hand-written
+        # kernels. hipBLASLt picks its own reduction order, so with it the update is deterministic per build and
+        # box but not order-pinned like lg_gemm; Learner.update pins full-fp32 matmul precision around it.
+        # TDMPC_LG_BLAS=0 puts every product on lg_gemm (set before the first update: the graph keeps it).
         self.blas = os.environ.get("TDMPC_LG_BLAS", "1") == "1"
         self._aux = {}
 
@@ -502,8 +505,10 @@ class Engine:
         R, R1 = H * B, (H + 1) * B
         b = self.bufs(B)
         if self.pix:
-            # RandomShiftsAug (helper.py:250-283) on the H next-observation stacks, then on obs (tdmpc.py:200, 207), as
-            # the reference's update draws them; the frames may come as uint8 from the replay buffer
+            # RandomShiftsAug (helper.py:250-283) on the H next-observation stacks, then on obs: the same shift
+            # distribution as the reference's update, NOT its random stream -- the reference draws aug(obs) first
+            # (tdmpc.py:200) and then one B-sized draw per horizon step (tdmpc.py:209), so at one seed the shifts
+            # differ; the frames may come as uint8 from the replay buffer
             # (NormalizeImg's x / 255 folded into the shift's gather: the conv stack reads normalised frames)
             nx = next_obses[:H].reshape(H * B, *next_obses.shape[2:])
             nxo_t = self.agent.aug(nx if nx.dtype == torch.float32 else nx.float(), div=255.0).contiguous()

@@ -61,6 +61,10 @@ def pack_told(pl, model):
         if key == pl._packed_key:
             return
     params = list(model.state_dict().values())
+    if pl._packed_model is not None and pl._packed_model is not model:
+        # another model object: re-key the buffer's job table (a graph captured over the old model's pack -- the
+        # learner's update -- then fails loudly if replayed, TDMPC_STATUS_PACK_STALE, instead of packing this one)
+        pl.L.tdmpc_pack_forget(C.c_void_p(pl.packed.data_ptr()))
     pl._packed_model, pl._packed_params = model, params
     key = tuple((p.data_ptr(), p._version) for p in params)
     params = [p.detach().to(pl.device, torch.float32).contiguous() for p in params]
@@ -345,9 +349,8 @@ class HipPlanner:
         """Raise for a nonzero device status (and clear it): the plan's outputs are NaN, never return them."""
         if st:
             self.status.zero_()
-            raise RuntimeError(f"tdmpc_plan failed on the device (status {st}: the persistent one-env plan timed out "
-                               "at a hand-off -- not every workgroup of its grid was resident). Its action is NaN; "
-                               "set TDMPC_PERSIST=0 to plan on the launch chain instead.")
+            raise RuntimeError(f"tdmpc_plan failed on the device (status {st}): {_lib.status_text(st)}. "
+                               "Its action is NaN.")
 
     def check_status(self):
         """Synchronising check of the sticky status word (for callers that plan with sync_metrics=False)."""

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 14
     for n in names:
         assert hasattr(L, n), n
-    assert L.tdmpc_abi_version() == _lib.ABI_VERSION == 7
+    assert L.tdmpc_abi_version() == _lib.ABI_VERSION == 8
 
 
 @pytest.mark.parametrize("name", ["cartpole-swingup", "cheetah-run", "humanoid-run", "humanoid-run-l512",

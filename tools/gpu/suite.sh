@@ -69,6 +69,23 @@ for stage in "$@"; do
         f=$(find "$OUT/s$i" -name '*counter_collection.csv' | head -1)
         python tools/pmc_stall.py wide_step_kernelILi4ELi7 131072 "$f" > "$OUT/s$i.txt" && cat "$OUT/s$i.txt"
       done ;;
+    ringpmc)
+      # the LDS-DMA ring probe's cases (tools/mb/dma_ring.hip: the wide step kernel's ring without its arithmetic),
+      # two SQ counter passes each: where the MFMA + DMA serialisation waits
+      R1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC"
+      R2="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
+      timeout -k 10 60 tools/mb/dma_ring 94 2304 > "$OUT/ring_times.txt" 2>&1 || { tail -5 "$OUT/ring_times.txt"; exit 1; }
+      cat "$OUT/ring_times.txt"
+      for c in mfma mfma_lds mfma_dma full dma; do
+        i=0
+        for P in "$R1" "$R2"; do
+          i=$((i+1))
+          timeout -s KILL 60 rocprofv3 --pmc $P -d "$OUT/r_$c$i" -o run --output-format csv -- tools/mb/dma_ring 94 2304 $c \
+            > "$OUT/r_$c$i.log" 2>&1 || { echo "ring pass $c $i failed"; tail -5 "$OUT/r_$c$i.log"; exit 1; }
+          f=$(find "$OUT/r_$c$i" -name '*counter_collection.csv' | head -1)
+          echo "== $c pass $i"; python tools/pmc_stall.py ring_kernel 131072 "$f" | tee "$OUT/r_$c$i.txt"
+        done
+      done ;;
     pytest:*)
       timeout -k 10 500 python -u -m pytest tests/test_gpu_plan.py tests/test_gpu_configs.py tests/test_gpu_sharded.py -m gpu -v -x \
         --timeout 200 --timeout-method thread -k "${stage#pytest:}" > "$OUT/tests_sel.txt" 2>&1 \

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 #include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
@@ -248,6 +249,16 @@ void run(int steps, long src_kb, bool rnd = false) {
 int main(int argc, char** argv) {
     const int steps = argc > 1 ? atoi(argv[1]) : 94;
     const long kb = argc > 2 ? atol(argv[2]) : 2304;
+    if (argc > 3) {   // one case only (PMC passes per case): full | mfma | mfma_dma | mfma_lds | dma
+        const char* c = argv[3];
+        if (!strcmp(c, "full")) run<4, 3, 6, 0, 0>(steps, kb);
+        else if (!strcmp(c, "mfma")) run<4, 3, 6, 0, 5>(steps, kb);
+        else if (!strcmp(c, "mfma_dma")) run<4, 3, 6, 0, 2>(steps, kb);
+        else if (!strcmp(c, "mfma_lds")) run<4, 3, 6, 0, 1>(steps, kb);
+        else if (!strcmp(c, "dma")) run<4, 3, 0, 0, 0>(steps, kb);
+        else { printf("unknown case %s\n", c); return 2; }
+        return 0;
+    }
     run<4, 3, 6, 0, 0>(steps, kb);          // full: every wave issues 3 DMAs right after the barrier
     run<4, 3, 6, 0, 5>(steps, kb);          // MFMA + barrier only (the floor)
     run10<4, 6>(steps, kb);                 // fp32 stream + one split per workgroup
