@@ -67,7 +67,7 @@ for stage in "$@"; do
         timeout -s KILL 150 rocprofv3 --pmc $P -d "$OUT/s$i" -o run --output-format csv -- python -u tools/quick_time.py humanoid-run 32 \
           > "$OUT/s$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/s$i.log"; exit 1; }
         f=$(find "$OUT/s$i" -name '*counter_collection.csv' | head -1)
-        python tools/pmc_stall.py wide_step_kernelILi4ELi7 131072 "$f" > "$OUT/s$i.txt" && cat "$OUT/s$i.txt"
+        python tools/pmc_stall.py "wide_step_kernel<4, 7>" 131072 "$f" > "$OUT/s$i.txt" && cat "$OUT/s$i.txt"
       done ;;
     ringpmc)
       # the LDS-DMA ring probe's cases (tools/mb/dma_ring.hip: the wide step kernel's ring without its arithmetic),
