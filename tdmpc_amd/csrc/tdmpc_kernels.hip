@@ -115,6 +115,12 @@ struct Layout {
     size_t x6qs, bqs;      // x6q [2][nsr][rup(Kx, 32)]; bias [2][nsr]
     size_t x6qf, bqf;      // the folded first layer diag(g1) (W1 - 1 wbar^T): x6q [2][M][rup(Kx, 32)]; g1 (b1 - bbar) [2][M]
     size_t qs_gram;        // fp64 scratch [2][nqs][nqs] (the Gram matrices)
+    // the folded first layer of TOLD.next for latent_dim == mlp_dim (pack_fold; wide_step.inc WS_OUTH): both heads'
+    // [W1a | W1z W3] in x6q [2M][rup(Kx, 32)] and b1 + W1z b3 [2M] -- the first layer of a step whose input latent
+    // columns hold the previous step's h2 instead of z (fold = 0: none)
+    int fold;
+    size_t x6qw, bfw;
+    size_t fold_w;         // fp32 scratch [2M][M]: W1z W3 (fp64 sums, rounded once)
     size_t total;
 };
 constexpr int PACK_MAX_JOBS = 96;              // job-table capacity (pack_jobs emits ~40-60)
@@ -222,6 +228,14 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
             w->bqf = take((size_t)2 * w->M);
             w->qs_gram = take((size_t)2 * n * n * 2);
         }
+    }
+    w->fold = 0;
+    w->x6qw = w->bfw = w->fold_w = 0;
+    if (w->M == 512 && w->Lp == w->M && w->Lr == w->M) {
+        w->fold = 1;
+        w->x6qw = take((size_t)2 * w->M * rup(w->Kx, 32) * 3 / 2);
+        w->bfw = take((size_t)2 * w->M);
+        w->fold_w = take((size_t)2 * w->M * w->M);
     }
     w->total = o;
     return true;
@@ -3191,8 +3205,8 @@ int init_attrs() {
     HIPCHK(hipFuncSetAttribute((const void*)cem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)plan1_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIPCHK(hipFuncSetAttribute((const void*)plan1_kernel<6>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-#define WIDE_ATTR(G1, NB3) \
-    HIPCHK(hipFuncSetAttribute((const void*)wide_step_kernel<G1, NB3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+#define WIDE_ATTR(G1, NB3, MODE) \
+    HIPCHK(hipFuncSetAttribute((const void*)wide_step_kernel<G1, NB3, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     WIDE_FOR_EACH(WIDE_ATTR)
 #undef WIDE_ATTR
 #define WIDE_HEADS_ATTR(G1P, NB3P, G1Q, NSTQ) \
@@ -3510,6 +3524,7 @@ struct Ctx {
     mutable RowMap split_map = {1 << 30, 0, 0};
     mutable int split_rows = 0, split_t = 0;
     int z0c_ready = 0;   // k.z0c holds this call's per-env first-layer z0 shares (tdmpc_plan)
+    int fold_ok = 0;     // tdmpc_plan: the sampled rows' rollout runs wide at every t with the folded first layer
 };
 
 float* Xt(const Ctx& c, int t) { return c.k.X + (size_t)t * c.k.x_stride; }
@@ -3686,10 +3701,18 @@ bool use_wide(const Ctx& c, int rows, const RowMap& map, bool z0c) {
     if (rows % 16 || map.G % 16 || map.S % 16 || map.O % 16) return false;   // a wave's 16 rows in one X panel block
     if (z0c && map.G % 128) return false;   // the per-env first-layer bias is per workgroup
     const int g1 = wide_g1(c, z0c), nb3 = (int)rup(c.w.L, 16) / 16;
-    if (g1 > 5 || (nb3 != 4 && nb3 != 7)) return false;
+    const bool inst = (g1 <= 5 && (nb3 == 4 || nb3 == 7)) || (nb3 == 32 && (g1 == 1 || g1 == 17));
+    if (!inst) return false;
     return c.path == TDMPC_PATH_WIDE || (rows + 127) / 128 * 2 >= num_cus();
 }
-int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, bool z0c) {
+// the folded first layer for a plan's sampled-row rollout (latent_dim == mlp_dim; TDMPC_FOLD=0 turns it off)
+bool fold_on() {
+    static const int v = [] { const char* e = getenv("TDMPC_FOLD"); return e ? atoi(e) : 1; }();
+    return v != 0;
+}
+// fold: this launch is a step of a rollout whose every step runs here with the folded layout (Ctx::fold_ok): steps
+// t >= 1 read the previous step's h2 through the folded first layer, every step but the last stores h2 instead of z'
+int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, bool z0c, bool fold = false) {
     const Layout& w = c.w;
     const int M = c.M;
     WideArgs a;
@@ -3697,9 +3720,15 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
     auto q6 = [&](int i) { return (const unsigned short*)(c.pw + w.x6q[i]); };
     a.g1s = (int)(rup(c.Kx, 32) / 32);
     const size_t rb1 = (size_t)(M / 16) * a.g1s * 1536;   // bf16 per M rows of x6q W1
+    const bool fold_in = fold && t >= 1 && !z0c, outh = fold && !last;
     a.p[0].X1 = q6(X6_W1X); a.p[1].X1 = q6(X6_W1X) + rb1;
     a.p[0].X2 = q6(X6_W2D); a.p[1].X2 = q6(X6_W2R);
     a.p[0].b1 = c.pw + w.b1x; a.p[1].b1 = c.pw + w.b1x + M;
+    if (fold_in) {
+        const unsigned short* xf = (const unsigned short*)(c.pw + w.x6qw);
+        a.p[0].X1 = xf; a.p[1].X1 = xf + rb1;
+        a.p[0].b1 = c.pw + w.bfw; a.p[1].b1 = c.pw + w.bfw + M;
+    }
     a.p[0].b2 = c.pw + w.b2d; a.p[1].b2 = c.pw + w.b2r;
     a.p[1].w3v = c.pw + w.w3r; a.p[1].b3v = c.pw + w.b3r;
     a.X3 = q6(X6_W3D); a.b3 = c.pw + w.b3d; a.nvalid = w.L; a.nstore = w.Lp;
@@ -3711,30 +3740,33 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
     if (z0c) { a.z0c = c.k.z0c; a.z0_G = map.G; }
     a.stamps = g_p1_stamps;   // (read only by a -DWS_STAMPS diagnostic build)
     const int g1 = wide_g1(c, z0c), nb3 = (int)rup(w.L, 16) / 16;
+    const int mode = (g1 > 5 ? WS_XS : 0) | (outh ? WS_OUTH : 0);
     const dim3 grid((unsigned)rup(a.nrb, 4) * 2), block(64 * WS_NW);
     // diagnostic timer (tdmpc_profile_begin cfg 4: the step kernel); t = 0 launches with the z0c first layer are not
     // timed (less than the algorithmic work), as in launch_chain
     Profiler& pf = g_prof;
     const bool prof = pf.armed && pf.cfg == 4 + CH_STEP && pf.n + 2 <= pf.cap && (pf.rows == 0 || rows == pf.rows) && !z0c;
     if (prof) {
-        snprintf(pf.kernel, sizeof pf.kernel, "wide_step_kernel<%d, %d>", g1, nb3);
+        if (mode) snprintf(pf.kernel, sizeof pf.kernel, "wide_step_kernel<%d, %d, %s%s%s>", g1, nb3,
+                           mode & WS_XS ? "XS" : "", mode == (WS_XS | WS_OUTH) ? "|" : "", mode & WS_OUTH ? "OUTH" : "");
+        else snprintf(pf.kernel, sizeof pf.kernel, "wide_step_kernel<%d, %d>", g1, nb3);
         HIPCHK(hipEventRecord(pf.ev[pf.n], c.s));
     }
     bool done = false;
-#define WIDE_LAUNCH(G1, NB3) \
-    if (!done && g1 == G1 && nb3 == NB3) { \
-        hipLaunchKernelGGL((wide_step_kernel<G1, NB3>), grid, block, ws_lds<G1>(), c.s, a); \
+#define WIDE_LAUNCH(G1, NB3, MODE) \
+    if (!done && g1 == G1 && nb3 == NB3 && mode == (MODE)) { \
+        hipLaunchKernelGGL((wide_step_kernel<G1, NB3, MODE>), grid, block, (wsm_lds<G1, MODE>()), c.s, a); \
         done = true; \
     }
     WIDE_FOR_EACH(WIDE_LAUNCH)
 #undef WIDE_LAUNCH
-    if (!done) { snprintf(g_err, sizeof g_err, "wide step: no instance for G1 %d NB3 %d", g1, nb3); return TDMPC_E_DIMS; }
+    if (!done) { snprintf(g_err, sizeof g_err, "wide step: no instance for G1 %d NB3 %d mode %d", g1, nb3, mode); return TDMPC_E_DIMS; }
     HIPCHK(hipGetLastError());
     if (prof) {
         HIPCHK(hipEventRecord(pf.ev[pf.n + 1], c.s));
         pf.n += 2;
-        const double K1 = w.L + w.A;
-        pf.flops += 2.0 * rows * (2 * (K1 * M + (double)M * M) + (double)M * w.L + M);
+        const double K1 = w.L + w.A;   // (executed products: WS_OUTH launches skip layer 3)
+        pf.flops += 2.0 * rows * (2 * (K1 * M + (double)M * M) + (outh ? 0.0 : (double)M * w.L) + M);
     }
     return 0;
 }
@@ -3766,10 +3798,11 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
             const bool z0c_rm = t == 0 && c.z0c_ready;   // (rm.G = N: use_wide checks N % 128 for the z0c bias)
             if (c.P > 0 && c.N + c.P == c.T && map.G == c.T && map.S == c.T && map.O == 0 && rows == envs * c.T &&
                 use_wide(c, envs * c.N, rm, z0c_rm)) {
-                if ((rc = launch_wide(c, t, envs * c.N, rm, disc, first, last, z0c_rm))) return rc;
+                if ((rc = launch_wide(c, t, envs * c.N, rm, disc, first, last, z0c_rm, c.fold_ok))) return rc;
                 return step_next(c, t, envs * c.P, pm, disc, first, last, 0, true);
             }
-            return launch_wide(c, t, rows, map, disc, first, last, z0c);
+            const bool sampled = map.G == c.N && map.S == c.T && map.O == 0;   // (the folded rollout's rows only)
+            return launch_wide(c, t, rows, map, disc, first, last, z0c, c.fold_ok && sampled);
         }
     }
     if (use_chain(c, rows, 2, CK_STEP)) {
@@ -4464,6 +4497,68 @@ __global__ void __launch_bounds__(PACK_WG) pack_fused_kernel(PackHdr* hdr, const
     }
 }
 
+// ---- the folded first layer (latent_dim == mlp_dim; Layout::fold): W1z W3 and b1 + W1z b3 for both TOLD.next heads,
+// from the packed fp32 panels (w1x's z columns [2M][Ap .. Ap + L), w3d [Lr][M], b3d, b1x), fp64 sums rounded once to
+// fp32, then split into the x6q planes with the a columns of w1x in front. A step whose input latent columns hold the
+// previous step's h2 = ELU(W2 h1 + b2) computes W1 [a; W3 h2 + b3] + b1 as [W1a | W1z W3] [a; h2] + (b1 + W1z b3).
+struct FoldArgs {
+    const float* w1x; const float* w3d; const float* b3; const float* b1x;
+    float* fw; float* bf; unsigned short* x6;   // W1z W3 [2M][M] fp32, folded bias [2M], x6q [2M][rup(Kx, 32)]
+    int M, L, Ap, Kx;
+};
+__global__ void __launch_bounds__(256) fold_gemm_kernel(const FoldArgs a) {
+    // 16 x 16 output tile per workgroup: rows i of both heads [0, 2M), columns j of W3 [0, M) -- tile column M / 16
+    // is the bias column (j = M: b3)
+    __shared__ double sA[16][17], sB[16][17];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
+    const int i = i0 + ty, j = j0 + tx;
+    double acc = 0.0;
+    for (int l0 = 0; l0 < a.L; l0 += 16) {
+        const int la = l0 + tx, lb = l0 + ty;
+        sA[ty][tx] = la < a.L ? (double)a.w1x[pidx(i, a.Ap + la, a.Kx)] : 0.0;
+        double b = 0.0;
+        if (lb < a.L) b = j < a.M ? (double)a.w3d[pidx(lb, j, a.M)] : (j == a.M ? (double)a.b3[lb] : 0.0);
+        sB[ty][tx] = b;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc = fma(sA[ty][k], sB[k][tx], acc);
+        __syncthreads();
+    }
+    if (j < a.M) a.fw[(size_t)i * a.M + j] = (float)acc;
+    else if (j == a.M) a.bf[i] = (float)((double)a.b1x[i] + acc);
+}
+__global__ void __launch_bounds__(256) fold_x6q_kernel(const FoldArgs a, long work) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= work) return;
+    const int j = (int)(i & 7), lane = (int)((i >> 3) & 63);
+    const long blk = i >> 9;
+    const int G = (a.Kx + 31) / 32;
+    const int g = (int)(blk % G), nb = (int)(blk / G);
+    const int r = 16 * nb + (lane & 15), k = 32 * g + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
+    float x = 0.f;
+    if (k < a.Ap) x = a.w1x[pidx(r, k, a.Kx)];
+    else if (k < a.Ap + a.M) x = a.fw[(size_t)r * a.M + (k - a.Ap)];
+    __bf16 h, m, l;
+    split3(x, h, m, l);
+    a.x6[(blk * 3 + 0) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, h);
+    a.x6[(blk * 3 + 1) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, m);
+    a.x6[(blk * 3 + 2) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, l);
+}
+int pack_fold(const Layout& w, float* pw, hipStream_t s) {
+    FoldArgs f;
+    memset(&f, 0, sizeof f);
+    f.w1x = pw + w.w1x; f.w3d = pw + w.w3d; f.b3 = pw + w.b3d; f.b1x = pw + w.b1x;
+    f.fw = pw + w.fold_w; f.bf = pw + w.bfw; f.x6 = (unsigned short*)(pw + w.x6qw);
+    f.M = w.M; f.L = w.L; f.Ap = w.Ap; f.Kx = w.Kx;
+    hipLaunchKernelGGL(fold_gemm_kernel, dim3(w.M / 16 + 1, 2 * w.M / 16), dim3(256), 0, s, f);
+    HIPCHK(hipGetLastError());
+    const long work = (long)(2 * w.M / 16) * (rup(w.Kx, 32) / 32) * 512;
+    hipLaunchKernelGGL(fold_x6q_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, f, work);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 // The job list of a layout and the reference tensors t (state_dict order, tdmpc_num_param_tensors of them)
 void pack_jobs(const Layout& w, const float* const* t, std::vector<PackJob>& jobs) {
     const int M = w.M, L = w.L, A = w.A;
@@ -4855,7 +4950,9 @@ int tdmpc_pack_weights(const tdmpc_dims* d, const float* const* t, int32_t n, vo
     std::vector<PackJob> jobs;
     pack_jobs(w, t, jobs);
     int rc = launch_pack(jobs, w, (float*)packed, (hipStream_t)stream);
-    if (rc || !w.nqs) return rc;
+    if (rc) return rc;
+    if (w.fold && (rc = pack_fold(w, (float*)packed, (hipStream_t)stream))) return rc;
+    if (!w.nqs) return 0;
     // helper.q's LayerNorm-1 statistics block from the packed first layer (wide_heads.inc): Gram, Cholesky, x6q
     float* pw = (float*)packed;
     QStatArgs q;
@@ -4961,6 +5058,11 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     if (z0c_eligible(c)) {
         if ((rc = z0c_launch(c))) return rc;
         c.z0c_ready = 1;
+    }
+    {   // latent 512: the sampled rows' rollout on the wide kernel at every t, through the folded first layer
+        const RowMap rm0 = {N, T, 0};
+        c.fold_ok = fold_on() && c.w.fold && H > 1 && use_wide(c, B * N, rm0, c.z0c_ready != 0) &&
+                    use_wide(c, B * N, rm0, false);
     }
 
     // pi pre-rollout (tdmpc.py:113-118) fused with CEM iteration 0: at each step t the policy rows get
