@@ -19,6 +19,8 @@
 #   lgbench          lg_gemm tile timings of the learner's products (tools/lg_gemm_bench.py)
 #   p1stamps         per-hand-off timeline of the one-env persistent plan (tools/p1_stamps.py)
 #   qt               tools/quick_time.py on CONFIG / ENVS (qt.txt)
+#   trace            per-kernel breakdown of one plan of CONFIG / ENVS (rocprofv3 kernel trace, tools/plan_trace.py)
+#   ringpmc          SQ counter passes of the LDS-DMA ring probe's cases (tools/mb/dma_ring)
 # Environment: CONFIG (default humanoid-run), ENVS (default 32).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -153,6 +155,13 @@ PY
     p1stamps)
       timeout -k 10 120 python -u tools/p1_stamps.py "$CONFIG" > "$OUT/p1_stamps.txt" 2>&1 || { tail -20 "$OUT/p1_stamps.txt"; exit 1; }
       tail -4 "$OUT/p1_stamps.txt" ;;
+    trace)
+      # per-kernel breakdown of one plan of CONFIG / ENVS (rocprofv3 kernel trace of tools/quick_time.py, eager-free
+      # graph replays; tools/plan_trace.py summarises the last complete plan)
+      timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d "$OUT/tr" -o run -- python -u tools/quick_time.py "$CONFIG" "$ENVS" \
+        > "$OUT/tr.log" 2>&1 || { tail -20 "$OUT/tr.log"; exit 1; }
+      f=$(find "$OUT/tr" -name '*kernel_trace.csv' | head -1)
+      python3 tools/plan_trace.py "$f" > "$OUT/plan_trace_${CONFIG}_b${ENVS}.txt" 2>&1; cat "$OUT/plan_trace_${CONFIG}_b${ENVS}.txt" ;;
     qt)
       timeout -k 10 120 python -u tools/quick_time.py "$CONFIG" "$ENVS" > "$OUT/qt.txt" 2>&1 || { tail -20 "$OUT/qt.txt"; exit 1; }
       grep -v amdgpu.ids "$OUT/qt.txt" ;;

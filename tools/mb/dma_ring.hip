@@ -44,7 +44,7 @@ ring_kernel(const char* src, long src_bytes, int steps, float* out) {
     };
     // V 6 / 7: only waves 4-7 / 0-3 issue (each the step's DMAs of itself and its SIMD partner wave ^ 4)
     auto issue = [&](int k) {
-        if constexpr (V == 1 || V == 4 || V == 5 || V == 8) return;
+        if constexpr (V == 1 || V == 4 || V == 5 || V == 8 || V == 11 || V == 13) return;
         if constexpr (V == 6 || V == 7) {
             if ((V == 6) != (wave >= 4)) return;
 #pragma unroll
@@ -63,7 +63,7 @@ ring_kernel(const char* src, long src_bytes, int steps, float* out) {
         glds<NT>(addr(k, d), voff, base + (k % NS) * SLOT + (wave * D + d) * 1024);
     };
     for (int k = 0; k < NS - 1; ++k) {
-        if constexpr (V == 8) { for (int d = 0; d < D; ++d) issue_one(k, d); }
+        if constexpr (V == 8 || V == 11 || V == 13) { for (int d = 0; d < D; ++d) issue_one(k, d); }
         else issue(k);
     }
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -87,6 +87,18 @@ ring_kernel(const char* src, long src_bytes, int steps, float* out) {
                                a2 = __builtin_bit_cast(bf16x8_t, w2);
                 if constexpr (V == 3) { acc[f & 7][0] += __builtin_bit_cast(float, w0.x ^ w1.y ^ w2.z); continue; }
                 if constexpr (V == 8) { if ((f & 1) && f / 2 < D) issue_one(k + NS - 1, f / 2); }
+                // V 11: DMA d of wave w after fragment (3w + d) % 8 -- three per fragment slot, SIMD partners (w, w + 4)
+                // never in the same slot; V 13: waves 0-3 after fragments 0-2, waves 4-7 after fragments 4-6
+                if constexpr (V == 11) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d)
+                        if (f == (3 * wave + d) % 8) issue_one(k + NS - 1, d);
+                }
+                if constexpr (V == 13) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d)
+                        if (f == d + (wave >= 4 ? 4 : 0)) issue_one(k + NS - 1, d);
+                }
 #pragma unroll
                 for (int m = 0; m < MF; ++m) {
                     const bf16x8_t a = m % 3 == 0 ? a0 : m % 3 == 1 ? a1 : a2;
@@ -181,6 +193,80 @@ ring10_kernel(const char* src, long src_bytes, int steps, float* out) {
     if (s == 12345.f) out[tid] = s;
 }
 
+// Interference probe: no barriers. Waves 0-3 (one per SIMD) run 96 MFMAs per step on register operands (a SIMD's
+// whole step of matrix work); waves 4-7 (their SIMD partners) either leave at once (L = 0) or stream 6 KiB per step
+// into their own LDS area with global_load_lds_dwordx4 (L = 1; vmcnt keeps one step in flight) -- does an LDS-DMA
+// stream on a SIMD slow its partner's MFMAs?  out[wave] = the wave's s_memtime cycles.
+template <int L>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+split_kernel(const char* src, long src_bytes, int steps, unsigned long long* out) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    if (wave < 4) {
+        floatx4 acc[8];
+        for (int j = 0; j < 8; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        const bf16x8_t a0 = __builtin_bit_cast(bf16x8_t, make_uint4(lane, 1, 2, 3));
+        const bf16x8_t a1 = __builtin_bit_cast(bf16x8_t, make_uint4(3, lane, 1, 2));
+        for (int k = 0; k < steps; ++k) {
+#pragma unroll
+            for (int m = 0; m < 96; ++m)
+                acc[m & 7] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m & 1 ? a0 : a1, a1, acc[m & 7], 0, 0, 0);
+        }
+        float s = 0.f;
+        for (int j = 0; j < 8; ++j) s += acc[j][0] + acc[j][3];
+        if (s == 12345.f) out[4096 + tid] = (unsigned long long)s;
+    } else if (L == 1) {
+        const unsigned base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)lds + (wave - 4) * 12 * 1024;
+        const unsigned voff = lane * 16;
+        const char* s0 = src + ((blockIdx.x & 7) >> 2) * src_bytes;
+        for (int k = 0; k < steps; ++k) {
+#pragma unroll
+            for (int d = 0; d < 6; ++d) {
+                const long off = ((long)k * 24 + (wave - 4) * 6 + d) * 1024 % src_bytes;
+                glds<0>(s0 + off, voff, base + ((k & 1) * 6 + d) * 1024);
+            }
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) out[blockIdx.x * 8 + wave] = t1 - t0;
+}
+
+template <int L>
+void run_split(int steps, long src_kb) {
+    const long sb = src_kb * 1024;
+    char* src;
+    CK(hipMalloc(&src, 2 * sb));
+    CK(hipMemset(src, 0, 2 * sb));
+    unsigned long long* out;
+    CK(hipMalloc(&out, 8192 * 8));
+    CK(hipFuncSetAttribute((const void*)split_kernel<L>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((split_kernel<L>), dim3(256), dim3(512), 48 * 1024, 0, src, sb, steps, out);
+    CK(hipDeviceSynchronize());
+    const int R = 20;
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < R; ++i) hipLaunchKernelGGL((split_kernel<L>), dim3(256), dim3(512), 48 * 1024, 0, src, sb, steps, out);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<unsigned long long> h(2048);
+    CK(hipMemcpy(h.data(), out, 2048 * 8, hipMemcpyDeviceToHost));
+    double cmp = 0, ld = 0;
+    for (int b = 0; b < 256; ++b)
+        for (int w = 0; w < 8; ++w) (w < 4 ? cmp : ld) += (double)h[b * 8 + w];
+    printf("split L=%d steps=%d: %.2f us/launch; MFMA waves %.0f memtime ticks/step, loader waves %.0f ticks/step\n", L, steps,
+           ms * 1e3 / R, cmp / 1024 / steps, ld / 1024 / steps);
+    CK(hipFree(src));
+    CK(hipFree(out));
+}
+
 template <int NS, int MF>
 void run10(int steps, long src_kb) {
     const long sb = src_kb * 1024;
@@ -256,6 +342,14 @@ int main(int argc, char** argv) {
         else if (!strcmp(c, "mfma_dma")) run<4, 3, 6, 0, 2>(steps, kb);
         else if (!strcmp(c, "mfma_lds")) run<4, 3, 6, 0, 1>(steps, kb);
         else if (!strcmp(c, "dma")) run<4, 3, 0, 0, 0>(steps, kb);
+        else if (!strcmp(c, "stagger")) {
+            for (int i = 0; i < 2; ++i) {
+                run<4, 3, 6, 0, 0>(steps, kb); run<4, 3, 6, 0, 8>(steps, kb); run<4, 3, 6, 0, 11>(steps, kb);
+                run<4, 3, 6, 0, 13>(steps, kb); run<4, 3, 6, 0, 5>(steps, kb);
+                run<5, 3, 6, 0, 11>(steps, kb);
+            }
+        }
+        else if (!strcmp(c, "split")) { run_split<0>(steps, kb); run_split<1>(steps, kb); run_split<0>(steps, kb); run_split<1>(steps, kb); }
         else { printf("unknown case %s\n", c); return 2; }
         return 0;
     }
