@@ -121,6 +121,9 @@ struct Layout {
     int fold;
     size_t x6qw, bfw;
     size_t fold_w;         // fp32 scratch [2M][M]: W1z W3 (fp64 sums, rounded once)
+    // ... and the terminal heads' first layers for the chain kernels (x6 layout), so the last step stores h2 too:
+    // pi [Wp1 W3] (M x Lp) with bp1 + Wp1 b3, Q1|Q2 [Wq1a | Wq1z W3] (2M x Kx) with bq1 + Wq1z b3
+    size_t fpi_x6, fpi_b, fq_x6, fq_b, fold_p, fold_q;
     size_t total;
 };
 constexpr int PACK_MAX_JOBS = 96;              // job-table capacity (pack_jobs emits ~40-60)
@@ -231,11 +234,21 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
     }
     w->fold = 0;
     w->x6qw = w->bfw = w->fold_w = 0;
+    w->fpi_x6 = w->fpi_b = w->fq_x6 = w->fq_b = w->fold_p = w->fold_q = 0;
     if (w->M == 512 && w->Lp == w->M && w->Lr == w->M) {
         w->fold = 1;
         w->x6qw = take((size_t)2 * w->M * rup(w->Kx, 32) * 3 / 2);
         w->bfw = take((size_t)2 * w->M);
         w->fold_w = take((size_t)2 * w->M * w->M);
+        int r, k;
+        x6_shape(*w, X6_WP1, &r, &k);
+        w->fpi_x6 = take(rup(r, 32) * rup(k, 16) * 3 / 2);
+        w->fpi_b = take((size_t)w->M);
+        x6_shape(*w, X6_WQ1X, &r, &k);
+        w->fq_x6 = take(rup(r, 32) * rup(k, 16) * 3 / 2);
+        w->fq_b = take((size_t)2 * w->M);
+        w->fold_p = take((size_t)w->M * w->M);
+        w->fold_q = take((size_t)2 * w->M * w->M);
     }
     w->total = o;
     return true;
@@ -3525,6 +3538,7 @@ struct Ctx {
     mutable int split_rows = 0, split_t = 0;
     int z0c_ready = 0;   // k.z0c holds this call's per-env first-layer z0 shares (tdmpc_plan)
     int fold_ok = 0;     // tdmpc_plan: the sampled rows' rollout runs wide at every t with the folded first layer
+    int fold_heads = 0;  // ... and their terminal pi / Q read h2_{H-1} through folded first layers (no z_H formed)
 };
 
 float* Xt(const Ctx& c, int t) { return c.k.X + (size_t)t * c.k.x_stride; }
@@ -3720,7 +3734,7 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
     auto q6 = [&](int i) { return (const unsigned short*)(c.pw + w.x6q[i]); };
     a.g1s = (int)(rup(c.Kx, 32) / 32);
     const size_t rb1 = (size_t)(M / 16) * a.g1s * 1536;   // bf16 per M rows of x6q W1
-    const bool fold_in = fold && t >= 1 && !z0c, outh = fold && !last;
+    const bool fold_in = fold && t >= 1 && !z0c, outh = fold && (!last || c.fold_heads);
     a.p[0].X1 = q6(X6_W1X); a.p[1].X1 = q6(X6_W1X) + rb1;
     a.p[0].X2 = q6(X6_W2D); a.p[1].X2 = q6(X6_W2R);
     a.p[0].b1 = c.pw + w.b1x; a.p[1].b1 = c.pw + w.b1x + M;
@@ -3894,17 +3908,24 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
 }
 
 // pi(z_t) with TruncatedNormal noise for `rows` rows of X_t -> X_t action columns (tdmpc.py:39-45).
+// fold: the rows' latent columns hold h2_{t-1} (Ctx::fold_heads): the first layer is the folded [Wp1 W3], bp1 + Wp1 b3
+// (chain x6 only)
 int policy(const Ctx& c, int t, int rows, RowMap map, const float* eps, long eps_env, int eps_G, long eps_off,
-           float min_std, float* mu_out = nullptr) {
+           float min_std, float* mu_out = nullptr, bool fold = false) {
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
+    if (fold && !(use_chain(c, rows, 1, CK_PI) && use_x6(c))) {
+        snprintf(g_err, sizeof g_err, "folded pi: chain x6 kernels only");
+        return TDMPC_E_DIMS;
+    }
     if (use_chain(c, rows, 1, CK_PI)) {
         ChainArgs a = chain0(c, rows, map, t, w.Lp, w.Ap / 4, 1);
         ChainProb& p = a.p[0];
         p.W1 = c.pw + w.wp1; p.b1 = c.pw + w.bp1; p.W2 = c.pw + w.wp2; p.b2 = c.pw + w.bp2;
         a.W3 = c.pw + w.wp3; a.b3 = c.pw + w.bp3; a.n3 = w.Ar; a.nvalid = w.A; a.nstore = w.Ap;
         if (a.x6) { p.X1 = x6p(c, X6_WP1); p.X2 = x6p(c, X6_WP2); a.X3 = x6p(c, X6_WP3); }
+        if (fold) { p.X1 = (const unsigned short*)(c.pw + w.fpi_x6); p.b1 = c.pw + w.fpi_b; }
         a.Xo = Xt(c, t); a.out_q0 = 0;
         a.eps = eps; a.eps_G = eps_G; a.eps_env = eps_env; a.eps_off = eps_off; a.A = w.A;
         a.min_std = min_std; a.lo = (float)(-1.0 + 1e-6); a.hi = (float)(1.0 - 1e-6);
@@ -4014,11 +4035,16 @@ int prep(const Ctx& c, const float* noise, int iter, const float* z0) {
 
 // helper.q for both heads over `rows` rows of X_H mapped by `map`, on the chain kernel: q_p per row into k.qv
 // (the value combination happens where it is consumed: cem_kernel / qvalue_kernel).
-int q_chain(const Ctx& c, int rows, RowMap map, const float* X = nullptr, float* qo = nullptr, int q_ld = 0) {
+int q_chain(const Ctx& c, int rows, RowMap map, const float* X = nullptr, float* qo = nullptr, int q_ld = 0,
+            bool fold = false) {
     const Layout& w = c.w;
     const int M = c.M;
     ChainArgs a = chain0(c, rows, map, c.H, c.Kx, 0, 2);
     if (X) a.X = X;
+    if (fold && !a.x6) {
+        snprintf(g_err, sizeof g_err, "folded Q: chain x6 kernels only");
+        return TDMPC_E_DIMS;
+    }
     for (int q = 0; q < 2; ++q) {
         ChainProb& p = a.p[q];
         p.W1 = c.pw + w.wq1x + (size_t)q * M * c.Kx; p.b1 = c.pw + w.bq1x + q * M;
@@ -4029,6 +4055,10 @@ int q_chain(const Ctx& c, int rows, RowMap map, const float* X = nullptr, float*
         if (a.x6) {
             p.X1 = x6p(c, X6_WQ1X) + (size_t)q * (M / 32) * (rup(c.Kx, 16) / 16) * 1536;
             p.X2 = x6p(c, X6_WQ2) + (size_t)q * (M / 32) * (M / 16) * 1536;
+        }
+        if (fold) {   // the rows' latent columns hold h2_{H-1}: [Wq1a | Wq1z W3], bq1 + Wq1z b3
+            p.X1 = (const unsigned short*)(c.pw + w.fq_x6) + (size_t)q * (M / 32) * (rup(c.Kx, 16) / 16) * 1536;
+            p.b1 = c.pw + w.fq_b + q * M;
         }
     }
     a.q = qo ? qo : c.k.qv; a.q_ld = qo ? q_ld : c.k.xrows;
@@ -4502,13 +4532,15 @@ __global__ void __launch_bounds__(PACK_WG) pack_fused_kernel(PackHdr* hdr, const
 // fp32, then split into the x6q planes with the a columns of w1x in front. A step whose input latent columns hold the
 // previous step's h2 = ELU(W2 h1 + b2) computes W1 [a; W3 h2 + b3] + b1 as [W1a | W1z W3] [a; h2] + (b1 + W1z b3).
 struct FoldArgs {
-    const float* w1x; const float* w3d; const float* b3; const float* b1x;
-    float* fw; float* bf; unsigned short* x6;   // W1z W3 [2M][M] fp32, folded bias [2M], x6q [2M][rup(Kx, 32)]
-    int M, L, Ap, Kx;
+    const float* W; int Kp, zoff;          // source first layer: fp32 panel [R][Kp], z in columns [zoff, zoff + L)
+    const float* w3d; const float* b3; const float* b;   // W3 panel [Lr][M], b3 [L], the source bias [R]
+    float* fw; float* bf;                  // W_z W3 [R][M] fp32 and b + W_z b3 [R]
+    unsigned short* x6; int kind, pk;      // planes of [W_a | W_z W3] (k < zoff from W, then fw): kind 0 x6q, 1 x6
+    int M, L;
 };
 __global__ void __launch_bounds__(256) fold_gemm_kernel(const FoldArgs a) {
-    // 16 x 16 output tile per workgroup: rows i of both heads [0, 2M), columns j of W3 [0, M) -- tile column M / 16
-    // is the bias column (j = M: b3)
+    // 16 x 16 output tile per workgroup: rows i [0, R), columns j of W3 [0, M) -- tile column M / 16 is the bias
+    // column (j = M: b3)
     __shared__ double sA[16][17], sB[16][17];
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
@@ -4516,7 +4548,7 @@ __global__ void __launch_bounds__(256) fold_gemm_kernel(const FoldArgs a) {
     double acc = 0.0;
     for (int l0 = 0; l0 < a.L; l0 += 16) {
         const int la = l0 + tx, lb = l0 + ty;
-        sA[ty][tx] = la < a.L ? (double)a.w1x[pidx(i, a.Ap + la, a.Kx)] : 0.0;
+        sA[ty][tx] = la < a.L ? (double)a.W[pidx(i0 + ty, a.zoff + la, a.Kp)] : 0.0;
         double b = 0.0;
         if (lb < a.L) b = j < a.M ? (double)a.w3d[pidx(lb, j, a.M)] : (j == a.M ? (double)a.b3[lb] : 0.0);
         sB[ty][tx] = b;
@@ -4526,37 +4558,58 @@ __global__ void __launch_bounds__(256) fold_gemm_kernel(const FoldArgs a) {
         __syncthreads();
     }
     if (j < a.M) a.fw[(size_t)i * a.M + j] = (float)acc;
-    else if (j == a.M) a.bf[i] = (float)((double)a.b1x[i] + acc);
+    else if (j == a.M) a.bf[i] = (float)((double)a.b[i] + acc);
 }
-__global__ void __launch_bounds__(256) fold_x6q_kernel(const FoldArgs a, long work) {
+__global__ void __launch_bounds__(256) fold_split_kernel(const FoldArgs a, long work) {
     const long i = (long)blockIdx.x * 256 + threadIdx.x;
     if (i >= work) return;
     const int j = (int)(i & 7), lane = (int)((i >> 3) & 63);
     const long blk = i >> 9;
-    const int G = (a.Kx + 31) / 32;
-    const int g = (int)(blk % G), nb = (int)(blk / G);
-    const int r = 16 * nb + (lane & 15), k = 32 * g + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
+    int r, k;
+    if (a.kind == 0) {   // x6q: 16-row x 32-k blocks (the wide kernels)
+        const int G = (a.pk + 31) / 32;
+        const int g = (int)(blk % G), nb = (int)(blk / G);
+        r = 16 * nb + (lane & 15);
+        k = 32 * g + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
+    } else {             // x6: 32-row x 16-k blocks (the chain kernels)
+        const int G = (a.pk + 15) / 16;
+        const int g = (int)(blk % G), nb = (int)(blk / G);
+        r = 32 * nb + (lane & 31);
+        k = 16 * g + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
+    }
     float x = 0.f;
-    if (k < a.Ap) x = a.w1x[pidx(r, k, a.Kx)];
-    else if (k < a.Ap + a.M) x = a.fw[(size_t)r * a.M + (k - a.Ap)];
+    if (k < a.zoff) x = a.W[pidx(r, k, a.Kp)];
+    else if (k < a.zoff + a.M && k < a.pk) x = a.fw[(size_t)r * a.M + (k - a.zoff)];
     __bf16 h, m, l;
     split3(x, h, m, l);
     a.x6[(blk * 3 + 0) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, h);
     a.x6[(blk * 3 + 1) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, m);
     a.x6[(blk * 3 + 2) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, l);
 }
-int pack_fold(const Layout& w, float* pw, hipStream_t s) {
+int fold_one(const Layout& w, float* pw, hipStream_t s, size_t W, int R, int Kp, int zoff, size_t b, size_t fw,
+             size_t bf, size_t x6, int kind, int pk) {
     FoldArgs f;
     memset(&f, 0, sizeof f);
-    f.w1x = pw + w.w1x; f.w3d = pw + w.w3d; f.b3 = pw + w.b3d; f.b1x = pw + w.b1x;
-    f.fw = pw + w.fold_w; f.bf = pw + w.bfw; f.x6 = (unsigned short*)(pw + w.x6qw);
-    f.M = w.M; f.L = w.L; f.Ap = w.Ap; f.Kx = w.Kx;
-    hipLaunchKernelGGL(fold_gemm_kernel, dim3(w.M / 16 + 1, 2 * w.M / 16), dim3(256), 0, s, f);
+    f.W = pw + W; f.Kp = Kp; f.zoff = zoff; f.w3d = pw + w.w3d; f.b3 = pw + w.b3d; f.b = pw + b;
+    f.fw = pw + fw; f.bf = pw + bf; f.x6 = (unsigned short*)(pw + x6); f.kind = kind; f.pk = pk;
+    f.M = w.M; f.L = w.L;
+    hipLaunchKernelGGL(fold_gemm_kernel, dim3(w.M / 16 + 1, R / 16), dim3(256), 0, s, f);
     HIPCHK(hipGetLastError());
-    const long work = (long)(2 * w.M / 16) * (rup(w.Kx, 32) / 32) * 512;
-    hipLaunchKernelGGL(fold_x6q_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, f, work);
+    const long work = kind == 0 ? (long)(R / 16) * ((pk + 31) / 32) * 512 : (long)((R + 31) / 32) * ((pk + 15) / 16) * 512;
+    hipLaunchKernelGGL(fold_split_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, f, work);
     HIPCHK(hipGetLastError());
     return 0;
+}
+int pack_fold(const Layout& w, float* pw, hipStream_t s) {
+    int rc, r, k;
+    // TOLD.next (both heads, the wide kernel's x6q): [W1a | W1z W3], b1 + W1z b3
+    if ((rc = fold_one(w, pw, s, w.w1x, 2 * w.M, w.Kx, w.Ap, w.b1x, w.fold_w, w.bfw, w.x6qw, 0, w.Kx))) return rc;
+    // pi (chain x6): [Wp1 W3], bp1 + Wp1 b3
+    x6_shape(w, X6_WP1, &r, &k);
+    if ((rc = fold_one(w, pw, s, w.wp1, w.M, w.Lp, 0, w.bp1, w.fold_p, w.fpi_b, w.fpi_x6, 1, k))) return rc;
+    // Q1 | Q2 (chain x6): [Wq1a | Wq1z W3], bq1 + Wq1z b3
+    x6_shape(w, X6_WQ1X, &r, &k);
+    return fold_one(w, pw, s, w.wq1x, 2 * w.M, w.Kx, w.Ap, w.bq1x, w.fold_q, w.fq_b, w.fq_x6, 1, k);
 }
 
 // The job list of a layout and the reference tensors t (state_dict order, tdmpc_num_param_tensors of them)
@@ -5063,6 +5116,10 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
         const RowMap rm0 = {N, T, 0};
         c.fold_ok = fold_on() && c.w.fold && H > 1 && use_wide(c, B * N, rm0, c.z0c_ready != 0) &&
                     use_wide(c, B * N, rm0, false);
+        // the terminal pi / Q of the sampled rows on the chain x6 kernels with folded first layers (the wide heads
+        // carry no folded form): then the last step stores h2 too and z_H is never formed
+        c.fold_heads = c.fold_ok && !use_wide_heads(c) && use_x6(c) && use_chain(c, B * N, 1, CK_PI) &&
+                       use_chain(c, B * N, 2, CK_Q) && (P == 0 || use_chain(c, B * P, 2, CK_Q));
     }
 
     // pi pre-rollout (tdmpc.py:113-118) fused with CEM iteration 0: at each step t the policy rows get
@@ -5097,7 +5154,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     ca.value_out = value_out;
     ca.pstatus = pack_status(c); ca.status = prm->status;
     const bool wide_heads = use_wide_heads(c);
-    if (wide_heads || use_chain(c, B * T, 2, CK_Q)) {   // q1, q2 per row in k.qv; cem_kernel forms the values
+    if (wide_heads || c.fold_heads || use_chain(c, B * T, 2, CK_Q)) {   // q1, q2 per row in k.qv; cem_kernel forms the values
         ca.G = c.k.G; ca.qv = c.k.qv; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H];
     }
     const size_t cem_lds = cem_lds_bytes(T, H, ca.K, c.A);
@@ -5121,6 +5178,19 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
                 if (rc || (rc = flush_split(c))) return rc;
             }
             if ((rc = terminal_wide(c, noise, toff, prm->min_std))) return rc;
+        } else if (c.fold_heads) {
+            // the sampled rows' X_H holds h2_{H-1} (folded first layers), the policy rows' holds z_H: one launch each
+            if ((rc = policy(c, H, B * N, rm, noise, c.eps_env, N, toff, prm->min_std, nullptr, true))) return rc;
+            if (P > 0) {
+                if (i == 0 || !pi_cache)
+                    rc = policy(c, H, B * P, pmH, noise, c.eps_env, P, toff + (long)N * c.A, prm->min_std,
+                                pi_cache ? c.k.pimu : nullptr);
+                else
+                    rc = policy_from_mu(c, B * P, pmH, noise, c.eps_env, P, toff + (long)N * c.A, prm->min_std);
+                if (rc) return rc;
+            }
+            if ((rc = q_chain(c, B * N, rm, nullptr, nullptr, 0, true))) return rc;
+            if (P > 0 && (rc = q_chain(c, B * P, pmH))) return rc;
         } else if (pi_cache && i > 0) {
             if ((rc = policy(c, H, B * N, rm, noise, c.eps_env, N, toff, prm->min_std))) return rc;
             if ((rc = flush_split(c))) return rc;
@@ -5130,7 +5200,7 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
                                 pi_cache ? c.k.pimu : nullptr))) {
             return rc;
         }
-        if (!wide_heads && (rc = terminal_q(c, prm->discount_pow[H]))) return rc;
+        if (!wide_heads && !c.fold_heads && (rc = terminal_q(c, prm->discount_pow[H]))) return rc;
         ca.final_iter = i == I - 1;
         ca.iter = i;
         hipLaunchKernelGGL(cem_kernel, dim3(B), dim3(1024), cem_lds, c.s, ca);
