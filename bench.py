@@ -673,10 +673,13 @@ def step_roofline(cfg, B, agent, one_step, n_r, dev, pmc_prefix):
         rb = 16 if name.startswith("chain16") else 32
         if wide:
             peak = X6_PEAK_TFLOPS
+            fold = ("; latent 512: x streamed through the ring (XS), the first layer folded to [W1a | W1z W3] on "
+                    "h2 of the previous step and h2 stored instead of z' (OUTH: no layer 3; FLOPs counted as executed)"
+                    if "OUTH" in name else "")
             kernel = (f"{name} (TOLD.next: dynamics + reward heads on 128-row "
                       f"workgroups, 8 waves x 16 rows x all {M} hidden columns in registers, layer 1 streamed into "
                       f"layer 2 by 64-column chunks, x6 weight fragments LDS-DMA'd once per workgroup into an LDS ring; "
-                      f"{rows} rows x 2 heads per launch), fp32 products from a three-way bf16 split of both "
+                      f"{rows} rows x 2 heads per launch{fold}), fp32 products from a three-way bf16 split of both "
                       f"operands: 6 v_mfma_f32_16x16x32_bf16 per product, fp32 accumulation (peak = dense BF16 / 6)")
         elif x6:
             peak = X6_PEAK_TFLOPS
@@ -736,9 +739,16 @@ def step_roofline(cfg, B, agent, one_step, n_r, dev, pmc_prefix):
         # each, 8 per step) from L2 into LDS once per launch -- 4 super-chunks x (G1 + 16) steps per head + 2 NB3
         # layer-3 steps of the dynamics head -- against the LDS-DMA rate measured with nothing else running
         # (tools/mb/dma_ring.hip: the kernel's own ring, 16.4-16.7 TB/s over the chip, profiles/r05/dma_ring_probe_*.txt)
-        g1, nb3 = (int(v) for v in name[name.index("<") + 1:name.index(">")].split(","))
+        # (latent 512: mode XS streams each first-layer step's x beside the weights, 16 KiB per workgroup and step;
+        # OUTH stores h2 for the folded first layer and runs no layer 3)
+        fields = [v.strip() for v in name[name.index("<") + 1:name.index(">")].split(",")]
+        g1, nb3 = int(fields[0]), int(fields[1])
+        mode = fields[2] if len(fields) > 2 else ""
         nrb = -(-rows // 128)
-        fill = float(nrb * (4 * (g1 + 16) * 2 + 2 * nb3) * 8 * 3072)
+        tail = 0 if "OUTH" in mode else (2 * nb3 if nb3 <= 8 else 16 * (nb3 // 8))
+        fill = float(nrb * (4 * (g1 + 16) * 2 + tail) * 8 * 3072)
+        if "XS" in mode:
+            fill += float(nrb * 2 * 4 * g1 * 8 * 2048)
         tbs = fill / avg_s / 1e12
         roof["weight_stream"] = {
             "bytes_per_launch": fill, "achieved_tbs": round(tbs, 3), "ceiling_tbs": LDSDMA_CEILING_TBS,
