@@ -734,6 +734,11 @@ def step_roofline(cfg, B, agent, one_step, n_r, dev, pmc_prefix):
     if roof["traffic"]:
         roof["hbm_gbs_pmc"] = round(roof["traffic"] / avg_s / 1e9, 1)
         roof["hbm_frac_pmc"] = round(roof["hbm_gbs_pmc"] / HBM_PEAK_GBS, 4)
+    if n > 0 and wide and "OUTH" in kernel:
+        # the folded rollout runs no layer 3 between steps: the reference's FLOPs of the same TOLD.next (layer 3
+        # included) over the same time, next to the executed-FLOP fraction above
+        per_row_exec = 2.0 * (2 * ((Lt + A) * M + M * M) + M)
+        roof["frac_algorithmic"] = round(achieved * (per_row_exec + 2.0 * M * Lt) / per_row_exec / peak, 4)
     if n > 0 and wide:
         # the wide kernel's weight stream: each workgroup fills its head's x6 weight fragments (3 KiB
         # each, 8 per step) from L2 into LDS once per launch -- 4 super-chunks x (G1 + 16) steps per head + 2 NB3

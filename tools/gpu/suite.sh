@@ -29,7 +29,7 @@ OUT=gpurun_out/$1; shift
 mkdir -p "$OUT"
 CONFIG=${CONFIG:-humanoid-run}; ENVS=${ENVS:-32}
 SHORT="--steps 3 --warmup 1 --no-cpu --no-single --no-replay --no-learner --no-icem --no-exact --no-roofline --sweep= --also="
-WK='wide_step_kernel<4, 7>'
+WK='wide_step_kernel<4, 7, 0>'
 
 for stage in "$@"; do
   case $stage in
