@@ -3836,6 +3836,7 @@ int launch_cs(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
     a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
     a.hx = c.k.cs_hx; a.pz = c.k.cs_pz; a.pr = c.k.cs_pr; a.cnt = c.k.cs_cnt;
     a.err = c.k.cs_cnt + (CS_CNT_WORDS - 64); a.status = c.status; a.ord = c.cs_ord++;
+    a.stamps = g_p1_stamps;   // (read only by a -DCS_STAMPS diagnostic build)
     const int g1 = a.g1s, nb3 = (int)rup(w.L, 16) / 16;
     const dim3 grid((unsigned)(32 * ((a.nrb + 3) / 4))), block(64 * WS_NW);
     Profiler& pf = g_prof;
