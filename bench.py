@@ -669,8 +669,7 @@ def step_roofline(cfg, B, agent, one_step, n_r, dev, pmc_prefix):
     if n > 0:
         name = L.tdmpc_profile_kernel().decode()   # the library names the kernel it launched
         wide = name.startswith("wide_step_kernel")
-        cs = name.startswith("cs_step_kernel")
-        x6 = wide or cs or name.endswith(", x6>")
+        x6 = wide or name.endswith(", x6>")
         rb = 16 if name.startswith("chain16") else 32
         if wide:
             peak = X6_PEAK_TFLOPS
@@ -682,14 +681,6 @@ def step_roofline(cfg, B, agent, one_step, n_r, dev, pmc_prefix):
                       f"layer 2 by 64-column chunks, x6 weight fragments LDS-DMA'd once per workgroup into an LDS ring; "
                       f"{rows} rows x 2 heads per launch{fold}), fp32 products from a three-way bf16 split of both "
                       f"operands: 6 v_mfma_f32_16x16x32_bf16 per product, fp32 accumulation (peak = dense BF16 / 6)")
-        elif cs:
-            peak = X6_PEAK_TFLOPS
-            kernel = (f"{name} (TOLD.next: dynamics + reward heads, column split -- four workgroups per 128-row block "
-                      f"and head, each a quarter of the {M} hidden columns, h1 exchanged through the XCD's L2, the "
-                      f"layer-3 / reward partials reduced in fixed order; x6 weight fragments and the streamed x / h1 "
-                      f"LDS-DMA'd into an LDS ring; {rows} rows x 2 heads per launch), fp32 products from a three-way "
-                      f"bf16 split of both operands: 6 v_mfma_f32_16x16x32_bf16 per product, fp32 accumulation "
-                      f"(peak = dense BF16 / 6)")
         elif x6:
             peak = X6_PEAK_TFLOPS
             kernel = (f"{name} (TOLD.next: dynamics + reward heads, {rb}-row blocks, hidden activations in LDS, weights streamed from L2; {rows} rows x 2 "
@@ -702,7 +693,7 @@ def step_roofline(cfg, B, agent, one_step, n_r, dev, pmc_prefix):
                       f"launch), fp32 {'v_mfma_f32_32x32x2_f32' if rb == 32 else 'v_mfma_f32_16x16x4_f32'}")
         kx = A + Lt
         alg_bytes = 4.0 * (rows * (kx + Lt + 2) + 2 * M * kx + 2 * M * M + M * Lt + M)
-        pmc_key = f"{pmc_prefix}/" + ("wide_step" if wide else "cs_step" if cs else "chain_step" + ("_x6" if x6 else ""))
+        pmc_key = f"{pmc_prefix}/" + ("wide_step" if wide else "chain_step" + ("_x6" if x6 else ""))
     else:
         n, ms, fl = timed(0, 0, M, rows)
         kernel = (f"linear_lds_kernel (128x128 LDS-staged tile): CEM rollout layer 2 (dynamics + reward "

@@ -28,7 +28,7 @@ def hipcc() -> str:
 def build(force: bool = False, verbose: bool = True, variant: str = "", defines=()) -> str:
     """The library (every source compiled in parallel, then linked); a variant (-DNAME defines, diagnostics or an A/B
     of a kernel knob) goes to libtdmpc_hip_<variant>.so, loaded with TDMPC_LIB_PATH."""
-    deps = SRCS + [os.path.join(HERE, "csrc", f) for f in ("plan1.inc", "wide_step.inc", "cs_step.inc", "wide_heads.inc")] + \
+    deps = SRCS + [os.path.join(HERE, "csrc", f) for f in ("plan1.inc", "wide_step.inc", "wide_heads.inc")] + \
         [os.path.join(REPO, "include", h) for h in ("tdmpc_hip.h", "tdmpc_replay.h", "tdmpc_learner.h")]
     out = OUT if not variant else os.path.join(HERE, f"libtdmpc_hip_{variant}.so")
     if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):

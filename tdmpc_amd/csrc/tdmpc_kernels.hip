@@ -284,15 +284,8 @@ struct Work {
     int xrows;       // rup(B*T, 32)
     char* p1;        // exchange region of the persistent one-env plan (plan1.inc), p1_bytes (0: not eligible)
     size_t p1_bytes;
-    // the column-split step kernel's exchange (cs_step.inc), for up to CS_MAX_ROWS rows per head
-    float* cs_hx;    // [2 CS_MAX_ROWS / 128 groups][128][512] h1 panels
-    float* cs_pz;    // [CS_MAX_ROWS / 128][4][128][Lr] partial z'
-    float* cs_pr;    // [CS_MAX_ROWS / 128][4][128] partial reward dots
-    unsigned* cs_cnt;   // [2 CS_MAX_ROWS / 128][32] hand-off counters (+ the error word after them)
     size_t total;
 };
-constexpr int CS_MAX_ROWS = 4096;
-constexpr int CS_CNT_WORDS = 2 * CS_MAX_ROWS / 128 * 32 + 64;
 
 size_t pixel_act_floats(const Layout& w) {
     size_t m = 0;
@@ -399,10 +392,6 @@ void make_work(const tdmpc_dims* d, const Layout& w, char* base, Work* k, int ex
     k->enc_tmp = (float*)take(d->modality ? 2 * B * pixel_act_floats(w) * 4 : 256);
     k->p1_bytes = p1_dims_ok(d, w) && !extra ? p1_region(d, w).total : 0;
     k->p1 = k->p1_bytes ? (char*)take(k->p1_bytes) : nullptr;
-    k->cs_hx = (float*)take((size_t)2 * CS_MAX_ROWS * 512 * 4);
-    k->cs_pz = (float*)take((size_t)CS_MAX_ROWS * 4 * w.Lr * 4);
-    k->cs_pr = (float*)take((size_t)CS_MAX_ROWS * 4 * 4);
-    k->cs_cnt = (unsigned*)take((size_t)CS_CNT_WORDS * 4);
     k->total = o;
 }
 
@@ -2767,7 +2756,6 @@ struct CemArgs {
     float* elite_out; float* score_out; float* mean_out; float* std_out;
     int no_pick; float* reward_out;     // tdmpc_cem_iter: stop after the refit; reward mean -> reward_out [B]
     const int* pstatus; int* status;    // the packed buffer's sticky pack status -> the caller's status word
-    const unsigned* cs_err;             // the column-split step kernel's error word (a hand-off gave up): NaN outputs
 };
 
 DEVI uint32_t f2ord(float v) {
@@ -2914,7 +2902,7 @@ __global__ void __launch_bounds__(1024) cem_kernel(const CemArgs a) {
         for (int i = tid; i < HKA; i += nt) a.elite_store[(size_t)e * a.Hmax * a.K * A + i] = EA[i];
     if (!a.final_iter) return;
     // a stale pack (PackHdr.status) poisoned the weights: raise it into the caller's word, NaN the outputs below
-    const int pst = (a.pstatus ? *a.pstatus : 0) | (a.cs_err && *a.cs_err ? TDMPC_STATUS_P1_TIMEOUT : 0);
+    const int pst = a.pstatus ? *a.pstatus : 0;
     if (pst && tid == 0 && a.status)
         __hip_atomic_fetch_or(a.status, pst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (a.elite_out)
@@ -3211,7 +3199,6 @@ int set_lds_attr() {
 
 #include "plan1.inc"
 #include "wide_step.inc"
-#include "cs_step.inc"
 #include "wide_heads.inc"
 
 #define FOR_EACH_LINEAR(X)                                                                          \
@@ -3235,10 +3222,6 @@ int init_attrs() {
     HIPCHK(hipFuncSetAttribute((const void*)wide_step_kernel<G1, NB3, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     WIDE_FOR_EACH(WIDE_ATTR)
 #undef WIDE_ATTR
-#define CS_ATTR(G1, NB3) \
-    HIPCHK(hipFuncSetAttribute((const void*)cs_step_kernel<G1, NB3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    CS_FOR_EACH(CS_ATTR)
-#undef CS_ATTR
 #define WIDE_HEADS_ATTR(G1P, NB3P, G1Q, NSTQ) \
     HIPCHK(hipFuncSetAttribute((const void*)wide_heads_kernel<G1P, NB3P, G1Q, NSTQ>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     WIDE_HEADS_FOR_EACH(WIDE_HEADS_ATTR)
@@ -3556,9 +3539,6 @@ struct Ctx {
     int z0c_ready = 0;   // k.z0c holds this call's per-env first-layer z0 shares (tdmpc_plan)
     int fold_ok = 0;     // tdmpc_plan: the sampled rows' rollout runs wide at every t with the folded first layer
     int fold_heads = 0;  // ... and their terminal pi / Q read h2_{H-1} through folded first layers (no z_H formed)
-    int cs_ok = 0;       // tdmpc_plan: narrow sampled-row steps may run on the column-split kernel (counters zeroed)
-    mutable unsigned cs_ord = 0;   // its launch ordinal within the plan
-    int* status = nullptr;         // the caller's sticky status word (tdmpc_plan)
 };
 
 float* Xt(const Ctx& c, int t) { return c.k.X + (size_t)t * c.k.x_stride; }
@@ -3805,65 +3785,6 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
     return 0;
 }
 
-// ---- the column-split step kernel (cs_step.inc) for narrow launches: 2,048-4,096 rows per head (dog-run's 8-env share),
-// inside tdmpc_plan only (its counters are zeroed per plan); TDMPC_CS=0 turns it off
-bool use_cs(const Ctx& c, int rows, const RowMap& map) {
-    static const int en = [] { const char* e = getenv("TDMPC_CS"); return e ? atoi(e) : 1; }();
-    if (!en || !c.cs_ok || c.path != TDMPC_PATH_AUTO || c.w.M != 512 || !use_x6(c) || !num_cus()) return false;
-    if (rows % 16 || map.G % 16 || map.S % 16 || map.O % 16 || rows > CS_MAX_ROWS || rows < 2048) return false;
-    const int g1 = (int)rup(c.Kx, 32) / 32, nb3 = (int)rup(c.w.L, 16) / 16;
-    const bool inst = (nb3 == 4 && (g1 == 2 || g1 == 3)) || (nb3 == 7 && (g1 == 4 || g1 == 5));
-    const int nrb = (rows + 127) / 128;
-    return inst && 32 * ((nrb + 3) / 4) <= num_cus();
-}
-int launch_cs(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last) {
-    const Layout& w = c.w;
-    const int M = c.M;
-    CsArgs a;
-    memset(&a, 0, sizeof a);
-    auto q6 = [&](int i) { return (const unsigned short*)(c.pw + w.x6q[i]); };
-    a.g1s = (int)(rup(c.Kx, 32) / 32);
-    const size_t rb1 = (size_t)(M / 16) * a.g1s * 1536;
-    a.p[0].X1 = q6(X6_W1X); a.p[1].X1 = q6(X6_W1X) + rb1;
-    a.p[0].X2 = q6(X6_W2D); a.p[1].X2 = q6(X6_W2R);
-    a.p[0].b1 = c.pw + w.b1x; a.p[1].b1 = c.pw + w.b1x + M;
-    a.p[0].b2 = c.pw + w.b2d; a.p[1].b2 = c.pw + w.b2r;
-    a.p[1].w3v = c.pw + w.w3r; a.p[1].b3v = c.pw + w.b3r;
-    a.X3 = q6(X6_W3D); a.b3 = c.pw + w.b3d; a.nvalid = w.L; a.nstore = w.Lp; a.Lr = w.Lr;
-    a.rows = rows; a.nrb = (rows + 127) / 128; a.amap = map;
-    a.X = Xt(c, t); a.x_ts = (long)c.Kx * 32; a.kq = c.Kx / 4;
-    a.Xo = Xt(c, t + 1); a.out_q0 = w.Ap / 4;
-    a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
-    a.hx = c.k.cs_hx; a.pz = c.k.cs_pz; a.pr = c.k.cs_pr; a.cnt = c.k.cs_cnt;
-    a.err = c.k.cs_cnt + (CS_CNT_WORDS - 64); a.status = c.status; a.ord = c.cs_ord++;
-    a.stamps = g_p1_stamps;   // (read only by a -DCS_STAMPS diagnostic build)
-    const int g1 = a.g1s, nb3 = (int)rup(w.L, 16) / 16;
-    const dim3 grid((unsigned)(32 * ((a.nrb + 3) / 4))), block(64 * WS_NW);
-    Profiler& pf = g_prof;
-    const bool prof = pf.armed && pf.cfg == 4 + CH_STEP && pf.n + 2 <= pf.cap && (pf.rows == 0 || rows == pf.rows);
-    if (prof) {
-        snprintf(pf.kernel, sizeof pf.kernel, "cs_step_kernel<%d, %d>", g1, nb3);
-        HIPCHK(hipEventRecord(pf.ev[pf.n], c.s));
-    }
-    bool done = false;
-#define CS_LAUNCH(G1, NB3) \
-    if (!done && g1 == G1 && nb3 == NB3) { \
-        hipLaunchKernelGGL((cs_step_kernel<G1, NB3>), grid, block, (size_t)CS_NS * CS_SLOT, c.s, a); \
-        done = true; \
-    }
-    CS_FOR_EACH(CS_LAUNCH)
-#undef CS_LAUNCH
-    if (!done) { snprintf(g_err, sizeof g_err, "cs step: no instance for G1 %d NB3 %d", g1, nb3); return TDMPC_E_DIMS; }
-    HIPCHK(hipGetLastError());
-    if (prof) {
-        HIPCHK(hipEventRecord(pf.ev[pf.n + 1], c.s));
-        pf.n += 2;
-        const double K1 = w.L + w.A;
-        pf.flops += 2.0 * rows * (2 * (K1 * M + (double)M * M) + (double)M * w.L + M);
-    }
-    return 0;
-}
-
 // defer = 1 (a loop of consecutive steps over the same rows, nothing reading X_{t+1}'s latents in between): on the
 // split path the finish of this step is folded into the next step's launch.
 
@@ -3896,22 +3817,6 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
             }
             const bool sampled = map.G == c.N && map.S == c.T && map.O == 0;   // (the folded rollout's rows only)
             return launch_wide(c, t, rows, map, disc, first, last, z0c, c.fold_ok && sampled);
-        }
-    }
-    if (!nowide && c.cs_ok) {
-        // narrow launches: the sampled rows on the column-split kernel, the policy rows (iteration 0's fused launch) on
-        // the chain kernel -- by role, as the wide split above
-        const RowMap rm = {c.N, map.S, 0}, pm = {c.P, map.S, c.N};
-        const int envs = rows / std::max(1, map.G);
-        if (c.P > 0 && c.N + c.P == c.T && map.G == c.T && map.S == c.T && map.O == 0 && rows == envs * c.T &&
-            use_cs(c, envs * c.N, rm)) {
-            if ((rc = flush_split(c))) return rc;
-            if ((rc = launch_cs(c, t, envs * c.N, rm, disc, first, last))) return rc;
-            return step_next(c, t, envs * c.P, pm, disc, first, last, 0, true);
-        }
-        if (map.G == c.N && map.S == c.T && map.O == 0 && use_cs(c, rows, map)) {
-            if ((rc = flush_split(c))) return rc;
-            return launch_cs(c, t, rows, map, disc, first, last);
         }
     }
     if (use_chain(c, rows, 2, CK_STEP)) {
@@ -5215,17 +5120,6 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
         // carry no folded form): then the last step stores h2 too and z_H is never formed
         c.fold_heads = c.fold_ok && !use_wide_heads(c) && use_x6(c) && use_chain(c, B * N, 1, CK_PI) &&
                        use_chain(c, B * N, 2, CK_Q) && (P == 0 || use_chain(c, B * P, 2, CK_Q));
-        // narrow batches: the sampled rows' steps on the column-split kernel (its hand-off counters and error word
-        // zeroed once per plan; launch ordinals from 0)
-        c.status = prm->status;
-        c.cs_ok = 1;
-        c.cs_ord = 0;
-        if (!use_cs(c, B * N, rm0) || use_wide(c, B * N, rm0, false)) {
-            c.cs_ok = 0;
-        } else {
-            hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(1024), 0, c.s, c.k.cs_cnt, CS_CNT_WORDS);
-            HIPCHK(hipGetLastError());
-        }
     }
 
     // pi pre-rollout (tdmpc.py:113-118) fused with CEM iteration 0: at each step t the policy rows get
@@ -5259,7 +5153,6 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     ca.elite_out = elite_out; ca.score_out = score_out; ca.mean_out = mean_out; ca.std_out = std_out;
     ca.value_out = value_out;
     ca.pstatus = pack_status(c); ca.status = prm->status;
-    ca.cs_err = c.cs_ok ? c.k.cs_cnt + (CS_CNT_WORDS - 64) : nullptr;
     const bool wide_heads = use_wide_heads(c);
     if (wide_heads || c.fold_heads || use_chain(c, B * T, 2, CK_Q)) {   // q1, q2 per row in k.qv; cem_kernel forms the values
         ca.G = c.k.G; ca.qv = c.k.qv; ca.q_ld = c.k.xrows; ca.discH = prm->discount_pow[H];
