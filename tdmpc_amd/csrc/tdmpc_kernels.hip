@@ -124,6 +124,7 @@ struct Layout {
     // ... and the terminal heads' first layers for the chain kernels (x6 layout), so the last step stores h2 too:
     // pi [Wp1 W3] (M x Lp) with bp1 + Wp1 b3, Q1|Q2 [Wq1a | Wq1z W3] (2M x Kx) with bq1 + Wq1z b3
     size_t fpi_x6, fpi_b, fq_x6, fq_b, fold_p, fold_q;
+    size_t fw1_x6;         // ... and TOLD.next's folded first layer again in the chain x6 layout (the policy rows)
     size_t total;
 };
 constexpr int PACK_MAX_JOBS = 96;              // job-table capacity (pack_jobs emits ~40-60)
@@ -234,7 +235,7 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
     }
     w->fold = 0;
     w->x6qw = w->bfw = w->fold_w = 0;
-    w->fpi_x6 = w->fpi_b = w->fq_x6 = w->fq_b = w->fold_p = w->fold_q = 0;
+    w->fpi_x6 = w->fpi_b = w->fq_x6 = w->fq_b = w->fold_p = w->fold_q = w->fw1_x6 = 0;
     if (w->M == 512 && w->Lp == w->M && w->Lr == w->M) {
         w->fold = 1;
         w->x6qw = take((size_t)2 * w->M * rup(w->Kx, 32) * 3 / 2);
@@ -249,6 +250,8 @@ bool make_layout(const tdmpc_dims* d, Layout* w) {
         w->fq_b = take((size_t)2 * w->M);
         w->fold_p = take((size_t)w->M * w->M);
         w->fold_q = take((size_t)2 * w->M * w->M);
+        x6_shape(*w, X6_W1X, &r, &k);
+        w->fw1_x6 = take(rup(r, 32) * rup(k, 16) * 3 / 2);
     }
     w->total = o;
     return true;
@@ -1070,6 +1073,9 @@ struct ChainArgs {
     const float* z0c; int z0_G, k1c;
     // CH_Q: q_p of row x at q[p * q_ld + x]
     float* q; int q_ld;
+    // CH_STEP (chain_kernel, latent_dim == mlp_dim): store h2 = ELU(W2 h1 + b2) into Xo's latent columns instead of
+    // running layer 3 -- the next step / the terminal heads read it through folded first layers (Layout::fold)
+    int outh;
 };
 
 // Weight ring: D k groups x TN 1-KiB wave loads of the weight panel in flight. ring_fill issues the first D
@@ -1636,6 +1642,18 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(X6
     lds_barrier();
     chain_store_lds<TN>(sH, v, cw0, r, h);
     lds_barrier();
+    if (MODE == CH_STEP && a.outh) {
+        // h2 where z' would go (M = Lp columns from quad out_q0): the folded first layers read it
+        for (int i = tid; i < (M >> 2) * 32; i += NTH) {
+            const int row = i & 31, cq = i >> 5, lm = m0 + row;
+            if (lm >= a.rows) continue;
+            const int xr = map_row(a.amap, lm);
+            *(float4*)(a.Xo + (size_t)(xr >> 5) * a.x_ts + (size_t)(a.out_q0 + cq) * 128 + (xr & 31) * 4) =
+                *(const float4*)(sH + (cq * 32 + row) * 4);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the layer-3 weight prefetch, unused here)
+        return;
+    }
 
     // ---- layer 3: [32 x M] . W3^T -> [32 x n3]; partial tiles meet in the activation block after the reads
     floatx16 a3a[1], a3b[1];
@@ -3539,6 +3557,7 @@ struct Ctx {
     int z0c_ready = 0;   // k.z0c holds this call's per-env first-layer z0 shares (tdmpc_plan)
     int fold_ok = 0;     // tdmpc_plan: the sampled rows' rollout runs wide at every t with the folded first layer
     int fold_heads = 0;  // ... and their terminal pi / Q read h2_{H-1} through folded first layers (no z_H formed)
+    int fold_policy = 0; // ... and the policy rows' pre-rollout carries h2 too (chain kernels, folded first layers)
 };
 
 float* Xt(const Ctx& c, int t) { return c.k.X + (size_t)t * c.k.x_stride; }
@@ -3788,8 +3807,10 @@ int launch_wide(const Ctx& c, int t, int rows, RowMap map, float disc, int first
 // defer = 1 (a loop of consecutive steps over the same rows, nothing reading X_{t+1}'s latents in between): on the
 // split path the finish of this step is folded into the next step's launch.
 
+// fold (the policy rows of a plan with Ctx::fold_policy, on chain_kernel x6): t >= 1 reads h2 through the folded first
+// layer, every step stores h2 (the terminal heads are folded too)
 int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, int last, int defer = 0,
-              bool nowide = false) {
+              bool nowide = false, bool fold = false) {
     const Layout& w = c.w;
     const int M = c.M;
     int rc;
@@ -3813,7 +3834,7 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
             if (c.P > 0 && c.N + c.P == c.T && map.G == c.T && map.S == c.T && map.O == 0 && rows == envs * c.T &&
                 use_wide(c, envs * c.N, rm, z0c_rm)) {
                 if ((rc = launch_wide(c, t, envs * c.N, rm, disc, first, last, z0c_rm, c.fold_ok))) return rc;
-                return step_next(c, t, envs * c.P, pm, disc, first, last, 0, true);
+                return step_next(c, t, envs * c.P, pm, disc, first, last, 0, true, c.fold_policy != 0);
             }
             const bool sampled = map.G == c.N && map.S == c.T && map.O == 0;   // (the folded rollout's rows only)
             return launch_wide(c, t, rows, map, disc, first, last, z0c, c.fold_ok && sampled);
@@ -3835,6 +3856,18 @@ int step_next(const Ctx& c, int t, int rows, RowMap map, float disc, int first, 
         a.Xo = Xt(c, t + 1); a.out_q0 = w.Ap / 4;
         a.G = c.k.G; a.rlast = c.k.rlast; a.disc = disc; a.first = first; a.last = last;
         if (t == 0 && c.z0c_ready && map.G % 32 == 0) { a.z0c = c.k.z0c; a.z0_G = map.G; a.k1c = z0c_k1c(c); }
+        if (fold) {
+            if (a.rb != 32 || !a.x6 || !c.w.fold) {
+                snprintf(g_err, sizeof g_err, "folded step: chain_kernel x6 only");
+                return TDMPC_E_DIMS;
+            }
+            if (t >= 1) {
+                const size_t rb1 = (size_t)(M / 32) * (rup(c.Kx, 16) / 16) * 1536;
+                d.X1 = (const unsigned short*)(c.pw + w.fw1_x6); r.X1 = d.X1 + rb1;
+                d.b1 = c.pw + w.bfw; r.b1 = c.pw + w.bfw + M;
+            }
+            a.outh = 1;
+        }
         return launch_chain(CH_STEP, a, 2, c.s);
     }
     if (use_split(c, rows)) {
@@ -4587,14 +4620,16 @@ __global__ void __launch_bounds__(256) fold_split_kernel(const FoldArgs a, long 
     a.x6[(blk * 3 + 2) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, l);
 }
 int fold_one(const Layout& w, float* pw, hipStream_t s, size_t W, int R, int Kp, int zoff, size_t b, size_t fw,
-             size_t bf, size_t x6, int kind, int pk) {
+             size_t bf, size_t x6, int kind, int pk, bool gemm = true) {
     FoldArgs f;
     memset(&f, 0, sizeof f);
     f.W = pw + W; f.Kp = Kp; f.zoff = zoff; f.w3d = pw + w.w3d; f.b3 = pw + w.b3d; f.b = pw + b;
     f.fw = pw + fw; f.bf = pw + bf; f.x6 = (unsigned short*)(pw + x6); f.kind = kind; f.pk = pk;
     f.M = w.M; f.L = w.L;
-    hipLaunchKernelGGL(fold_gemm_kernel, dim3(w.M / 16 + 1, R / 16), dim3(256), 0, s, f);
-    HIPCHK(hipGetLastError());
+    if (gemm) {
+        hipLaunchKernelGGL(fold_gemm_kernel, dim3(w.M / 16 + 1, R / 16), dim3(256), 0, s, f);
+        HIPCHK(hipGetLastError());
+    }
     const long work = kind == 0 ? (long)(R / 16) * ((pk + 31) / 32) * 512 : (long)((R + 31) / 32) * ((pk + 15) / 16) * 512;
     hipLaunchKernelGGL(fold_split_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, f, work);
     HIPCHK(hipGetLastError());
@@ -4604,6 +4639,9 @@ int pack_fold(const Layout& w, float* pw, hipStream_t s) {
     int rc, r, k;
     // TOLD.next (both heads, the wide kernel's x6q): [W1a | W1z W3], b1 + W1z b3
     if ((rc = fold_one(w, pw, s, w.w1x, 2 * w.M, w.Kx, w.Ap, w.b1x, w.fold_w, w.bfw, w.x6qw, 0, w.Kx))) return rc;
+    // (the same product split again into the chain kernels' x6 layout)
+    x6_shape(w, X6_W1X, &r, &k);
+    if ((rc = fold_one(w, pw, s, w.w1x, 2 * w.M, w.Kx, w.Ap, w.b1x, w.fold_w, w.bfw, w.fw1_x6, 1, k, false))) return rc;
     // pi (chain x6): [Wp1 W3], bp1 + Wp1 b3
     x6_shape(w, X6_WP1, &r, &k);
     if ((rc = fold_one(w, pw, s, w.wp1, w.M, w.Lp, 0, w.bp1, w.fold_p, w.fpi_b, w.fpi_x6, 1, k))) return rc;
@@ -5120,6 +5158,12 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
         // carry no folded form): then the last step stores h2 too and z_H is never formed
         c.fold_heads = c.fold_ok && !use_wide_heads(c) && use_x6(c) && use_chain(c, B * N, 1, CK_PI) &&
                        use_chain(c, B * N, 2, CK_Q) && (P == 0 || use_chain(c, B * P, 2, CK_Q));
+        // the policy rows' pre-rollout (iteration 0's pi + TOLD.next on the chain kernels) through the folded layers
+        // too: needs the 32-row x6 chain kernel for their steps (its h2 epilogue)
+        if (c.fold_heads && P > 0 && use_chain(c, B * P, 2, CK_STEP) && use_chain(c, B * P, 1, CK_PI)) {
+            const ChainArgs probe = chain0(c, B * P, RowMap{P, T, N}, 0, c.Kx, 0, 2);
+            c.fold_policy = probe.rb == 32 && probe.x6;
+        }
     }
 
     // pi pre-rollout (tdmpc.py:113-118) fused with CEM iteration 0: at each step t the policy rows get
@@ -5132,7 +5176,8 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     const RowMap rm = {N, T, 0};
     if (P > 0) {
         for (int t = 0; t < H; ++t) {
-            if ((rc = policy(c, t, B * P, pm, noise, c.eps_env, P, (long)t * P * c.A, prm->min_std)))
+            if ((rc = policy(c, t, B * P, pm, noise, c.eps_env, P, (long)t * P * c.A, prm->min_std, nullptr,
+                             c.fold_policy && t >= 1)))
                 return rc;
             if ((rc = step_next(c, t, B * T, all, prm->discount_pow[t], t == 0, t == H - 1)))
                 return rc;
@@ -5184,13 +5229,13 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
             if (P > 0) {
                 if (i == 0 || !pi_cache)
                     rc = policy(c, H, B * P, pmH, noise, c.eps_env, P, toff + (long)N * c.A, prm->min_std,
-                                pi_cache ? c.k.pimu : nullptr);
+                                pi_cache ? c.k.pimu : nullptr, c.fold_policy != 0);
                 else
                     rc = policy_from_mu(c, B * P, pmH, noise, c.eps_env, P, toff + (long)N * c.A, prm->min_std);
                 if (rc) return rc;
             }
             if ((rc = q_chain(c, B * N, rm, nullptr, nullptr, 0, true))) return rc;
-            if (P > 0 && (rc = q_chain(c, B * P, pmH))) return rc;
+            if (P > 0 && (rc = q_chain(c, B * P, pmH, nullptr, nullptr, 0, c.fold_policy != 0))) return rc;
         } else if (pi_cache && i > 0) {
             if ((rc = policy(c, H, B * N, rm, noise, c.eps_env, N, toff, prm->min_std))) return rc;
             if ((rc = flush_split(c))) return rc;
