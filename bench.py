@@ -375,7 +375,7 @@ def replay_bench(cfg, dev, cpu=True, reps=200):
     return out
 
 
-def learner_bench(cfg, dev, cpu=True, reps=30, pixels=True, modes=("graph", "eager", "all_lg_gemm")):
+def learner_bench(cfg, dev, cpu=True, reps=30, pixels=True, modes=("graph", "eager", "hipblaslt")):
     """TDMPC.update (batch 512, horizon 5, the task's TOLD) fed by the device replay buffer
     (50k transitions): HIP-graph replay of the whole update vs the same update issued eagerly (the reference's
     execution model on a GPU), and the oracle restatement of the reference update on the host CPU."""
@@ -393,15 +393,15 @@ def learner_bench(cfg, dev, cpu=True, reps=30, pixels=True, modes=("graph", "eag
                          reward=torch.from_numpy(rs.standard_normal(L).astype(np.float32)))
     out = {"config": f"{lcfg.task}: batch {lcfg.batch_size}, horizon {lcfg.horizon}, latent {lcfg.latent_dim}, "
                      f"mlp {lcfg.mlp_dim}, replay 50k transitions"}
-    for mode, warm in (("graph", 3), ("eager", 10**9), ("all_lg_gemm", 3)):
+    for mode, warm in (("graph", 3), ("eager", 10**9), ("hipblaslt", 3)):
         if mode not in modes:
             continue
         agent = TDMPC(lcfg)
         agent.model.load_state_dict(synthetic_state_dict(lcfg, 0))
         agent.model_target.load_state_dict(synthetic_state_dict(lcfg, 1))
         lrn = agent.learner(graph=True, warmup=warm)
-        if mode == "all_lg_gemm" and lrn.engine is not None:
-            lrn.engine.blas = False   # the heads' plain M x M products on lg_gemm too (the default: hipBLASLt)
+        if mode == "hipblaslt" and lrn.engine is not None:
+            lrn.engine.blas = True    # the heads' products on hipBLASLt (the default: tdmpc_lg_gemm's macro tiles)
         buf = ReplayBuffer(rc, latent_plan=True)
         for _ in range(50_000 // L - 1):
             buf.add(ep)
@@ -414,9 +414,9 @@ def learner_bench(cfg, dev, cpu=True, reps=30, pixels=True, modes=("graph", "eag
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t) / reps
         out[mode] = {"value": round(1.0 / dt, 1), "unit": "updates/s", "ms_per_update": round(dt * 1e3, 3)}
-        if mode == "all_lg_gemm":
-            out[mode]["note"] = ("the same graph-replayed update with the heads' plain M x M products on the "
-                                 "hand-written lg_gemm instead of hipBLASLt (TDMPC_LG_BLAS=0)")
+        if mode == "hipblaslt":
+            out[mode]["note"] = ("the same graph-replayed update with the heads' products on hipBLASLt (torch.mm + "
+                                 "an activation launch, TDMPC_LG_BLAS=1) instead of tdmpc_lg_gemm's macro tiles")
     if "eager" in out and "graph" in out:
         out["graph_speedup_vs_eager"] = round(out["eager"]["ms_per_update"] / out["graph"]["ms_per_update"], 2)
     if pixels:

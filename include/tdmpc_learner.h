@@ -84,7 +84,9 @@ typedef struct tdmpc_lg_job {
 
 /* Up to 12 GEMMs in one launch; tile 1: 32x32 output tiles, 2: 64x64 (4 waves split K inside a workgroup).
  * Products are fp32-accurate x6 (three bf16 parts per operand, six bf16 MFMAs per pair, fp32 accumulation);
- * tile | TDMPC_LG_TILE_EXACT runs the exact v_mfma_f32_32x32x2_f32 products instead. */
+ * tile | TDMPC_LG_TILE_EXACT runs the exact v_mfma_f32_32x32x2_f32 products instead.
+ * tile 3 / 4 / 5: LDS-staged macro tiles of 64x64 / 64x128 / 128x128 outputs (m x n) per workgroup on the exact f32
+ * MFMA (the EXACT bit is implied), for the large products: every segment amode 0 without a ones column, splits 1. */
 #define TDMPC_LG_TILE_EXACT 0x100
 int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* stream);
 

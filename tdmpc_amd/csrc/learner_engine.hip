@@ -55,6 +55,7 @@ struct KJob {
 struct KArgs {
     KJob job[LG_MAXJ];
     int njobs;
+    int diag;   // (timing diagnostics of the macro tiles, TDMPC_LG_DIAG: 1 no loads after the prologue, 2 no products)
 };
 
 __device__ __forceinline__ float wsum(float v) {
@@ -403,6 +404,198 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
     }
 }
 
+// ---- LDS-staged macro tiles (tdmpc_lg_gemm tile 3 / 4 / 5: 64 x 64 / 64 x 128 / 128 x 128 outputs per workgroup) for
+// the large products (the heads' layers over H B = 2,560 - 3,072 rows, tdmpc.py:199-245). Four waves in 2 x 2, each
+// a (32 TM) x (32 TN) tile of v_mfma_f32_32x32x2_f32 accumulators over ALL of K (no K split, no LDS reduction). K
+// runs in chunks of 32 staged through LDS, double buffered: the next chunk's global loads are in flight in registers
+// while the current chunk is multiplied, then go to the other buffer; one barrier per chunk. Per chunk and operand
+// the LDS holds [kq = 0..7][row or column] float4s (k = 4 kq .. 4 kq + 3), each kq row padded by one float4 so the
+// eight lanes of a ds_write_b128 group (one row, kq 0..7) land on eight different 16-B slots; MFMA lane (r, h) reads
+// the float4 at kq = 2 g + h of its row / column r (16 consecutive float4 per ds_read_b128 lane group). The k order
+// inside a group of 8 is lg_gemm's (steps .x .. .w pair k and k + 4), and the groups of 8 go to NACC chains by their
+// index within the chunk: every output is a fixed-order sum of fixed-order f32 fma chains.
+// FORM (one per launch, from the host): LGB_AV -- every A segment takes 16-B loads (row stride and K multiples of 4,
+// aligned base), else four 4-B loads per float4; LGB_BT -- B(k, n) = b[k ldb + n] (bmode 1) for every segment, else
+// b[n ldb + k]; LGB_BV -- (bmode 0) 16-B loads of B. Branch-free loads let the compiler count the ring's vmcnt.
+enum { LGB_AV = 1, LGB_BT = 2, LGB_BV = 4 };
+
+template <int TM, int TN, int FORM, int KC, int D>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) lg_big_kernel(const KArgs P) {
+    constexpr bool AV = FORM & LGB_AV, BT = FORM & LGB_BT, BV = (FORM & LGB_BV) && !BT;
+    constexpr int BM = 64 * TM, BN = 64 * TN, SA = BM + 1, SB = BN + 1;
+    constexpr int KQ = KC / 4, NG = KC / 8;               // k quads and MFMA k groups of 8 per chunk
+    constexpr int NA = BM * KQ / 256, NB = BN * KQ / 256;  // float4 per thread per chunk and operand
+    constexpr int BUF = KQ * (SA + SB);                    // float4 per buffer
+    constexpr int LC = KC == 64 ? 6 : 5;                   // log2 KC
+    extern __shared__ float4 lg_lds[];
+    int jb = 0;
+    for (int q = 1; q < P.njobs; ++q)
+        if ((int)blockIdx.x >= P.job[q].block0) jb = q;
+    const KJob& J = P.job[jb];
+    const int tile = (int)blockIdx.x - J.block0;
+    const int m0 = (tile % J.tiles_m) * BM, n0 = (tile / J.tiles_m) * BN;
+    const int M = J.j.m, N = J.j.n;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int wm = (wave & 1) * 32 * TM, wn = (wave >> 1) * 32 * TN;
+
+    // NACC independent accumulator chains per output tile (k group g of a chunk -> chain g % NACC, summed in a fixed
+    // order at the end): one v_mfma_f32_32x32x2_f32 chain alone runs at about half the issue rate
+    constexpr int NACC = TM * TN >= 4 ? 1 : 4 / (TM * TN);
+    floatx16 acc[NACC][TM][TN];
+#pragma unroll
+    for (int q = 0; q < NACC; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[q][i][j][e] = 0.f;
+
+    // the segments' chunk ranges (nseg <= 3): chunk c is segment (c >= e0) + (c >= e1)
+    const int nseg = J.j.nseg;
+    const int c0n = (J.j.seg[0].k + KC - 1) >> LC;
+    const int c1n = nseg > 1 ? (J.j.seg[1].k + KC - 1) >> LC : 0;
+    const int c2n = nseg > 2 ? (J.j.seg[2].k + KC - 1) >> LC : 0;
+    const int e0 = c0n, e1 = c0n + c1n, nch = e1 + c2n;
+
+    float4 ra[D][NA], rb[D][NB];   // a ring of D chunks in flight in registers
+    // chunk c of the job's segments -> registers (zeros past M / N / the segment's K)
+    auto gload = [&](int c, float4 (&sa)[NA], float4 (&sb)[NB]) {
+        const int s = (c >= e0) + (c >= e1);
+        const tdmpc_lg_seg& S = J.j.seg[s];
+        const int k0 = (c - (s >= 1 ? e0 : 0) - (s >= 2 ? c1n : 0)) * KC, kh = S.k, lda = S.lda, ldb = S.ldb;
+        const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)S.a, (short)0, (int)LG_OOB, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)S.b, (short)0, (int)LG_OOB, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int u = tid + 256 * i, m = m0 + u / KQ, k = k0 + 4 * (u % KQ);
+            if constexpr (AV) {
+                const unsigned off = (m < M && k < kh) ? (unsigned)(m * lda + k) * 4u : LG_OOB;
+                sa[i] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rsa, (int)off, 0, 0));
+            } else {
+                float e[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const unsigned off = (m < M && k + q < kh) ? (unsigned)(m * lda + k + q) * 4u : LG_OOB;
+                    e[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsa, (int)off, 0, 0));
+                }
+                sa[i] = make_float4(e[0], e[1], e[2], e[3]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            if constexpr (!BT) {   // B(k, n) = b[n ldb + k]: a Linear weight, k contiguous (as A)
+                const int u = tid + 256 * j, n = n0 + u / KQ, k = k0 + 4 * (u % KQ);
+                if constexpr (BV) {
+                    const unsigned off = (n < N && k < kh) ? (unsigned)(n * ldb + k) * 4u : LG_OOB;
+                    sb[j] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rsb, (int)off, 0, 0));
+                } else {
+                    float e[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const unsigned off = (n < N && k + q < kh) ? (unsigned)(n * ldb + k + q) * 4u : LG_OOB;
+                        e[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsb, (int)off, 0, 0));
+                    }
+                    sb[j] = make_float4(e[0], e[1], e[2], e[3]);
+                }
+            } else {               // B(k, n) = b[k ldb + n]: a lane takes one column, 4 k (coalesced rows)
+                const int u = tid + 256 * j, n = n0 + u % BN, k = k0 + 4 * (u / BN);
+                float e[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const unsigned off = (n < N && k + q < kh) ? (unsigned)((k + q) * ldb + n) * 4u : LG_OOB;
+                    e[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsb, (int)off, 0, 0));
+                }
+                sb[j] = make_float4(e[0], e[1], e[2], e[3]);
+            }
+        }
+    };
+    auto sstore = [&](float4* buf, const float4 (&sa)[NA], const float4 (&sb)[NB]) {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int u = tid + 256 * i;
+            buf[(u % KQ) * SA + u / KQ] = sa[i];
+        }
+        float4* bs = buf + KQ * SA;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int u = tid + 256 * j;
+            if constexpr (!BT) bs[(u % KQ) * SB + u / KQ] = sb[j];
+            else bs[(u / BN) * SB + u % BN] = sb[j];
+        }
+    };
+    // a chunk: all four k groups' operands read first (the reads of later groups land under earlier products)
+    auto compute = [&](const float4* buf) {
+        const float4* as = buf + wm + r;
+        const float4* bs = buf + KQ * SA + wn + r;
+        float4 a[NG][TM], b[NG][TN];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) a[g][i] = as[(2 * g + h) * SA + 32 * i];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) b[g][j] = bs[(2 * g + h) * SB + 32 * j];
+        }
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    floatx16& t = acc[g % NACC][i][j];
+                    t = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g][i].x, b[g][j].x, t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g][i].y, b[g][j].y, t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g][i].z, b[g][j].z, t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g][i].w, b[g][j].w, t, 0, 0, 0);
+                }
+    };
+
+    // chunk c + 1 goes to LDS as chunk c is multiplied; chunk c + 1 + D is then loaded into its registers, so
+    // every chunk's loads have D chunks of products to land. The barrier waits for the LDS stores only
+    // (__syncthreads' fence would also drain the global loads in flight: vmcnt(0) every chunk)
+    auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+        if (d < nch) gload(d, ra[d], rb[d]);
+    sstore(lg_lds, ra[0], rb[0]);
+    if (D < nch) gload(D, ra[0], rb[0]);
+    lds_barrier();
+    for (int c0 = 0; c0 < nch; c0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int c = c0 + d;
+            if (c >= nch) break;
+            // chunk c + 1 to the other buffer first (its last readers, chunk c - 1's products, passed the last
+            // barrier): the stores then drain under chunk c's products
+            const int dn = (d + 1) % D;
+            if (c + 1 < nch) {
+                sstore(lg_lds + ((c + 1) & 1) * BUF, ra[dn], rb[dn]);
+                if (c + 1 + D < nch && !(P.diag & 1)) gload(c + 1 + D, ra[dn], rb[dn]);
+            }
+            if (!(P.diag & 2)) compute(lg_lds + (c & 1) * BUF);
+            lds_barrier();
+        }
+    }
+
+    // C/D map of the 32x32 MFMA: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int row = m0 + wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h, col = n0 + wn + 32 * j + r;
+                float v;
+                if constexpr (NACC == 4) v = (acc[0][i][j][e] + acc[1][i][j][e]) + (acc[2][i][j][e] + acc[3][i][j][e]);
+                else if constexpr (NACC == 2) v = acc[0][i][j][e] + acc[1][i][j][e];
+                else v = acc[0][i][j][e];
+                if (row < M && col < N) lg_store(J.j, 1, 0, row, col, v);
+            }
+}
+
+template <int TM, int TN, int KC>
+constexpr size_t lg_big_lds() { return (size_t)2 * (KC / 4) * (64 * TM + 1 + 64 * TN + 1) * sizeof(float4); }
+
 // ---------------------------------------------------------------------------------------------------- rows
 template <int NC>
 __global__ void __launch_bounds__(256) lg_rows_fwd_kernel(const tdmpc_lg_rows a) {
@@ -708,15 +901,19 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
     if (!jobs) return TDMPC_E_NULL;
     const bool x6 = !(tile & TDMPC_LG_TILE_EXACT);   // x6 products unless the caller asks for the exact f32 MFMA
     tile &= ~TDMPC_LG_TILE_EXACT;
-    if (njobs <= 0 || njobs > LG_MAXJ || tile < 1 || tile > 2) return bad("tdmpc_lg_gemm: njobs / tile");
+    if (njobs <= 0 || njobs > LG_MAXJ || tile < 1 || tile > 4) return bad("tdmpc_lg_gemm: njobs / tile");
     KArgs P;
     memset(&P, 0, sizeof P);
-    const int tw = tile == 2 ? 64 : 32;
+    const bool big = tile >= 3;   // LDS-staged macro tiles (exact f32 MFMA)
+    const int twm = tile == 1 ? 32 : 64, twn = tile == 1 ? 32 : tile == 2 || tile == 3 ? 64 : 128;
     long blocks = 0;
     for (int q = 0; q < njobs; ++q) {
         const tdmpc_lg_job& j = jobs[q];
         if (!j.c || j.m <= 0 || j.n <= 0 || j.nseg < 1 || j.nseg > 3 || j.splits < 1 || j.splits > 64)
             return bad("tdmpc_lg_gemm: job shape");
+        if (big && j.splits != 1) return bad("tdmpc_lg_gemm: split-K job on a macro tile");
+        for (int s = 0; s < j.nseg && big; ++s)
+            if (j.seg[s].amode != 0 || j.seg[s].ones_col >= 0) return bad("tdmpc_lg_gemm: macro tiles take amode 0 only");
         if (j.splits > 1 && (j.bias || j.res || j.epi != TDMPC_LG_EPI_NONE || j.c2))
             return bad("tdmpc_lg_gemm: split-K job with an epilogue");
         if ((j.epi == TDMPC_LG_EPI_PI && (!j.aux || !j.c2)) ||
@@ -731,14 +928,57 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
             P.job[q].nb_mem[s] = S.ones_col >= 0 ? S.ones_col : j.n;
             if (P.job[q].nb_mem[s] < 1) return bad("tdmpc_lg_gemm: ones column");
         }
-        const int tm = (j.m + tw - 1) / tw, tn = (j.n + tw - 1) / tw;
+        const int tm = (j.m + twm - 1) / twm, tn = (j.n + twn - 1) / twn;
         P.job[q].tiles_m = tm;
         P.job[q].block0 = (int)blocks;
         blocks += (long)tm * tn * j.splits;
     }
     P.njobs = njobs;
+    static const int diag = getenv("TDMPC_LG_DIAG") ? atoi(getenv("TDMPC_LG_DIAG")) : 0;
+    P.diag = diag;
     if (blocks >= (1L << 31)) return bad("tdmpc_lg_gemm: grid");
     const dim3 g((unsigned)blocks), b(256);
+    if (big) {
+        // one operand form per launch (lg_big_kernel FORM)
+        bool av = true, bv = true;
+        const int bt = jobs[0].seg[0].bmode;
+        for (int q = 0; q < njobs; ++q)
+            for (int s = 0; s < jobs[q].nseg; ++s) {
+                const tdmpc_lg_seg& S = jobs[q].seg[s];
+                if (S.bmode != bt) return bad("tdmpc_lg_gemm: macro tiles take one bmode per launch");
+                av = av && S.lda % 4 == 0 && S.k % 4 == 0 && ((uintptr_t)S.a & 15) == 0;
+                bv = bv && S.ldb % 4 == 0 && S.k % 4 == 0 && ((uintptr_t)S.b & 15) == 0;
+            }
+        const int form = (av ? LGB_AV : 0) | (bt ? LGB_BT : (bv ? LGB_BV : 0));
+        // (development knob: the chunk depth of the macro tiles)
+        static const int kc = getenv("TDMPC_LG_BIG_KC") ? atoi(getenv("TDMPC_LG_BIG_KC")) : 32;
+        static bool attr = false;
+#define LG_BIG_FORMS(X, TM, TN, KC) X(TM, TN, 0, KC) X(TM, TN, 1, KC) X(TM, TN, 2, KC) X(TM, TN, 3, KC) X(TM, TN, 4, KC) X(TM, TN, 5, KC)
+#define LG_BIG_EACH(X) LG_BIG_FORMS(X, 1, 1, 32) LG_BIG_FORMS(X, 1, 2, 32) LG_BIG_FORMS(X, 1, 1, 64) LG_BIG_FORMS(X, 1, 2, 64)
+        if (!attr) {
+#define LG_BIG_ATTR(TM, TN, F, KC) \
+            if (hipFuncSetAttribute((const void*)lg_big_kernel<TM, TN, F, KC, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                    (int)lg_big_lds<TM, TN, KC>()) != hipSuccess) \
+                return fail(hipGetLastError(), "gemm (LDS attribute)");
+            LG_BIG_EACH(LG_BIG_ATTR)
+#undef LG_BIG_ATTR
+            attr = true;
+        }
+        const int tm = 1, tn = tile == 3 ? 1 : 2;
+        bool done = false;
+#define LG_BIG_LAUNCH(TM, TN, F, KC) \
+        if (!done && tm == TM && tn == TN && form == F && kc == KC) { \
+            constexpr size_t lds = lg_big_lds<TM, TN, KC>(); \
+            hipLaunchKernelGGL((lg_big_kernel<TM, TN, F, KC, 2>), g, b, lds, (hipStream_t)stream, P); \
+            done = true; \
+        }
+        LG_BIG_EACH(LG_BIG_LAUNCH)
+#undef LG_BIG_LAUNCH
+#undef LG_BIG_EACH
+#undef LG_BIG_FORMS
+        if (!done) return bad("tdmpc_lg_gemm: macro tile form / chunk");
+        return launched("gemm (macro tiles)");
+    }
     if (tile == 1 && x6) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, true>), g, b, 0, (hipStream_t)stream, P);
     else if (tile == 1) hipLaunchKernelGGL((lg_gemm_kernel<1, 1>), g, b, 0, (hipStream_t)stream, P);
     else if (x6) hipLaunchKernelGGL((lg_gemm_kernel<2, 2, true>), g, b, 0, (hipStream_t)stream, P);

@@ -127,15 +127,19 @@ class Engine:
         self.x6 = os.environ.get("TDMPC_LG_X6", "0") == "1"
         # 64 x 64 tiles from this many 64 x 64 output tiles per launch (measured: profiles/r04/learner_tile_ab.txt)
         self.t64 = 240
+        # products over at least this many rows (the heads over H B rows; 0 = never) and >= 256 columns run on the
+        # LDS-staged macro tiles, tdmpc_lg_gemm tile `big_tile` (tools/lg_gemm_bench.py --big); narrower ones (the
+        # latent / action outputs) keep the K-split register tiles
+        self.big_rows = int(os.environ.get("TDMPC_LG_BIG_ROWS", "1024"))
+        self.big_tile = int(os.environ.get("TDMPC_LG_BIG_TILE", "3"))
         # every grouped product of prod() -- the heads' Q / reward / policy layers over R = H B rows and their dX,
-        # including the ones whose ELU (pi's layers, the Q / reward first layers) or ELU' (dX) epilogue lg_gemm would
-        # fuse: those run torch.mm / addmm plus one tdmpc_lg_act launch -- on hipBLASLt: 1.25 vs 1.37 ms per humanoid
-        # update with them on lg_gemm, graph replay (profiles/r05/learner_blas_ab.txt). The products inside the
-        # rollout chain (gemm() / _pair), the grouped weight gradients, rows, losses and Adam stay on the hand-written
-        # kernels. hipBLASLt picks its own reduction order, so with it the update is deterministic per build and
-        # box but not order-pinned like lg_gemm; Learner.update pins full-fp32 matmul precision around it.
-        # TDMPC_LG_BLAS=0 puts every product on lg_gemm (set before the first update: the graph keeps it).
-        self.blas = os.environ.get("TDMPC_LG_BLAS", "1") == "1"
+        # with their ELU (pi's layers, the reward first layer) or ELU' (dX) epilogues fused -- runs as ONE grouped
+        # tdmpc_lg_gemm launch on the macro tiles: 1.196-1.200 ms per humanoid update against 1.205-1.209 with
+        # those products on hipBLASLt (torch.mm / addmm + a tdmpc_lg_act launch) and 1.317-1.320 on the register
+        # tiles, graph replay (profiles/r06/learner_macro_tiles_ab.txt). Every sum in a fixed order (graph == eager
+        # bitwise). TDMPC_LG_BLAS=1 sends them to hipBLASLt instead (the library picks its own reduction order;
+        # Learner.update pins full-fp32 matmul precision around it); set before the first update: the graph keeps it.
+        self.blas = os.environ.get("TDMPC_LG_BLAS", "0") == "1"
         self._aux = {}
 
     def _alias(self, model, flat):
@@ -260,12 +264,17 @@ class Engine:
             J.std_ = j.get("std", 0.0)
             J.splits, J.slice = j.get("splits", 1), j.get("slice", 0)
             tiles64 += -(-j["m"] // 64) * -(-j["n"] // 64) * J.splits
+        if tile is None and self.big_rows and max(j["m"] for j in jobs) >= self.big_rows and \
+                min(j["n"] for j in jobs) >= 256 and all(j.get("splits", 1) == 1 for j in jobs) and \
+                all(sg[5] == 0 and sg[7] < 0 for j in jobs for sg in j["segs"]):
+            tile = self.big_tile   # LDS-staged macro tiles (exact f32 MFMA) for the products over H B rows
         if tile is None:
             # 64 x 64 tiles only for wide launches of row-major operands; a transposed weight operand (the
             # backward's dX) runs 15-25 % faster on 32 x 32 tiles (tools/lg_gemm_bench.py)
             tbw = any(sg[6] == 1 for j in jobs for sg in j["segs"])
             tile = 2 if tiles64 >= self.t64 and not tbw else 1
-        tile |= 0 if self.x6 else TILE_EXACT
+        if tile < 3:
+            tile |= 0 if self.x6 else TILE_EXACT
         _lib.check(self.lib.tdmpc_lg_gemm(arr, len(jobs), tile, self._stream()), "tdmpc_lg_gemm")
 
     def rows(self, heads, n, bwd=False, **kw):

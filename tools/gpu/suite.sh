@@ -16,6 +16,7 @@
 #   stamps           per-step shader stamps of the wide step kernel (needs the `ws` variant: -DWS_STAMPS)
 #   learner:VAR=v1,v2  the learner / train-loop / adam tests, then an A/B of VAR on the humanoid update time
 #   lab:VAR=v1,v2    the humanoid update-time A/B of `learner:` without its tests
+#   labs:A=1 B=2|A=0 the same over whole environment settings ('|' between settings)
 #   lgbench          lg_gemm tile timings of the learner's products (tools/lg_gemm_bench.py)
 #   p1stamps         per-hand-off timeline of the one-env persistent plan (tools/p1_stamps.py)
 #   qt               tools/quick_time.py on CONFIG / ENVS (qt.txt)
@@ -147,6 +148,15 @@ PY
         for v in ${vals//,/ }; do
           env "$var=$v" timeout -k 10 120 python -u tools/quick_learner.py humanoid-run 2>&1 | grep -v amdgpu.ids | \
             python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('$var=$v', d['graph'])" || exit 1
+        done
+      done ;;
+    labs:*)   # labs:A=1 B=2|A=0 -- the update-time A/B over whole environment settings ('|' between settings)
+      sets=${stage#labs:}
+      for i in 1 2 3; do
+        IFS='|' read -ra arr <<< "$sets"
+        for st in "${arr[@]}"; do
+          env $st timeout -k 10 120 python -u tools/quick_learner.py humanoid-run 2>&1 | grep -v amdgpu.ids | \
+            python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('$st', d['graph'])" || exit 1
         done
       done ;;
     lgbench)
