@@ -85,8 +85,9 @@ typedef struct tdmpc_lg_job {
 /* Up to 12 GEMMs in one launch; tile 1: 32x32 output tiles, 2: 64x64 (4 waves split K inside a workgroup).
  * Products are fp32-accurate x6 (three bf16 parts per operand, six bf16 MFMAs per pair, fp32 accumulation);
  * tile | TDMPC_LG_TILE_EXACT runs the exact v_mfma_f32_32x32x2_f32 products instead.
- * tile 3 / 4 / 5: LDS-staged macro tiles of 64x64 / 64x128 / 128x128 outputs (m x n) per workgroup on the exact f32
- * MFMA (the EXACT bit is implied), for the large products: every segment amode 0 without a ones column, splits 1. */
+ * tile 3 / 4: LDS-staged macro tiles of 64x64 / 64x128 outputs (m x n) per workgroup on the exact f32 MFMA (the
+ * EXACT bit is implied), for the large products: every segment amode 0 without a ones column, splits 1, one bmode
+ * per launch. */
 #define TDMPC_LG_TILE_EXACT 0x100
 int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* stream);
 
@@ -118,7 +119,8 @@ int tdmpc_lg_rows_bwd(const tdmpc_lg_rows* a, int32_t nwg, void* stream);
 int tdmpc_lg_pi_loss(const float* q1, const float* q2, const float* rho, int32_t nt, int32_t bsz, float* out,
                      void* stream);
 
-/* Gradient finalisation: parameter tensor i occupies g[dst, dst + rows * cols); its gradient is the sum of
+/* Gradient finalisation: parameter tensor i occupies g[dst, dst + rows * cols) (in increasing dst order, no
+ * overlap; gaps between tensors are left alone); its gradient is the sum of
  * nslices slices src + s * sstride, element (r, c) at src[r * ld + c]. Writes g, per-workgroup sums of squares to
  * normp (one workgroup per 2048 elements of a tensor; nblk = the capacity of normp, whose unused tail must hold
  * zeros) and step[0] += 1 (the optimiser's step count). */

@@ -404,7 +404,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
     }
 }
 
-// ---- LDS-staged macro tiles (tdmpc_lg_gemm tile 3 / 4 / 5: 64 x 64 / 64 x 128 / 128 x 128 outputs per workgroup) for
+// ---- LDS-staged macro tiles (tdmpc_lg_gemm tile 3 / 4: 64 x 64 / 64 x 128 outputs per workgroup) for
 // the large products (the heads' layers over H B = 2,560 - 3,072 rows, tdmpc.py:199-245). Four waves in 2 x 2, each
 // a (32 TM) x (32 TN) tile of v_mfma_f32_32x32x2_f32 accumulators over ALL of K (no K split, no LDS reduction). K
 // runs in chunks of 32 staged through LDS, double buffered: the next chunk's global loads are in flight in registers
@@ -1037,9 +1037,10 @@ int tdmpc_lg_finalize(const tdmpc_lg_gsrc* t, int32_t nt, float* g, float* normp
     long off = 0;
     int blocks = 0;
     for (int i = 0; i < nt; ++i) {
-        if (!t[i].src || t[i].dst != off || t[i].rows <= 0 || t[i].cols <= 0 || t[i].nslices <= 0 ||
+        if (!t[i].src || t[i].dst < off || t[i].rows <= 0 || t[i].cols <= 0 || t[i].nslices <= 0 ||
             t[i].ld < t[i].cols)
-            return bad("tdmpc_lg_finalize: tensors must tile [0, total) in order");
+            return bad("tdmpc_lg_finalize: tensors must lie in order without overlap");
+        off = t[i].dst;
         F.t[i] = t[i];
         F.block0[i] = blocks;
         const long n = (long)t[i].rows * t[i].cols;

@@ -92,14 +92,17 @@ class Engine:
         sd = agent.model.state_dict()
         names = [k for pre in order for k in sd if k.startswith(pre + ".")]
         assert len(names) == len(sd), "unexpected TOLD parameters"
-        total = sum(sd[k].numel() for k in names)
-        self.P = torch.empty(total, device=self.dev)
-        self.PT = torch.empty(total, device=self.dev)
-        self.G = torch.zeros(total, device=self.dev)
+        # every tensor starts on a 16-byte boundary (the scalar heads' 1-float biases would leave the next weights
+        # misaligned and their products on 4-byte loads); the gaps hold zeros in P, PT, G and the Adam moments
         off = 0
         for k in names:
+            off = (off + 3) & ~3
             self.off[k] = (off, tuple(sd[k].shape))
             off += sd[k].numel()
+        total = (off + 3) & ~3
+        self.P = torch.zeros(total, device=self.dev)
+        self.PT = torch.zeros(total, device=self.dev)
+        self.G = torch.zeros(total, device=self.dev)
         self.n_main = self.off["_pi.0.weight"][0]
         self._alias(agent.model, self.P)
         self._alias(agent.model_target, self.PT)
