@@ -414,8 +414,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
 // the float4 at kq = 2 g + h of its row / column r (16 consecutive float4 per ds_read_b128 lane group). The k order
 // inside a group of 8 is lg_gemm's (steps .x .. .w pair k and k + 4), and the groups of 8 go to NACC chains by their
 // index within the chunk: every output is a fixed-order sum of fixed-order f32 fma chains.
-// FORM (one per launch, from the host): LGB_AV -- every A segment takes 16-B loads (row stride and K multiples of 4,
-// aligned base), else four 4-B loads per float4; LGB_BT -- B(k, n) = b[k ldb + n] (bmode 1) for every segment, else
+// FORM (one per launch, from the host): LGB_AV -- every A segment takes 16-B loads (row stride a multiple of 4,
+// aligned base; a quad past K is zeroed), else four 4-B loads per float4; LGB_BT -- B(k, n) = b[k ldb + n] (bmode 1) for every segment, else
 // b[n ldb + k]; LGB_BV -- (bmode 0) 16-B loads of B. Branch-free loads let the compiler count the ring's vmcnt.
 enum { LGB_AV = 1, LGB_BT = 2, LGB_BV = 4 };
 
@@ -469,9 +469,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
             const int u = tid + 256 * i, m = m0 + u / KQ, k = k0 + 4 * (u % KQ);
-            if constexpr (AV) {
+            if constexpr (AV) {   // (a quad straddling K stays inside the row, lda % 4 == 0; its tail is zeroed)
                 const unsigned off = (m < M && k < kh) ? (unsigned)(m * lda + k) * 4u : LG_OOB;
                 sa[i] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rsa, (int)off, 0, 0));
+                sa[i].y = k + 1 < kh ? sa[i].y : 0.f;
+                sa[i].z = k + 2 < kh ? sa[i].z : 0.f;
+                sa[i].w = k + 3 < kh ? sa[i].w : 0.f;
             } else {
                 float e[4];
 #pragma unroll
@@ -489,6 +492,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
                 if constexpr (BV) {
                     const unsigned off = (n < N && k < kh) ? (unsigned)(n * ldb + k) * 4u : LG_OOB;
                     sb[j] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rsb, (int)off, 0, 0));
+                    sb[j].y = k + 1 < kh ? sb[j].y : 0.f;
+                    sb[j].z = k + 2 < kh ? sb[j].z : 0.f;
+                    sb[j].w = k + 3 < kh ? sb[j].w : 0.f;
                 } else {
                     float e[4];
 #pragma unroll
@@ -946,8 +952,8 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
             for (int s = 0; s < jobs[q].nseg; ++s) {
                 const tdmpc_lg_seg& S = jobs[q].seg[s];
                 if (S.bmode != bt) return bad("tdmpc_lg_gemm: macro tiles take one bmode per launch");
-                av = av && S.lda % 4 == 0 && S.k % 4 == 0 && ((uintptr_t)S.a & 15) == 0;
-                bv = bv && S.ldb % 4 == 0 && S.k % 4 == 0 && ((uintptr_t)S.b & 15) == 0;
+                av = av && S.lda % 4 == 0 && S.lda >= S.k && ((uintptr_t)S.a & 15) == 0;
+                bv = bv && S.ldb % 4 == 0 && S.ldb >= S.k && ((uintptr_t)S.b & 15) == 0;
             }
         const int form = (av ? LGB_AV : 0) | (bt ? LGB_BT : (bv ? LGB_BV : 0));
         // (development knob: the chunk depth of the macro tiles)

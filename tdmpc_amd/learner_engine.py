@@ -11,7 +11,7 @@ Layout (device, float32):
   * every TOLD parameter is a view into ONE flat buffer P (likewise the target into PT), ordered encoder, dynamics,
     reward, Q1, Q2 | pi, so the main optimiser is one Adam pass over P[:n_main] and the policy optimiser one over
     P[n_main:]; gradients go to the flat G, Adam moments to flat M / V;
-  * X0 [(H+1) B][L+A]: rows t*B..t*B+B-1 hold (z_t, a_t) -- the encoder writes z_0, dynamics step t writes z_{t+1}
+  * X0 [(H+1) B][L+A, padded to a multiple of 4]: rows t*B..t*B+B-1 hold (z_t, a_t) -- the encoder writes z_0, dynamics step t writes z_{t+1}
     into block t+1 -- so the Q / reward heads read all H steps as one [H B][L+A] operand and the policy update reads
     the H+1 latents in place (stride L+A);
   * activations saved for the backward: each hidden layer's output (ELU / Tanh output; the derivative is a function
@@ -87,6 +87,8 @@ class Engine:
             self.flat = 32 * hw[-1] * hw[-1]
         self.A, self.M, self.H = int(cfg.action_dim), int(cfg.mlp_dim), int(cfg.horizon)
         self.LA = self.L + self.A
+        # X0 / Xtd rows padded to a multiple of 4 floats: their products take 16-byte loads
+        self.LAP = (self.LA + 3) & ~3
         order = ["_encoder", "_dynamics", "_reward", "_Q1", "_Q2", "_pi"]
         self.off = {}
         sd = agent.model.state_dict()
@@ -338,16 +340,16 @@ class Engine:
         b = self._bufs.get(B)
         if b is not None:
             return b
-        H, L, A, M, E, O, LA = self.H, self.L, self.A, self.M, self.E, self.O, self.LA
+        H, L, A, M, E, O, LA, LAP = self.H, self.L, self.A, self.M, self.E, self.O, self.LA, self.LAP
         R, R1 = H * B, (H + 1) * B
         z = lambda *s: torch.zeros(*s, device=self.dev)  # noqa: E731
         b = dict(
             eps=z((2 * H + 1) * B, A),
             # TD target
-            Yt1=z(R, E), Yo1=z(R, E), NZ=z(R, L), Xtd=z(R, LA), T1=z(R, M), T2=z(R, M), MUtd=z(R, A),
+            Yt1=z(R, E), Yo1=z(R, E), NZ=z(R, L), Xtd=z(R, LAP), T1=z(R, M), T2=z(R, M), MUtd=z(R, A),
             TQ=z(2, R), TD=z(R), PAt=z(2, R, M), PBt=z(2, R, M),
             # main forward
-            Ye1=z(B, E), X0=z(R1, LA), Yd1=z(R, M), Yd2=z(R, M), ZP=z(R, L),
+            Ye1=z(B, E), X0=z(R1, LAP), Yd1=z(R, M), Yd2=z(R, M), ZP=z(R, L),
             PA=z(3, R1, M), PB=z(3, R1, M), Y1=z(2, R1, M), Y2=z(3, R1, M), XH1=z(2, R1, M), XH2=z(2, R1, M),
             RS1=z(2, R1), RS2=z(2, R1), Q=z(3, R1),
             lrows=z(5, B), scal=z(6), dZP=z(R1, L), dq=z(3, R),
@@ -380,7 +382,7 @@ class Engine:
         """tdmpc.py:184-190 for all H steps: online encoder + pi (TruncatedNormal draws `eps`), target Q, and the
         target encoder's next_z (tdmpc.py:206-207) -> b["TD"], b["NZ"]. A generator: yields after each launch
         (see _pair)."""
-        O, E, L, A, M, LA = self.O, self.E, self.L, self.A, self.M, self.LA
+        O, E, L, A, M, LA, LAP = self.O, self.E, self.L, self.A, self.M, self.LA, self.LAP
         w, wt = self.w, (lambda k: self.w(k, True))
         nxo = _p(nxo_t)
         if self.pix:   # the conv stacks of both encoders, then their Linear
@@ -390,7 +392,7 @@ class Engine:
             self.gemm([dict(segs=[_seg(_p(b["yt"][3]), F, wt(LIN_NAME + ".weight"), F, F)], m=R, n=L, c=_p(b["NZ"]),
                             ldc=L, bias=wt(LIN_NAME + ".bias")),
                        dict(segs=[_seg(_p(b["yo"][3]), F, w(LIN_NAME + ".weight"), F, F)], m=R, n=L, c=_p(b["Xtd"]),
-                            ldc=LA, bias=w(LIN_NAME + ".bias"))])
+                            ldc=LAP, bias=w(LIN_NAME + ".bias"))])
             yield
         else:
             self.gemm([dict(segs=[_seg(nxo, O, wt("_encoder.0.weight"), O, O)], m=R, n=E, c=_p(b["Yt1"]), ldc=E,
@@ -401,18 +403,18 @@ class Engine:
             self.gemm([dict(segs=[_seg(_p(b["Yt1"]), E, wt("_encoder.2.weight"), E, E)], m=R, n=L, c=_p(b["NZ"]),
                             ldc=L, bias=wt("_encoder.2.bias")),
                        dict(segs=[_seg(_p(b["Yo1"]), E, w("_encoder.2.weight"), E, E)], m=R, n=L, c=_p(b["Xtd"]),
-                            ldc=LA, bias=w("_encoder.2.bias"))])
+                            ldc=LAP, bias=w("_encoder.2.bias"))])
             yield
         self.prod([([(b["Xtd"][:, :L], 0, L)], "_pi.0.weight", b["T1"], "_pi.0.bias", False, False, EPI_ELU, None)])
         yield
         self.prod([([(b["T1"], 0, M)], "_pi.2.weight", b["T2"], "_pi.2.bias", False, False, EPI_ELU, None)])
         yield
         self.gemm([dict(segs=[_seg(_p(b["T2"]), M, w("_pi.4.weight"), M, M)], m=R, n=A, c=_p(b["Xtd"], L),
-                        ldc=LA, bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MUtd"]), ldc2=A,
+                        ldc=LAP, bias=w("_pi.4.bias"), epi=EPI_PI, aux=eps, ldaux=A, c2=_p(b["MUtd"]), ldc2=A,
                         std=float(self.cfg.min_std))])
         yield
         PA, PB = b["PAt"], b["PBt"]
-        self.prod([([(b["Xtd"], 0, LA)], f"_Q{h + 1}.0.weight", PA[h, :R], f"_Q{h + 1}.0.bias", True, False,
+        self.prod([([(b["Xtd"][:, :LA], 0, LA)], f"_Q{h + 1}.0.weight", PA[h, :R], f"_Q{h + 1}.0.bias", True, False,
                     EPI_NONE, None) for h in range(2)])
         yield
         self.rows([dict(x=_p(PA[h]), y=_p(PB[h]), ln=1, g=wt(f"_Q{h + 1}.1.weight"), beta=wt(f"_Q{h + 1}.1.bias"),
@@ -428,40 +430,40 @@ class Engine:
     def _fwd_steps(self, b, obs, action, B):
         """The update's forward (tdmpc.py:199-213): encoder, latent rollout, heads over the H B rollout rows. A
         generator: yields after each launch (see _pair)."""
-        H, O, E, L, M, LA = self.H, self.O, self.E, self.L, self.M, self.LA
+        H, O, E, L, M, LA, LAP = self.H, self.O, self.E, self.L, self.M, self.LA, self.LAP
         R = H * B
         w, X0 = self.w, b["X0"]
         if self.pix:
             F = self.flat
             self.conv_stack(obs, B, [b["ym"]])
             yield
-            self.gemm([dict(segs=[_seg(_p(b["ym"][3]), F, w(LIN_NAME + ".weight"), F, F)], m=B, n=L, c=_p(X0), ldc=LA,
+            self.gemm([dict(segs=[_seg(_p(b["ym"][3]), F, w(LIN_NAME + ".weight"), F, F)], m=B, n=L, c=_p(X0), ldc=LAP,
                             bias=w(LIN_NAME + ".bias"))])
             yield
         else:
             self.gemm([dict(segs=[_seg(_p(obs), O, w("_encoder.0.weight"), O, O)], m=B, n=E, c=_p(b["Ye1"]), ldc=E,
                             bias=w("_encoder.0.bias"), epi=EPI_ELU)])
             yield
-            self.gemm([dict(segs=[_seg(_p(b["Ye1"]), E, w("_encoder.2.weight"), E, E)], m=B, n=L, c=_p(X0), ldc=LA,
+            self.gemm([dict(segs=[_seg(_p(b["Ye1"]), E, w("_encoder.2.weight"), E, E)], m=B, n=L, c=_p(X0), ldc=LAP,
                             bias=w("_encoder.2.bias"))])
             yield
-        X0.view(H + 1, B, LA)[:H, :, L:].copy_(action[:H])
+        X0.view(H + 1, B, LAP)[:H, :, L:LA].copy_(action[:H])
         yield
         for t in range(H):
-            self.gemm([dict(segs=[_seg(_p(X0, t * B * LA), LA, w("_dynamics.0.weight"), LA, LA)], m=B, n=M,
+            self.gemm([dict(segs=[_seg(_p(X0, t * B * LAP), LAP, w("_dynamics.0.weight"), LA, LA)], m=B, n=M,
                             c=_p(b["Yd1"], t * B * M), ldc=M, bias=w("_dynamics.0.bias"), epi=EPI_ELU)])
             yield
             self.gemm([dict(segs=[_seg(_p(b["Yd1"], t * B * M), M, w("_dynamics.2.weight"), M, M)], m=B, n=M,
                             c=_p(b["Yd2"], t * B * M), ldc=M, bias=w("_dynamics.2.bias"), epi=EPI_ELU)])
             yield
             self.gemm([dict(segs=[_seg(_p(b["Yd2"], t * B * M), M, w("_dynamics.4.weight"), M, M)], m=B, n=L,
-                            c=_p(X0, (t + 1) * B * LA), ldc=LA, bias=w("_dynamics.4.bias"),
+                            c=_p(X0, (t + 1) * B * LAP), ldc=LAP, bias=w("_dynamics.4.bias"),
                             c2=_p(b["ZP"], t * B * L), ldc2=L)])
             yield
         # reward head layer 1 (ELU) rides in its own slot 2 of PA / Y2 buffers, in the Q heads' first-layer launch
         PA = b["PA"]
         PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = self.q_forward(
-            b, R, [(X0[:R], 0, LA)], extra=[([(X0[:R], 0, LA)], "_reward.0.weight", PA[2, :R], "_reward.0.bias",
+            b, R, [(X0[:R, :LA], 0, LA)], extra=[([(X0[:R, :LA], 0, LA)], "_reward.0.weight", PA[2, :R], "_reward.0.bias",
                                               False, False, EPI_ELU, None)])
         yield
         self.prod([([(Y1[h, :R], 0, M)], f"_Q{h + 1}.3.weight", PB[h, :R], f"_Q{h + 1}.3.bias", False, False,
@@ -582,10 +584,10 @@ class Engine:
         # ---- the heads' weight gradients (side stream) beside the latent rollout's backward ----
         sp = 4 if R >= 1024 else 1
         dw_h = [("_reward.2", M, M, [_seg(_p(dP2[2]), M, _p(PA[2]), M, R, 1, 1, M)], sp),
-                ("_reward.0", M, LA, [_seg(_p(dP1[2]), M, _p(X0), LA, R, 1, 1, LA)], sp)]
+                ("_reward.0", M, LA, [_seg(_p(dP1[2]), M, _p(X0), self.LAP, R, 1, 1, LA)], sp)]
         for h in range(2):
             dw_h += [(f"_Q{h + 1}.3", M, M, [_seg(_p(dP2[h]), M, _p(Y1[h]), M, R, 1, 1, M)], sp),
-                     (f"_Q{h + 1}.0", M, LA, [_seg(_p(dP1[h]), M, _p(X0), LA, R, 1, 1, LA)], sp)]
+                     (f"_Q{h + 1}.0", M, LA, [_seg(_p(dP1[h]), M, _p(X0), self.LAP, R, 1, 1, LA)], sp)]
         # pi's forward over the detached latents z_0..z_H for update_pi (reads X0 and pi's weights only, which the
         # main optimiser step does not touch) rides on the side stream after them
         slots = {}
@@ -616,7 +618,7 @@ class Engine:
         dw = dw_enc + [
               ("_dynamics.4", L, M, g_dyn3, sp),
               ("_dynamics.2", M, M, [_seg(_p(dP2d), M, _p(b["Yd1"]), M, R, 1, 1, M)], sp),
-              ("_dynamics.0", M, LA, [_seg(_p(dP1d), M, _p(X0), LA, R, 1, 1, LA)], sp)]
+              ("_dynamics.0", M, LA, [_seg(_p(dP1d), M, _p(X0), self.LAP, R, 1, 1, LA)], sp)]
         slots.update(self._dw(b, "main", dw))
         main.wait_stream(self.side)   # the heads' slices ready
         dw += dw_h

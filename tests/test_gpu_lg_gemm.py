@@ -4,7 +4,7 @@ The learner's products (tdmpc.py:165-245 as learner_engine.py writes them out) r
 (1 / 2, the exact f32 MFMA with TDMPC_LG_TILE_EXACT) and the LDS-staged macro tiles (3 / 4 / 5) for the large ones.
 Every tile must give C = epi(sum over segments A B + bias + res) within fp32 accumulation error of the float64
 product, bitwise the same on a second launch, for the operand forms the engine uses: row-major activations with
-16-B aligned and unaligned row strides (the 121-float X rows), Linear weights [N][K] and their transpose [K][N],
+16-B aligned and unaligned row strides (121-float rows, and rows padded to 124 whose last quad straddles K), Linear weights [N][K] and their transpose [K][N],
 K tails (100 / 121), two segments over one weight's column ranges, row counts and widths off the tile grid, and
 several jobs of different shapes in one launch. Tolerance: |C - C64| <= 4e-6 (|A| |B| + |bias| + |res|) -- an f32
 fma chain over K <= 1024 stays below ~1.5e-7 of that sum per the MI355X guide's measurement; the margin covers the
@@ -80,6 +80,7 @@ CASES = [
     (2560, 512, [(512, 0)], 0, EPI_NONE, 0, True, False),      # the heads' hidden layers (R = H B rows)
     (3072, 512, [(512, 0)], 1, EPI_ELU_BWD, 0, False, False),  # a dX through W (transpose) with ELU'
     (2560, 512, [(121, 0)], 0, EPI_ELU, 0, True, False),       # first layer over [z, a], unaligned rows, K tail
+    (2560, 512, [(121, 0)], 0, EPI_NONE, 3, True, False),      # rows padded to 124: a 16-B quad straddles K
     (3072, 512, [(100, 0), (21, 100)], 0, EPI_NONE, 0, True, False),  # two segments over W's column ranges
     (1000, 100, [(512, 0)], 0, EPI_NONE, 3, True, True),       # off-grid rows / width, padded rows, residual
     (300, 21, [(512, 0)], 1, EPI_NONE, 0, False, False),       # a narrow output through W^T
