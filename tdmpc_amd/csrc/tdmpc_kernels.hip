@@ -4493,6 +4493,8 @@ struct PackJob {
 };
 static_assert(sizeof(PackJob) <= PACK_JOB_BYTES, "job-table slot");
 constexpr int PACK_WG = 256, PACK_PER = 8;   // threads per workgroup, items per thread
+// elements per item: an x6 / x6q lane's 8 values (16-B stores per plane), a panel's k quad, else one
+__host__ __device__ constexpr int pack_per_item(int kind) { return kind == PJ_X6 || kind == PJ_X6Q ? 8 : kind == PJ_PANEL ? 4 : 1; }
 
 __global__ void __launch_bounds__(PACK_WG) pack_fused_kernel(PackHdr* hdr, const PackJob* jobs, int nj, float* pw,
                                                               unsigned long long nonce, long nweights) {
@@ -4514,8 +4516,9 @@ __global__ void __launch_bounds__(PACK_WG) pack_fused_kernel(PackHdr* hdr, const
     }
     const PackJob& J = jobs[lo];
     const long base = (long)(blockIdx.x - J.blk0) * PACK_WG * PACK_PER;
+    const int epi = pack_per_item(J.kind);
     for (int u = 0; u < PACK_PER; ++u) {
-        const long i = base + (long)u * PACK_WG + threadIdx.x;
+        const long i = (base + (long)u * PACK_WG + threadIdx.x) * epi;   // first element of the thread's item
         if (i >= J.work) break;
         switch (J.kind) {
             case PJ_COPY: pw[J.dst + i] = i < J.n ? J.src[i] : 0.f; break;
@@ -4524,36 +4527,51 @@ __global__ void __launch_bounds__(PACK_WG) pack_fused_kernel(PackHdr* hdr, const
                 pw[J.dst + i] = J.src[r * J.cols + c];
                 break;
             }
-            case PJ_PANEL: {   // dst index i = pidx(r, k, pk): [r / 32][k / 4][r % 32][k % 4]
-                const int e = i & 3, rr = (i >> 2) & 31;
+            case PJ_PANEL: {   // dst index i = pidx(r, k, pk): [r / 32][k / 4][r % 32][k % 4]; the item: one k quad
+                const int rr = (i >> 2) & 31;
                 const long q = i >> 7;
                 const int kq = (int)(q % (J.pk / 4));
-                const int r = (int)(q / (J.pk / 4)) * 32 + rr, k = kq * 4 + e;
-                pw[J.dst + i] = pack_val(J.m, r, k);
+                const int r = (int)(q / (J.pk / 4)) * 32 + rr, k = kq * 4;
+                *(float4*)(pw + J.dst + i) = make_float4(pack_val(J.m, r, k), pack_val(J.m, r, k + 1),
+                                                         pack_val(J.m, r, k + 2), pack_val(J.m, r, k + 3));
                 break;
             }
-            case PJ_X6: case PJ_X6Q: {
-                const int j = i & 7, lane = (i >> 3) & 63;
+            case PJ_X6: case PJ_X6Q: {   // the item: one lane's 8 values of a block, 16 B per plane
+                const int lane = (i >> 3) & 63;
                 const long blk = i >> 9;
-                int r, k;
+                int r, k0, k1;   // values j = 0..3 at k0 + j, j = 4..7 at k1 + j - 4
                 if (J.kind == PJ_X6) {   // the x6 layout (Layout::x6): 32-row x 16-k blocks
                     const int G = (J.pk + 15) / 16;
                     const int g = (int)(blk % G), nb = (int)(blk / G);
                     r = 32 * nb + (lane & 31);
-                    k = 16 * g + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
+                    k0 = 16 * g + 4 * (lane >> 5);
+                    k1 = k0 + 8;
                 } else {                 // the x6q layout (Layout::x6q): 16-row x 32-k blocks
                     const int G = (J.pk + 31) / 32;
                     const int g = (int)(blk % G), nb = (int)(blk / G);
                     r = 16 * nb + (lane & 15);
-                    k = 32 * g + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
+                    k0 = 32 * g + 4 * (lane >> 4);
+                    k1 = k0 + 16;
                 }
-                const float x = k < J.pk && r < J.prow ? pack_val(J.m, r, k) : 0.f;
-                __bf16 h, m, l;
-                split3(x, h, m, l);
-                unsigned short* d = (unsigned short*)(pw + J.dst);
-                d[(blk * 3 + 0) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, h);
-                d[(blk * 3 + 1) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, m);
-                d[(blk * 3 + 2) * 512 + lane * 8 + j] = __builtin_bit_cast(unsigned short, l);
+                unsigned short hv[8], mv[8], lv[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int k = (j < 4 ? k0 : k1) + (j & 3);
+                    const float x = k < J.pk && r < J.prow ? pack_val(J.m, r, k) : 0.f;
+                    __bf16 h, m, l;
+                    split3(x, h, m, l);
+                    hv[j] = __builtin_bit_cast(unsigned short, h);
+                    mv[j] = __builtin_bit_cast(unsigned short, m);
+                    lv[j] = __builtin_bit_cast(unsigned short, l);
+                }
+                auto pk8 = [](const unsigned short (&v)[8]) {
+                    return make_uint4(v[0] | (unsigned)v[1] << 16, v[2] | (unsigned)v[3] << 16, v[4] | (unsigned)v[5] << 16,
+                                      v[6] | (unsigned)v[7] << 16);
+                };
+                uint4* d = (uint4*)(pw + J.dst);   // 1 KiB per plane and block, 16 B per lane
+                d[(blk * 3 + 0) * 64 + lane] = pk8(hv);
+                d[(blk * 3 + 1) * 64 + lane] = pk8(mv);
+                d[(blk * 3 + 2) * 64 + lane] = pk8(lv);
                 break;
             }
         }
@@ -4802,7 +4820,8 @@ int launch_pack(std::vector<PackJob>& jobs, const Layout& w, float* pw, hipStrea
     int blk = 0;
     for (PackJob& j : jobs) {
         j.blk0 = blk;
-        blk += (int)((j.work + PACK_WG * PACK_PER - 1) / (PACK_WG * PACK_PER));
+        const long per_blk = (long)PACK_WG * PACK_PER * pack_per_item(j.kind);
+        blk += (int)((j.work + per_blk - 1) / per_blk);
     }
     const size_t nb = jobs.size() * sizeof(PackJob);
     int device = 0;

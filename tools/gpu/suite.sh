@@ -159,8 +159,8 @@ PY
             python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('$st', d['graph'])" || exit 1
         done
       done ;;
-    lgbench)
-      timeout -k 10 200 python -u tools/lg_gemm_bench.py > "$OUT/lg_gemm.txt" 2>&1 || { tail -20 "$OUT/lg_gemm.txt"; exit 1; }
+    lgbench*)
+      timeout -k 10 200 python -u tools/lg_gemm_bench.py ${stage#lgbench} > "$OUT/lg_gemm.txt" 2>&1 || { tail -20 "$OUT/lg_gemm.txt"; exit 1; }
       grep -v amdgpu.ids "$OUT/lg_gemm.txt" | tail -30 ;;
     p1stamps)
       timeout -k 10 120 python -u tools/p1_stamps.py "$CONFIG" > "$OUT/p1_stamps.txt" 2>&1 || { tail -20 "$OUT/p1_stamps.txt"; exit 1; }

@@ -40,7 +40,7 @@ def _time(fn, reps):
 
 def run(m, n, k, amode, bmode, tile, splits=1, reps=50, njobs=1, lda=None):
     lda = lda or (k if amode == 0 else m)
-    As = [torch.randn(m * lda, device=dev) for _ in range(njobs)]
+    As = [torch.randn((m if amode == 0 else k) * lda, device=dev) for _ in range(njobs)]
     Bs = [torch.randn(n * k, device=dev) for _ in range(njobs)]
     Cs = [torch.zeros(splits * m * n, device=dev) for _ in range(njobs)]
     arr = (_lib.LgJob * njobs)()
@@ -82,6 +82,20 @@ def run_torch(m, n, k, bmode, reps=50, njobs=1, lda=None):
           f"{2 * m * n * k * njobs / us / 1e6:6.1f} TFLOP/s", flush=True)
 
 
+if "--roll" in sys.argv:   # the latent rollout's 512-row products (forward, then the backward's dX through W^T)
+    for (m, n, k, am, bm, lda) in [(512, 512, 121, 0, 0, 124), (512, 512, 512, 0, 0, None), (512, 100, 512, 0, 0, None),
+                                   (512, 512, 100, 0, 1, None), (512, 512, 512, 0, 1, None), (512, 100, 512, 0, 1, None)]:
+        for tile in (1 | EXACT, 5 | EXACT, 7):
+            run(m, n, k, am, bm, tile, lda=lda)
+    sys.exit(0)
+if "--diag" in sys.argv:   # fixed costs of the register tile (TDMPC_LG_DIAG read once per process: one per run)
+    print("TDMPC_LG_DIAG", os.environ.get("TDMPC_LG_DIAG", "0"))
+    for (m, n, k) in [(512, 512, 512), (512, 512, 32), (32, 32, 32)]:
+        run(m, n, k, 0, 0, 1 | EXACT)
+    x = torch.zeros(4096, device=dev)
+    us = _time(lambda: lib.tdmpc_lg_act(x.data_ptr(), None, 4096, 0, C.c_void_p(torch.cuda.current_stream().cuda_stream)), 50)
+    print(f"tdmpc_lg_act on 4096 floats (one workgroup): {us:.2f} us")
+    sys.exit(0)
 if "--small" in sys.argv:
     for (m, n, k, am, bm) in [(512, 512, 512, 0, 0), (512, 512, 121, 0, 0), (512, 100, 512, 0, 0),
                               (512, 512, 100, 0, 1), (512, 512, 512, 0, 1), (512, 100, 512, 0, 1)]:
