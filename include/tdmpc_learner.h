@@ -87,11 +87,7 @@ typedef struct tdmpc_lg_job {
  * tile | TDMPC_LG_TILE_EXACT runs the exact v_mfma_f32_32x32x2_f32 products instead.
  * tile 3 / 4: LDS-staged macro tiles of 64x64 / 64x128 outputs (m x n) per workgroup on the exact f32 MFMA (the
  * EXACT bit is implied), for the large products: every segment amode 0 without a ones column, splits 1, one bmode
- * per launch.
- * tile 5 / 6: tile 1 with 8 / 16 waves splitting K. tile 7: the whole-K staged tile for narrow products (32 x 32
- * outputs per workgroup, A rows and B columns over all of K staged in LDS, v_mfma_f32_16x16x4_f32; exact f32): every
- * job one amode-0 segment with K <= 512, no ones column, splits 1, one bmode per launch, a 16-B aligned with lda a
- * multiple of 4 and >= K rounded up to 4 (B: any stride >= its row length; 16-B loads where rows are whole quads). */
+ * per launch. */
 #define TDMPC_LG_TILE_EXACT 0x100
 int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* stream);
 

@@ -340,11 +340,11 @@ __device__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15)
 
 // (amdgpu_waves_per_eu(2): left to itself the compiler gave the 64 x 64 form 224 VGPRs + 128 AGPRs, one wave per SIMD;
 // bounded, 210 VGPRs and no spills: two)
-// NW waves per workgroup split K (wave w takes every NW-th group of 8 k, 16 for x6): 4 (tiles 1 / 2), or 8 / 16
-// (tiles 5 / 6: the 32 x 32 tile of a narrow product -- the latent rollout's 512-row layers -- with 2 / 4 waves per
-// SIMD, so a wave's whole K share is in flight at once)
+// NW waves per workgroup split K (wave w takes every NW-th group of 8 k, 16 for x6). (8 and 16 waves -- 2 / 4 per
+// SIMD, a wave's whole K share in flight at once -- measured no faster on the 512-row products and slower for the
+// update: profiles/r06/lg_rollout_tiles.txt)
 template <int TM, int TN, bool X6 = false, int NW = 4>
-__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW >= 8 ? NW / 4 : 2))) lg_gemm_kernel(const KArgs P) {
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) lg_gemm_kernel(const KArgs P) {
     __shared__ float red[NW][TM * TN * 16][64];
     int jb = 0;
     for (int q = 1; q < P.njobs; ++q)
@@ -612,132 +612,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
 
 template <int TM, int TN, int KC>
 constexpr size_t lg_big_lds() { return (size_t)2 * (KC / 4) * (64 * TM + 1 + 64 * TN + 1) * sizeof(float4); }
-
-// ---- tile 7: the whole-K staged tile for the narrow products (the latent rollout's B = 512-row layers and their dX,
-// tdmpc.py:203-205 as learner_engine.py writes them out). The register tiles spend most of such a launch on load
-// traffic -- a 32-row MFMA operand loaded straight into registers touches 32 cache lines per instruction, 32 B of
-// each -- and on the K-split reduction. Here a workgroup's 32 x 32 output tile takes its A rows and B columns over
-// ALL of K into LDS with full-line loads (a row's consecutive 16-B quads on consecutive lanes; a transposed weight,
-// B(k, n) = b[k ldb + n], read as 128-B k rows and transposed in registers), in NS stages issued up front so the
-// later stages land under the earlier stages' products; each wave then owns a 16 x 16 quadrant over all of K
-// (v_mfma_f32_16x16x4_f32, two accumulator chains summed in a fixed order): no cross-wave reduction. LDS rows are
-// padded to 4 mod 64 floats (conflict-free ds_read_b128 over 16 rows). K <= 512 (132 KiB of LDS at K = 512).
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-constexpr int LGS_NS = 4, LGS_PER = 4;   // stages; float4 per thread, operand and stage (K <= 512)
-
-__host__ __device__ constexpr int lgs_pitch(int k) { return (((k + 3) / 4 * 4 + 63) / 64) * 64 + 4; }
-
-template <bool BT, bool BV>
-__global__ void __launch_bounds__(256) lg_stage_kernel(const KArgs P) {
-    extern __shared__ float4 lg_lds[];
-    int jb = 0;
-    for (int q = 1; q < P.njobs; ++q)
-        if ((int)blockIdx.x >= P.job[q].block0) jb = q;
-    const KJob& J = P.job[jb];
-    const tdmpc_lg_seg& S = J.j.seg[0];
-    const int tile = (int)blockIdx.x - J.block0;
-    const int m0 = (tile % J.tiles_m) * 32, n0 = (tile / J.tiles_m) * 32;
-    const int M = J.j.m, N = J.j.n, K = S.k, lda = S.lda, ldb = S.ldb;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // k quads (rounded up to whole 16-deep groups; quads past K load zeros), quads per stage
-    const int KQ = ((K + 15) >> 4) << 2, QS = (KQ + LGS_NS - 1) / LGS_NS;
-    const int KP = lgs_pitch(K);                                    // LDS row pitch (floats)
-    float* As = (float*)lg_lds;
-    float* Bs = As + 32 * KP;
-    float* scratch = Bs + 32 * KP;   // 16 B past the tiles
-    const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)S.a, (short)0, (int)LG_OOB, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)S.b, (short)0, (int)LG_OOB, 0x00020000);
-
-    // every stage's loads issued up front: A rows (and B rows of a [N][K] weight) as row-major quads, u -> (row u / QS,
-    // quad u % QS of the stage); a [K][N] weight as 4 k rows x 4 columns per thread (t & 7: column quad, t >> 3: k quad)
-    float4 ra[LGS_NS][LGS_PER], rb[LGS_NS][LGS_PER][BT ? 4 : 1];
-    auto ld4 = [&](const __amdgpu_buffer_rsrc_t& rs, bool ok, unsigned idx) {
-        return u2f4(__builtin_amdgcn_raw_buffer_load_b128(rs, (int)(ok ? idx * 4u : LG_OOB), 0, 0));
-    };
-    // B's quad: one 16-B load (BV), else four 4-B loads (rows of a stride that is not a multiple of 4: the first
-    // layer's weight [M][L + A]); element e valid while e < lim
-    auto ldb4 = [&](bool ok, unsigned idx, int e0, int lim) {
-        if constexpr (BV) {
-            return ld4(rsb, ok, idx);
-        } else {
-            float e[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                e[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                    rsb, (int)(ok && e0 + c < lim ? (idx + c) * 4u : LG_OOB), 0, 0));
-            return make_float4(e[0], e[1], e[2], e[3]);
-        }
-    };
-#pragma unroll
-    for (int st = 0; st < LGS_NS; ++st)
-#pragma unroll
-        for (int i = 0; i < LGS_PER; ++i) {
-            const int u = tid + 256 * i, row = u / QS, kq = st * QS + u % QS;
-            const bool in = row < 32 && 4 * kq < K;   // (a quad starting inside K stays inside the row: lda >= K rounded to 4)
-            ra[st][i] = ld4(rsa, in && m0 + row < M, (unsigned)((m0 + row) * lda + 4 * kq));
-            if constexpr (!BT) {
-                rb[st][i][0] = ldb4(in && n0 + row < N, (unsigned)((n0 + row) * ldb + 4 * kq), 4 * kq, K);
-            } else {
-                const int nq = tid & 7, kb = st * QS + (tid >> 3) + 32 * i;   // k quad
-                const bool bin = (tid >> 3) + 32 * i < QS && kb < KQ && n0 + 4 * nq < N;
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    rb[st][i][c] = ldb4(bin && 4 * kb + c < K, (unsigned)((4 * kb + c) * ldb + n0 + 4 * nq), n0 + 4 * nq, N);
-            }
-        }
-    auto zk = [&](float4 v, int k) {   // zero the quad's elements at k >= K
-        v.x = k < K ? v.x : 0.f;
-        v.y = k + 1 < K ? v.y : 0.f;
-        v.z = k + 2 < K ? v.z : 0.f;
-        v.w = k + 3 < K ? v.w : 0.f;
-        return v;
-    };
-    // wave (wr, wc): output rows 16 wr .. + 15, columns 16 wc .. + 15; lane (j = lane & 15, q = lane >> 4)
-    const int wr = wave & 1, wc = wave >> 1, j = lane & 15, q = lane >> 4;
-    const float* pa = As + (16 * wr + j) * KP + 4 * q;
-    const float* pb = Bs + (16 * wc + j) * KP + 4 * q;
-    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int st = 0; st < LGS_NS; ++st) {
-#pragma unroll
-        for (int i = 0; i < LGS_PER; ++i) {
-            // (branch-free: an item past the tile writes a scratch slot -- a guarded store let the compiler sink the
-            // stage's loads into the branch and wait for every load in flight there)
-            const int u = tid + 256 * i, row = u / QS, kq = st * QS + u % QS;
-            const bool ok = row < 32 && kq < KQ;
-            *(float4*)(ok ? As + row * KP + 4 * kq : scratch) = zk(ra[st][i], 4 * kq);
-            if constexpr (!BT) *(float4*)(ok ? Bs + row * KP + 4 * kq : scratch) = zk(rb[st][i][0], 4 * kq);
-            if constexpr (BT) {
-                const int nq = tid & 7, kb = st * QS + (tid >> 3) + 32 * i;
-                const bool okb = (tid >> 3) + 32 * i < QS && kb < KQ;
-                const float4* v = rb[st][i];
-                float* bq = Bs + 4 * nq * KP + 4 * kb;
-                *(float4*)(okb ? bq : scratch) = make_float4(v[0].x, v[1].x, v[2].x, v[3].x);
-                *(float4*)(okb ? bq + KP : scratch) = make_float4(v[0].y, v[1].y, v[2].y, v[3].y);
-                *(float4*)(okb ? bq + 2 * KP : scratch) = make_float4(v[0].z, v[1].z, v[2].z, v[3].z);
-                *(float4*)(okb ? bq + 3 * KP : scratch) = make_float4(v[0].w, v[1].w, v[2].w, v[3].w);
-            }
-        }
-        // (the LDS stores only: __syncthreads' fence would also wait for the later stages' loads)
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        // the stage's 16-deep k groups: lane (j, q) reads k = 16 g + 4 q .. + 3 of its row / column; MFMA step e
-        // sums k = 16 g + 4 q + e over q (a permutation of the group's k)
-        const int g0 = (st * QS) >> 2, g1 = min(((st + 1) * QS) >> 2, KQ >> 2);
-        for (int g = g0; g < g1; ++g) {
-            const float4 a = *(const float4*)(pa + 16 * g), b = *(const float4*)(pb + 16 * g);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc1, 0, 0, 0);
-        }
-    }
-    // C/D map of the 16x16 MFMA: col = lane & 15, row = 4 (lane >> 4) + e
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const int row = m0 + 16 * wr + 4 * q + e, col = n0 + 16 * wc + j;
-        if (row < M && col < N) lg_store(J.j, 1, 0, row, col, acc0[e] + acc1[e]);
-    }
-}
 
 // ---------------------------------------------------------------------------------------------------- rows
 template <int NC>
@@ -1044,58 +918,11 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
     if (!jobs) return TDMPC_E_NULL;
     const bool x6 = !(tile & TDMPC_LG_TILE_EXACT);   // x6 products unless the caller asks for the exact f32 MFMA
     tile &= ~TDMPC_LG_TILE_EXACT;
-    if (njobs <= 0 || njobs > LG_MAXJ || tile < 1 || tile > 7) return bad("tdmpc_lg_gemm: njobs / tile");
+    if (njobs <= 0 || njobs > LG_MAXJ || tile < 1 || tile > 4) return bad("tdmpc_lg_gemm: njobs / tile");
     KArgs P;
     memset(&P, 0, sizeof P);
     const bool big = tile == 3 || tile == 4;   // LDS-staged macro tiles (exact f32 MFMA)
-    if (tile == 7) {   // the whole-K staged tile (lg_stage_kernel): one segment, amode 0, K <= 512, 16-B loads
-        KArgs Q;
-        memset(&Q, 0, sizeof Q);
-        long nb = 0;
-        int kmax = 1;
-        bool bv = true;
-        const int bt = jobs[0].seg[0].bmode;
-        for (int q = 0; q < njobs; ++q) {
-            const tdmpc_lg_job& j = jobs[q];
-            const tdmpc_lg_seg& S = j.seg[0];
-            if (!j.c || j.m <= 0 || j.n <= 0 || j.nseg != 1 || j.splits != 1 || !S.a || !S.b || S.k <= 0 || S.k > 512 ||
-                S.amode != 0 || S.ones_col >= 0 || S.bmode != bt)
-                return bad("tdmpc_lg_gemm: tile 7 takes one amode-0 segment with K <= 512, one bmode per launch");
-            const int k4 = (S.k + 3) & ~3;
-            if (S.lda % 4 || S.lda < k4 || ((uintptr_t)S.a & 15) || (bt == 0 && S.ldb < S.k) || (bt == 1 && S.ldb < j.n))
-                return bad("tdmpc_lg_gemm: tile 7 needs a 16-B aligned A with rows of whole quads");
-            // B by 16-B loads when every row is whole quads at 16-B alignment, else by 4-B loads
-            bv = bv && S.ldb % 4 == 0 && ((uintptr_t)S.b & 15) == 0 && (bt == 0 ? S.ldb >= k4 : j.n % 4 == 0);
-            if ((j.epi == TDMPC_LG_EPI_PI && (!j.aux || !j.c2)) ||
-                ((j.epi == TDMPC_LG_EPI_ELU_BWD || j.epi == TDMPC_LG_EPI_PI_BWD || j.epi == TDMPC_LG_EPI_RELU_BWD) && !j.aux))
-                return bad("tdmpc_lg_gemm: epilogue operand missing");
-            Q.job[q].j = j;
-            Q.job[q].tiles_m = (j.m + 31) / 32;
-            Q.job[q].block0 = (int)nb;
-            Q.job[q].nb_mem[0] = j.n;
-            nb += (long)Q.job[q].tiles_m * ((j.n + 31) / 32);
-            kmax = std::max(kmax, S.k);
-        }
-        Q.njobs = njobs;
-        static bool attr7 = false;
-        if (!attr7) {
-            const int lmax = (2 * 32 * lgs_pitch(512) + 4) * (int)sizeof(float);
-            const void* fns[4] = {(const void*)lg_stage_kernel<false, false>, (const void*)lg_stage_kernel<false, true>,
-                                  (const void*)lg_stage_kernel<true, false>, (const void*)lg_stage_kernel<true, true>};
-            for (const void* f : fns)
-                if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lmax) != hipSuccess)
-                    return fail(hipGetLastError(), "gemm (tile 7 LDS attribute)");
-            attr7 = true;
-        }
-        const size_t lds = (size_t)(2 * 32 * lgs_pitch(kmax) + 4) * sizeof(float);
-        const dim3 g7((unsigned)nb), b7(256);
-        if (bt && bv) hipLaunchKernelGGL((lg_stage_kernel<true, true>), g7, b7, lds, (hipStream_t)stream, Q);
-        else if (bt) hipLaunchKernelGGL((lg_stage_kernel<true, false>), g7, b7, lds, (hipStream_t)stream, Q);
-        else if (bv) hipLaunchKernelGGL((lg_stage_kernel<false, true>), g7, b7, lds, (hipStream_t)stream, Q);
-        else hipLaunchKernelGGL((lg_stage_kernel<false, false>), g7, b7, lds, (hipStream_t)stream, Q);
-        return launched("gemm (tile 7)");
-    }
-    const int twm = tile == 1 || tile >= 5 ? 32 : 64, twn = tile == 1 || tile >= 5 ? 32 : tile == 2 || tile == 3 ? 64 : 128;
+    const int twm = tile == 1 ? 32 : 64, twn = tile == 1 ? 32 : tile == 2 || tile == 3 ? 64 : 128;
     long blocks = 0;
     for (int q = 0; q < njobs; ++q) {
         const tdmpc_lg_job& j = jobs[q];
@@ -1169,11 +996,7 @@ int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* s
         if (!done) return bad("tdmpc_lg_gemm: macro tile form / chunk");
         return launched("gemm (macro tiles)");
     }
-    if (tile == 5 && x6) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, true, 8>), g, dim3(512), 0, (hipStream_t)stream, P);
-    else if (tile == 5) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, false, 8>), g, dim3(512), 0, (hipStream_t)stream, P);
-    else if (tile == 6 && x6) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, true, 16>), g, dim3(1024), 0, (hipStream_t)stream, P);
-    else if (tile == 6) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, false, 16>), g, dim3(1024), 0, (hipStream_t)stream, P);
-    else if (tile == 1 && x6) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, true>), g, b, 0, (hipStream_t)stream, P);
+    if (tile == 1 && x6) hipLaunchKernelGGL((lg_gemm_kernel<1, 1, true>), g, b, 0, (hipStream_t)stream, P);
     else if (tile == 1) hipLaunchKernelGGL((lg_gemm_kernel<1, 1>), g, b, 0, (hipStream_t)stream, P);
     else if (x6) hipLaunchKernelGGL((lg_gemm_kernel<2, 2, true>), g, b, 0, (hipStream_t)stream, P);
     else hipLaunchKernelGGL((lg_gemm_kernel<2, 2>), g, b, 0, (hipStream_t)stream, P);

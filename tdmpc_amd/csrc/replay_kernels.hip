@@ -521,20 +521,22 @@ __global__ void rp_update_write_kernel(float* prio, const unsigned long long* la
 
 __global__ void rp_update_bump_kernel(unsigned* gen) { *gen += 1u; }
 
-// n <= RP_UPD_ONE (a learner batch): the whole update in ONE workgroup -- the indices in LDS, thread i writes its
-// value unless a later j > i names the same index (the last occurrence wins, as the three-kernel path's keys decide)
+// n <= RP_UPD_ONE (a learner batch): the three kernels above as the phases of ONE workgroup, a barrier between them
+// (the generation-tagged keys are the same, so the paths mix across calls)
 constexpr int RP_UPD_ONE = 1024;
-__global__ void __launch_bounds__(RP_UPD_ONE) rp_update_one_kernel(float* prio, const int64_t* idxs, const float* v,
+__global__ void __launch_bounds__(RP_UPD_ONE) rp_update_one_kernel(float* prio, unsigned long long* last,
+                                                                   unsigned* gen, const int64_t* idxs, const float* v,
                                                                    int n, float eps) {
-    __shared__ int64_t sidx[RP_UPD_ONE];
     const int i = threadIdx.x;
-    const int64_t k = i < n ? idxs[i] : -1;
-    sidx[i] = k;
+    const unsigned g = *gen + 1u;
+    const unsigned long long key = ((unsigned long long)g << 32) | (unsigned)i;
+    const int64_t k = i < n ? idxs[i] : 0;
+    if (i < n) atomicMax(last + k, key);
     __syncthreads();
-    if (i >= n) return;
-    bool last = true;
-    for (int j = i + 1; j < n; ++j) last = last && sidx[j] != k;
-    if (last) prio[k] = __fadd_rn(v[i], eps);
+    if (i < n && __hip_atomic_load(last + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key)
+        prio[k] = __fadd_rn(v[i], eps);
+    __syncthreads();
+    if (i == 0) *gen = g;
 }
 
 }  // namespace
@@ -580,7 +582,8 @@ int tdmpc_replay_update_priorities(const tdmpc_replay_dims* d, float* prio, cons
     if (!n) return 0;
     hipStream_t s = (hipStream_t)stream;
     if (n <= RP_UPD_ONE) {
-        hipLaunchKernelGGL(rp_update_one_kernel, dim3(1), dim3(RP_UPD_ONE), 0, s, prio, idxs, values, n, eps);
+        hipLaunchKernelGGL(rp_update_one_kernel, dim3(1), dim3(RP_UPD_ONE), 0, s, prio, w.last, w.gen, idxs, values, n,
+                           eps);
         RCHK(hipGetLastError());
         return 0;
     }

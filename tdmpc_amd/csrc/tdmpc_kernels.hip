@@ -4493,8 +4493,11 @@ struct PackJob {
 };
 static_assert(sizeof(PackJob) <= PACK_JOB_BYTES, "job-table slot");
 constexpr int PACK_WG = 256, PACK_PER = 8;   // threads per workgroup, items per thread
-// elements per item: an x6 / x6q lane's 8 values (16-B stores per plane), a panel's k quad, else one
+// elements per item: an x6 / x6q lane's 8 values (16-B stores per plane), a panel's k quad, else one; items per
+// thread: one for those (the split and the gathered reads of 4 - 8 values already give each thread its work), else
+// PACK_PER
 __host__ __device__ constexpr int pack_per_item(int kind) { return kind == PJ_X6 || kind == PJ_X6Q ? 8 : kind == PJ_PANEL ? 4 : 1; }
+__host__ __device__ constexpr int pack_items(int kind) { return pack_per_item(kind) > 1 ? 1 : PACK_PER; }
 
 __global__ void __launch_bounds__(PACK_WG) pack_fused_kernel(PackHdr* hdr, const PackJob* jobs, int nj, float* pw,
                                                               unsigned long long nonce, long nweights) {
@@ -4515,9 +4518,9 @@ __global__ void __launch_bounds__(PACK_WG) pack_fused_kernel(PackHdr* hdr, const
         else hi = mid - 1;
     }
     const PackJob& J = jobs[lo];
-    const long base = (long)(blockIdx.x - J.blk0) * PACK_WG * PACK_PER;
-    const int epi = pack_per_item(J.kind);
-    for (int u = 0; u < PACK_PER; ++u) {
+    const int epi = pack_per_item(J.kind), ipt = pack_items(J.kind);
+    const long base = (long)(blockIdx.x - J.blk0) * PACK_WG * ipt;
+    for (int u = 0; u < ipt; ++u) {
         const long i = (base + (long)u * PACK_WG + threadIdx.x) * epi;   // first element of the thread's item
         if (i >= J.work) break;
         switch (J.kind) {
@@ -4820,7 +4823,7 @@ int launch_pack(std::vector<PackJob>& jobs, const Layout& w, float* pw, hipStrea
     int blk = 0;
     for (PackJob& j : jobs) {
         j.blk0 = blk;
-        const long per_blk = (long)PACK_WG * PACK_PER * pack_per_item(j.kind);
+        const long per_blk = (long)PACK_WG * pack_items(j.kind) * pack_per_item(j.kind);
         blk += (int)((j.work + per_blk - 1) / per_blk);
     }
     const size_t nb = jobs.size() * sizeof(PackJob);

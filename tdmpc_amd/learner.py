@@ -306,10 +306,7 @@ class Learner:
                     # so the planner holds the live tensors and the pack's job table exists before the capture
                     self.agent.planner.pack(self.agent.model)
                 graph = torch.cuda.CUDAGraph()
-                cap = None
-                if self.engine is not None and self.engine.prio:
-                    cap = self._cap_stream = getattr(self, "_cap_stream", None) or torch.cuda.Stream(priority=-1)
-                with torch.cuda.graph(graph, stream=cap):
+                with torch.cuda.graph(graph):
                     out = self.step(buffer)
                 g = self._graphs[key] = (graph, out)
                 # capture recorded the kernels without running them: run this call's update

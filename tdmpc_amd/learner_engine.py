@@ -126,11 +126,6 @@ class Engine:
         # the learner's HIP graph as parallel branches): the TD target beside the encoder + latent rollout, the
         # heads' weight gradients beside the rollout's backward. Both pairs touch disjoint buffers.
         self.side = torch.cuda.Stream(self.dev)
-        # (A/B knob TDMPC_LG_PRIO=1: the forward's side branch -- the TD target, the critical one there -- on a
-        # high-priority stream, the backward's -- the heads' weight gradients beside the latent rollout's backward --
-        # on a default one; the learner then captures on a high-priority stream)
-        self.prio = os.environ.get("TDMPC_LG_PRIO", "0") == "1"
-        self.side_hi = torch.cuda.Stream(self.dev, priority=-1) if self.prio else self.side
         # lg_gemm's products: the exact f32 MFMA (default: as fast as x6 on the learner's shapes, which are launch-
         # and latency-bound rather than MFMA-bound) or the x6 form (TDMPC_LG_X6=1; set before the first update: the
         # captured graph keeps the choice)
@@ -150,11 +145,6 @@ class Engine:
         # bitwise). TDMPC_LG_BLAS=1 sends them to hipBLASLt instead (the library picks its own reduction order;
         # Learner.update pins full-fp32 matmul precision around it); set before the first update: the graph keeps it.
         self.blas = os.environ.get("TDMPC_LG_BLAS", "0") == "1"
-        # the register tile for the narrow products (the latent rollout's B-row layers and their dX, the encoder,
-        # pi's action layer): tdmpc_lg_gemm tile 1 (4 waves split K) or 5 / 6 (8 / 16 waves)
-        self.small_tile = int(os.environ.get("TDMPC_LG_SMALL_TILE", "1"))
-        # tile 5 (8 waves) for the narrow products whose every segment has K >= this (0: never)
-        self.nw8_k = int(os.environ.get("TDMPC_LG_NW8_K", "0"))
         self._aux = {}
 
     def _alias(self, model, flat):
@@ -244,22 +234,14 @@ class Engine:
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
 
-    def _pair(self, main_steps, side_steps, side=None):
+    def _pair(self, main_steps, side_steps):
         """Issue two independent launch sequences (generators that yield after each launch): main_steps on the
         caller's stream, side_steps on self.side (forked from it here; the caller joins it back), one launch from
         each in turn. In the captured graph the main branch (the critical path) then leads: 1.20 vs 1.21 ms per
         humanoid update against capturing the side branch whole first (profiles/r05/learner_branches.txt)."""
         main = torch.cuda.current_stream(self.dev)
-        side = side or self.side
-        side.wait_stream(main)
-        live = [(main, main_steps), (side, side_steps)]
-        order = os.environ.get("TDMPC_LG_PAIR", "1")   # (A/B knob: 0 side branch whole first, 2 main whole first)
-        if order in ("0", "2"):
-            for st, steps in (live if order == "2" else live[::-1]):
-                with torch.cuda.stream(st):
-                    for _ in steps:
-                        pass
-            return
+        self.side.wait_stream(main)
+        live = [(main, main_steps), (self.side, side_steps)]
         while live:
             for e in list(live):
                 with torch.cuda.stream(e[0]):
@@ -295,25 +277,10 @@ class Engine:
             # 64 x 64 tiles only for wide launches of row-major operands; a transposed weight operand (the
             # backward's dX) runs 15-25 % faster on 32 x 32 tiles (tools/lg_gemm_bench.py)
             tbw = any(sg[6] == 1 for j in jobs for sg in j["segs"])
-            tile = 2 if tiles64 >= self.t64 and not tbw else self.small_tile
-            if tile == 1 and self.nw8_k and min(sg[4] for j in jobs for sg in j["segs"]) >= self.nw8_k:
-                tile = 5
-            if tile == 7 and not all(self._stage_ok(j) for j in jobs) or \
-                    tile == 7 and len({j["segs"][0][6] for j in jobs}) > 1:
-                tile = 1
-        if tile not in (3, 4):
+            tile = 2 if tiles64 >= self.t64 and not tbw else 1
+        if tile < 3:
             tile |= 0 if self.x6 else TILE_EXACT
         _lib.check(self.lib.tdmpc_lg_gemm(arr, len(jobs), tile, self._stream()), "tdmpc_lg_gemm")
-
-    @staticmethod
-    def _stage_ok(j):
-        """tdmpc_lg_gemm tile 7's operand contract (include/tdmpc_learner.h)."""
-        if len(j["segs"]) != 1 or j.get("splits", 1) != 1:
-            return False
-        a, b, lda, ldb, k, am, bm, ones = j["segs"][0]
-        k4 = (k + 3) & ~3
-        return (am == 0 and ones < 0 and k <= 512 and lda % 4 == 0 and lda >= k4 and a % 16 == 0 and
-                ldb >= (k if bm == 0 else j["n"]))
 
     def rows(self, heads, n, bwd=False, **kw):
         a = _lib.LgRows()
@@ -575,11 +542,11 @@ class Engine:
 
         # ---- forward (encoder, latent rollout, heads) beside the TD targets and target latents (no gradient) ----
         main = torch.cuda.current_stream(dev)
-        self._pair(self._fwd_steps(b, obs, action, B), self._td_steps(b, nxo_t, rew, R, _p(eps)), self.side_hi)
+        self._pair(self._fwd_steps(b, obs, action, B), self._td_steps(b, nxo_t, rew, R, _p(eps)))
         X0, Q = b["X0"], b["Q"]
         PA, PB, Y1, Y2, XH1, XH2, RS1, RS2 = (b[k] for k in ("PA", "PB", "Y1", "Y2", "XH1", "XH2", "RS1", "RS2"))
 
-        main.wait_stream(self.side_hi)   # TD / NZ ready
+        main.wait_stream(self.side)   # TD / NZ ready
         # ---- losses (fused HIP loss, include/tdmpc_learner.h) ----
         la = _lib.LossArgs(_p(b["ZP"]), _p(b["NZ"]), _p(Q[0]), _p(Q[1]), _p(Q[2]), rew, _p(b["TD"]), _p(weights),
                            _p(self.rho), H, B, L, float(cfg.consistency_coef), float(cfg.reward_coef),
