@@ -57,10 +57,11 @@ def _hip_steps(p0, grads):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["finite_clipped", "finite_unclipped", "nan_entry", "inf_entry"])
+@pytest.mark.parametrize("case", ["finite_clipped", "finite_unclipped", "nan_entry", "inf_entry", "finite_tail"])
 def test_lg_adam_matches_torch_clip_and_adam(case):
     gen = torch.Generator().manual_seed(7)
-    n = 70_000   # > 256 x 256: several grid-stride rounds of the kernel
+    # > 256 x 256: several grid-stride rounds of the kernel; finite_tail: not a multiple of 4 (16-B body + element tail)
+    n = 70_003 if case == "finite_tail" else 70_000
     p0 = torch.randn(n, generator=gen)
     scale = 1.0 if case != "finite_unclipped" else 1e-3
     grads = [torch.randn(n, generator=gen) * scale for _ in range(2)]
