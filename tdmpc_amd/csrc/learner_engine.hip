@@ -614,44 +614,71 @@ template <int TM, int TN, int KC>
 constexpr size_t lg_big_lds() { return (size_t)2 * (KC / 4) * (64 * TM + 1 + 64 * TN + 1) * sizeof(float4); }
 
 // ---------------------------------------------------------------------------------------------------- rows
+// Lane l of a row's wave holds features 4 l + 256 c + j (c < NC / 4, j < 4): 16-B loads and stores. Every head's
+// row is loaded before the first reduction (the heads' latencies overlap).
 template <int NC>
 __global__ void __launch_bounds__(256) lg_rows_fwd_kernel(const tdmpc_lg_rows a) {
+    constexpr int NQ = NC / 4;   // float4 per lane
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= a.rows) return;
     const int m = a.m;
     const float inv_m = 1.f / (float)m;
-    float outv[3] = {0.f, 0.f, 0.f};
-    for (int hh = 0; hh < a.nh; ++hh) {
-        const tdmpc_lg_rowhead& H = a.hd[hh];
-        float x[NC];
+    float4 x[3][NQ];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) x[c] = H.x[(size_t)r * H.ldx + lane + 64 * c];
+    for (int hh = 0; hh < 3; ++hh)
+        if (hh < a.nh) {
+            const tdmpc_lg_rowhead& H = a.hd[hh];
+#pragma unroll
+            for (int c = 0; c < NQ; ++c) x[hh][c] = *(const float4*)(H.x + (size_t)r * H.ldx + 4 * lane + 256 * c);
+        }
+    float outv[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int hh = 0; hh < 3; ++hh) {
+        if (hh >= a.nh) break;
+        const tdmpc_lg_rowhead& H = a.hd[hh];
+        float v[NC];
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) {
+            v[4 * c] = x[hh][c].x; v[4 * c + 1] = x[hh][c].y; v[4 * c + 2] = x[hh][c].z; v[4 * c + 3] = x[hh][c].w;
+        }
         if (H.ln) {
             float s = 0.f;
 #pragma unroll
-            for (int c = 0; c < NC; ++c) s += x[c];
+            for (int c = 0; c < NC; ++c) s += v[c];
             const float mean = wsum(s) * inv_m;
             float d = 0.f;
 #pragma unroll
-            for (int c = 0; c < NC; ++c) d += (x[c] - mean) * (x[c] - mean);
+            for (int c = 0; c < NC; ++c) d += (v[c] - mean) * (v[c] - mean);
             const float rs = 1.f / sqrtf(wsum(d) * inv_m + 1e-5f);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                const int n = lane + 64 * c;
-                const float xh = (x[c] - mean) * rs;
-                if (H.xhat) H.xhat[(size_t)r * m + n] = xh;
-                x[c] = xh * H.g[n] + H.beta[n];
+            for (int c = 0; c < NQ; ++c) {
+                const int n = 4 * lane + 256 * c;
+                const float4 g = *(const float4*)(H.g + n), be = *(const float4*)(H.beta + n);
+                float4 xh;
+                xh.x = (v[4 * c] - mean) * rs; xh.y = (v[4 * c + 1] - mean) * rs;
+                xh.z = (v[4 * c + 2] - mean) * rs; xh.w = (v[4 * c + 3] - mean) * rs;
+                if (H.xhat) *(float4*)(H.xhat + (size_t)r * m + n) = xh;
+                v[4 * c] = xh.x * g.x + be.x; v[4 * c + 1] = xh.y * g.y + be.y;
+                v[4 * c + 2] = xh.z * g.z + be.z; v[4 * c + 3] = xh.w * g.w + be.w;
             }
             if (H.rstd && lane == 0) H.rstd[r] = rs;
         }
         float dot = 0.f;
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            const int n = lane + 64 * c;
-            const float y = H.act == 1 ? tanhf(x[c]) : H.act == 2 ? elu_f(x[c]) : x[c];
-            if (H.y) H.y[(size_t)r * H.ldy + n] = y;
-            if (H.tail) dot += y * H.w3[n];
+        for (int c = 0; c < NQ; ++c) {
+            const int n = 4 * lane + 256 * c;
+            float y[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float u = v[4 * c + j];
+                y[j] = H.act == 1 ? tanhf(u) : H.act == 2 ? elu_f(u) : u;
+            }
+            if (H.y) *(float4*)(H.y + (size_t)r * H.ldy + n) = make_float4(y[0], y[1], y[2], y[3]);
+            if (H.tail) {
+                const float4 w = *(const float4*)(H.w3 + n);
+                dot += y[0] * w.x + y[1] * w.y + y[2] * w.z + y[3] * w.w;
+            }
         }
         if (H.tail) {
             const float o = wsum(dot) + H.b3[0];
@@ -662,22 +689,36 @@ __global__ void __launch_bounds__(256) lg_rows_fwd_kernel(const tdmpc_lg_rows a)
     if (a.td && lane == 0) a.td[r] = a.reward[r] + a.gamma * fminf(outv[0], outv[1]);
 }
 
-template <int NC>
-__global__ void __launch_bounds__(256) lg_rows_bwd_kernel(const tdmpc_lg_rows a) {
-    __shared__ float red[4][3 * NC * 64 + 1];
+// NW waves per workgroup (16 for m <= 512: four rows in flight per SIMD), a wave per row, the workgroup's column
+// partials summed over its waves in a fixed order; features as in lg_rows_fwd_kernel.
+template <int NC, int NW>
+__global__ void __launch_bounds__(64 * NW) lg_rows_bwd_kernel(const tdmpc_lg_rows a) {
+    constexpr int NQ = NC / 4;
+    __shared__ float red[NW][3 * NC * 64 + 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int m = a.m;
     const float inv_m = 1.f / (float)m;
-    const int stride = gridDim.x * 4;
+    const int stride = gridDim.x * NW;
     for (int hh = 0; hh < a.nh; ++hh) {
         const tdmpc_lg_rowhead& H = a.hd[hh];
         float pg[NC], pb[NC], pw[NC], pq = 0.f;
 #pragma unroll
         for (int c = 0; c < NC; ++c) pg[c] = pb[c] = pw[c] = 0.f;
-        for (int r = blockIdx.x * 4 + wave; r < a.rows; r += stride) {
-            float d[NC], y[NC];
+        for (int r = blockIdx.x * NW + wave; r < a.rows; r += stride) {
+            float d[NC], y[NC], xh[NC];
 #pragma unroll
-            for (int c = 0; c < NC; ++c) y[c] = H.yact[(size_t)r * m + lane + 64 * c];
+            for (int c = 0; c < NQ; ++c) {
+                const float4 v = *(const float4*)(H.yact + (size_t)r * m + 4 * lane + 256 * c);
+                y[4 * c] = v.x; y[4 * c + 1] = v.y; y[4 * c + 2] = v.z; y[4 * c + 3] = v.w;
+                if (H.ln) {
+                    const float4 u = *(const float4*)(H.xhat + (size_t)r * m + 4 * lane + 256 * c);
+                    xh[4 * c] = u.x; xh[4 * c + 1] = u.y; xh[4 * c + 2] = u.z; xh[4 * c + 3] = u.w;
+                }
+                if (!H.tail) {
+                    const float4 u = *(const float4*)(H.x + (size_t)r * H.ldx + 4 * lane + 256 * c);
+                    d[4 * c] = u.x; d[4 * c + 1] = u.y; d[4 * c + 2] = u.z; d[4 * c + 3] = u.w;
+                }
+            }
             if (H.tail) {
                 float dq;
                 if (a.q1) {   // update_pi: d(-sum_t rho^t mean_b min(q1, q2)) / dq_head
@@ -688,30 +729,33 @@ __global__ void __launch_bounds__(256) lg_rows_bwd_kernel(const tdmpc_lg_rows a)
                     dq = H.dq[r];
                 }
 #pragma unroll
-                for (int c = 0; c < NC; ++c) {
-                    d[c] = dq * H.w3[lane + 64 * c];
-                    pw[c] += dq * y[c];
+                for (int c = 0; c < NQ; ++c) {
+                    const float4 w = *(const float4*)(H.w3 + 4 * lane + 256 * c);
+                    d[4 * c] = dq * w.x; d[4 * c + 1] = dq * w.y; d[4 * c + 2] = dq * w.z; d[4 * c + 3] = dq * w.w;
                 }
-                pq += dq;
-            } else {
 #pragma unroll
-                for (int c = 0; c < NC; ++c) d[c] = H.x[(size_t)r * H.ldx + lane + 64 * c];
+                for (int c = 0; c < NC; ++c) pw[c] += dq * y[c];
+                pq += dq;
             }
 #pragma unroll
             for (int c = 0; c < NC; ++c)
                 d[c] *= H.act == 1 ? 1.f - y[c] * y[c] : H.act == 2 ? (y[c] > 0.f ? 1.f : y[c] + 1.f) : 1.f;
             if (H.ln) {
                 const float rs = H.rstd[r];
-                float xh[NC], s1 = 0.f, s2 = 0.f;
+                float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-                for (int c = 0; c < NC; ++c) {
-                    const int n = lane + 64 * c;
-                    xh[c] = H.xhat[(size_t)r * m + n];
-                    pb[c] += d[c];
-                    pg[c] += d[c] * xh[c];
-                    d[c] *= H.g[n];
-                    s1 += d[c];
-                    s2 += d[c] * xh[c];
+                for (int c = 0; c < NQ; ++c) {
+                    const float4 g = *(const float4*)(H.g + 4 * lane + 256 * c);
+                    const float gg[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int e = 4 * c + j;
+                        pb[e] += d[e];
+                        pg[e] += d[e] * xh[e];
+                        d[e] *= gg[j];
+                        s1 += d[e];
+                        s2 += d[e] * xh[e];
+                    }
                 }
                 s1 = wsum(s1) * inv_m;
                 s2 = wsum(s2) * inv_m;
@@ -719,28 +763,37 @@ __global__ void __launch_bounds__(256) lg_rows_bwd_kernel(const tdmpc_lg_rows a)
                 for (int c = 0; c < NC; ++c) d[c] = rs * (d[c] - s1 - xh[c] * s2);
             }
 #pragma unroll
-            for (int c = 0; c < NC; ++c) H.y[(size_t)r * H.ldy + lane + 64 * c] = d[c];
+            for (int c = 0; c < NQ; ++c)
+                *(float4*)(H.y + (size_t)r * H.ldy + 4 * lane + 256 * c) =
+                    make_float4(d[4 * c], d[4 * c + 1], d[4 * c + 2], d[4 * c + 3]);
         }
         if (!H.part) continue;
-        // partial column sums of this workgroup: [dg (m), dbeta (m)] if ln, then [dW3 (m), db3] if tail
+        // partial column sums of this workgroup: [dg (m), dbeta (m)] if ln, then [dW3 (m), db3] if tail; feature n of
+        // element e = 4 c + j is 4 lane + 256 c + j
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            red[wave][c * 64 + lane] = pg[c];
-            red[wave][(NC + c) * 64 + lane] = pb[c];
-            red[wave][(2 * NC + c) * 64 + lane] = pw[c];
-        }
-        if (lane == 0) red[wave][3 * NC * 64] = pq;   // the same in every lane (dq is a per-row scalar)
+        for (int c = 0; c < NQ; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int n = 4 * lane + 256 * c + j, e = 4 * c + j;
+                red[wave][n] = pg[e];
+                red[wave][m + n] = pb[e];
+                red[wave][2 * m + n] = pw[e];
+            }
+        if (lane == 0) red[wave][3 * m] = pq;   // the same in every lane (dq is a per-row scalar)
         __syncthreads();
         const int pw_n = (H.ln ? 2 * m : 0) + (H.tail ? m + 1 : 0);
         float* out = H.part + (size_t)blockIdx.x * pw_n;
-        for (int i = threadIdx.x; i < pw_n; i += 256) {
+        for (int i = threadIdx.x; i < pw_n; i += 64 * NW) {
             int src;
             if (H.ln && i < 2 * m) src = i;                       // dg | dbeta
             else {
                 const int t = i - (H.ln ? 2 * m : 0);
-                src = t < m ? 2 * m + t : 3 * NC * 64;          // dW3 | db3
+                src = t < m ? 2 * m + t : 3 * m;                  // dW3 | db3
             }
-            out[i] = red[0][src] + red[1][src] + red[2][src] + red[3][src];
+            float v = red[0][src];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) v += red[w][src];
+            out[i] = v;
         }
         __syncthreads();
     }
@@ -1021,6 +1074,13 @@ static int rows_ok(const tdmpc_lg_rows* a) {
     if (!a) return TDMPC_E_NULL;
     if (a->nh < 1 || a->nh > 3 || a->rows <= 0 || (a->m != 256 && a->m != 512 && a->m != 1024))
         return bad("tdmpc_lg_rows: nh / rows / m");
+    for (int h = 0; h < a->nh; ++h) {   // 16-B row accesses
+        const tdmpc_lg_rowhead& H = a->hd[h];
+        const void* ps[] = {H.x, H.y, H.xhat, H.yact, H.g, H.beta, H.w3};
+        for (const void* q : ps)
+            if ((uintptr_t)q & 15) return bad("tdmpc_lg_rows: a row operand is not 16-B aligned");
+        if ((H.x && H.ldx % 4) || (H.y && H.ldy % 4)) return bad("tdmpc_lg_rows: row strides must be multiples of 4");
+    }
     return 0;
 }
 
@@ -1045,9 +1105,9 @@ int tdmpc_lg_rows_bwd(const tdmpc_lg_rows* a, int32_t nwg, void* stream) {
             return TDMPC_E_NULL;
     }
     hipStream_t s = (hipStream_t)stream;
-    if (a->m == 256) hipLaunchKernelGGL(lg_rows_bwd_kernel<4>, dim3(nwg), dim3(256), 0, s, *a);
-    else if (a->m == 512) hipLaunchKernelGGL(lg_rows_bwd_kernel<8>, dim3(nwg), dim3(256), 0, s, *a);
-    else hipLaunchKernelGGL(lg_rows_bwd_kernel<16>, dim3(nwg), dim3(256), 0, s, *a);
+    if (a->m == 256) hipLaunchKernelGGL((lg_rows_bwd_kernel<4, 16>), dim3(nwg), dim3(1024), 0, s, *a);
+    else if (a->m == 512) hipLaunchKernelGGL((lg_rows_bwd_kernel<8, 16>), dim3(nwg), dim3(1024), 0, s, *a);
+    else hipLaunchKernelGGL((lg_rows_bwd_kernel<16, 4>), dim3(nwg), dim3(256), 0, s, *a);
     return launched("rows_bwd");
 }
 
