@@ -689,45 +689,35 @@ __global__ void __launch_bounds__(256) lg_rows_fwd_kernel(const tdmpc_lg_rows a)
     if (a.td && lane == 0) a.td[r] = a.reward[r] + a.gamma * fminf(outv[0], outv[1]);
 }
 
-// NW waves per workgroup, a wave per row and every head of it (the heads' loads issued together), the workgroup's
-// column partials summed over its waves in a fixed order; features as in lg_rows_fwd_kernel.
+// NW waves per workgroup (16 for m <= 512: four rows in flight per SIMD), a wave per row, the workgroup's column
+// partials summed over its waves in a fixed order; features as in lg_rows_fwd_kernel.
 template <int NC, int NW>
 __global__ void __launch_bounds__(64 * NW) lg_rows_bwd_kernel(const tdmpc_lg_rows a) {
     constexpr int NQ = NC / 4;
     __shared__ float red[NW][3 * NC * 64 + 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int m = a.m, nh = a.nh;
+    const int m = a.m;
     const float inv_m = 1.f / (float)m;
     const int stride = gridDim.x * NW;
-    float pg[3][NC], pb[3][NC], pw[3][NC], pq[3] = {0.f, 0.f, 0.f};
+    for (int hh = 0; hh < a.nh; ++hh) {
+        const tdmpc_lg_rowhead& H = a.hd[hh];
+        float pg[NC], pb[NC], pw[NC], pq = 0.f;
 #pragma unroll
-    for (int hh = 0; hh < 3; ++hh)
-#pragma unroll
-        for (int c = 0; c < NC; ++c) pg[hh][c] = pb[hh][c] = pw[hh][c] = 0.f;
-    for (int r = blockIdx.x * NW + wave; r < a.rows; r += stride) {
-        float4 yv[3][NQ], hv[3][NQ], xv[3][NQ];
-#pragma unroll
-        for (int hh = 0; hh < 3; ++hh) {
-            if (hh >= nh) break;
-            const tdmpc_lg_rowhead& H = a.hd[hh];
-#pragma unroll
-            for (int c = 0; c < NQ; ++c) {
-                const size_t o = (size_t)r * m + 4 * lane + 256 * c;
-                yv[hh][c] = *(const float4*)(H.yact + o);
-                if (H.ln) hv[hh][c] = *(const float4*)(H.xhat + o);
-                if (!H.tail) xv[hh][c] = *(const float4*)(H.x + (size_t)r * H.ldx + 4 * lane + 256 * c);
-            }
-        }
-#pragma unroll
-        for (int hh = 0; hh < 3; ++hh) {
-            if (hh >= nh) break;
-            const tdmpc_lg_rowhead& H = a.hd[hh];
+        for (int c = 0; c < NC; ++c) pg[c] = pb[c] = pw[c] = 0.f;
+        for (int r = blockIdx.x * NW + wave; r < a.rows; r += stride) {
             float d[NC], y[NC], xh[NC];
 #pragma unroll
             for (int c = 0; c < NQ; ++c) {
-                y[4 * c] = yv[hh][c].x; y[4 * c + 1] = yv[hh][c].y; y[4 * c + 2] = yv[hh][c].z; y[4 * c + 3] = yv[hh][c].w;
-                xh[4 * c] = hv[hh][c].x; xh[4 * c + 1] = hv[hh][c].y; xh[4 * c + 2] = hv[hh][c].z; xh[4 * c + 3] = hv[hh][c].w;
-                d[4 * c] = xv[hh][c].x; d[4 * c + 1] = xv[hh][c].y; d[4 * c + 2] = xv[hh][c].z; d[4 * c + 3] = xv[hh][c].w;
+                const float4 v = *(const float4*)(H.yact + (size_t)r * m + 4 * lane + 256 * c);
+                y[4 * c] = v.x; y[4 * c + 1] = v.y; y[4 * c + 2] = v.z; y[4 * c + 3] = v.w;
+                if (H.ln) {
+                    const float4 u = *(const float4*)(H.xhat + (size_t)r * m + 4 * lane + 256 * c);
+                    xh[4 * c] = u.x; xh[4 * c + 1] = u.y; xh[4 * c + 2] = u.z; xh[4 * c + 3] = u.w;
+                }
+                if (!H.tail) {
+                    const float4 u = *(const float4*)(H.x + (size_t)r * H.ldx + 4 * lane + 256 * c);
+                    d[4 * c] = u.x; d[4 * c + 1] = u.y; d[4 * c + 2] = u.z; d[4 * c + 3] = u.w;
+                }
             }
             if (H.tail) {
                 float dq;
@@ -744,8 +734,8 @@ __global__ void __launch_bounds__(64 * NW) lg_rows_bwd_kernel(const tdmpc_lg_row
                     d[4 * c] = dq * w.x; d[4 * c + 1] = dq * w.y; d[4 * c + 2] = dq * w.z; d[4 * c + 3] = dq * w.w;
                 }
 #pragma unroll
-                for (int c = 0; c < NC; ++c) pw[hh][c] += dq * y[c];
-                pq[hh] += dq;
+                for (int c = 0; c < NC; ++c) pw[c] += dq * y[c];
+                pq += dq;
             }
 #pragma unroll
             for (int c = 0; c < NC; ++c)
@@ -760,8 +750,8 @@ __global__ void __launch_bounds__(64 * NW) lg_rows_bwd_kernel(const tdmpc_lg_row
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int e = 4 * c + j;
-                        pb[hh][e] += d[e];
-                        pg[hh][e] += d[e] * xh[e];
+                        pb[e] += d[e];
+                        pg[e] += d[e] * xh[e];
                         d[e] *= gg[j];
                         s1 += d[e];
                         s2 += d[e] * xh[e];
@@ -777,11 +767,6 @@ __global__ void __launch_bounds__(64 * NW) lg_rows_bwd_kernel(const tdmpc_lg_row
                 *(float4*)(H.y + (size_t)r * H.ldy + 4 * lane + 256 * c) =
                     make_float4(d[4 * c], d[4 * c + 1], d[4 * c + 2], d[4 * c + 3]);
         }
-    }
-#pragma unroll
-    for (int hh = 0; hh < 3; ++hh) {
-        if (hh >= nh) break;
-        const tdmpc_lg_rowhead& H = a.hd[hh];
         if (!H.part) continue;
         // partial column sums of this workgroup: [dg (m), dbeta (m)] if ln, then [dW3 (m), db3] if tail; feature n of
         // element e = 4 c + j is 4 lane + 256 c + j
@@ -790,11 +775,11 @@ __global__ void __launch_bounds__(64 * NW) lg_rows_bwd_kernel(const tdmpc_lg_row
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int n = 4 * lane + 256 * c + j, e = 4 * c + j;
-                red[wave][n] = pg[hh][e];
-                red[wave][m + n] = pb[hh][e];
-                red[wave][2 * m + n] = pw[hh][e];
+                red[wave][n] = pg[e];
+                red[wave][m + n] = pb[e];
+                red[wave][2 * m + n] = pw[e];
             }
-        if (lane == 0) red[wave][3 * m] = pq[hh];   // the same in every lane (dq is a per-row scalar)
+        if (lane == 0) red[wave][3 * m] = pq;   // the same in every lane (dq is a per-row scalar)
         __syncthreads();
         const int pw_n = (H.ln ? 2 * m : 0) + (H.tail ? m + 1 : 0);
         float* out = H.part + (size_t)blockIdx.x * pw_n;
@@ -1120,8 +1105,8 @@ int tdmpc_lg_rows_bwd(const tdmpc_lg_rows* a, int32_t nwg, void* stream) {
             return TDMPC_E_NULL;
     }
     hipStream_t s = (hipStream_t)stream;
-    if (a->m == 256) hipLaunchKernelGGL((lg_rows_bwd_kernel<4, 8>), dim3(nwg), dim3(512), 0, s, *a);
-    else if (a->m == 512) hipLaunchKernelGGL((lg_rows_bwd_kernel<8, 8>), dim3(nwg), dim3(512), 0, s, *a);
+    if (a->m == 256) hipLaunchKernelGGL((lg_rows_bwd_kernel<4, 16>), dim3(nwg), dim3(1024), 0, s, *a);
+    else if (a->m == 512) hipLaunchKernelGGL((lg_rows_bwd_kernel<8, 16>), dim3(nwg), dim3(1024), 0, s, *a);
     else hipLaunchKernelGGL((lg_rows_bwd_kernel<16, 4>), dim3(nwg), dim3(256), 0, s, *a);
     return launched("rows_bwd");
 }
