@@ -91,7 +91,8 @@ typedef struct tdmpc_lg_job {
 #define TDMPC_LG_TILE_EXACT 0x100
 int tdmpc_lg_gemm(const tdmpc_lg_job* jobs, int32_t njobs, int32_t tile, void* stream);
 
-/* Row kernels over [rows][m] activations (one wave per row; m in {256, 512, 1024}), up to 3 heads.
+/* Row kernels over [rows][m] activations (one wave per row; m in {256, 512, 1024}), up to 3 heads. Every row operand
+ * (x, y, xhat, yact, g, beta, w3) 16-B aligned and ldx / ldy multiples of 4 (16-B row accesses), else TDMPC_E_DIMS.
  * Forward, per head: v = x (ln: v = layer_norm(x) * g + beta, saving xhat [rows][m] and rstd [rows]); y = act(v)
  * (act 1 tanh, 2 elu) -> y (ldy); tail: out[r] = y . w3 + b3[0]. td != null: td[r] = reward[r] + gamma *
  * min(out_0[r], out_1[r]) (TDMPC._td_target, tdmpc.py:184-190).
