@@ -2499,9 +2499,8 @@ struct PiMuArgs {
     const float* eps; int eps_G; long eps_env; long eps_off; float min_std, lo, hi;
 };
 
-__global__ void __launch_bounds__(256) pi_from_mu_kernel(const PiMuArgs a) {
+DEVI void pi_from_mu_item(const PiMuArgs& a, long i) {
     const int nq = a.Ap / 4;
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const int row = (int)(i / nq), q = (int)(i % nq);
     if (row >= a.rows) return;
     const int xr = map_row(a.amap, row);
@@ -2524,6 +2523,10 @@ __global__ void __launch_bounds__(256) pi_from_mu_kernel(const PiMuArgs a) {
         o[cc] = x;
     }
     *(float4*)(a.Xo + (size_t)(xr >> 5) * a.x_ts + (size_t)q * 128 + (xr & 31) * 4) = make_float4(o[0], o[1], o[2], o[3]);
+}
+
+__global__ void __launch_bounds__(256) pi_from_mu_kernel(const PiMuArgs a) {
+    pi_from_mu_item(a, (long)blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 
@@ -2654,12 +2657,15 @@ struct PrepArgs {
     const float* eps; long eps_env; long eps_off;        // candidate noise [H][N][A] at eps_off per env
     const float* z0;                                     // [B][Lp] or null (no broadcast)
     long n_zq, n_sq;                                     // work items: z quads, sample quads
+    PiMuArgs pm; long n_pm;                              // ... and the policy rows' terminal redraw (pi_from_mu)
 };
 
 __global__ void __launch_bounds__(256) prep_kernel(const PrepArgs a) {
-    const long total = a.n_zq + a.n_sq;
+    const long total = a.n_zq + a.n_sq + a.n_pm;
     for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total; it += (long)gridDim.x * blockDim.x) {
-        if (it < a.n_zq) {
+        if (it >= a.n_zq + a.n_sq) {
+            pi_from_mu_item(a.pm, it - a.n_zq - a.n_sq);
+        } else if (it < a.n_zq) {
             // (e, q, row) with row fastest: X_0[e*T + row] latent quad q = z0[e][4q..4q+3]
             const int row = (int)(it % a.T);
             const long r2 = it / a.T;
@@ -4030,7 +4036,7 @@ int pi_cache_on() {
 }
 
 // pi(z_H) of `rows` rows from the cached means k.pimu (pi_from_mu_kernel) -> X_H action columns.
-int policy_from_mu(const Ctx& c, int rows, RowMap map, const float* eps, long eps_env, int eps_G, long eps_off,
+PiMuArgs pimu_args(const Ctx& c, int rows, RowMap map, const float* eps, long eps_env, int eps_G, long eps_off,
                    float min_std, float* Xo = nullptr, const RowMap* mmap = nullptr) {
     PiMuArgs f;
     memset(&f, 0, sizeof f);
@@ -4038,6 +4044,12 @@ int policy_from_mu(const Ctx& c, int rows, RowMap map, const float* eps, long ep
     f.Xo = Xo ? Xo : Xt(c, c.H); f.x_ts = (long)c.Kx * 32;
     f.eps = eps; f.eps_G = eps_G; f.eps_env = eps_env; f.eps_off = eps_off; f.min_std = min_std;
     f.lo = (float)(-1.0 + 1e-6); f.hi = (float)(1.0 - 1e-6);
+    return f;
+}
+
+int policy_from_mu(const Ctx& c, int rows, RowMap map, const float* eps, long eps_env, int eps_G, long eps_off,
+                   float min_std, float* Xo = nullptr, const RowMap* mmap = nullptr) {
+    const PiMuArgs f = pimu_args(c, rows, map, eps, eps_env, eps_G, eps_off, min_std, Xo, mmap);
     const long nth = (long)rows * (c.w.Ap / 4);
     if (!nth) return 0;
     hipLaunchKernelGGL(pi_from_mu_kernel, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, c.s, f);
@@ -4047,8 +4059,9 @@ int policy_from_mu(const Ctx& c, int rows, RowMap map, const float* eps, long ep
 
 // Terminal value: Q(z_H, pi(z_H)) for all T rows of every env (tdmpc.py:91-92).
 // prep_kernel launch: candidates of CEM iteration `iter` for all H steps (if noise) and, with z0, the
-// latent columns of X_0 for every row.
-int prep(const Ctx& c, const float* noise, int iter, const float* z0) {
+// latent columns of X_0 for every row; with pm, the policy rows' terminal redraw of that iteration in the same launch
+// (it reads only the cached pi mean and the noise, so it need not wait for the rollout).
+int prep(const Ctx& c, const float* noise, int iter, const float* z0, const PiMuArgs* pm = nullptr) {
     PrepArgs a;
     memset(&a, 0, sizeof a);
     a.X = c.k.X; a.x_stride = c.k.x_stride; a.Kx = c.Kx; a.apq = c.w.Ap / 4; a.lpq = c.w.Lp / 4;
@@ -4058,7 +4071,11 @@ int prep(const Ctx& c, const float* noise, int iter, const float* z0) {
     a.z0 = z0;
     a.n_zq = z0 ? (long)c.B * a.lpq * c.T : 0;
     a.n_sq = noise ? (long)c.B * c.H * a.apq * c.N : 0;
-    const long total = a.n_zq + a.n_sq;
+    if (pm) {
+        a.pm = *pm;
+        a.n_pm = (long)pm->rows * (pm->Ap / 4);
+    }
+    const long total = a.n_zq + a.n_sq + a.n_pm;
     if (!total) return 0;
     const int blocks = (int)std::min<long>((total + 255) / 256, 2048);
     hipLaunchKernelGGL(prep_kernel, dim3(blocks), dim3(256), 0, c.s, a);
@@ -5232,16 +5249,20 @@ int tdmpc_plan(const tdmpc_dims* d, const tdmpc_plan_params* prm, const void* pa
     const bool pi_cache = pi_cache_on() && P > 0 && use_chain(c, B * T, 1, CK_PI);
     const RowMap pmH = {P, T, N};
     for (int i = 0; i < I; ++i) {
-        if (i > 0 && (rc = prep(c, noise, i, nullptr))) return rc;
+        const long toff = c.eps_cem_off + (long)i * c.eps_iter + c.eps_term_off;
+        // wide heads: the policy rows' terminal redraw (pi_from_mu) rides in this iteration's prep launch
+        const bool pm_in_prep = wide_heads && P > 0 && i > 0;
+        if (i > 0) {
+            const PiMuArgs pm = pimu_args(c, B * P, pmH, noise, c.eps_env, P, toff + (long)N * c.A, prm->min_std);
+            if ((rc = prep(c, noise, i, nullptr, pm_in_prep ? &pm : nullptr))) return rc;
+        }
         if (i > 0 || P == 0)
             for (int t = 0; t < H; ++t)
                 if ((rc = step_next(c, t, B * N, rm, prm->discount_pow[t], t == 0, t == H - 1, 1)))
                     return rc;
-        const long toff = c.eps_cem_off + (long)i * c.eps_iter + c.eps_term_off;
         if (wide_heads) {
             if (P > 0) {
                 if (i == 0) rc = policy(c, H, B * P, pmH, noise, c.eps_env, P, toff + (long)N * c.A, prm->min_std, c.k.pimu);
-                else rc = policy_from_mu(c, B * P, pmH, noise, c.eps_env, P, toff + (long)N * c.A, prm->min_std);
                 if (rc || (rc = flush_split(c))) return rc;
             }
             if ((rc = terminal_wide(c, noise, toff, prm->min_std))) return rc;
